@@ -1,0 +1,206 @@
+"""ctypes mirror of include/avr_model.h (`avr_model_desc`) plus the state-block offsets, and
+`build_desc()` which turns a compiled scene (`avr/data/*.npz`) into a descriptor.
+
+The descriptor only holds pointers; `ModelDesc` keeps the numpy arrays alive.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
+
+# ---- capacities / offsets (must match include/avr_model.h) ----
+MAX_LINKS, MAX_DOF, MAX_FREE, MAX_HUMAN, MAX_CONTACTS = 16, 12, 10, 20, 96
+MAX_FOOD, ACT_DIM, OBS_DIM, INFO_DIM = 8, 7, 25, 2
+FB_WORDS, CP_WORDS = 13, 16
+S_Q = 0
+S_QD = S_Q + MAX_DOF
+S_QTGT = S_QD + MAX_DOF
+S_KP = S_QTGT + MAX_DOF
+S_MAXIMP = S_KP + MAX_DOF
+S_FREE = S_MAXIMP + MAX_DOF
+S_TASK = S_FREE + MAX_FREE * FB_WORDS
+T_TARGET, T_ITER, T_SUCCESS, T_ALIVE, T_HIT, T_GENDER, T_FLAGS, T_NCP, T_WORDS = 0, 3, 4, 5, 6, 7, 8, 9, 16
+S_HUMAN = S_TASK + T_WORDS
+S_CP = S_HUMAN + MAX_HUMAN * 7
+STATE_WORDS = S_CP + MAX_CONTACTS * CP_WORDS
+CP_SA, CP_SB, CP_LA, CP_LB, CP_N, CP_DIST, CP_IMP, CP_LIFE, CP_PAIR = 0, 1, 2, 5, 8, 11, 12, 13, 14
+
+PI32 = C.POINTER(C.c_int32)
+PF64 = C.POINTER(C.c_double)
+
+
+class avr_model_desc(C.Structure):
+    _fields_ = [
+        ('n_links', C.c_int32), ('n_dof', C.c_int32),
+        ('rl_parent', PI32), ('rl_jtype', PI32), ('rl_dof', PI32), ('rl_has_limit', PI32),
+        ('rl_jpos', PF64), ('rl_jquat', PF64), ('rl_axis', PF64),
+        ('rl_com_pos', PF64), ('rl_com_quat', PF64), ('rl_mass', PF64), ('rl_inertia', PF64),
+        ('rl_lower', PF64), ('rl_upper', PF64),
+        ('robot_base', PF64),
+        ('n_free', C.c_int32),
+        ('fb_mass', PF64), ('fb_inertia', PF64), ('fb_gravity', PF64),
+        ('n_static', C.c_int32),
+        ('st_pose', PF64),
+        ('n_human', C.c_int32),
+        ('n_bodies', C.c_int32),
+        ('body_kind', PI32), ('body_index', PI32), ('body_shape_start', PI32), ('body_shape_count', PI32),
+        ('body_flags', PI32),
+        ('body_friction', PF64), ('body_threshold', PF64),
+        ('body_aabb', PF64),
+        ('n_shapes', C.c_int32),
+        ('shape_kind', PI32), ('shape_body', PI32), ('shape_gender', PI32), ('shape_hull', PI32),
+        ('shape_pose', PF64), ('shape_param', PF64), ('shape_margin', PF64), ('shape_aabb', PF64),
+        ('n_hull_verts', C.c_int32), ('n_hull_planes', C.c_int32),
+        ('hull_verts', PF64), ('hull_planes', PF64),
+        ('n_pairs', C.c_int32),
+        ('pair_a', PI32), ('pair_b', PI32),
+        ('n_arm', C.c_int32), ('arm_dofs', C.c_int32 * 8),
+        ('n_finger', C.c_int32), ('finger_dofs', C.c_int32 * 4),
+        ('tool_link', C.c_int32), ('torso_link', C.c_int32), ('head_slot', C.c_int32),
+        ('spoon_free', C.c_int32), ('bowl_free', C.c_int32), ('food_free0', C.c_int32), ('n_food', C.c_int32),
+        ('table_body', C.c_int32), ('bowl_body', C.c_int32), ('spoon_body', C.c_int32), ('food_body0', C.c_int32),
+        ('human_body0', C.c_int32), ('n_human_bodies', C.c_int32), ('robot_body0', C.c_int32), ('n_robot_bodies', C.c_int32),
+        ('tool_offset', C.c_double * 7),
+        ('mouth_offset', (C.c_double * 3) * 2),
+        ('arm_lower', C.c_double * 8), ('arm_upper', C.c_double * 8),
+        ('time_step', C.c_double),
+        ('num_sub_steps', C.c_int32), ('frame_skip', C.c_int32), ('solver_iterations', C.c_int32),
+        ('max_episode_steps', C.c_int32),
+        ('erp', C.c_double), ('warmstart', C.c_double), ('linear_damping', C.c_double),
+        ('angular_damping', C.c_double), ('max_coord_vel', C.c_double),
+        ('default_motor_impulse', C.c_double),
+        ('robot_gain', C.c_double), ('robot_force', C.c_double),
+        ('finger_gain', C.c_double), ('finger_force', C.c_double), ('finger_target', C.c_double),
+        ('fixed_max_force', C.c_double),
+        ('w_distance', C.c_double), ('w_action', C.c_double), ('w_food', C.c_double),
+        ('w_velocity', C.c_double), ('w_force_nontarget', C.c_double), ('w_high_forces', C.c_double),
+        ('w_food_hit', C.c_double), ('w_food_velocities', C.c_double), ('task_success_threshold', C.c_double),
+    ]
+
+
+# FeedingJaco physics / task constants.  Values marked [ext] are assumed Bullet/PyBullet
+# defaults; the rest are cited to the reference.
+FEEDING_PARAMS = dict(
+    time_step=0.02,              # world_creation.py:75
+    num_sub_steps=2,             # feeding.py:289
+    frame_skip=5,                # feeding.py:18
+    solver_iterations=10,        # feeding.py:289
+    max_episode_steps=200,       # assistive_gym/__init__.py:270-274
+    erp=0.2,                     # [ext] btContactSolverInfo::m_erp
+    warmstart=0.85,              # [ext] btContactSolverInfo::m_warmstartingFactor
+    linear_damping=0.04,         # [ext] btMultiBody default damping
+    angular_damping=0.04,        # [ext]
+    max_coord_vel=100.0,         # [ext] btMultiBody::m_maxCoordinateVelocity
+    default_motor_impulse=1.0,   # [ext] PyBullet createJointMotors default velocity motor
+    robot_gain=0.005,            # config.ini:21 (feeding robot_gains)
+    robot_force=1.0,             # config.ini:22
+    finger_gain=0.05,            # world_creation.py:328
+    finger_force=500.0,          # world_creation.py:328
+    finger_target=1.33,          # feeding.py:279
+    fixed_max_force=500.0,       # world_creation.py:364
+    w_distance=1.0, w_action=0.01, w_food=1.0,                       # config.ini:23-25
+    w_velocity=0.25, w_force_nontarget=0.01, w_high_forces=0.05,     # config.ini:37-39
+    w_food_hit=1.0, w_food_velocities=1.0,                           # config.ini:40-41
+    task_success_threshold=0.75,                                     # config.ini:26
+)
+
+
+def load_scene(name='feeding_jaco'):
+    return dict(np.load(os.path.join(DATA_DIR, name + '.npz')))
+
+
+class ModelDesc:
+    """Owns the arrays behind an `avr_model_desc`."""
+
+    def __init__(self, A, params=None):
+        P = dict(FEEDING_PARAMS)
+        if params:
+            P.update(params)
+        self.A = {}
+        self.params = P
+        d = avr_model_desc()
+
+        def arr(key, dtype):
+            a = np.ascontiguousarray(A[key], dtype=dtype)
+            if a.size == 0:
+                a = np.zeros(1, dtype=dtype)
+            self.A[key] = a
+            return a.ctypes.data_as(PI32 if dtype == np.int32 else PF64)
+
+        d.n_links = int(A['n_links'])
+        d.n_dof = int(A['n_dof'])
+        for k in ('rl_parent', 'rl_jtype', 'rl_dof', 'rl_has_limit'):
+            setattr(d, k, arr(k, np.int32))
+        for k in ('rl_jpos', 'rl_jquat', 'rl_axis', 'rl_com_pos', 'rl_com_quat', 'rl_mass', 'rl_inertia',
+                  'rl_lower', 'rl_upper', 'robot_base'):
+            setattr(d, k, arr(k, np.float64))
+        d.n_free = len(A['fb_mass'])
+        for k in ('fb_mass', 'fb_inertia', 'fb_gravity'):
+            setattr(d, k, arr(k, np.float64))
+        d.n_static = len(A['st_pose'])
+        d.st_pose = arr('st_pose', np.float64)
+        d.n_human = len(A['human_slot_link'])
+        d.n_bodies = len(A['body_kind'])
+        for k in ('body_kind', 'body_index', 'body_shape_start', 'body_shape_count', 'body_flags'):
+            setattr(d, k, arr(k, np.int32))
+        for k in ('body_friction', 'body_threshold', 'body_aabb'):
+            setattr(d, k, arr(k, np.float64))
+        d.n_shapes = len(A['shape_kind'])
+        for k in ('shape_kind', 'shape_body', 'shape_gender', 'shape_hull'):
+            setattr(d, k, arr(k, np.int32))
+        for k in ('shape_pose', 'shape_param', 'shape_margin', 'shape_aabb'):
+            setattr(d, k, arr(k, np.float64))
+        d.n_hull_verts = len(A['hull_verts'])
+        d.n_hull_planes = 0
+        d.hull_verts = arr('hull_verts', np.float64)
+        self.A['hull_planes'] = np.zeros(4)
+        d.hull_planes = self.A['hull_planes'].ctypes.data_as(PF64)
+        d.n_pairs = len(A['pair_a'])
+        d.pair_a = arr('pair_a', np.int32)
+        d.pair_b = arr('pair_b', np.int32)
+        arm = [int(x) for x in A['task_arm_dofs']]
+        fin = [int(x) for x in A['task_finger_dofs']]
+        d.n_arm = len(arm)
+        for i, x in enumerate(arm):
+            d.arm_dofs[i] = x
+        d.n_finger = len(fin)
+        for i, x in enumerate(fin):
+            d.finger_dofs[i] = x
+        d.tool_link = int(A['task_tool_link'])
+        d.torso_link = int(A['task_torso_link'])
+        d.head_slot = int(A['task_head_slot'])
+        d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, 1, 2, 8
+        d.table_body = int(A['task_table_body'])
+        d.bowl_body = int(A['task_bowl_body'])
+        d.spoon_body = int(A['task_spoon_body'])
+        d.food_body0 = int(A['task_food_body0'])
+        d.human_body0 = int(A['task_human_body0'])
+        d.n_human_bodies = int(np.sum(A['body_kind'] == 3))
+        d.robot_body0 = 0
+        d.n_robot_bodies = int(np.sum(A['body_kind'] == 0))
+        for i, x in enumerate(A['task_tool_offset']):
+            d.tool_offset[i] = float(x)
+        for i in range(3):
+            d.mouth_offset[0][i] = float(A['task_mouth_male'][i])
+            d.mouth_offset[1][i] = float(A['task_mouth_female'][i])
+        # take_step limit zeroing uses getJointInfo limits; continuous joints -> +-1e10
+        # (world_creation.py:122-124)
+        dof_link = {int(A['rl_dof'][l]): l for l in range(int(A['n_links'])) if A['rl_dof'][l] >= 0}
+        for i, dof in enumerate(arm):
+            l = dof_link[dof]
+            if A['rl_has_limit'][l]:
+                d.arm_lower[i], d.arm_upper[i] = float(A['rl_lower'][l]), float(A['rl_upper'][l])
+            else:
+                d.arm_lower[i], d.arm_upper[i] = -1e10, 1e10
+        for k, v in P.items():
+            setattr(d, k, v)
+        self.desc = d
+        self.n_dof = d.n_dof
+        self.arm_dofs = arm
+        self.finger_dofs = fin
+        self.dof_link = dof_link
+
+    def ptr(self):
+        return C.byref(self.desc)

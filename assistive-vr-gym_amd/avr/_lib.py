@@ -1,0 +1,187 @@
+"""ctypes binding of libavr.so (include/avr.h) -- the product path.
+
+The library is built in-tree (`python -m avr.build` or `__graft_entry__.build()`) for gfx950.
+There is no fallback: if the shared object or a GPU is missing, the calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as ABI
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libavr.so')
+
+EXPORTS = [
+    'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',
+    'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
+    'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_state_words', 'avr_abi_version',
+    'avr_kernel_info', 'avr_last_error', 'avr_substep',
+]
+
+
+class avr_config(C.Structure):
+    _fields_ = [('n_envs', C.c_int32), ('device', C.c_int32), ('env_offset', C.c_int32), ('flags', C.c_int32),
+                ('seed', C.c_uint64)]
+
+
+_LIB = None
+
+
+def load(path=LIB_PATH):
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError('libavr.so not built (%s); run __graft_entry__.build()' % path)
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    lib.avr_create.argtypes = [C.POINTER(avr_config), vp, C.POINTER(vp)]
+    lib.avr_destroy.argtypes = [vp]
+    lib.avr_set_state.argtypes = [vp, vp]
+    lib.avr_get_state.argtypes = [vp, vp]
+    lib.avr_set_state_masked.argtypes = [vp, vp, vp]
+    lib.avr_settle.argtypes = [vp, C.c_int32, vp]
+    lib.avr_step.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.avr_step_device.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.avr_step_random_device.argtypes = [vp, C.c_int64, vp, vp, vp, vp]
+    lib.avr_random_actions_device.argtypes = [vp, C.c_int64, vp]
+    lib.avr_sync.argtypes = [vp]
+    lib.avr_stream.argtypes = [vp]
+    lib.avr_stream.restype = vp
+    lib.avr_state_device_ptr.argtypes = [vp]
+    lib.avr_state_device_ptr.restype = vp
+    lib.avr_n_envs.argtypes = [vp]
+    lib.avr_state_words.restype = C.c_int32
+    lib.avr_abi_version.restype = C.c_int32
+    lib.avr_kernel_info.argtypes = [vp, vp]
+    lib.avr_last_error.argtypes = [vp]
+    lib.avr_last_error.restype = C.c_char_p
+    lib.avr_substep.argtypes = [vp, C.c_float]
+    _LIB = lib
+    return lib
+
+
+class Sim:
+    """One libavr handle = one GPU, n_envs environments."""
+
+    def __init__(self, md, n_envs, device=0, seed=1001, env_offset=0):
+        self.lib = load()
+        self.md = md
+        self.n = int(n_envs)
+        cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=0, seed=seed)
+        h = C.c_void_p()
+        rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))
+        self.h = h
+        if rc:
+            msg = self.lib.avr_last_error(h).decode() if h.value else 'avr_create failed'
+            if h.value:
+                self.lib.avr_destroy(h)
+                self.h = None
+            raise RuntimeError('avr_create failed (%d): %s' % (rc, msg))
+        self.words = self.lib.avr_state_words()
+
+    def _chk(self, rc):
+        if rc:
+            raise RuntimeError(self.lib.avr_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.avr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_state(self, S):
+        S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
+        self._chk(self.lib.avr_set_state(self.h, S.ctypes.data))
+
+    def set_state_masked(self, mask, S):
+        S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
+        mask = np.ascontiguousarray(mask, np.uint8)
+        self._chk(self.lib.avr_set_state_masked(self.h, mask.ctypes.data, S.ctypes.data))
+
+    def get_state(self):
+        S = np.zeros((self.n, self.words), np.float32)
+        self._chk(self.lib.avr_get_state(self.h, S.ctypes.data))
+        return S
+
+    def settle(self, frames=100):
+        obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        self._chk(self.lib.avr_settle(self.h, frames, obs.ctypes.data))
+        return obs
+
+    def substep(self, dt):
+        self._chk(self.lib.avr_substep(self.h, dt))
+
+    def step(self, act):
+        act = np.ascontiguousarray(act, np.float32).reshape(self.n, ABI.ACT_DIM)
+        obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        rew = np.zeros(self.n, np.float32)
+        done = np.zeros(self.n, np.uint8)
+        info = np.zeros((self.n, ABI.INFO_DIM), np.float32)
+        self._chk(self.lib.avr_step(self.h, act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data, info.ctypes.data))
+        return obs, rew, done.astype(bool), info
+
+    # device-pointer variants (torch tensors' data_ptr()); asynchronous on the handle's stream
+    def step_device(self, d_act, d_obs, d_rew, d_done, d_info):
+        self._chk(self.lib.avr_step_device(self.h, d_act, d_obs, d_rew, d_done, d_info))
+
+    def step_random_device(self, t, d_obs=None, d_rew=None, d_done=None, d_info=None):
+        self._chk(self.lib.avr_step_random_device(self.h, int(t), d_obs, d_rew, d_done, d_info))
+
+    def random_actions_device(self, t, d_act):
+        self._chk(self.lib.avr_random_actions_device(self.h, int(t), d_act))
+
+    def sync(self):
+        self._chk(self.lib.avr_sync(self.h))
+
+    def stream(self):
+        return self.lib.avr_stream(self.h)
+
+    def kernel_info(self):
+        out = np.zeros(4, np.int32)
+        self._chk(self.lib.avr_kernel_info(self.h, out.ctypes.data))
+        return dict(vgprs=int(out[0]), lds_bytes=int(out[2]), scratch_bytes=int(out[3]))
+
+
+# ---------------------------------------------------------------- Philox4x32-10 (host mirror)
+M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+
+
+def philox4x32_10(c, k0, k1):
+    """Vectorised Philox4x32-10 on uint64 arrays holding 32-bit values; c: (4, N)."""
+    c = [np.asarray(x, np.uint64) & 0xFFFFFFFF for x in c]
+    k0 = np.uint64(k0 & 0xFFFFFFFF)
+    k1 = np.uint64(k1 & 0xFFFFFFFF)
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(M0) * c[0]
+        p1 = np.uint64(M1) * c[2]
+        h0, l0 = p0 >> np.uint64(32), p0 & mask
+        h1, l1 = p1 >> np.uint64(32), p1 & mask
+        c = [h1 ^ c[1] ^ k0, l1, h0 ^ c[3] ^ k1, l0]
+        k0 = (k0 + np.uint64(W0)) & mask
+        k1 = (k1 + np.uint64(W1)) & mask
+    return c
+
+
+def random_actions(seed, env_ids, t, act_dim=ABI.ACT_DIM):
+    """a[e, j] ~ U(-1,1) float32 from Philox4x32-10 keyed by (seed, env, t) -- identical to the
+    device generator (examples/random_actions.py semantics with a counter-based stream)."""
+    env_ids = np.asarray(env_ids, np.uint64)
+    out = np.zeros((len(env_ids), act_dim), np.float32)
+    for blk in range((act_dim + 3) // 4):
+        c = [env_ids, np.full_like(env_ids, t & 0xFFFFFFFF), np.full_like(env_ids, blk), np.full_like(env_ids, (t >> 32) & 0xFFFFFFFF)]
+        r = philox4x32_10(c, seed, seed >> 32)
+        for k in range(4):
+            j = 4 * blk + k
+            if j < act_dim:
+                x = (r[k] >> np.uint64(8)).astype(np.float32)
+                out[:, j] = x * np.float32(1.0 / 16777216.0) * np.float32(2.0) - np.float32(1.0)
+    return out

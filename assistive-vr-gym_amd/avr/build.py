@@ -1,0 +1,56 @@
+"""In-tree build of the native artefacts: libavr.so (hipcc, gfx950) and the CPU oracle (gcc).
+
+`python -m avr.build` or `__graft_entry__.build()`.  No torch extension machinery: the product
+is a plain C-ABI shared library loaded with ctypes.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, 'csrc')
+LIB = os.path.join(HERE, 'libavr.so')
+ARCH = os.environ.get('AVR_OFFLOAD_ARCH', 'gfx950')
+SOURCES = ['avr_kernel.hip', 'avr_capi.hip']
+HEADERS = ['avr_math.h', 'avr_kmodel.h']
+
+
+def _hipcc():
+    for c in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError('hipcc not found')
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force=False, extra=()):
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result',
+           '-o', LIB] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
+    subprocess.check_call(cmd)
+    return LIB
+
+
+def build_oracle():
+    subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
+
+
+def build_all(force=False):
+    build_lib(force=force)
+    build_oracle()
+
+
+if __name__ == '__main__':
+    build_all(force='--force' in sys.argv)
+    print(LIB)

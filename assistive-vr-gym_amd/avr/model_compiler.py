@@ -1,0 +1,691 @@
+"""Offline model compiler: reference assets (URDF / DAE / VHACD-OBJ) + the human link tables
+-> one flat, self-contained scene description (`avr/data/<task>.npz`).
+
+It runs only in the build container (it reads `/root/reference`); the compiled `.npz` is what
+ships.  Nothing here is on the step path.  What it restates, with reference citations:
+
+* Link numbering is the multibody DFS pre-order of the URDF tree, children in declaration
+  order (checked against the hard-coded indices `world_creation.py:283`
+  arm [1..7], `world_creation.py:320` fingers [9,11,13], tool link 8 `world_creation.py:334`).
+* Inertia is recomputed from the collision compound's AABB because Jaco/spoon/bowl are loaded
+  without URDF_USE_INERTIA_FROM_FILE (`world_creation.py:282`, `feeding.py:185`,
+  `world_creation.py:343`); the URDF inertial origin is kept.  (Bullet behaviour)
+* DAE collision meshes become one convex hull of all vertices; OBJ files with several `o`
+  objects become a compound of one hull per object.  URDF shapes get margin 0.001.
+* The human is `HumanCreation.create_human` (`human_creation.py:57-301`) with its creation
+  order remapped to DFS order (legend `human_creation.py:5-45`).
+* Collision filters: Jaco self-collision except parent/child (`world_creation.py:282`),
+  spoon vs gripper links 7..14 off (`world_creation.py:359-361`), static-vs-static never.
+"""
+import os
+import re
+import xml.etree.ElementTree as ET
+
+import numpy as np
+from scipy.spatial import ConvexHull
+
+from . import geom as G
+
+REF_ASSETS = '/root/reference/assistive_gym/envs/assets'
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
+
+URDF_MARGIN = 0.001          # gUrdfDefaultCollisionMargin (assumed Bullet default)
+CONTACT_BREAKING = 0.02      # gContactBreakingThreshold (assumed Bullet default)
+
+SPHERE, CAPSULE, BOX, HULL = 0, 1, 2, 3
+KIND_ROBOT, KIND_FREE, KIND_STATIC, KIND_HUMAN = 0, 1, 2, 3
+J_FIXED, J_REVOLUTE, J_PRISMATIC = 0, 1, 2
+
+
+# ----------------------------------------------------------------------------- meshes
+def dae_vertices(path):
+    s = open(path).read()
+    out = []
+    for m in re.finditer(r'<float_array id="[^"]*positions-array" count="(\d+)">([^<]*)<', s):
+        out.append(np.array(m.group(2).split(), float).reshape(-1, 3))
+    return np.concatenate(out, 0)
+
+
+def obj_groups(path):
+    groups, cur = [], None
+    for line in open(path):
+        if line.startswith('o ') or line.startswith('g '):
+            cur = []
+            groups.append(cur)
+        elif line.startswith('v '):
+            if cur is None:
+                cur = []
+                groups.append(cur)
+            cur.append([float(x) for x in line.split()[1:4]])
+    return [np.array(g, float) for g in groups if len(g) >= 4]
+
+
+class Hull:
+    """Convex hull of a point set: hull vertices + merged face planes n.x <= d (core, no margin)."""
+
+    def __init__(self, pts):
+        pts = np.asarray(pts, float)
+        h = ConvexHull(pts)
+        self.verts = pts[h.vertices]
+        planes = []
+        for eq in h.equations:
+            n, d = eq[:3], -eq[3]
+            dup = False
+            for p in planes:
+                if np.dot(p[:3], n) > 1.0 - 1e-9 and abs(p[3] - d) < 1e-9:
+                    dup = True
+                    break
+            if not dup:
+                planes.append(np.array([n[0], n[1], n[2], d]))
+        self.planes = np.array(planes)
+
+
+# ----------------------------------------------------------------------------- shapes
+class Shape:
+    def __init__(self, kind, pos=(0, 0, 0), quat=(0, 0, 0, 1), radius=0.0, half_height=0.0,
+                 half_extents=(0, 0, 0), hull=None, margin=URDF_MARGIN, gender=-1):
+        self.kind = kind
+        self.pos = np.asarray(pos, float)
+        self.quat = np.asarray(quat, float)
+        self.radius = float(radius)
+        self.half_height = float(half_height)
+        self.half_extents = np.asarray(half_extents, float)
+        self.hull = hull
+        self.margin = float(margin) if kind in (BOX, HULL) else float(radius)
+        self.gender = gender
+
+    def local_aabb(self):
+        """(center, half) of the shape's AABB in its OWN frame, Bullet getAabb semantics."""
+        if self.kind == SPHERE:
+            return np.zeros(3), np.full(3, self.radius)
+        if self.kind == CAPSULE:
+            return np.zeros(3), np.array([self.radius, self.radius, self.radius + self.half_height])
+        if self.kind == BOX:
+            return np.zeros(3), self.half_extents.copy()
+        v = self.hull.verts
+        lo, hi = v.min(0) - self.margin, v.max(0) + self.margin
+        # btTransformAabb adds the margin again on top of the cached local AABB (Bullet quirk)
+        return 0.5 * (lo + hi), 0.5 * (hi - lo) + self.margin
+
+    def aabb_in(self, pos, quat):
+        """AABB of this shape (placed at self.pos/self.quat in a parent frame) expressed in
+        the frame (pos, quat) * parent."""
+        c, h = self.local_aabb()
+        p, q = G.tf_mul(pos, quat, self.pos, self.quat)
+        R = G.quat_to_mat(q)
+        cw = p + R @ c
+        hw = np.abs(R) @ h
+        return cw - hw, cw + hw
+
+
+def compound_aabb(shapes):
+    lo = np.full(3, np.inf)
+    hi = np.full(3, -np.inf)
+    for s in shapes:
+        a, b = s.aabb_in(np.zeros(3), np.array([0, 0, 0, 1.0]))
+        lo, hi = np.minimum(lo, a), np.maximum(hi, b)
+    return lo, hi
+
+
+def box_inertia(mass, lo, hi):
+    lx, ly, lz = hi - lo
+    return mass / 12.0 * np.array([ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly])
+
+
+def breaking_threshold(shapes):
+    """btCollisionShape::getContactBreakingThreshold = angular-motion disc * 0.02, disc from the
+    root shape's bounding sphere (CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD)."""
+    lo, hi = compound_aabb(shapes)
+    c = 0.5 * (lo + hi)
+    r = 0.5 * np.linalg.norm(hi - lo)
+    return CONTACT_BREAKING * (r + np.linalg.norm(c))
+
+
+# ----------------------------------------------------------------------------- URDF
+def _origin(el):
+    if el is None:
+        return np.zeros(3), np.array([0, 0, 0, 1.0])
+    xyz = np.array([float(x) for x in el.get('xyz', '0 0 0').split()])
+    rpy = [float(x) for x in el.get('rpy', '0 0 0').split()]
+    return xyz, G.quat_from_euler(rpy)
+
+
+class Link:
+    pass
+
+
+def parse_urdf(path):
+    root = ET.parse(path).getroot()
+    base_dir = os.path.dirname(path)
+    links = {}
+    order = []
+    for le in root.findall('link'):
+        L = Link()
+        L.name = le.get('name')
+        ine = le.find('inertial')
+        if ine is not None:
+            L.mass = float(ine.find('mass').get('value'))
+            L.com_pos, L.com_quat = _origin(ine.find('origin'))
+        else:
+            L.mass = 0.0
+            L.com_pos, L.com_quat = np.zeros(3), np.array([0, 0, 0, 1.0])
+        L.collisions = []
+        for ce in le.findall('collision'):
+            pos, quat = _origin(ce.find('origin'))
+            ge = ce.find('geometry')
+            me, be, se = ge.find('mesh'), ge.find('box'), ge.find('sphere')
+            if me is not None:
+                scale = np.array([float(x) for x in me.get('scale', '1 1 1').split()])
+                L.collisions.append(('mesh', os.path.join(base_dir, me.get('filename')), scale, pos, quat))
+            elif be is not None:
+                size = np.array([float(x) for x in be.get('size').split()])
+                L.collisions.append(('box', size, None, pos, quat))
+            elif se is not None:
+                L.collisions.append(('sphere', float(se.get('radius')), None, pos, quat))
+        friction = 0.5
+        ct = le.find('contact')
+        if ct is not None and ct.find('lateral_friction') is not None:
+            friction = float(ct.find('lateral_friction').get('value'))
+        L.friction = friction
+        links[L.name] = L
+        order.append(L.name)
+    joints = []
+    for je in root.findall('joint'):
+        J = dict(name=je.get('name'), type=je.get('type'), parent=je.find('parent').get('link'),
+                 child=je.find('child').get('link'))
+        J['pos'], J['quat'] = _origin(je.find('origin'))
+        ax = je.find('axis')
+        J['axis'] = np.array([float(x) for x in ax.get('xyz').split()]) if ax is not None else np.zeros(3)
+        lim = je.find('limit')
+        J['lower'] = float(lim.get('lower', 0)) if lim is not None else 0.0
+        J['upper'] = float(lim.get('upper', -1)) if lim is not None else -1.0
+        joints.append(J)
+    children = {}
+    child_set = set()
+    for J in joints:
+        children.setdefault(J['parent'], []).append(J)
+        child_set.add(J['child'])
+    root_name = [n for n in order if n not in child_set][0]
+    # DFS pre-order over joints, children in declaration order
+    dfs = []
+
+    def visit(name, parent_idx):
+        for J in children.get(name, []):
+            idx = len(dfs)
+            dfs.append((J, parent_idx))
+            visit(J['child'], idx)
+    visit(root_name, -1)
+    return links, root_name, dfs
+
+
+def urdf_shapes(L, scale_override=None):
+    """Collision shapes of a URDF link, placed relative to the link's INERTIAL frame."""
+    inv_p, inv_q = G.tf_inv(L.com_pos, L.com_quat)
+    shapes = []
+    for kind, a, b, pos, quat in L.collisions:
+        p, q = G.tf_mul(inv_p, inv_q, pos, quat)
+        if kind == 'mesh':
+            path, scale = a, b
+            if path.endswith('.dae'):
+                shapes.append(Shape(HULL, p, q, hull=Hull(dae_vertices(path) * scale)))
+            else:
+                for g in obj_groups(path):
+                    shapes.append(Shape(HULL, p, q, hull=Hull(g * scale)))
+        elif kind == 'box':
+            shapes.append(Shape(BOX, p, q, half_extents=0.5 * a))
+        elif kind == 'sphere':
+            shapes.append(Shape(SPHERE, p, q, radius=a))
+    return shapes
+
+
+# ----------------------------------------------------------------------------- human
+def _capsule(radius, length, pos=(0, 0, 0), orient=(0, 0, 0, 1)):
+    return Shape(CAPSULE, pos, orient, radius=radius, half_height=0.5 * length)
+
+
+def _sphere(radius, pos=(0, 0, 0)):
+    return Shape(SPHERE, pos, (0, 0, 0, 1), radius=radius)
+
+
+def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
+    """Restatement of HumanCreation.create_human (human_creation.py:57-301), non-`new`,
+    non-cloth.  Returns (base_shapes, links[DFS]); each link dict carries parent (DFS index or
+    -1 for base), joint type, axis, origin (relative to parent COM frame), limits, mass,
+    shapes (relative to the link frame == its COM frame, inertial offsets are zero)."""
+    mass = {'male': 78.4, 'female': 62.5}[gender]               # config.ini:46-53
+    rs, hs = 1.0, 1.0
+    if hipbone_to_mouth_height is None:
+        hipbone_to_mouth_height = 0.6 if gender == 'male' else 0.54  # feeding.py:174
+    hs *= hipbone_to_mouth_height / (0.6 if gender == 'male' else 0.54)   # :60-63,75
+    q_y90 = G.quat_from_euler([0, np.pi / 2, 0])
+    q_x90 = G.quat_from_euler([np.pi / 2, 0, 0])
+    head_orient = G.quat_from_euler([np.pi / 2.0, 0, 0])
+    head_dir = os.path.join(REF_ASSETS, 'head_female_male')
+    if gender == 'male':                                          # human_creation.py:76-115
+        chest = _capsule(0.127 * rs, 0.056, orient=q_y90)
+        r_sh = _capsule(0.106 * rs, 0.253 / 8, pos=[-0.253 / 2.5 + 0.253 / 16, 0, 0], orient=q_y90)
+        l_sh = _capsule(0.106 * rs, 0.253 / 8, pos=[0.253 / 2.5 - 0.253 / 16, 0, 0], orient=q_y90)
+        neck = _capsule(0.06 * rs, 0.124 * hs, pos=[0, 0, (0.2565 - 0.1415 - 0.025) * hs])
+        upperarm = lambda: _capsule(0.043 * rs, 0.279 * hs, pos=[0, 0, -0.279 / 2.0 * hs])
+        forearm = lambda: _capsule(0.033 * rs, 0.257 * hs, pos=[0, 0, -0.257 / 2.0 * hs])
+        hand = lambda: _sphere(0.043 * rs, pos=[0, 0, -0.043 * rs])
+        waist = _capsule(0.1205 * rs, 0.049, orient=q_y90)
+        hips = _capsule(0.1335 * rs, 0.094, pos=[0, 0, -0.08125 * hs], orient=q_y90)
+        thigh = lambda: _capsule(0.08 * rs, 0.424 * hs, pos=[0, 0, -0.424 / 2.0 * hs])
+        shin = lambda: _capsule(0.05 * rs, 0.403 * hs, pos=[0, 0, -0.403 / 2.0 * hs])
+        foot = lambda: _capsule(0.05 * rs, 0.215 * hs, pos=[0, -0.1, -0.025 * rs], orient=q_x90)
+        head_file = 'BaseHeadMeshes_v5_male_cropped_reduced_compressed_vhacd.obj'
+        head_pos = [0.09, 0.08, -0.07 + 0.01]
+        chest_p = [0, 0, 0.156 * hs]
+        shoulders_p = [0, 0, 0.1415 / 2 * hs]
+        neck_p = [0, 0, 0.1515 * hs]
+        head_p = [0, 0, (0.399 - 0.1415 - 0.1205) * hs]
+        right_upperarm_p = [-0.106 * rs - 0.073, 0, 0]
+        left_upperarm_p = [0.106 * rs + 0.073, 0, 0]
+        forearm_p = [0, 0, -0.279 * hs]
+        hand_p = [0, 0, -(0.033 * rs + 0.257 * hs)]
+        waist_p = [0, 0, 0.08125 * hs]
+        right_thigh_p = [-0.08 * rs - 0.009, 0, -0.08125 * hs]
+        left_thigh_p = [0.08 * rs + 0.009, 0, -0.08125 * hs]
+        shin_p = [0, 0, -0.424 * hs]
+        foot_p = [0, 0, -0.403 * hs - 0.025]
+    else:                                                         # human_creation.py:117-161
+        chest = _capsule(0.127 * rs, 0.01, orient=q_y90)
+        r_sh = _capsule(0.092 * rs, 0.225 / 8, pos=[-0.225 / 2.5 + 0.225 / 16, 0, 0], orient=q_y90)
+        l_sh = _capsule(0.092 * rs, 0.225 / 8, pos=[0.225 / 2.5 - 0.225 / 16, 0, 0], orient=q_y90)
+        neck = _capsule(0.05 * rs, 0.121 * hs, pos=[0, 0, (0.2565 - 0.1415 - 0.025) * hs])
+        upperarm = lambda: _capsule(0.0355 * rs, 0.264 * hs, pos=[0, 0, -0.264 / 2.0 * hs])
+        forearm = lambda: _capsule(0.027 * rs, 0.234 * hs, pos=[0, 0, -0.234 / 2.0 * hs])
+        hand = lambda: _sphere(0.0355 * rs, pos=[0, 0, -0.0355 * rs])
+        waist = _capsule(0.11 * rs, 0.009, orient=q_y90)
+        hips = _capsule(0.127 * rs, 0.117, pos=[0, 0, -0.15 / 2 * hs], orient=q_y90)
+        thigh = lambda: _capsule(0.0775 * rs, 0.391 * hs, pos=[0, 0, -0.391 / 2.0 * hs])
+        shin = lambda: _capsule(0.045 * rs, 0.367 * hs, pos=[0, 0, -0.367 / 2.0 * hs])
+        foot = lambda: _capsule(0.045 * rs, 0.195 * hs, pos=[0, -0.09, -0.0225 * rs], orient=q_x90)
+        head_file = 'BaseHeadMeshes_v5_female_cropped_reduced_compressed_vhacd.obj'
+        head_pos = [-0.089, -0.09, -0.07]
+        chest_p = [0, 0, 0.15 * hs]
+        shoulders_p = [0, 0, 0.132 / 2 * hs]
+        neck_p = [0, 0, 0.132 * hs]
+        head_p = [0, 0, 0.12 * hs]
+        right_upperarm_p = [-0.092 * rs - 0.067, 0, 0]
+        left_upperarm_p = [0.092 * rs + 0.067, 0, 0]
+        forearm_p = [0, 0, -0.264 * hs]
+        hand_p = [0, 0, -(0.027 * rs + 0.234 * hs)]
+        waist_p = [0, 0, 0.15 / 2 * hs]
+        right_thigh_p = [-0.0775 * rs - 0.0145, 0, -0.15 / 2 * hs]
+        left_thigh_p = [0.0775 * rs + 0.0145, 0, -0.15 / 2 * hs]
+        shin_p = [0, 0, -0.391 * hs]
+        foot_p = [0, 0, -0.367 * hs - 0.045 / 2]
+    gidx = 0 if gender == 'male' else 1
+    head_shapes = [Shape(HULL, head_pos, head_orient, hull=Hull(g * 0.89), gender=gidx)
+                   for g in obj_groups(os.path.join(head_dir, head_file))]
+    jp = [0, 0, 0]
+    d = np.deg2rad
+    R, F = J_REVOLUTE, J_FIXED
+    # creation-order tables (human_creation.py:177-274); parent indices are 1-based (0 = base)
+    C = []   # (mass_frac, shapes, pos, parent1, jtype, axis, lo, hi)
+    C += [(0, [], waist_p, 0, F, [0, 0, 0], 0, 0), (0, [], jp, 1, F, [0, 0, 0], 0, 0),
+          (0.13, [waist], jp, 2, F, [0, 0, 0], 0, 0), (0.1, [chest], chest_p, 3, F, [0, 0, 0], 0, 0)]
+    ls = limit_scale
+    C += [(0, [], shoulders_p, 4, F, [0, 0, 0], 0, 0), (0, [], shoulders_p, 5, F, [0, 0, 0], 0, 0),
+          (0.05, [r_sh], jp, 6, F, [0, 0, 0], 0, 0), (0, [], shoulders_p, 4, F, [0, 0, 0], 0, 0),
+          (0, [], shoulders_p, 8, F, [0, 0, 0], 0, 0), (0.05, [l_sh], jp, 9, F, [0, 0, 0], 0, 0),
+          (0.01, [neck], neck_p, 4, R, [1, 0, 0], d(-10) * ls, d(20) * ls),
+          (0, [], head_p, 11, R, [1, 0, 0], d(-50) * ls, d(50) * ls),
+          (0, [], jp, 12, R, [0, 1, 0], d(-34) * ls, d(34) * ls),
+          (0.07, head_shapes, jp, 13, R, [0, 0, 1], d(-70) * ls, d(70) * ls)]
+    arm_axes = [[0, 1, 0], [1, 0, 0], [0, 0, 1], [1, 0, 0], [0, 0, 1], [1, 0, 0], [0, 1, 0]]
+    ra_lo = [5, -188, -90, -128, -90, -81, -27]
+    ra_hi = [198, 61, 90, 0, 90, 90, 47]
+    la_lo = [-198, -188, -90, -128, -90, -81, -47]
+    la_hi = [-5, 61, 90, 0, 90, 90, 27]
+    arm_mass = [0, 0, 0.033, 0, 0.019, 0, 0.0065]
+    for side, up_p, par0, lo, hi in (('r', right_upperarm_p, 7, ra_lo, ra_hi), ('l', left_upperarm_p, 10, la_lo, la_hi)):
+        shp = [[], [], [upperarm()], [], [forearm()], [], [hand()]]
+        pos = [up_p, jp, jp, forearm_p, jp, hand_p, jp]
+        base = len(C)
+        for k in range(7):
+            C.append((arm_mass[k], shp[k], pos[k], par0 if k == 0 else base + k, R, arm_axes[k],
+                      d(lo[k]) * ls, d(hi[k]) * ls))
+    leg_axes = [[1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]]
+    rl_lo, rl_hi = [-127, -40, -45, 0, -35, -23, -43], [30, 45, 40, 130, 38, 24, 35]
+    ll_lo, ll_hi = [-127, -45, -40, 0, -35, -24, -35], [30, 40, 45, 130, 38, 23, 43]
+    leg_mass = [0, 0, 0.105, 0.0475, 0, 0, 0.014]
+    for th_p, lo, hi in ((right_thigh_p, rl_lo, rl_hi), (left_thigh_p, ll_lo, ll_hi)):
+        shp = [[], [], [thigh()], [shin()], [], [], [foot()]]
+        pos = [th_p, jp, jp, shin_p, foot_p, jp, jp]
+        base = len(C)
+        for k in range(7):
+            C.append((leg_mass[k], shp[k], pos[k], 0 if k == 0 else base + k, R, leg_axes[k],
+                      d(lo[k]), d(hi[k])))
+    assert len(C) == 42
+    # DFS remap: children (in creation order) of each creation node; base = -1
+    kids = {}
+    for i, c in enumerate(C):
+        kids.setdefault(c[3] - 1, []).append(i)
+    dfs_of = {}
+    order = []
+
+    def visit(node):
+        for ch in kids.get(node, []):
+            dfs_of[ch] = len(order)
+            order.append(ch)
+            visit(ch)
+    visit(-1)
+    links = []
+    for ci in order:
+        mf, shp, pos, par1, jt, ax, lo, hi = C[ci]
+        links.append(dict(parent=-1 if par1 == 0 else dfs_of[par1 - 1], jtype=jt, axis=np.array(ax, float),
+                          pos=np.array(pos, float), lower=lo, upper=hi, mass=mass * mf, shapes=shp))
+    return [hips], links
+
+
+def human_fk(links, base_pos, base_quat, q):
+    """World poses of the human link frames (== COM frames) for joint angles q[42]."""
+    n = len(links)
+    P = np.zeros((n, 3))
+    Q = np.zeros((n, 4))
+    for i, L in enumerate(links):
+        if L['parent'] < 0:
+            pp, pq = np.asarray(base_pos, float), np.asarray(base_quat, float)
+        else:
+            pp, pq = P[L['parent']], Q[L['parent']]
+        p, qq = G.tf_mul(pp, pq, L['pos'], [0, 0, 0, 1])
+        if L['jtype'] == J_REVOLUTE:
+            qq = G.quat_mul(qq, G.quat_axis_angle(L['axis'], q[i]))
+        P[i], Q[i] = p, qq
+    return P, Q
+
+
+# ----------------------------------------------------------------------------- scene
+class Scene:
+    """Flat scene description consumed by the C-ABI (see include/avr_model.h)."""
+
+    def __init__(self):
+        self.bodies = []     # dicts: kind, index, shapes(list[Shape]), friction, name
+        self.robot = None
+        self.free = []
+        self.static = []
+        self.pairs = []
+        self.task = {}
+
+    def add_body(self, kind, index, shapes, friction, name, single=False):
+        # single=True: a bare (non-compound) collision shape (createMultiBody without a frame
+        # offset) -- Bullet runs convex-convex on it directly, no child AABB culling.
+        self.bodies.append(dict(kind=kind, index=index, shapes=shapes, friction=friction, name=name, single=single))
+        return len(self.bodies) - 1
+
+
+def build_jaco():
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, 'jaco', 'j2s7s300_gym.urdf'))
+    rob = dict(name=[], parent=[], jtype=[], dof=[], jpos=[], jquat=[], axis=[], com_pos=[], com_quat=[],
+               mass=[], inertia=[], lower=[], upper=[], has_limit=[], shapes=[], friction=[])
+    ndof = 0
+    for J, parent in dfs:
+        L = links[J['child']]
+        t = {'fixed': J_FIXED, 'revolute': J_REVOLUTE, 'continuous': J_REVOLUTE, 'prismatic': J_PRISMATIC}[J['type']]
+        rob['name'].append(L.name)
+        rob['parent'].append(parent)
+        rob['jtype'].append(t)
+        rob['dof'].append(ndof if t != J_FIXED else -1)
+        if t != J_FIXED:
+            ndof += 1
+        rob['jpos'].append(J['pos'])
+        rob['jquat'].append(J['quat'])
+        rob['axis'].append(J['axis'] / max(np.linalg.norm(J['axis']), 1e-12) if t != J_FIXED else np.zeros(3))
+        rob['com_pos'].append(L.com_pos)
+        rob['com_quat'].append(L.com_quat)
+        rob['mass'].append(L.mass)
+        shapes = urdf_shapes(L)
+        rob['shapes'].append(shapes)
+        if shapes and L.mass > 0:
+            lo, hi = compound_aabb(shapes)
+            rob['inertia'].append(box_inertia(L.mass, lo, hi))
+        else:
+            rob['inertia'].append(np.zeros(3))
+        # continuous joints are reported as (0,-1) = no limit (world_creation.py:122-124)
+        lim = t == J_REVOLUTE and J['type'] == 'revolute' and J['lower'] <= J['upper']
+        rob['lower'].append(J['lower'] if lim else 0.0)
+        rob['upper'].append(J['upper'] if lim else -1.0)
+        rob['has_limit'].append(1 if lim else 0)
+        rob['friction'].append(L.friction)
+    rob['ndof'] = ndof
+    return rob
+
+
+def build_free_urdf(rel):
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, rel))
+    assert not dfs
+    L = links[root]
+    shapes = urdf_shapes(L)
+    lo, hi = compound_aabb(shapes)
+    return dict(mass=L.mass, inertia=box_inertia(L.mass, lo, hi), shapes=shapes, friction=L.friction)
+
+
+def build_static_urdf(rel):
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, rel))
+    L = links[root]
+    return dict(shapes=urdf_shapes(L), friction=L.friction)
+
+
+def compile_feeding_jaco():
+    """FeedingJaco-v0 scene (feeding.py:144-331 + world_creation.py:27-93,274-293,330-365)."""
+    S = Scene()
+    rob = build_jaco()
+    S.robot = rob
+    S.robot_base_pos = np.array([-0.35, -0.3, 0.36])                      # feeding.py:188
+    S.robot_base_quat = np.array([0.0, 0.0, -0.7071067811865475, 0.7071067811865476])
+    robot_body = {}
+    for i in range(len(rob['name'])):
+        if rob['shapes'][i]:
+            robot_body[i] = S.add_body(KIND_ROBOT, i, rob['shapes'][i], rob['friction'][i], rob['name'][i])
+    # free bodies: spoon, bowl, 8 food spheres (feeding.py:280,185,291-308)
+    spoon = build_free_urdf('dinnerware/spoon.urdf')
+    bowl = build_free_urdf('dinnerware/bowl.urdf')
+    food_r, food_m = 0.005, 0.001
+    food_shape = [Shape(SPHERE, radius=food_r)]
+    S.free = [dict(name='spoon', mass=spoon['mass'], inertia=spoon['inertia'], gravity=np.zeros(3)),
+              dict(name='bowl', mass=bowl['mass'], inertia=bowl['inertia'], gravity=np.array([0, 0, -9.81]))]
+    for k in range(8):
+        S.free.append(dict(name='food%d' % k, mass=food_m, inertia=np.full(3, 0.4 * food_m * food_r * food_r),
+                           gravity=np.array([0, 0, -9.81])))
+    free_body = [S.add_body(KIND_FREE, 0, spoon['shapes'], spoon['friction'], 'spoon'),
+                 S.add_body(KIND_FREE, 1, bowl['shapes'], bowl['friction'], 'bowl')]
+    for k in range(8):
+        free_body.append(S.add_body(KIND_FREE, 2 + k, food_shape, 0.5, 'food%d' % k, single=True))
+    # statics: plane, wheelchair, table (world_creation.py:37,45-49; feeding.py:182)
+    plane = build_static_urdf('plane/plane.urdf')
+    chair = build_static_urdf('wheelchair/wheelchair.urdf')
+    table = build_static_urdf('table/table_tall.urdf')
+    S.static = [dict(name='plane', pos=np.zeros(3), quat=np.array([0, 0, 0, 1.0])),
+                dict(name='wheelchair', pos=np.array([0.0, 0.09, -0.01]),
+                     quat=G.quat_from_euler([np.pi / 2.0, 0, -np.pi / 2.0 - 0.05])),
+                dict(name='table', pos=np.array([0.35, -0.9, 0]), quat=np.array([0, 0, 0, 1.0]))]
+    static_body = [S.add_body(KIND_STATIC, 0, plane['shapes'], plane['friction'], 'plane'),
+                   S.add_body(KIND_STATIC, 1, chair['shapes'], chair['friction'], 'wheelchair'),
+                   S.add_body(KIND_STATIC, 2, table['shapes'], table['friction'], 'table')]
+    # human: per-env static bodies; shapes of both genders are compiled, a per-env gender
+    # selects which (head VHACD differs; capsule dims differ -> one slot set per gender).
+    S.human = {}
+    human_body = {}
+    for gender in ('male', 'female'):
+        base_shapes, hl = build_human(gender)
+        S.human[gender] = (base_shapes, hl)
+    # human slot list: base + DFS links that carry shapes; the slot set is identical for both
+    # genders, shapes differ -> store per-gender shapes on the same slot (gender-tagged).
+    slot_links = [-1] + [i for i, L in enumerate(S.human['male'][1]) if L['shapes']]
+    S.human_slots = slot_links
+    for si, li in enumerate(slot_links):
+        shapes = []
+        for gi, gender in enumerate(('male', 'female')):
+            base_shapes, hl = S.human[gender]
+            for s in (base_shapes if li < 0 else hl[li]['shapes']):
+                s.gender = gi
+                shapes.append(s)
+        human_body[li] = S.add_body(KIND_HUMAN, si, shapes, 0.5, 'human%d' % li)
+    # candidate body pairs (broadphase filter)
+    rb = sorted(robot_body.items())
+    dyn = [b for _, b in rb] + free_body
+    stat = static_body + [human_body[k] for k in slot_links]
+    parent = rob['parent']
+    pairs = []
+    for ia in range(len(rb)):
+        for ib in range(ia + 1, len(rb)):
+            la, lb = rb[ia][0], rb[ib][0]
+            if parent[lb] == la or parent[la] == lb:
+                continue                      # self-collision excludes parent/child
+            pairs.append((rb[ia][1], rb[ib][1]))
+    for li, b in rb:
+        for fb in free_body:
+            if fb == free_body[0] and 7 <= li <= 14:
+                continue                      # spoon vs gripper links (world_creation.py:359-361)
+            pairs.append((b, fb))
+        for sb in stat:
+            pairs.append((b, sb))
+    for i in range(len(free_body)):
+        for j in range(i + 1, len(free_body)):
+            pairs.append((free_body[i], free_body[j]))
+        for sb in stat:
+            pairs.append((free_body[i], sb))
+    S.pairs = pairs
+    S.robot_body = robot_body
+    S.table_body = static_body[2]
+    S.free_body = free_body
+    S.static_body = static_body
+    S.human_body = human_body
+    S.task = dict(
+        arm_dofs=[rob['dof'][j] for j in range(1, 8)],        # joints 1..7 (world_creation.py:283)
+        finger_dofs=[rob['dof'][j] for j in (9, 11, 13)],      # world_creation.py:320
+        tool_link=8, torso_link=0,                             # world_creation.py:363, feeding.py:124
+        tool_pos_offset=np.array([0.1, -0.0225, 0.03]),        # feeding.py:280
+        tool_orient_offset=G.quat_from_euler([-0.1, -np.pi / 2.0, 0]),
+        head_link=27, mouth_pos={'male': [0, -0.11, 0.03], 'female': [0, -0.1, 0.03]},  # feeding.py:253
+    )
+    return S
+
+
+def to_arrays(S):
+    """Flatten a Scene into the arrays of include/avr_model.h (float64 / int32)."""
+    rob = S.robot
+    A = {}
+    nl = len(rob['name'])
+    A['rl_parent'] = np.array(rob['parent'], np.int32)
+    A['rl_jtype'] = np.array(rob['jtype'], np.int32)
+    A['rl_dof'] = np.array(rob['dof'], np.int32)
+    A['rl_jpos'] = np.array(rob['jpos'])
+    A['rl_jquat'] = np.array(rob['jquat'])
+    A['rl_axis'] = np.array(rob['axis'])
+    A['rl_com_pos'] = np.array(rob['com_pos'])
+    A['rl_com_quat'] = np.array(rob['com_quat'])
+    A['rl_mass'] = np.array(rob['mass'])
+    A['rl_inertia'] = np.array(rob['inertia'])
+    A['rl_lower'] = np.array(rob['lower'])
+    A['rl_upper'] = np.array(rob['upper'])
+    A['rl_has_limit'] = np.array(rob['has_limit'], np.int32)
+    A['robot_base'] = np.concatenate([S.robot_base_pos, S.robot_base_quat])
+    A['fb_mass'] = np.array([f['mass'] for f in S.free])
+    A['fb_inertia'] = np.array([f['inertia'] for f in S.free])
+    A['fb_gravity'] = np.array([f['gravity'] for f in S.free])
+    A['st_pose'] = np.array([np.concatenate([s['pos'], s['quat']]) for s in S.static])
+    # shapes, sorted by body
+    shape_rows, hv = [], []
+    b_start, b_count, b_kind, b_index, b_fric, b_thr, b_aabb, b_flags = [], [], [], [], [], [], [], []
+    for b in S.bodies:
+        b_start.append(len(shape_rows))
+        b_count.append(len(b['shapes']))
+        b_kind.append(b['kind'])
+        b_index.append(b['index'])
+        b_fric.append(b['friction'])
+        if b['kind'] == KIND_HUMAN:
+            # per-gender AABBs; threshold: min over genders (they differ by <10%)
+            per = [[s for s in b['shapes'] if s.gender == g] for g in (0, 1)]
+            thr = min(breaking_threshold(p) for p in per)
+            boxes = [compound_aabb(p) for p in per]
+        else:
+            thr = breaking_threshold(b['shapes'])
+            boxes = [compound_aabb(b['shapes'])] * 2
+        b_thr.append(thr)
+        b_aabb.append(np.concatenate([np.concatenate([0.5 * (lo + hi), 0.5 * (hi - lo)]) for lo, hi in boxes]))
+        b_flags.append(1 if b.get('single', False) else 0)
+        for s in b['shapes']:
+            c, h = s.local_aabb()
+            row = dict(kind=s.kind, body=len(b_start) - 1, pos=s.pos, quat=s.quat, margin=s.margin,
+                       gender=s.gender, aabb=np.concatenate([c, h]))
+            if s.kind == SPHERE:
+                row['param'] = [s.radius, 0, 0, 0]
+            elif s.kind == CAPSULE:
+                row['param'] = [s.radius, s.half_height, 0, 0]
+            elif s.kind == BOX:
+                row['param'] = [s.half_extents[0], s.half_extents[1], s.half_extents[2], 0]
+            else:
+                row['param'] = [0, 0, 0, 0]
+            if s.kind == HULL:
+                row['hull'] = [len(hv), len(s.hull.verts), 0, 0]
+                hv.extend(s.hull.verts)
+            else:
+                row['hull'] = [0, 0, 0, 0]
+            shape_rows.append(row)
+    A['body_kind'] = np.array(b_kind, np.int32)
+    A['body_index'] = np.array(b_index, np.int32)
+    A['body_shape_start'] = np.array(b_start, np.int32)
+    A['body_shape_count'] = np.array(b_count, np.int32)
+    A['body_friction'] = np.array(b_fric)
+    A['body_threshold'] = np.array(b_thr)
+    A['body_aabb'] = np.array(b_aabb)
+    A['body_flags'] = np.array(b_flags, np.int32)
+    A['shape_kind'] = np.array([r['kind'] for r in shape_rows], np.int32)
+    A['shape_body'] = np.array([r['body'] for r in shape_rows], np.int32)
+    A['shape_gender'] = np.array([r['gender'] for r in shape_rows], np.int32)
+    A['shape_hull'] = np.array([r['hull'] for r in shape_rows], np.int32)
+    A['shape_pose'] = np.array([np.concatenate([r['pos'], r['quat']]) for r in shape_rows])
+    A['shape_param'] = np.array([r['param'] for r in shape_rows], float)
+    A['shape_margin'] = np.array([r['margin'] for r in shape_rows])
+    A['shape_aabb'] = np.array([r['aabb'] for r in shape_rows])
+    A['hull_verts'] = np.array(hv).reshape(-1, 3)
+    A['pair_a'] = np.array([p[0] for p in S.pairs], np.int32)
+    A['pair_b'] = np.array([p[1] for p in S.pairs], np.int32)
+    A['n_links'] = np.int32(nl)
+    A['n_dof'] = np.int32(rob['ndof'])
+    return A
+
+
+def compile_all(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    S = compile_feeding_jaco()
+    A = to_arrays(S)
+    # human kinematic tables (host reset path) for both genders
+    for gender in ('male', 'female'):
+        base_shapes, hl = S.human[gender]
+        A['human_%s_parent' % gender] = np.array([L['parent'] for L in hl], np.int32)
+        A['human_%s_jtype' % gender] = np.array([L['jtype'] for L in hl], np.int32)
+        A['human_%s_axis' % gender] = np.array([L['axis'] for L in hl])
+        A['human_%s_pos' % gender] = np.array([L['pos'] for L in hl])
+        A['human_%s_lower' % gender] = np.array([L['lower'] for L in hl])
+        A['human_%s_upper' % gender] = np.array([L['upper'] for L in hl])
+    A['human_slot_link'] = np.array(S.human_slots, np.int32)
+    t = S.task
+    A['task_arm_dofs'] = np.array(t['arm_dofs'], np.int32)
+    A['task_finger_dofs'] = np.array(t['finger_dofs'], np.int32)
+    A['task_tool_link'] = np.int32(t['tool_link'])
+    A['task_torso_link'] = np.int32(t['torso_link'])
+    A['task_tool_offset'] = np.concatenate([t['tool_pos_offset'], t['tool_orient_offset']])
+    A['task_head_link'] = np.int32(t['head_link'])
+    A['task_mouth_male'] = np.array(t['mouth_pos']['male'], float)
+    A['task_mouth_female'] = np.array(t['mouth_pos']['female'], float)
+    A['task_spoon_body'] = np.int32(S.free_body[0])
+    A['task_bowl_body'] = np.int32(S.free_body[1])
+    A['task_food_body0'] = np.int32(S.free_body[2])
+    A['task_table_body'] = np.int32(S.table_body)
+    A['task_human_body0'] = np.int32(S.human_body[S.human_slots[0]])
+    A['task_head_slot'] = np.int32(S.human_slots.index(t['head_link']))
+    path = os.path.join(out_dir, 'feeding_jaco.npz')
+    np.savez_compressed(path, **A)
+    return path, A
+
+
+if __name__ == '__main__':
+    path, A = compile_all()
+    print(path)
+    for k, v in A.items():
+        print('%-24s %s %s' % (k, getattr(v, 'shape', ()), getattr(v, 'dtype', type(v))))

@@ -1,0 +1,261 @@
+"""Host-side reset path for FeedingJaco-v0 (FeedingEnv.reset, feeding.py:144-331).
+
+It produces the initial per-env state block that the device step consumes:
+  * human pose: setup_human_joints + enforce_joint_limits (world_creation.py:135-179,110-133)
+    with the Feeding joint targets (feeding.py:242-245) -> per-env world poses of the human's
+    collision links (the human is fully static unless the impairment is 'tremor');
+  * bowl position jitter (feeding.py:184), IK of the Jaco tool link to the spoon-above-bowl
+    target (feeding.py:276-278; util.py:34-105 -- restated as damped least squares with random
+    restarts, because p.calculateInverseKinematics is a Bullet internal);
+  * gripper (feeding.py:279, world_creation.py:309-328), spoon on the tool frame
+    (world_creation.py:330-365), 8 food spheres above the spoon (feeding.py:291-308).
+The 100 settling stepSimulation calls (feeding.py:319-320) run on the device (avr_settle).
+
+Per-env randomness: numpy Generator seeded with (seed, env_id), so resets do not depend on
+how envs are sharded over GPUs.  (The reference draws from one np_random stream per env
+object; those draws cannot be reproduced bit-for-bit and are not part of the step path.)
+"""
+import numpy as np
+
+from . import _abi as ABI
+from . import geom as G
+
+HUMAN_SCALED = set(range(7, 14)) | set(range(17, 24)) | set(range(24, 28))   # limit_scale joints
+
+
+# ----------------------------------------------------------------------------- Jaco FK / IK
+def robot_fk(A, q):
+    """Link frames and COM frames of the robot for DoF vector q (same recursion as the kernel)."""
+    nl = int(A['n_links'])
+    base_p, base_q = A['robot_base'][:3], A['robot_base'][3:]
+    LP = np.zeros((nl, 3)); LQ = np.zeros((nl, 4))
+    CP = np.zeros((nl, 3)); CQ = np.zeros((nl, 4))
+    AX = np.zeros((nl, 3)); OR = np.zeros((nl, 3))
+    for i in range(nl):
+        p = A['rl_parent'][i]
+        pp, pq = (base_p, base_q) if p < 0 else (LP[p], LQ[p])
+        tp, tq = G.tf_mul(pp, pq, A['rl_jpos'][i], A['rl_jquat'][i])
+        OR[i] = tp
+        AX[i] = G.quat_rotate(tq, A['rl_axis'][i])
+        dof = A['rl_dof'][i]
+        if A['rl_jtype'][i] == 1:
+            tq = G.quat_mul(tq, G.quat_axis_angle(A['rl_axis'][i], q[dof]))
+        elif A['rl_jtype'][i] == 2:
+            tp = tp + AX[i] * q[dof]
+        LP[i], LQ[i] = tp, tq
+        CP[i], CQ[i] = G.tf_mul(tp, tq, A['rl_com_pos'][i], A['rl_com_quat'][i])
+    return LP, LQ, CP, CQ, AX, OR
+
+
+def _chain(A, link):
+    out = []
+    k = link
+    while k >= 0:
+        out.append(k)
+        k = A['rl_parent'][k]
+    return out
+
+
+def _rot_err(q_tgt, q_cur):
+    dq = G.quat_mul(q_tgt, G.quat_conj(q_cur))
+    if dq[3] < 0:
+        dq = -dq
+    s = np.linalg.norm(dq[:3])
+    if s < 1e-12:
+        return np.zeros(3)
+    ang = 2.0 * np.arctan2(s, dq[3])
+    return dq[:3] / s * ang
+
+
+def table_clear(A, q, margin=0.05):
+    """True if no robot hull vertex lies inside the (inflated) table box.  Stands in for the
+    reference's collision screening of IK restarts (util.py:41-46) so that reset states do not
+    start with the arm buried in the table."""
+    _, _, CP, CQ, _, _ = robot_fk(A, q)
+    tb = int(A['task_table_body'])
+    s0 = A['body_shape_start'][tb]
+    tpose = A['st_pose'][A['body_index'][tb]]
+    sp = A['shape_pose'][s0]
+    c = tpose[:3] + sp[:3]
+    he = A['shape_param'][s0][:3] + margin
+    for b in range(len(A['body_kind'])):
+        if A['body_kind'][b] != 0:
+            continue
+        l = A['body_index'][b]
+        for s in range(A['body_shape_start'][b], A['body_shape_start'][b] + A['body_shape_count'][b]):
+            if A['shape_kind'][s] != 3:
+                continue
+            v0, nv = A['shape_hull'][s][:2]
+            V = A['hull_verts'][v0:v0 + nv]
+            p, qq = G.tf_mul(CP[l], CQ[l], A['shape_pose'][s][:3], A['shape_pose'][s][3:])
+            W = V @ G.quat_to_mat(qq).T + p
+            inside = np.all(np.abs(W - c) <= he, axis=1)   # box inflated by `margin` on all sides
+            if inside.any():
+                return False
+    return True
+
+
+def ik(A, link, target_pos, target_quat, arm_dofs, lower, upper, rng, q0=None,
+       iters=300, restarts=40, tol=0.01):
+    """Damped-least-squares IK for the COM frame of `link` (util.py:34-57 semantics: random
+    rest pose per restart, accept at < tol position and quaternion error)."""
+    nd = int(A['n_dof'])
+    best, best_err = None, np.inf
+    chain = _chain(A, link)
+    for r in range(restarts):
+        q = np.zeros(nd) if q0 is None else q0.copy()
+        q[arm_dofs] = rng.uniform(lower, upper)
+        for it in range(iters):
+            _, _, CP, CQ, AX, OR = robot_fk(A, q)
+            ep = target_pos - CP[link]
+            er = _rot_err(target_quat, CQ[link])
+            err = np.concatenate([ep, er])
+            if np.linalg.norm(ep) < 1e-5 and np.linalg.norm(er) < 1e-4:
+                break
+            J = np.zeros((6, len(arm_dofs)))
+            for c, dof in enumerate(arm_dofs):
+                l = [k for k in chain if A['rl_dof'][k] == dof]
+                if not l:
+                    continue
+                l = l[0]
+                J[:3, c] = np.cross(AX[l], CP[link] - OR[l])
+                J[3:, c] = AX[l]
+            lam = 1e-2
+            dq = J.T @ np.linalg.solve(J @ J.T + lam * lam * np.eye(6), err)
+            q[arm_dofs] = np.clip(q[arm_dofs] + dq, lower, upper)
+        _, _, CP, CQ, _, _ = robot_fk(A, q)
+        pe = np.linalg.norm(target_pos - CP[link])
+        qe = min(np.linalg.norm(target_quat - CQ[link]), np.linalg.norm(target_quat + CQ[link]))
+        if pe < tol and qe < tol and table_clear(A, q):
+            return q, True
+        if pe < best_err:
+            best, best_err = q.copy(), pe
+    return best, False
+
+
+# ----------------------------------------------------------------------------- human
+def human_joint_angles(A, gender, rng, limit_scale=1.0):
+    """Feeding (non-VR, non-new) human joint setup: fixed arm/leg poses + random head
+    (feeding.py:242-245), clamped by enforce_joint_limits (world_creation.py:110-133)."""
+    n = len(A['human_%s_parent' % gender])
+    q = np.zeros(n)
+    for j, ang in [(10, -90), (20, -90), (28, -90), (31, 80), (35, -90), (38, 80)]:
+        q[j] = np.deg2rad(ang)
+    for j in (25, 26, 27):
+        q[j] = rng.uniform(np.deg2rad(-30), np.deg2rad(30))
+    lo = A['human_%s_lower' % gender].copy()
+    hi = A['human_%s_upper' % gender].copy()
+    for j in HUMAN_SCALED:
+        lo[j] *= limit_scale
+        hi[j] *= limit_scale
+    jt = A['human_%s_jtype' % gender]
+    for j in range(n):
+        if jt[j] != 1:
+            continue
+        l, u = lo[j], hi[j]
+        if l == 0 and u == -1:
+            continue
+        q[j] = min(max(q[j], l), u)
+    return q
+
+
+def human_link_poses(A, gender, q):
+    """World poses (link == COM frames) of the 42 human links; base pose from feeding.py:245."""
+    base_p = np.array([0, 0.03, 0.89 - 0.23725 if gender == 'male' else 0.86 - 0.225])
+    base_q = np.array([0, 0, 0, 1.0])
+    par = A['human_%s_parent' % gender]
+    jt = A['human_%s_jtype' % gender]
+    ax = A['human_%s_axis' % gender]
+    pos = A['human_%s_pos' % gender]
+    n = len(par)
+    P = np.zeros((n, 3)); Q = np.zeros((n, 4))
+    for i in range(n):
+        pp, pq = (base_p, base_q) if par[i] < 0 else (P[par[i]], Q[par[i]])
+        p, qq = G.tf_mul(pp, pq, pos[i], [0, 0, 0, 1])
+        if jt[i] == 1:
+            qq = G.quat_mul(qq, G.quat_axis_angle(ax[i], q[i]))
+        P[i], Q[i] = p, qq
+    return base_p, base_q, P, Q
+
+
+def human_slot_poses(A, gender, q):
+    base_p, base_q, P, Q = human_link_poses(A, gender, q)
+    out = np.zeros((ABI.MAX_HUMAN, 7))
+    for s, l in enumerate(A['human_slot_link']):
+        if l < 0:
+            out[s] = np.concatenate([base_p, base_q])
+        else:
+            out[s] = np.concatenate([P[l], Q[l]])
+    return out
+
+
+# ----------------------------------------------------------------------------- full reset
+def feeding_reset_state(A, md, seed, env_id, gender=None, impairment='none'):
+    """One env's initial state block (float64[STATE_WORDS]) before the settle frames."""
+    rng = np.random.default_rng([int(seed), int(env_id)])
+    if gender is None:
+        gender = 'male' if rng.integers(2) == 0 else 'female'     # feeding.py:169
+    limit_scale = rng.uniform(0.5, 1.0) if impairment == 'limits' else 1.0   # world_creation.py:71
+    st = np.zeros(ABI.STATE_WORDS)
+    qh = human_joint_angles(A, gender, rng, limit_scale)
+    st[ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, gender, qh).ravel()
+    bowl_pos = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
+    target_pos = bowl_pos + np.array([0, -0.1, 0.4]) + rng.uniform(-0.05, 0.05, size=3)
+    target_quat = G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])
+    arm = md.arm_dofs
+    lower = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
+    upper = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
+    tool = int(A['task_tool_link'])
+    q0 = np.zeros(int(A['n_dof']))
+    for d in md.finger_dofs:
+        q0[d] = md.params['finger_target']
+    q, ok = ik(A, tool, target_pos, target_quat, arm, lower, upper, rng, q0=q0)
+    st[ABI.S_Q:ABI.S_Q + len(q)] = q
+    # motors: arm keeps PyBullet's default velocity motors until the first take_step;
+    # gripper position motors (world_creation.py:328)
+    for d in arm:
+        st[ABI.S_KP + d] = 0.0
+        st[ABI.S_QTGT + d] = 0.0
+        st[ABI.S_MAXIMP + d] = md.params['default_motor_impulse']
+    for d in md.finger_dofs:
+        st[ABI.S_KP + d] = md.params['finger_gain']
+        st[ABI.S_QTGT + d] = md.params['finger_target']
+        st[ABI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+    # spoon at tool frame (x) offset (world_creation.py:332-343)
+    _, _, CP, CQ, _, _ = robot_fk(A, q)
+    off = A['task_tool_offset']
+    sp, sq = G.tf_mul(CP[tool], CQ[tool], off[:3], off[3:])
+    fb = ABI.S_FREE
+    st[fb:fb + 3] = sp
+    st[fb + 3:fb + 7] = sq
+    bq = G.quat_from_euler([np.pi / 2.0, 0, 0])
+    b = ABI.S_FREE + ABI.FB_WORDS
+    st[b:b + 3] = bowl_pos
+    st[b + 3:b + 7] = bq
+    r = 0.005
+    k = 0
+    for i in range(2):
+        for j in range(2):
+            for kk in range(2):
+                f = ABI.S_FREE + ABI.FB_WORDS * (2 + k)
+                st[f:f + 3] = np.array([i * 2 * r - 0.005, j * 2 * r, kk * 2 * r + 0.02]) + sp
+                st[f + 3:f + 7] = [0, 0, 0, 1]
+                k += 1
+    t = ABI.S_TASK
+    gi = 0 if gender == 'male' else 1
+    head = st[ABI.S_HUMAN + 7 * int(A['task_head_slot']):][:7]
+    mouth = A['task_mouth_male'] if gi == 0 else A['task_mouth_female']
+    st[t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
+    st[t + ABI.T_ALIVE] = (1 << 8) - 1
+    st[t + ABI.T_GENDER] = gi
+    return st, dict(gender=gender, ik_ok=ok, bowl_pos=bowl_pos, target_pos=target_pos)
+
+
+def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='none'):
+    S = np.zeros((len(env_ids), ABI.STATE_WORDS))
+    meta = []
+    for k, e in enumerate(env_ids):
+        g = None if genders is None else genders[k]
+        S[k], m = feeding_reset_state(A, md, seed, e, gender=g, impairment=impairment)
+        meta.append(m)
+    return S, meta

@@ -1,0 +1,307 @@
+// avr_capi.hip -- C-ABI of libavr.so (include/avr.h): device arenas, scene upload, launches.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/avr.h"
+
+// KModel is defined in avr_kernel.hip; it is mirrored here field by field via a shared header
+// section to keep one definition.
+#define AVR_KMODEL_ONLY
+#include "avr_kmodel.h"
+
+extern "C" hipError_t avr_launch_step(const KModel *m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
+                                      float *info, int mode, long long t, int n_envs, hipStream_t stream);
+extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
+                                                hipStream_t stream);
+extern "C" hipError_t avr_kernel_attrs(int *out4);
+
+struct avr_sim {
+    avr_config cfg;
+    KModel km;
+    hipStream_t stream;
+    std::vector<void *> allocs;
+    float *d_state;
+    float *d_act, *d_obs, *d_rew, *d_info;
+    unsigned char *d_done;
+    char err[512];
+};
+
+static int fail(avr_sim *s, int code, const char *fmt, ...) {
+    if (s) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(s->err, sizeof(s->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(s, x)                                                                      \
+    do {                                                                                  \
+        hipError_t _e = (x);                                                              \
+        if (_e != hipSuccess) return fail((s), -3, "%s: %s", #x, hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+static int upload(avr_sim *s, const std::vector<T> &h, const T **out) {
+    void *d = nullptr;
+    size_t n = h.size() ? h.size() : 1;
+    HIPCHK(s, hipMalloc(&d, n * sizeof(T)));
+    s->allocs.push_back(d);
+    if (h.size()) HIPCHK(s, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = (const T *)d;
+    return 0;
+}
+
+static std::vector<float> cvt(const double *p, size_t n, int stride_in = 1, int stride_out = 1, int count = -1) {
+    if (count < 0) {
+        std::vector<float> v(n);
+        for (size_t i = 0; i < n; i++) v[i] = (float)p[i];
+        return v;
+    }
+    std::vector<float> v((size_t)count * stride_out, 0.f);
+    for (int i = 0; i < count; i++)
+        for (int k = 0; k < stride_in; k++) v[(size_t)i * stride_out + k] = (float)p[(size_t)i * stride_in + k];
+    return v;
+}
+
+static std::vector<int> ivec(const int32_t *p, size_t n) { return std::vector<int>(p, p + n); }
+
+// pose arrays: [n][pos3 + quat4] -> [n][8]
+static std::vector<float> poses(const double *pos, const double *quat, int n) {
+    std::vector<float> v((size_t)n * 8, 0.f);
+    for (int i = 0; i < n; i++) {
+        for (int k = 0; k < 3; k++) v[8 * i + k] = (float)pos[3 * i + k];
+        for (int k = 0; k < 4; k++) v[8 * i + 3 + k] = (float)quat[4 * i + k];
+    }
+    return v;
+}
+
+extern "C" int32_t avr_state_words(void) { return AVR_STATE_WORDS; }
+extern "C" int32_t avr_abi_version(void) { return AVR_ABI_VERSION; }
+
+extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
+    if (!cfg || !d || !out) return -1;
+    *out = nullptr;
+    avr_sim *s = new avr_sim();
+    memset(s->err, 0, sizeof(s->err));
+    s->cfg = *cfg;
+    if (cfg->n_envs <= 0) { int r = fail(s, -1, "n_envs must be > 0"); *out = s; return r; }
+    if (d->n_links > AVR_MAX_LINKS || d->n_dof > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
+        d->n_bodies > 64 || d->n_arm > AVR_ACT_DIM) {
+        int r = fail(s, -2, "model exceeds compiled capacities");
+        *out = s;
+        return r;
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) { int r = fail(s, -4, "no HIP device available (%s)", hipGetErrorString(e)); *out = s; return r; }
+    if (cfg->device < 0 || cfg->device >= ndev) { int r = fail(s, -4, "device %d out of range (%d devices)", cfg->device, ndev); *out = s; return r; }
+    *out = s;
+    HIPCHK(s, hipSetDevice(cfg->device));
+    HIPCHK(s, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    KModel &k = s->km;
+    memset(&k, 0, sizeof(k));
+    int nl = d->n_links, nb = d->n_bodies, ns = d->n_shapes;
+    k.nl = nl; k.nd = d->n_dof; k.nf = d->n_free; k.nb = nb; k.ns = ns; k.np = d->n_pairs; k.nh = d->n_human;
+    int r;
+    if ((r = upload(s, ivec(d->rl_parent, nl), &k.rl_parent))) return r;
+    if ((r = upload(s, ivec(d->rl_jtype, nl), &k.rl_jtype))) return r;
+    if ((r = upload(s, ivec(d->rl_dof, nl), &k.rl_dof))) return r;
+    if ((r = upload(s, ivec(d->rl_has_limit, nl), &k.rl_has_limit))) return r;
+    if ((r = upload(s, poses(d->rl_jpos, d->rl_jquat, nl), &k.rl_jorig))) return r;
+    if ((r = upload(s, poses(d->rl_com_pos, d->rl_com_quat, nl), &k.rl_com))) return r;
+    if ((r = upload(s, cvt(d->rl_axis, 0, 3, 4, nl), &k.rl_axis))) return r;
+    if ((r = upload(s, cvt(d->rl_inertia, 0, 3, 4, nl), &k.rl_inertia))) return r;
+    if ((r = upload(s, cvt(d->rl_mass, nl), &k.rl_mass))) return r;
+    if ((r = upload(s, cvt(d->rl_lower, nl), &k.rl_lower))) return r;
+    if ((r = upload(s, cvt(d->rl_upper, nl), &k.rl_upper))) return r;
+    for (int i = 0; i < 7; i++) k.base[i] = (float)d->robot_base[i];
+    if ((r = upload(s, cvt(d->fb_mass, d->n_free), &k.fb_mass))) return r;
+    if ((r = upload(s, cvt(d->fb_inertia, 0, 3, 4, d->n_free), &k.fb_inertia))) return r;
+    if ((r = upload(s, cvt(d->fb_gravity, 0, 3, 4, d->n_free), &k.fb_gravity))) return r;
+    if ((r = upload(s, cvt(d->st_pose, 0, 7, 8, d->n_static), &k.st_pose))) return r;
+    if ((r = upload(s, ivec(d->body_kind, nb), &k.body_kind))) return r;
+    if ((r = upload(s, ivec(d->body_index, nb), &k.body_index))) return r;
+    if ((r = upload(s, ivec(d->body_shape_start, nb), &k.body_shape_start))) return r;
+    if ((r = upload(s, ivec(d->body_shape_count, nb), &k.body_shape_count))) return r;
+    if ((r = upload(s, ivec(d->body_flags, nb), &k.body_flags))) return r;
+    if ((r = upload(s, cvt(d->body_friction, nb), &k.body_friction))) return r;
+    if ((r = upload(s, cvt(d->body_threshold, nb), &k.body_threshold))) return r;
+    if ((r = upload(s, cvt(d->body_aabb, (size_t)nb * 12), &k.body_aabb))) return r;
+    if ((r = upload(s, ivec(d->shape_kind, ns), &k.shape_kind))) return r;
+    if ((r = upload(s, ivec(d->shape_body, ns), &k.shape_body))) return r;
+    if ((r = upload(s, ivec(d->shape_gender, ns), &k.shape_gender))) return r;
+    if ((r = upload(s, ivec(d->shape_hull, (size_t)ns * 4), &k.shape_hull))) return r;
+    if ((r = upload(s, cvt(d->shape_pose, 0, 7, 8, ns), &k.shape_pose))) return r;
+    if ((r = upload(s, cvt(d->shape_param, (size_t)ns * 4), &k.shape_param))) return r;
+    if ((r = upload(s, cvt(d->shape_margin, ns), &k.shape_margin))) return r;
+    {
+        std::vector<float> a((size_t)ns * 8, 0.f);
+        for (int i = 0; i < ns; i++) {
+            for (int q = 0; q < 3; q++) a[8 * i + q] = (float)d->shape_aabb[6 * i + q];
+            for (int q = 0; q < 3; q++) a[8 * i + 4 + q] = (float)d->shape_aabb[6 * i + 3 + q];
+        }
+        if ((r = upload(s, a, &k.shape_aabb))) return r;
+    }
+    {
+        std::vector<float4> hv((size_t)d->n_hull_verts);
+        for (int i = 0; i < d->n_hull_verts; i++)
+            hv[i] = make_float4((float)d->hull_verts[3 * i], (float)d->hull_verts[3 * i + 1], (float)d->hull_verts[3 * i + 2], 0.f);
+        if ((r = upload(s, hv, &k.hull_verts))) return r;
+    }
+    if ((r = upload(s, ivec(d->pair_a, d->n_pairs), &k.pair_a))) return r;
+    if ((r = upload(s, ivec(d->pair_b, d->n_pairs), &k.pair_b))) return r;
+    k.n_arm = d->n_arm;
+    for (int i = 0; i < 8; i++) { k.arm_dofs[i] = d->arm_dofs[i]; k.arm_lower[i] = (float)d->arm_lower[i]; k.arm_upper[i] = (float)d->arm_upper[i]; }
+    for (int i = d->n_arm; i < 8; i++) { k.arm_lower[i] = -1e10f; k.arm_upper[i] = 1e10f; }
+    k.n_finger = d->n_finger;
+    for (int i = 0; i < 4; i++) k.finger_dofs[i] = d->finger_dofs[i];
+    k.tool_link = d->tool_link; k.torso_link = d->torso_link; k.head_slot = d->head_slot;
+    k.spoon_free = d->spoon_free; k.bowl_free = d->bowl_free; k.food_free0 = d->food_free0; k.n_food = d->n_food;
+    k.table_body = d->table_body; k.bowl_body = d->bowl_body; k.spoon_body = d->spoon_body; k.food_body0 = d->food_body0;
+    k.tool_body = -1;
+    for (int i = 0; i < 7; i++) k.tool_offset[i] = (float)d->tool_offset[i];
+    for (int g = 0; g < 2; g++)
+        for (int i = 0; i < 3; i++) k.mouth[g][i] = (float)d->mouth_offset[g][i];
+    k.time_step = (float)d->time_step;
+    k.nsub = d->num_sub_steps; k.frame_skip = d->frame_skip; k.iters = d->solver_iterations; k.max_steps = d->max_episode_steps;
+    k.erp = (float)d->erp; k.warmstart = (float)d->warmstart; k.lin_damp = (float)d->linear_damping; k.ang_damp = (float)d->angular_damping;
+    k.max_vel = (float)d->max_coord_vel; k.robot_gain = (float)d->robot_gain; k.robot_force = (float)d->robot_force;
+    k.fixed_max_imp = (float)(d->fixed_max_force * d->time_step);
+    k.w_distance = (float)d->w_distance; k.w_action = (float)d->w_action; k.w_food = (float)d->w_food;
+    k.w_velocity = (float)d->w_velocity; k.w_force_nontarget = (float)d->w_force_nontarget; k.w_high_forces = (float)d->w_high_forces;
+    k.w_food_hit = (float)d->w_food_hit; k.w_food_velocities = (float)d->w_food_velocities;
+    k.task_success_threshold = (float)d->task_success_threshold;
+    k.seed = cfg->seed;
+    k.env_offset = cfg->env_offset;
+    for (int i = 0; i < AVR_MAX_DOF; i++) k.dof_link[i] = 0;
+    for (int l = 0; l < nl; l++)
+        if (d->rl_dof[l] >= 0) k.dof_link[d->rl_dof[l]] = l;
+    for (int l = 0; l < nl; l++) {
+        unsigned mask = 0;
+        for (int q = l; q >= 0; q = d->rl_parent[q]) mask |= 1u << q;
+        k.anc_mask[l] = mask;
+    }
+    size_t E = (size_t)cfg->n_envs;
+    HIPCHK(s, hipMalloc(&s->d_state, E * AVR_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMemset(s->d_state, 0, E * AVR_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_act, E * AVR_ACT_DIM * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_obs, E * AVR_OBS_DIM * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_rew, E * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_done, E));
+    HIPCHK(s, hipMalloc(&s->d_info, E * AVR_INFO_DIM * sizeof(float)));
+    return 0;
+}
+
+extern "C" int avr_destroy(avr_sim *s) {
+    if (!s) return -1;
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (void *p : s->allocs) (void)hipFree(p);
+    if (s->d_state) (void)hipFree(s->d_state);
+    if (s->d_act) (void)hipFree(s->d_act);
+    if (s->d_obs) (void)hipFree(s->d_obs);
+    if (s->d_rew) (void)hipFree(s->d_rew);
+    if (s->d_done) (void)hipFree(s->d_done);
+    if (s->d_info) (void)hipFree(s->d_info);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return 0;
+}
+
+extern "C" const char *avr_last_error(avr_sim *s) { return s ? s->err : "null handle"; }
+extern "C" void *avr_stream(avr_sim *s) { return s ? (void *)s->stream : nullptr; }
+extern "C" void *avr_state_device_ptr(avr_sim *s) { return s ? (void *)s->d_state : nullptr; }
+extern "C" int32_t avr_n_envs(avr_sim *s) { return s ? s->cfg.n_envs : 0; }
+
+#define CHECK_SIM(s) \
+    if (!(s) || !(s)->d_state) return -1
+
+extern "C" int avr_set_state(avr_sim *s, const float *h) {
+    CHECK_SIM(s);
+    HIPCHK(s, hipMemcpyAsync(s->d_state, h, (size_t)s->cfg.n_envs * AVR_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float *h) {
+    CHECK_SIM(s);
+    const size_t W = AVR_STATE_WORDS * sizeof(float);
+    for (int e = 0; e < s->cfg.n_envs; e++)
+        if (!mask || mask[e]) HIPCHK(s, hipMemcpyAsync(s->d_state + (size_t)e * AVR_STATE_WORDS, h + (size_t)e * AVR_STATE_WORDS, W, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_get_state(avr_sim *s, float *h) {
+    CHECK_SIM(s);
+    HIPCHK(s, hipMemcpyAsync(h, s->d_state, (size_t)s->cfg.n_envs * AVR_STATE_WORDS * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
+    CHECK_SIM(s);
+    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 2, n_frames, s->cfg.n_envs, s->stream));
+    if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_substep(avr_sim *s, float dt) {
+    CHECK_SIM(s);
+    long long t = 0;
+    memcpy(&t, &dt, sizeof(float));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 3, t, s->cfg.n_envs, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
+    CHECK_SIM(s);
+    HIPCHK(s, avr_launch_step(&s->km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, 0, 0, s->cfg.n_envs, s->stream));
+    return 0;
+}
+
+extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
+    CHECK_SIM(s);
+    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
+                              d_info ? d_info : s->d_info, 1, t, s->cfg.n_envs, s->stream));
+    return 0;
+}
+
+extern "C" int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {
+    CHECK_SIM(s);
+    HIPCHK(s, avr_launch_random_actions(s->cfg.seed, s->cfg.env_offset, t, d_act, s->cfg.n_envs, s->km.n_arm, s->stream));
+    return 0;
+}
+
+extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
+    CHECK_SIM(s);
+    size_t E = (size_t)s->cfg.n_envs;
+    HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(info, s->d_info, E * AVR_INFO_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_sync(avr_sim *s) {
+    CHECK_SIM(s);
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_kernel_info(avr_sim *s, int32_t *out4) {
+    (void)s;
+    hipError_t e = avr_kernel_attrs(out4);
+    return e == hipSuccess ? 0 : -3;
+}

@@ -1,0 +1,1650 @@
+// avr_kernel.hip -- MI355X (gfx950) step kernel for the Assistive Gym FeedingJaco-v0 hot path.
+//
+// One environment per wavefront (workgroup = 64 lanes).  A launch advances every env by one
+// gym step: take_step glue (env.py:274-337), frame_skip x numSubSteps Bullet sub-steps
+// (env.py:341-349, feeding.py:289), then get_total_force / get_food_rewards / _get_obs / reward
+// (feeding.py:56-142, env.py:412-448).  The per-env state block (avr_model.h) is staged in LDS
+// for the whole launch and written back once; model data (hull vertices, link tables) is
+// read-only global memory shared by all envs and stays L2/MALL resident.
+//
+// Work decomposition inside a wave:
+//   * lanes over bodies / candidate pairs / child-shape pairs (broadphase, AABB culling);
+//   * one lane per child-shape pair for the narrowphase of small shapes (spheres, capsules,
+//     boxes, hulls <= SMALL_NV vertices), the whole wave per pair for large hulls (support
+//     mapping = parallel vertex scan + wave argmax) and for EPA;
+//   * one lane per manifold for the persistent-manifold update (prefix-sum compaction);
+//   * lanes over mass-matrix entries, over constraint rows (Jacobians, M^-1 J^T);
+//   * the projected Gauss-Seidel sweep is inherently sequential (Bullet semantics): it runs
+//     wave-uniform out of LDS.
+// No MFMA: this is branchy small-body dynamics.  The algorithm is identical to the CPU oracle
+// (oracle/avr_oracle.c), which cites the Bullet/PyBullet behaviour it restates.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/avr.h"
+#include "avr_math.h"
+
+#include "avr_kmodel.h"
+
+// --------------------------------------------------------------------------- device model
+
+
+// --------------------------------------------------------------------------- LDS layout
+struct NCRow {                 // limit / motor / fixed-constraint row (robot endpoint A)
+    float JA[MAXD], MA[MAXD];  // robot part
+    float JB[6], MB[6];        // free-body part (fixed constraint) or zero
+    float inv, rhs, lo, hi, imp;
+    int fb;                    // free body index of endpoint B, -1 if none
+    int pad[2];
+};
+struct CRow {                  // one contact point = 1 normal + 2 friction rows
+    float n[3], t1[3], t2[3];
+    float rA[3], rB[3];        // lever arms from the free bodies' COM (if free)
+    float inv[3], rhs[3], imp[3];
+    float fric;
+    int kA, iA, kB, iB;        // endpoint kinds: 0 none, 1 robot, 2 free
+    int rs;                    // first robot slot (rows use rs, rs+1, rs+2 per robot endpoint)
+    int cp;                    // contact point index
+};
+struct EnvLDS {
+    float st[AVR_STATE_WORDS];
+    float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
+    float btf[MAXB][8], bmin[MAXB][4], bmax[MAXB][4];
+    float Mi[MAXD][MAXD];
+    float vq[MAXD], dq[MAXD];
+    float fv[MAXF][4], fw[MAXF][4], dfv[MAXF][4], dfw[MAXF][4];
+    float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
+    float h[MAXD], qdd[MAXD];
+    float rn[6][MAXL][4];   // RNEA temporaries: omega, v_com, alpha, a_com, F, N
+    int nsp, nap, n_nc, n_c, n_rs, flags, gender, pad;
+    union {
+        struct {
+            int sp_a[MAXSP], sp_b[MAXSP], sp_pair[MAXSP];
+            float res[MAXSP][8];           // flag, n3, p3, d
+            int apair[MAXAP];
+            float newcp[AVR_MAX_CONTACTS][AVR_CP_WORDS];
+            float eW[EPA_MAX_V][9];        // minkowski vertex + support on A + support on B
+            int eFi[EPA_MAX_F][4];         // i j k alive
+            float eFn[EPA_MAX_F][4];       // normal + d
+            int eEdge[EPA_MAX_F * 3][2];
+        } c;
+        struct {
+            NCRow nc[MAXNC];
+            CRow cr[AVR_MAX_CONTACTS];
+            float rsJ[MAXRS][MAXD];
+            float rsM[MAXRS][MAXD];
+        } s;
+    } u;
+};
+
+#define SYNC() __syncthreads()
+
+// --------------------------------------------------------------------------- kinematics
+// robot_fk: serial recursion over the (DFS-ordered) links on lane 0, frames published in LDS.
+AVR_DI void robot_fk(const KModel &m, EnvLDS &L) {
+    if (lane_id() == 0) {
+        tf base = ldtf(m.base);
+        for (int i = 0; i < m.nl; i++) {
+            int p = m.rl_parent[i];
+            tf par = p < 0 ? base : ldtf(L.lk[p]);
+            tf t = tfmul(par, ldtf(m.rl_jorig + 8 * i));
+            v3 axl = ld3(m.rl_axis + 4 * i);
+            v3 axw = qrot(t.q, axl);
+            int dof = m.rl_dof[i];
+            int jt = m.rl_jtype[i];
+            st3(L.org[i], t.p);
+            st3(L.ax[i], axw);
+            if (jt == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(axl, L.st[AVR_S_Q + dof]));
+            else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(axw, L.st[AVR_S_Q + dof]));
+            sttf(L.lk[i], t);
+            sttf(L.cm[i], tfmul(t, ldtf(m.rl_com + 8 * i)));
+        }
+    }
+    SYNC();
+}
+
+AVR_DI bool is_ancestor(const KModel &m, int link, int anc) { return (m.anc_mask[link] >> anc) & 1u; }
+
+AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &ang) {
+    v3 a = ld3(L.ax[j]);
+    if (m.rl_jtype[j] == AVR_J_REVOLUTE) {
+        ang = a;
+        lin = crs(a, sub(p, ld3(L.org[j])));
+    } else {
+        ang = V(0, 0, 0);
+        lin = a;
+    }
+}
+
+// Mass matrix: one lane per lower-triangle entry (a,b); Cholesky on lane 0 in LDS.  Rows and
+// columns beyond nd are padded with the identity so M^-1 solves run over MAXD unrolled.
+AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
+    const int nd = m.nd;
+    const int lane = lane_id();
+    const int ne = MAXD * (MAXD + 1) / 2;
+    for (int e = lane; e < ne; e += 64) {
+        int a = 0, rem = e;
+        while (rem > a) { rem -= a + 1; a++; }
+        int b = rem;
+        float s = 0.f;
+        if (a < nd && b < nd) {
+            int la = m.dof_link[a], lb = m.dof_link[b];
+            for (int i = 0; i < m.nl; i++) {
+                float mi = m.rl_mass[i];
+                if (mi <= 0.f) continue;
+                if (!is_ancestor(m, i, la) || !is_ancestor(m, i, lb)) continue;
+                v3 c = ld3(L.cm[i]);
+                qt q = ldq(L.cm[i] + 3);
+                v3 lina, anga, linb, angb;
+                dof_col(m, L, la, c, lina, anga);
+                dof_col(m, L, lb, c, linb, angb);
+                v3 Ia = inertia_mul(q, ld3(m.rl_inertia + 4 * i), anga);
+                s += mi * dot(lina, linb) + dot(Ia, angb);
+            }
+        } else if (a == b) s = 1.f;
+        L.Mi[a][b] = s;
+        if (a != b) L.Mi[b][a] = 0.f;
+    }
+    SYNC();
+    int ok = 1;
+    if (lane == 0) {
+        for (int j = 0; j < MAXD; j++) {
+            float s = L.Mi[j][j];
+            for (int k = 0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
+            if (s <= 0.f) ok = 0;
+            float d = sqrtf(fmaxf(s, 1e-30f));
+            L.Mi[j][j] = d;
+            for (int i = j + 1; i < MAXD; i++) {
+                float t = L.Mi[i][j];
+                for (int k = 0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
+                L.Mi[i][j] = t / d;
+            }
+        }
+        L.pad = ok;
+    }
+    SYNC();
+    return L.pad != 0;
+}
+
+// x = M^-1 b with the Cholesky factor in LDS; fixed-size, fully unrolled (register arrays)
+AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x) {
+    (void)m;
+    float y[MAXD];
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) {
+        float s = b[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) s -= L.Mi[i][k] * y[k];
+        y[i] = s / L.Mi[i][i];
+    }
+#pragma unroll
+    for (int i = MAXD - 1; i >= 0; i--) {
+        float s = y[i];
+#pragma unroll
+        for (int k = i + 1; k < MAXD; k++) s -= L.Mi[k][i] * x[k];
+        x[i] = s / L.Mi[i][i];
+    }
+}
+
+// Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping) on lane 0,
+// temporaries in LDS; result in L.h.
+AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
+    if (lane_id() == 0) {
+        float (*OM)[4] = L.rn[0], (*VC)[4] = L.rn[1], (*AL)[4] = L.rn[2], (*AC)[4] = L.rn[3], (*FF)[4] = L.rn[4], (*NN)[4] = L.rn[5];
+        const float k1l = m.lin_damp, k1a = m.ang_damp;
+        tf base = ldtf(m.base);
+        for (int i = 0; i < m.nl; i++) {
+            int p = m.rl_parent[i];
+            v3 omp = p < 0 ? V(0, 0, 0) : ld3(OM[p]);
+            v3 vp = p < 0 ? V(0, 0, 0) : ld3(VC[p]);
+            v3 alp = p < 0 ? V(0, 0, 0) : ld3(AL[p]);
+            v3 acp = p < 0 ? V(0, 0, 0) : ld3(AC[p]);
+            v3 cp = p < 0 ? base.p : ld3(L.cm[p]);
+            int dof = m.rl_dof[i];
+            float qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
+            v3 o = ld3(L.org[i]), c = ld3(L.cm[i]);
+            v3 axw = ld3(L.ax[i]);
+            v3 rpo = sub(o, cp), roc = sub(c, o);
+            v3 vo = add(vp, crs(omp, rpo));
+            v3 ao = add(acp, add(crs(alp, rpo), crs(omp, crs(omp, rpo))));
+            int jt = m.rl_jtype[i];
+            v3 om, vc, al, ac;
+            if (jt == AVR_J_REVOLUTE) {
+                v3 wj = scl(axw, qd);
+                om = add(omp, wj);
+                al = add(alp, crs(omp, wj));
+                vc = add(vo, crs(om, roc));
+                ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
+            } else if (jt == AVR_J_PRISMATIC) {
+                v3 vj = scl(axw, qd);
+                om = omp;
+                al = alp;
+                vc = add(add(vo, vj), crs(om, roc));
+                ac = add(add(ao, scl(crs(omp, vj), 2.f)), add(crs(al, roc), crs(om, crs(om, roc))));
+            } else {
+                om = omp;
+                al = alp;
+                vc = add(vo, crs(om, roc));
+                ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
+            }
+            float mi = m.rl_mass[i];
+            qt q = ldq(L.cm[i] + 3);
+            v3 I = ld3(m.rl_inertia + 4 * i);
+            v3 Iw = inertia_mul(q, I, om);
+            float vn = len(vc), wn = len(om);
+            v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
+            v3 tdamp = scl(Iw, -(k1a + k1a * wn));
+            st3(OM[i], om); st3(VC[i], vc); st3(AL[i], al); st3(AC[i], ac);
+            st3(FF[i], sub(scl(ac, mi), fdamp));
+            st3(NN[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
+        }
+        for (int d = 0; d < MAXD; d++) L.h[d] = 0.f;
+        for (int i = m.nl - 1; i >= 0; i--) {
+            int dof = m.rl_dof[i];
+            v3 o = ld3(L.org[i]), c = ld3(L.cm[i]);
+            v3 axw = ld3(L.ax[i]);
+            v3 F = ld3(FF[i]), N = ld3(NN[i]);
+            if (dof >= 0) {
+                if (m.rl_jtype[i] == AVR_J_REVOLUTE) L.h[dof] = dot(axw, add(N, crs(sub(c, o), F)));
+                else L.h[dof] = dot(axw, F);
+            }
+            int p = m.rl_parent[i];
+            if (p >= 0) {
+                st3(FF[p], add(ld3(FF[p]), F));
+                st3(NN[p], add(ld3(NN[p]), add(N, crs(sub(c, ld3(L.cm[p])), F))));
+            }
+        }
+    }
+    SYNC();
+}
+
+// --------------------------------------------------------------------------- shapes
+struct WShape {
+    int kind, nv, vs;
+    tf t;
+    float margin;
+    v3 he;
+};
+
+AVR_DI WShape make_wshape(const KModel &m, int s, tf body) {
+    WShape w;
+    w.kind = m.shape_kind[s];
+    w.t = tfmul(body, ldtf(m.shape_pose + 8 * s));
+    w.margin = m.shape_margin[s];
+    const float *pa = m.shape_param + 4 * s;
+    if (w.kind == AVR_BOX) w.he = V(fmaxf(pa[0] - w.margin, 0.f), fmaxf(pa[1] - w.margin, 0.f), fmaxf(pa[2] - w.margin, 0.f));
+    else if (w.kind == AVR_CAPSULE) w.he = V(pa[0], pa[1], 0.f);
+    else w.he = V(pa[0], 0.f, 0.f);
+    w.vs = m.shape_hull[4 * s + 0];
+    w.nv = w.kind == AVR_HULL ? m.shape_hull[4 * s + 1] : 0;
+    return w;
+}
+
+// support point of the CORE in world direction d; COOP: the whole wave scans a big hull
+template <bool COOP>
+AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
+    v3 l = qrot(qconj(s.t.q), d);
+    v3 r;
+    if (s.kind == AVR_SPHERE) r = V(0, 0, 0);
+    else if (s.kind == AVR_CAPSULE) r = V(0, 0, l.z >= 0.f ? s.he.y : -s.he.y);
+    else if (s.kind == AVR_BOX) r = V(l.x >= 0.f ? s.he.x : -s.he.x, l.y >= 0.f ? s.he.y : -s.he.y, l.z >= 0.f ? s.he.z : -s.he.z);
+    else {
+        const float4 *hv = m.hull_verts + s.vs;
+        if (COOP) {
+            float best = -BIGF;
+            int bi = 0x7fffffff;
+            for (int i = lane_id(); i < s.nv; i += 64) {
+                float4 v = hv[i];
+                float dd = l.x * v.x + l.y * v.y + l.z * v.z;
+                if (dd > best) { best = dd; bi = i; }
+            }
+            bi = wave_argmax(best, bi);
+            float4 v = hv[bi];
+            r = V(v.x, v.y, v.z);
+        } else {
+            float best = -BIGF;
+            int bi = 0;
+            for (int i = 0; i < s.nv; i++) {
+                float4 v = hv[i];
+                float dd = l.x * v.x + l.y * v.y + l.z * v.z;
+                if (dd > best) { best = dd; bi = i; }
+            }
+            float4 v = hv[bi];
+            r = V(v.x, v.y, v.z);
+        }
+    }
+    return tfpt(s.t, r);
+}
+
+// --------------------------------------------------------------------------- GJK
+struct Simplex { v3 w[4], a[4], b[4]; int n; };
+
+AVR_DI void sx_copy(Simplex &S, int dst, int src) { S.w[dst] = S.w[src]; S.a[dst] = S.a[src]; S.b[dst] = S.b[src]; }
+
+AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]);
+
+AVR_DI int tri_closest(Simplex &S, v3 &vout, float lam[4]) {
+    v3 A = S.w[0], B = S.w[1], C = S.w[2];
+    v3 ab = sub(B, A), ac = sub(C, A), ap = scl(A, -1.f);
+    float d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0.f && d2 <= 0.f) { S.n = 1; lam[0] = 1.f; vout = A; return 0; }
+    v3 bp = scl(B, -1.f);
+    float d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0.f && d4 <= d3) { sx_copy(S, 0, 1); S.n = 1; lam[0] = 1.f; vout = B; return 0; }
+    float vc = d1 * d4 - d3 * d2;
+    if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+        float v = d1 / (d1 - d3);
+        S.n = 2; lam[0] = 1.f - v; lam[1] = v; vout = add(A, scl(ab, v)); return 0;
+    }
+    v3 cp = scl(C, -1.f);
+    float d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0.f && d5 <= d6) { sx_copy(S, 0, 2); S.n = 1; lam[0] = 1.f; vout = C; return 0; }
+    float vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+        float wv = d2 / (d2 - d6);
+        sx_copy(S, 1, 2); S.n = 2;
+        lam[0] = 1.f - wv; lam[1] = wv; vout = add(A, scl(ac, wv)); return 0;
+    }
+    float va = d3 * d6 - d5 * d4;
+    if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+        float wv = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        sx_copy(S, 0, 1); sx_copy(S, 1, 2); S.n = 2;
+        lam[0] = 1.f - wv; lam[1] = wv; vout = add(B, scl(sub(C, B), wv)); return 0;
+    }
+    float den = 1.f / (va + vb + vc);
+    float v = vb * den, wv = vc * den;
+    lam[0] = 1.f - v - wv; lam[1] = v; lam[2] = wv;
+    vout = add(A, add(scl(ab, v), scl(ac, wv)));
+    return 0;
+}
+
+AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
+    if (S.n == 1) { lam[0] = 1.f; vout = S.w[0]; return 0; }
+    if (S.n == 2) {
+        v3 A = S.w[0], B = S.w[1], ab = sub(B, A);
+        float t = -dot(A, ab), dd = dot(ab, ab);
+        if (t <= 0.f || dd <= 0.f) { S.n = 1; lam[0] = 1.f; vout = A; return 0; }
+        if (t >= dd) { sx_copy(S, 0, 1); S.n = 1; lam[0] = 1.f; vout = B; return 0; }
+        t /= dd;
+        lam[0] = 1.f - t; lam[1] = t;
+        vout = add(A, scl(ab, t));
+        return 0;
+    }
+    if (S.n == 3) return tri_closest(S, vout, lam);
+    const int F[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
+    float best = BIGF;
+    Simplex bestS;
+    bestS.n = 0;
+    float bestL[4] = {0, 0, 0, 0};
+    v3 bestv = V(0, 0, 0);
+    bool outside_any = false;
+    for (int f = 0; f < 4; f++) {
+        v3 A = S.w[F[f][0]], B = S.w[F[f][1]], C = S.w[F[f][2]], D = S.w[F[f][3]];
+        v3 n = crs(sub(B, A), sub(C, A));
+        float sp = dot(scl(A, -1.f), n), sd = dot(sub(D, A), n);
+        if (sd * sd < 1e-30f) continue;
+        if (sp * sd < 0.f) {
+            outside_any = true;
+            Simplex T;
+            for (int k = 0; k < 3; k++) { T.w[k] = S.w[F[f][k]]; T.a[k] = S.a[F[f][k]]; T.b[k] = S.b[F[f][k]]; }
+            T.n = 3;
+            float Lx[4] = {0, 0, 0, 0};
+            v3 v;
+            tri_closest(T, v, Lx);
+            float d2 = len2(v);
+            if (d2 < best) { best = d2; bestS = T; bestv = v; for (int k = 0; k < 4; k++) bestL[k] = Lx[k]; }
+        }
+    }
+    if (!outside_any) { lam[0] = lam[1] = lam[2] = lam[3] = 0.f; vout = V(0, 0, 0); return 1; }
+    S = bestS;
+    for (int k = 0; k < 4; k++) lam[k] = bestL[k];
+    vout = bestv;
+    return 0;
+}
+
+#define GJK_SEPARATED 0
+#define GJK_FAR 1
+#define GJK_PENETRATING 2
+
+template <bool COOP>
+AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S) {
+    v3 v = sub(A.t.p, B.t.p);
+    if (len2(v) < 1e-20f) v = V(1, 0, 0);
+    S.n = 0;
+    float lam[4] = {1, 0, 0, 0};
+    float prev = BIGF;
+    int status = GJK_SEPARATED;
+    for (int it = 0; it < GJK_MAX_IT; it++) {
+        v3 sa = support<COOP>(m, A, scl(v, -1.f)), sb = support<COOP>(m, B, v);
+        v3 wv = sub(sa, sb);
+        float vv = len2(v), vw = dot(v, wv);
+        if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
+        bool dup = false;
+        for (int k = 0; k < S.n; k++)
+            if (S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
+        if (dup && S.n > 0) break;
+        if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) break;
+        S.w[S.n] = wv; S.a[S.n] = sa; S.b[S.n] = sb; S.n++;
+        v3 nv;
+        if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; break; }
+        float nvv = len2(nv);
+        if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; break; }
+        if (nvv >= prev) { v = nv; break; }
+        prev = nvv;
+        v = nv;
+    }
+    if (status == GJK_PENETRATING) return GJK_PENETRATING;
+    v3 a = V(0, 0, 0), b = V(0, 0, 0);
+    for (int k = 0; k < S.n; k++) { a = add(a, scl(S.a[k], lam[k])); b = add(b, scl(S.b[k], lam[k])); }
+    pa = a; pb = b;
+    dist = len(sub(a, b));
+    return GJK_SEPARATED;
+}
+
+// --------------------------------------------------------------------------- EPA (wave-cooperative; polytope in LDS)
+AVR_DI int epa_add_face(EnvLDS &L, int &nf, int i, int j, int k) {
+    if (nf >= EPA_MAX_F) return -1;
+    v3 Wi = ld3(L.u.c.eW[i]), Wj = ld3(L.u.c.eW[j]), Wk = ld3(L.u.c.eW[k]);
+    v3 n = crs(sub(Wj, Wi), sub(Wk, Wi));
+    float l = len(n);
+    if (l < 1e-18f) return -2;
+    n = scl(n, 1.f / l);
+    SYNC();
+    if (lane_id() == 0) {
+        L.u.c.eFi[nf][0] = i; L.u.c.eFi[nf][1] = j; L.u.c.eFi[nf][2] = k; L.u.c.eFi[nf][3] = 1;
+        st3(L.u.c.eFn[nf], n);
+        L.u.c.eFn[nf][3] = dot(n, Wi);
+    }
+    SYNC();
+    nf++;
+    return 0;
+}
+
+AVR_DI void epa_set_vert(EnvLDS &L, int vi, v3 w, v3 a, v3 b) {
+    SYNC();
+    if (lane_id() == 0) { st3(L.u.c.eW[vi], w); st3(L.u.c.eW[vi] + 3, a); st3(L.u.c.eW[vi] + 6, b); }
+    SYNC();
+}
+
+AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, const Simplex &S, v3 &normal_out, float &depth, v3 &pa, v3 &pb) {
+    int nv = 0;
+    for (int k = 0; k < S.n; k++) epa_set_vert(L, nv++, S.w[k], S.a[k], S.b[k]);
+    const float dirs[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+    for (int di = 0; di < 6 && nv < 4; di++) {
+        v3 d = V(dirs[di][0], dirs[di][1], dirs[di][2]);
+        if (nv == 2) {
+            v3 e = sub(ld3(L.u.c.eW[1]), ld3(L.u.c.eW[0]));
+            v3 c = crs(e, d);
+            if (len2(c) < 1e-12f) continue;
+            d = c;
+        } else if (nv == 3) {
+            v3 W0 = ld3(L.u.c.eW[0]);
+            d = crs(sub(ld3(L.u.c.eW[1]), W0), sub(ld3(L.u.c.eW[2]), W0));
+            if (di & 1) d = scl(d, -1.f);
+            if (len2(d) < 1e-24f) continue;
+        }
+        v3 sa = support<true>(m, A, d), sb = support<true>(m, B, scl(d, -1.f));
+        v3 wv = sub(sa, sb);
+        bool dup = false;
+        for (int k = 0; k < nv; k++)
+            if (len2(sub(ld3(L.u.c.eW[k]), wv)) < 1e-20f) dup = true;
+        if (dup) continue;
+        epa_set_vert(L, nv++, wv, sa, sb);
+    }
+    if (nv < 4) return -1;
+    {
+        v3 W0 = ld3(L.u.c.eW[0]), W1 = ld3(L.u.c.eW[1]), W2 = ld3(L.u.c.eW[2]), W3 = ld3(L.u.c.eW[3]);
+        if (dot(crs(sub(W1, W0), sub(W2, W0)), sub(W3, W0)) > 0.f) {
+            float t1[9], t2[9];
+            for (int k = 0; k < 9; k++) { t1[k] = L.u.c.eW[1][k]; t2[k] = L.u.c.eW[2][k]; }
+            SYNC();
+            if (lane_id() == 0)
+                for (int k = 0; k < 9; k++) { L.u.c.eW[1][k] = t2[k]; L.u.c.eW[2][k] = t1[k]; }
+            SYNC();
+        }
+    }
+    int nf = 0;
+    if (epa_add_face(L, nf, 0, 1, 2) || epa_add_face(L, nf, 0, 3, 1) || epa_add_face(L, nf, 0, 2, 3) || epa_add_face(L, nf, 1, 3, 2)) return -1;
+    int best = -1;
+    for (int it = 0; it < EPA_MAX_IT; it++) {
+        best = -1;
+        float bd = BIGF;
+        for (int f = 0; f < nf; f++)
+            if (L.u.c.eFi[f][3] && L.u.c.eFn[f][3] < bd) { bd = L.u.c.eFn[f][3]; best = f; }
+        if (best < 0) return -1;
+        v3 n = ld3(L.u.c.eFn[best]);
+        v3 sa = support<true>(m, A, n), sb = support<true>(m, B, scl(n, -1.f));
+        v3 wv = sub(sa, sb);
+        float dist = dot(wv, n);
+        if (dist - L.u.c.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
+        int vi = nv++;
+        epa_set_vert(L, vi, wv, sa, sb);
+        int ne = 0;
+        for (int f = 0; f < nf; f++) {
+            if (!L.u.c.eFi[f][3]) continue;
+            if (dot(ld3(L.u.c.eFn[f]), sub(wv, ld3(L.u.c.eW[L.u.c.eFi[f][0]]))) > 0.f) {
+                int fi = L.u.c.eFi[f][0], fj = L.u.c.eFi[f][1], fk = L.u.c.eFi[f][2];
+                SYNC();
+                if (lane_id() == 0) L.u.c.eFi[f][3] = 0;
+                SYNC();
+                int e3[3][2] = {{fi, fj}, {fj, fk}, {fk, fi}};
+                for (int e = 0; e < 3; e++) {
+                    int found = -1;
+                    for (int q = 0; q < ne; q++)
+                        if (L.u.c.eEdge[q][0] == e3[e][1] && L.u.c.eEdge[q][1] == e3[e][0]) { found = q; break; }
+                    int n0 = L.u.c.eEdge[ne - 1 < 0 ? 0 : ne - 1][0], n1 = L.u.c.eEdge[ne - 1 < 0 ? 0 : ne - 1][1];
+                    SYNC();
+                    if (lane_id() == 0) {
+                        if (found >= 0) { L.u.c.eEdge[found][0] = n0; L.u.c.eEdge[found][1] = n1; }
+                        else { L.u.c.eEdge[ne][0] = e3[e][0]; L.u.c.eEdge[ne][1] = e3[e][1]; }
+                    }
+                    SYNC();
+                    if (found >= 0) ne--; else ne++;
+                }
+            }
+        }
+        // compact dead faces (uniform read, lane 0 writes in order)
+        int k = 0;
+        for (int f = 0; f < nf; f++) {
+            int alive = L.u.c.eFi[f][3];
+            if (alive) {
+                int a0 = L.u.c.eFi[f][0], a1 = L.u.c.eFi[f][1], a2 = L.u.c.eFi[f][2];
+                float n0 = L.u.c.eFn[f][0], n1 = L.u.c.eFn[f][1], n2 = L.u.c.eFn[f][2], n3 = L.u.c.eFn[f][3];
+                SYNC();
+                if (lane_id() == 0) {
+                    L.u.c.eFi[k][0] = a0; L.u.c.eFi[k][1] = a1; L.u.c.eFi[k][2] = a2; L.u.c.eFi[k][3] = 1;
+                    L.u.c.eFn[k][0] = n0; L.u.c.eFn[k][1] = n1; L.u.c.eFn[k][2] = n2; L.u.c.eFn[k][3] = n3;
+                }
+                SYNC();
+                k++;
+            }
+        }
+        nf = k;
+        for (int e = 0; e < ne; e++)
+            if (epa_add_face(L, nf, L.u.c.eEdge[e][0], L.u.c.eEdge[e][1], vi) == -1) return -1;
+    }
+    if (best < 0) return -1;
+    v3 n = ld3(L.u.c.eFn[best]);
+    float fd = L.u.c.eFn[best][3];
+    v3 p = scl(n, fd);
+    int fi = L.u.c.eFi[best][0], fj = L.u.c.eFi[best][1], fk = L.u.c.eFi[best][2];
+    v3 a = ld3(L.u.c.eW[fi]), b = ld3(L.u.c.eW[fj]), c = ld3(L.u.c.eW[fk]);
+    v3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
+    float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
+    float den = d00 * d11 - d01 * d01;
+    float lv = 0.f, lw = 0.f;
+    if (fabsf(den) > 1e-30f) { lv = (d11 * d20 - d01 * d21) / den; lw = (d00 * d21 - d01 * d20) / den; }
+    float lu = 1.f - lv - lw;
+    pa = add(add(scl(ld3(L.u.c.eW[fi] + 3), lu), scl(ld3(L.u.c.eW[fj] + 3), lv)), scl(ld3(L.u.c.eW[fk] + 3), lw));
+    pb = add(add(scl(ld3(L.u.c.eW[fi] + 6), lu), scl(ld3(L.u.c.eW[fj] + 6), lv)), scl(ld3(L.u.c.eW[fk] + 6), lw));
+    normal_out = n;
+    depth = fd;
+    return 0;
+}
+
+// --------------------------------------------------------------------------- narrowphase
+// returns: 0 no contact, 1 contact (nB, pB, dist), 2 needs the cooperative path
+template <bool COOP>
+AVR_DI int narrowphase(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist) {
+    int ka = A.kind, kb = B.kind;
+    if (ka == AVR_SPHERE && kb == AVR_SPHERE) {
+        v3 diff = sub(A.t.p, B.t.p);
+        float l = len(diff), ra = A.he.x, rb = B.he.x;
+        if (l > ra + rb) return 0;
+        float d = l - (ra + rb);
+        v3 n = V(1, 0, 0);
+        if (l > 1.1920928955078125e-07f) n = scl(diff, 1.f / l);
+        nB = n; pB = add(B.t.p, scl(n, rb)); dist = d;
+        return d <= thr ? 1 : 0;
+    }
+    if ((ka == AVR_SPHERE && kb == AVR_BOX) || (ka == AVR_BOX && kb == AVR_SPHERE)) {
+        bool swapped = ka == AVR_BOX;
+        const WShape &Sp = swapped ? B : A;
+        const WShape &X = swapped ? A : B;
+        v3 rel = tfinvpt(X.t, Sp.t.p);
+        v3 he = X.he;
+        v3 cp = V(fminf(he.x, fmaxf(-he.x, rel.x)), fminf(he.y, fmaxf(-he.y, rel.y)), fminf(he.z, fmaxf(-he.z, rel.z)));
+        float r = Sp.he.x, inter = r + X.margin, cdist = inter + thr;
+        v3 n = sub(rel, cp);
+        float d2 = len2(n), d;
+        if (d2 > cdist * cdist) return 0;
+        if (d2 <= 1.1920928955078125e-07f) {
+            float fd = he.x - rel.x, md = fd;
+            cp = rel; cp.x = he.x; n = V(1, 0, 0);
+            fd = he.x + rel.x; if (fd < md) { md = fd; cp = rel; cp.x = -he.x; n = V(-1, 0, 0); }
+            fd = he.y - rel.y; if (fd < md) { md = fd; cp = rel; cp.y = he.y; n = V(0, 1, 0); }
+            fd = he.y + rel.y; if (fd < md) { md = fd; cp = rel; cp.y = -he.y; n = V(0, -1, 0); }
+            fd = he.z - rel.z; if (fd < md) { md = fd; cp = rel; cp.z = he.z; n = V(0, 0, 1); }
+            fd = he.z + rel.z; if (fd < md) { md = fd; cp = rel; cp.z = -he.z; n = V(0, 0, -1); }
+            d = -md;
+        } else {
+            d = sqrtf(d2);
+            n = scl(n, 1.f / d);
+        }
+        v3 pbox = tfpt(X.t, add(cp, scl(n, X.margin)));
+        v3 nw = qrot(X.t.q, n);
+        float pen = d - inter;
+        if (pen > thr) return 0;
+        if (!swapped) { nB = nw; pB = pbox; dist = pen; }
+        else { nB = scl(nw, -1.f); pB = add(pbox, scl(nw, pen)); dist = pen; }
+        return 1;
+    }
+    if ((ka == AVR_SPHERE || ka == AVR_CAPSULE) && (kb == AVR_SPHERE || kb == AVR_CAPSULE) && !(ka == AVR_CAPSULE && kb == AVR_CAPSULE)) {
+        bool swapped = ka == AVR_CAPSULE;
+        const WShape &Sp = swapped ? B : A;
+        const WShape &Cp = swapped ? A : B;
+        v3 az = qrot(Cp.t.q, V(0, 0, 1));
+        v3 p0 = sub(Cp.t.p, scl(az, Cp.he.y)), p1 = add(Cp.t.p, scl(az, Cp.he.y));
+        v3 e = sub(p1, p0);
+        float t = dot(sub(Sp.t.p, p0), e) / fmaxf(dot(e, e), 1e-30f);
+        t = fminf(1.f, fmaxf(0.f, t));
+        v3 q = add(p0, scl(e, t));
+        v3 diff = sub(Sp.t.p, q);
+        float l = len(diff);
+        v3 n = l > 1e-12f ? scl(diff, 1.f / l) : V(1, 0, 0);
+        float d = l - Sp.he.x - Cp.he.x;
+        if (d > thr) return 0;
+        if (!swapped) { nB = n; pB = add(q, scl(n, Cp.he.x)); dist = d; }
+        else { nB = scl(n, -1.f); pB = sub(Sp.t.p, scl(n, Sp.he.x)); dist = d; }
+        return 1;
+    }
+    float ma = A.margin, mb = B.margin;
+    float maxd = ma + mb + thr;
+    v3 pa, pb;
+    float cd;
+    Simplex S;
+    int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S);
+    if (st == GJK_FAR) return 0;
+    v3 n;
+    float d;
+    if (st == GJK_SEPARATED && cd > 1e-9f) {
+        n = scl(sub(pa, pb), 1.f / cd);
+        d = cd - ma - mb;
+    } else {
+        if (!COOP) return 2;
+        float depth;
+        v3 en;
+        if (epa(m, L, A, B, S, en, depth, pa, pb)) return 0;
+        n = scl(en, -1.f);
+        d = -depth - ma - mb;
+    }
+    if (d > thr) return 0;
+    nB = n;
+    pB = add(pb, scl(n, mb));
+    dist = d;
+    return 1;
+}
+
+// --------------------------------------------------------------------------- bodies
+AVR_DI tf body_tf(const KModel &m, const EnvLDS &L, int b) {
+    int kind = m.body_kind[b], idx = m.body_index[b];
+    if (kind == AVR_BODY_ROBOT) return ldtf(L.cm[idx]);
+    if (kind == AVR_BODY_FREE) return ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * idx);
+    if (kind == AVR_BODY_STATIC) return ldtf(m.st_pose + 8 * idx);
+    return ldtf(L.st + AVR_S_HUMAN + 7 * idx);
+}
+
+AVR_DI void aabb_of(tf t, v3 c, v3 h, v3 &mn, v3 &mx) {
+    m3 R = qmat(t.q);
+    v3 cw = tfpt(t, c);
+    v3 hw = V(fabsf(R.m[0][0]) * h.x + fabsf(R.m[0][1]) * h.y + fabsf(R.m[0][2]) * h.z,
+              fabsf(R.m[1][0]) * h.x + fabsf(R.m[1][1]) * h.y + fabsf(R.m[1][2]) * h.z,
+              fabsf(R.m[2][0]) * h.x + fabsf(R.m[2][1]) * h.y + fabsf(R.m[2][2]) * h.z);
+    mn = sub(cw, hw);
+    mx = add(cw, hw);
+}
+
+AVR_DI bool overlap(v3 a0, v3 a1, v3 b0, v3 b1) {
+    return a0.x <= b1.x && a1.x >= b0.x && a0.y <= b1.y && a1.y >= b0.y && a0.z <= b1.z && a1.z >= b0.z;
+}
+
+AVR_DI void shape_aabb(const KModel &m, int s, tf body, v3 &mn, v3 &mx) {
+    tf t = tfmul(body, ldtf(m.shape_pose + 8 * s));
+    const float *a = m.shape_aabb + 8 * s;
+    aabb_of(t, ld3(a), ld3(a + 4), mn, mx);
+}
+
+AVR_DI bool shape_enabled(const KModel &m, int s, int gender) {
+    int g = m.shape_gender[s];
+    return g < 0 || g == gender;
+}
+
+// --------------------------------------------------------------------------- manifolds (one lane per shape pair)
+struct Manifold { float p[AVR_MANIFOLD_POINTS][AVR_CP_WORDS]; int n; };
+
+AVR_DI void mf_copy(float *dst, const float *src) {
+    for (int k = 0; k < AVR_CP_WORDS; k++) dst[k] = src[k];
+}
+
+AVR_DI int sort_cached(const Manifold &M, v3 la_new, float d_new) {
+    int maxi = -1;
+    float maxpen = d_new;
+    for (int i = 0; i < 4; i++)
+        if (M.p[i][AVR_CP_DIST] < maxpen) { maxi = i; maxpen = M.p[i][AVR_CP_DIST]; }
+    v3 p[4];
+    for (int i = 0; i < 4; i++) p[i] = ld3(M.p[i] + AVR_CP_LA);
+    float res[4] = {0, 0, 0, 0};
+    if (maxi != 0) res[0] = len2(crs(sub(la_new, p[1]), sub(p[3], p[2])));
+    if (maxi != 1) res[1] = len2(crs(sub(la_new, p[0]), sub(p[3], p[2])));
+    if (maxi != 2) res[2] = len2(crs(sub(la_new, p[0]), sub(p[3], p[1])));
+    if (maxi != 3) res[3] = len2(crs(sub(la_new, p[0]), sub(p[2], p[1])));
+    int bi = 0;
+    float bv = -1.f;
+    for (int i = 0; i < 4; i++)
+        if (fabsf(res[i]) > bv) { bv = fabsf(res[i]); bi = i; }
+    return bi;
+}
+
+AVR_DI void manifold_add(Manifold &M, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB, float dist, float thr) {
+    if (dist > thr) return;
+    v3 pA = add(pB, scl(nB, dist));
+    v3 la = tfinvpt(ta, pA), lb = tfinvpt(tb, pB);
+    float shortest = thr * thr;
+    int near = -1;
+    for (int k = 0; k < M.n; k++) {
+        float d2 = len2(sub(ld3(M.p[k] + AVR_CP_LA), la));
+        if (d2 < shortest) { shortest = d2; near = k; }
+    }
+    int slot;
+    if (near >= 0) slot = near;
+    else if (M.n == AVR_MANIFOLD_POINTS) {
+        slot = sort_cached(M, la, dist);
+        M.p[slot][AVR_CP_IMP] = 0.f; M.p[slot][AVR_CP_LIFE] = 0.f;
+    } else {
+        slot = M.n++;
+        M.p[slot][AVR_CP_IMP] = 0.f; M.p[slot][AVR_CP_LIFE] = 0.f;
+    }
+    float *c = M.p[slot];
+    c[AVR_CP_SA] = (float)sa; c[AVR_CP_SB] = (float)sb; c[AVR_CP_PAIR] = (float)pair; c[AVR_CP_SLOT] = 0.f;
+    st3(c + AVR_CP_LA, la); st3(c + AVR_CP_LB, lb); st3(c + AVR_CP_N, nB);
+    c[AVR_CP_DIST] = dist;
+}
+
+AVR_DI void manifold_refresh(Manifold &M, tf ta, tf tb, float thr) {
+    for (int k = M.n - 1; k >= 0; k--) {
+        float *c = M.p[k];
+        v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
+        c[AVR_CP_DIST] = dot(sub(pa, pb), ld3(c + AVR_CP_N));
+        c[AVR_CP_LIFE] += 1.f;
+    }
+    for (int k = M.n - 1; k >= 0; k--) {
+        float *c = M.p[k];
+        bool rm = false;
+        if (c[AVR_CP_DIST] > thr) rm = true;
+        else {
+            v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
+            v3 nrm = ld3(c + AVR_CP_N);
+            v3 dd = sub(pb, sub(pa, scl(nrm, c[AVR_CP_DIST])));
+            if (len2(dd) > thr * thr) rm = true;
+        }
+        if (rm) {
+            if (k != M.n - 1) mf_copy(c, M.p[M.n - 1]);
+            M.n--;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------- collision detection
+AVR_DI void collide(const KModel &m, EnvLDS &L) {
+    const int lane = lane_id();
+    const int gender = L.gender;
+    // body transforms + fattened AABBs
+    for (int b = lane; b < m.nb; b += 64) {
+        tf t = body_tf(m, L, b);
+        int g = m.body_kind[b] == AVR_BODY_HUMAN ? gender : 0;
+        const float *a = m.body_aabb + 12 * b + 6 * g;
+        v3 mn, mx;
+        aabb_of(t, ld3(a), ld3(a + 3), mn, mx);
+        v3 e = V(BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND);
+        sttf(L.btf[b], t);
+        st3(L.bmin[b], sub(mn, e));
+        st3(L.bmax[b], add(mx, e));
+    }
+    SYNC();
+    // broadphase over the candidate pair list, order-preserving compaction
+    int nap = 0;
+    for (int base = 0; base < m.np; base += 64) {
+        int p = base + lane;
+        bool act = false;
+        if (p < m.np) {
+            int ba = m.pair_a[p], bb = m.pair_b[p];
+            act = overlap(ld3(L.bmin[ba]), ld3(L.bmax[ba]), ld3(L.bmin[bb]), ld3(L.bmax[bb]));
+        }
+        int tot;
+        int pre = ballot_prefix(act, &tot);
+        if (act && nap + pre < MAXAP) L.u.c.apair[nap + pre] = p;
+        nap += tot;
+    }
+    if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
+    SYNC();
+    // child-level shape pairs (compound culling), i-major / j-minor within each body pair
+    int nsp = 0;
+    for (int k = 0; k < nap; k++) {
+        int p = L.u.c.apair[k];
+        int ba = m.pair_a[p], bb = m.pair_b[p];
+        int sa0 = m.body_shape_start[ba], na = m.body_shape_count[ba];
+        int sb0 = m.body_shape_start[bb], nb = m.body_shape_count[bb];
+        bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
+        tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+        int nitems = na * nb;
+        for (int base = 0; base < nitems; base += 64) {
+            int it = base + lane;
+            bool act = false;
+            int sa = 0, sb = 0;
+            if (it < nitems) {
+                sa = sa0 + it / nb;
+                sb = sb0 + it % nb;
+                if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
+                    if (bare) act = true;
+                    else {
+                        v3 a0, a1, b0, b1;
+                        shape_aabb(m, sa, ta, a0, a1);
+                        shape_aabb(m, sb, tb, b0, b1);
+                        act = overlap(a0, a1, b0, b1);
+                    }
+                }
+            }
+            int tot;
+            int pre = ballot_prefix(act, &tot);
+            if (act && nsp + pre < MAXSP) {
+                L.u.c.sp_a[nsp + pre] = sa;
+                L.u.c.sp_b[nsp + pre] = sb;
+                L.u.c.sp_pair[nsp + pre] = p;
+            }
+            nsp += tot;
+        }
+    }
+    if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; nsp = MAXSP; }
+    SYNC();
+    // narrowphase pass A: one lane per small shape pair; big hulls and EPA deferred
+    for (int q = lane; q < nsp; q += 64) {
+        int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q];
+        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
+        float *r = L.u.c.res[q];
+        if (A.nv > SMALL_NV || B.nv > SMALL_NV) { r[0] = 2.f; continue; }
+        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+        float d = 0.f;
+        int rc = narrowphase<false>(m, L, A, B, thr, nB, pB, d);
+        r[0] = (float)rc;
+        st3(r + 1, nB); st3(r + 4, pB); r[7] = d;
+    }
+    SYNC();
+    // pass B: wave-cooperative narrowphase (big hulls, EPA), in pair order
+    for (int q = 0; q < nsp; q++) {
+        if (L.u.c.res[q][0] != 2.f) continue;
+        int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q];
+        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
+        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+        float d = 0.f;
+        int rc = narrowphase<true>(m, L, A, B, thr, nB, pB, d);
+        SYNC();
+        if (lane == 0) {
+            float *r = L.u.c.res[q];
+            r[0] = (float)rc;
+            st3(r + 1, nB); st3(r + 4, pB); r[7] = d;
+        }
+        SYNC();
+    }
+    // pass C: rebuild the contact pool, one lane per manifold, order-preserving
+    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    int nnew = 0;
+    for (int base = 0; base < nsp; base += 64) {
+        int q = base + lane;
+        Manifold M;
+        M.n = 0;
+        int sa = 0, sb = 0, p = 0, ba = 0, bb = 0;
+        float thr = 0.f;
+        if (q < nsp) {
+            sa = L.u.c.sp_a[q]; sb = L.u.c.sp_b[q]; p = L.u.c.sp_pair[q];
+            ba = m.shape_body[sa]; bb = m.shape_body[sb];
+            thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+            for (int i = 0; i < nold && M.n < AVR_MANIFOLD_POINTS; i++) {
+                const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * i;
+                if ((int)c[AVR_CP_SA] == sa && (int)c[AVR_CP_SB] == sb) { mf_copy(M.p[M.n], c); M.n++; }
+            }
+            tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+            const float *r = L.u.c.res[q];
+            if (r[0] == 1.f) manifold_add(M, sa, sb, p, ta, tb, ld3(r + 1), ld3(r + 4), r[7], thr);
+            manifold_refresh(M, ta, tb, thr);
+        }
+        // exclusive prefix sum of survivor counts across lanes
+        int cnt = M.n, incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        int excl = incl - cnt;
+        int tot = __shfl(incl, 63, 64);
+        for (int k = 0; k < M.n; k++) {
+            int dst = nnew + excl + k;
+            if (dst < AVR_MAX_CONTACTS) mf_copy(L.u.c.newcp[dst], M.p[k]);
+        }
+        nnew += tot;
+    }
+    if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
+    SYNC();
+    for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) L.st[AVR_S_CP + i] = (&L.u.c.newcp[0][0])[i];
+    if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
+    SYNC();
+}
+
+// --------------------------------------------------------------------------- constraint rows
+AVR_DI void robot_jac(const KModel &m, const EnvLDS &L, int link, v3 p, v3 lin, v3 ang, float *J) {
+    const unsigned am = m.anc_mask[link];
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+        float v = 0.f;
+        if (d < m.nd) {
+            int k = m.dof_link[d];
+            if ((am >> k) & 1u) {
+                v3 cl, ca;
+                dof_col(m, L, k, p, cl, ca);
+                v = dot(lin, cl) + dot(ang, ca);
+            }
+        }
+        J[d] = v;
+    }
+}
+
+AVR_DI float free_dot(const EnvLDS &L, int f, v3 lin, v3 ang, bool delta) {
+    v3 v = delta ? ld3(L.dfv[f]) : ld3(L.fv[f]);
+    v3 w = delta ? ld3(L.dfw[f]) : ld3(L.fw[f]);
+    return dot(lin, v) + dot(ang, w);
+}
+
+AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
+    const float *I = L.Iinv[f];
+    return V(I[0] * a.x + I[1] * a.y + I[2] * a.z, I[3] * a.x + I[4] * a.y + I[5] * a.z, I[6] * a.x + I[7] * a.y + I[8] * a.z);
+}
+
+AVR_DI float robot_dot(const KModel &m, const EnvLDS &L, const float *J, bool delta) {
+    (void)m;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) s += J[d] * (delta ? L.dq[d] : L.vq[d]);
+    return s;
+}
+
+// Non-contact rows (limits, motors, fixed constraint); lanes build rows in parallel.
+AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
+    const int lane = lane_id();
+    const float erp = m.erp;
+    // enumerate: violated limits (link order, lower then upper), motors (link order), fixed (6)
+    int nrow = 0;
+    // limits
+    for (int i = 0; i < m.nl; i++) {
+        if (!m.rl_has_limit[i]) continue;
+        int dof = m.rl_dof[i];
+        float q = L.st[AVR_S_Q + dof];
+        for (int side = 0; side < 2; side++) {
+            float pen = side == 0 ? q - m.rl_lower[i] : m.rl_upper[i] - q;
+            if (pen > 0.f) continue;
+            if (nrow < MAXNC && lane == (nrow & 63)) {
+                NCRow &r = L.u.s.nc[nrow];
+                for (int d = 0; d < MAXD; d++) r.JA[d] = 0.f;
+                r.JA[dof] = side == 0 ? 1.f : -1.f;
+                float MA[MAXD];
+                chol_solve(m, L, r.JA, MA);
+                float den = 0.f;
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) { r.MA[d] = MA[d]; den += r.JA[d] * MA[d]; }
+                r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+                float rel = robot_dot(m, L, r.JA, false);
+                r.rhs = (-pen * erp / dt - rel) * r.inv;
+                r.lo = 0.f; r.hi = 100.f; r.imp = 0.f; r.fb = -1;
+            }
+            nrow++;
+        }
+    }
+    // motors
+    for (int i = 0; i < m.nl; i++) {
+        int dof = m.rl_dof[i];
+        if (dof < 0) continue;
+        if (nrow < MAXNC && lane == (nrow & 63)) {
+            NCRow &r = L.u.s.nc[nrow];
+            for (int d = 0; d < MAXD; d++) r.JA[d] = 0.f;
+            r.JA[dof] = 1.f;
+            float MA[MAXD];
+            chol_solve(m, L, r.JA, MA);
+            float den = 0.f;
+#pragma unroll
+            for (int d = 0; d < MAXD; d++) { r.MA[d] = MA[d]; den += r.JA[d] * MA[d]; }
+            r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+            float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
+            float kp = L.st[AVR_S_KP + dof], kd = 1.f;
+            float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
+            float rel = robot_dot(m, L, r.JA, false);
+            r.rhs = (desired - rel) * r.inv;
+            float mi = L.st[AVR_S_MAXIMP + dof];
+            r.lo = -mi; r.hi = mi; r.imp = 0.f; r.fb = -1;
+        }
+        nrow++;
+    }
+    // fixed constraint robot tool link <-> spoon
+    {
+        int link = m.tool_link, fb = m.spoon_free;
+        tf ta = ldtf(L.cm[link]);
+        tf off = ldtf(m.tool_offset);
+        v3 pivA = tfpt(ta, off.p);
+        qt frA = qmul(ta.q, off.q);
+        tf tb = ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * fb);
+        v3 pivB = tb.p;
+        m3 FA = qmat(frA), FB = qmat(tb.q);
+        m3 rr;
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) {
+                float s = 0.f;
+                for (int k = 0; k < 3; k++) s += FA.m[k][a] * FB.m[k][b];
+                rr.m[a][b] = s;
+            }
+#define ME(i) rr.m[(i) % 3][(i) / 3]
+        v3 ang;
+        float fi = ME(2);
+        if (fi < 1.f) {
+            if (fi > -1.f) ang = V(atan2f(-ME(5), ME(8)), asinf(ME(2)), atan2f(-ME(1), ME(0)));
+            else ang = V(-atan2f(ME(3), ME(4)), -1.5707963267948966f, 0.f);
+        } else ang = V(atan2f(ME(3), ME(4)), 1.5707963267948966f, 0.f);
+#undef ME
+        float mi = m.fixed_max_imp;
+        for (int i = 0; i < 6; i++) {
+            int row = nrow + i;
+            if (row < MAXNC && lane == (row & 63)) {
+                NCRow &r = L.u.s.nc[row];
+                v3 lin = V(0, 0, 0), an = V(0, 0, 0);
+                float pos;
+                float JA[MAXD];
+                v3 jbl, jba;
+                if (i < 3) {
+                    if (i == 0) lin.x = 1.f; else if (i == 1) lin.y = 1.f; else lin.z = 1.f;
+                    pos = dot(sub(pivA, pivB), lin);
+                    robot_jac(m, L, link, pivA, lin, V(0, 0, 0), JA);
+                    jbl = scl(lin, -1.f);
+                    jba = crs(sub(pivB, tb.p), jbl);
+                } else {
+                    an = V(FA.m[0][i - 3], FA.m[1][i - 3], FA.m[2][i - 3]);
+                    pos = i == 3 ? ang.x : i == 4 ? ang.y : ang.z;
+                    robot_jac(m, L, link, pivA, V(0, 0, 0), an, JA);
+                    jbl = V(0, 0, 0);
+                    jba = scl(an, -1.f);
+                }
+                float MA[MAXD];
+                chol_solve(m, L, JA, MA);
+                float den = 0.f;
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) { r.JA[d] = JA[d]; r.MA[d] = MA[d]; den += JA[d] * MA[d]; }
+                float im = 1.f / m.fb_mass[fb];
+                v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
+                st3(r.JB, jbl); st3(r.JB + 3, jba); st3(r.MB, mbl); st3(r.MB + 3, mba);
+                den += dot(jbl, mbl) + dot(jba, mba);
+                r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+                float rel = robot_dot(m, L, r.JA, false) + free_dot(L, fb, jbl, jba, false);
+                r.rhs = (-pos * erp / dt - rel) * r.inv;
+                r.lo = -mi; r.hi = mi; r.imp = 0.f; r.fb = fb;
+            }
+        }
+        nrow += 6;
+    }
+    if (nrow > MAXNC) { if (lane == 0) L.flags |= 16; nrow = MAXNC; }
+    if (lane == 0) L.n_nc = nrow;
+    SYNC();
+}
+
+AVR_DI void plane_space(v3 n, v3 &p, v3 &q) {
+    if (fabsf(n.z) > 0.7071067811865475244f) {
+        float a = n.y * n.y + n.z * n.z, k = 1.f / sqrtf(a);
+        p = V(0, -n.z * k, n.y * k);
+        q = V(a * k, -n.x * p.z, n.x * p.y);
+    } else {
+        float a = n.x * n.x + n.y * n.y, k = 1.f / sqrtf(a);
+        p = V(-n.y * k, n.x * k, 0);
+        q = V(-n.z * p.y, n.z * p.x, a * k);
+    }
+}
+
+AVR_DI void body_endpoint(const KModel &m, int b, int &kind, int &idx) {
+    int k = m.body_kind[b];
+    if (k == AVR_BODY_ROBOT) { kind = 1; idx = m.body_index[b]; }
+    else if (k == AVR_BODY_FREE) { kind = 2; idx = m.body_index[b]; }
+    else { kind = 0; idx = 0; }
+}
+
+// Contact rows: one lane per contact point.  Robot endpoints take robot slots (prefix sum).
+AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float dt) {
+    const int lane = lane_id();
+    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    const float erp = m.erp;
+    int rs_base = 0;
+    for (int base = 0; base < ncp; base += 64) {
+        int i = base + lane;
+        bool valid = i < ncp;
+        int kA = 0, iA = 0, kB = 0, iB = 0;
+        const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * (valid ? i : 0);
+        int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
+        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        body_endpoint(m, ba, kA, iA);
+        body_endpoint(m, bb, kB, iB);
+        int need = valid ? 3 * ((kA == 1) + (kB == 1)) : 0;
+        int incl = need;
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        int myrs = rs_base + incl - need;
+        int tot = __shfl(incl, 63, 64);
+        if (valid) {
+            CRow &r = L.u.s.cr[i];
+            tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+            v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
+            v3 n = ld3(c + AVR_CP_N);
+            v3 t1, t2;
+            plane_space(n, t1, t2);
+            st3(r.n, n); st3(r.t1, t1); st3(r.t2, t2);
+            v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
+            st3(r.rA, rA); st3(r.rB, rB);
+            float fr = m.body_friction[ba] * m.body_friction[bb];
+            r.fric = fminf(fr, 10.f);
+            r.kA = kA; r.iA = iA; r.kB = kB; r.iB = iB;
+            r.cp = i;
+            bool fits = myrs + need <= MAXRS;
+            r.rs = fits ? myrs : -1;
+            int slot = myrs;
+            for (int k = 0; k < 3; k++) {
+                v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
+                float den = 0.f, rel = 0.f;
+                if (kA == 1) {
+                    if (fits) {
+                        float J[MAXD], MJ[MAXD];
+                        robot_jac(m, L, iA, pa, dir, V(0, 0, 0), J);
+                        chol_solve(m, L, J, MJ);
+#pragma unroll
+                        for (int d = 0; d < MAXD; d++) { L.u.s.rsJ[slot][d] = J[d]; L.u.s.rsM[slot][d] = MJ[d]; den += J[d] * MJ[d]; rel += J[d] * L.vq[d]; }
+                    }
+                    slot++;
+                } else if (kA == 2) {
+                    v3 ja = crs(rA, dir);
+                    den += dot(dir, dir) / m.fb_mass[iA] + dot(ja, iinv_mul(L, iA, ja));
+                    rel += free_dot(L, iA, dir, ja, false);
+                }
+                v3 nd = scl(dir, -1.f);
+                if (kB == 1) {
+                    if (fits) {
+                        float J[MAXD], MJ[MAXD];
+                        robot_jac(m, L, iB, pb, nd, V(0, 0, 0), J);
+                        chol_solve(m, L, J, MJ);
+#pragma unroll
+                        for (int d = 0; d < MAXD; d++) { L.u.s.rsJ[slot][d] = J[d]; L.u.s.rsM[slot][d] = MJ[d]; den += J[d] * MJ[d]; rel += J[d] * L.vq[d]; }
+                    }
+                    slot++;
+                } else if (kB == 2) {
+                    v3 jb = crs(rB, nd);
+                    den += dot(nd, nd) / m.fb_mass[iB] + dot(jb, iinv_mul(L, iB, jb));
+                    rel += free_dot(L, iB, nd, jb, false);
+                }
+                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+                r.inv[k] = inv;
+                if (k == 0) {
+                    float pen = c[AVR_CP_DIST];
+                    float velerr = -rel, poserr = 0.f;
+                    if (pen > 0.f) velerr -= pen / dt;
+                    else poserr = -pen * erp / dt;
+                    r.rhs[0] = (poserr + velerr) * inv;
+                    r.imp[0] = c[AVR_CP_IMP] * m.warmstart;
+                } else {
+                    r.rhs[k] = -rel * inv;
+                    r.imp[k] = 0.f;
+                }
+            }
+        }
+        rs_base += tot;
+    }
+    if (rs_base > MAXRS && lane == 0) L.flags |= 32;
+    if (lane == 0) L.n_c = ncp;
+    SYNC();
+}
+
+// apply impulse of contact row k of contact c to the delta velocities (uniform, lane 0 writes)
+AVR_DI void crow_apply(const KModel &m, EnvLDS &L, const CRow &r, int k, float imp, int lane) {
+    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
+    int slot = r.rs + k * ((r.kA == 1) + (r.kB == 1));
+    if (r.kA == 1) {
+        if (lane < m.nd) L.dq[lane] += L.u.s.rsM[slot][lane] * imp;
+        slot++;
+    } else if (r.kA == 2) {
+        v3 ja = crs(ld3(r.rA), dir);
+        v3 dl = scl(dir, imp / m.fb_mass[r.iA]);
+        v3 da = scl(iinv_mul(L, r.iA, ja), imp);
+        if (lane == 0) { st3(L.dfv[r.iA], add(ld3(L.dfv[r.iA]), dl)); st3(L.dfw[r.iA], add(ld3(L.dfw[r.iA]), da)); }
+    }
+    if (r.kB == 1) {
+        if (lane < m.nd) L.dq[lane] += L.u.s.rsM[slot][lane] * imp;
+    } else if (r.kB == 2) {
+        v3 nd = scl(dir, -1.f);
+        v3 jb = crs(ld3(r.rB), nd);
+        v3 dl = scl(nd, imp / m.fb_mass[r.iB]);
+        v3 da = scl(iinv_mul(L, r.iB, jb), imp);
+        if (lane == 0) { st3(L.dfv[r.iB], add(ld3(L.dfv[r.iB]), dl)); st3(L.dfw[r.iB], add(ld3(L.dfw[r.iB]), da)); }
+    }
+}
+
+AVR_DI float crow_dot(const KModel &m, const EnvLDS &L, const CRow &r, int k) {
+    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
+    int slot = r.rs + k * ((r.kA == 1) + (r.kB == 1));
+    float s = 0.f;
+    if (r.kA == 1) { s += robot_dot(m, L, L.u.s.rsJ[slot], true); slot++; }
+    else if (r.kA == 2) s += free_dot(L, r.iA, dir, crs(ld3(r.rA), dir), true);
+    if (r.kB == 1) s += robot_dot(m, L, L.u.s.rsJ[slot], true);
+    else if (r.kB == 2) { v3 nd = scl(dir, -1.f); s += free_dot(L, r.iB, nd, crs(ld3(r.rB), nd), true); }
+    return s;
+}
+
+// Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order).
+AVR_DI void solve(const KModel &m, EnvLDS &L) {
+    const int lane = lane_id();
+    const int n_nc = L.n_nc, n_c = L.n_c;
+    // warm start, in contact order
+    for (int i = 0; i < n_c; i++) {
+        CRow &r = L.u.s.cr[i];
+        if (r.rs < 0 && (r.kA == 1 || r.kB == 1)) continue;
+        float imp = r.imp[0];
+        if (imp != 0.f) crow_apply(m, L, r, 0, imp, lane);
+        SYNC();
+    }
+    for (int it = 0; it < m.iters; it++) {
+        for (int j = 0; j < n_nc; j++) {
+            int k = (it & 1) ? j : n_nc - 1 - j;
+            NCRow &r = L.u.s.nc[k];
+            float dv = robot_dot(m, L, r.JA, true);
+            if (r.fb >= 0) dv += free_dot(L, r.fb, ld3(r.JB), ld3(r.JB + 3), true);
+            float delta = r.rhs - dv * r.inv;
+            float sum = r.imp + delta;
+            float ni;
+            if (sum < r.lo) { delta = r.lo - r.imp; ni = r.lo; }
+            else if (sum > r.hi) { delta = r.hi - r.imp; ni = r.hi; }
+            else ni = sum;
+            SYNC();
+            if (lane < m.nd) L.dq[lane] += r.MA[lane] * delta;
+            if (lane == 0) {
+                r.imp = ni;
+                if (r.fb >= 0) {
+                    st3(L.dfv[r.fb], add(ld3(L.dfv[r.fb]), scl(ld3(r.MB), delta)));
+                    st3(L.dfw[r.fb], add(ld3(L.dfw[r.fb]), scl(ld3(r.MB + 3), delta)));
+                }
+            }
+            SYNC();
+        }
+        for (int pass = 0; pass < 3; pass++) {
+            // pass 0: normals; passes 1,2 interleaved friction rows (t1 then t2 per contact)
+            if (pass == 2) break;
+            for (int i = 0; i < n_c; i++) {
+                CRow &r = L.u.s.cr[i];
+                if (r.rs < 0 && (r.kA == 1 || r.kB == 1)) continue;
+                if (pass == 0) {
+                    float dv = crow_dot(m, L, r, 0);
+                    float delta = r.rhs[0] - dv * r.inv[0];
+                    float sum = r.imp[0] + delta, ni;
+                    if (sum < 0.f) { delta = -r.imp[0]; ni = 0.f; }
+                    else if (sum > 1e10f) { delta = 1e10f - r.imp[0]; ni = 1e10f; }
+                    else ni = sum;
+                    SYNC();
+                    crow_apply(m, L, r, 0, delta, lane);
+                    if (lane == 0) r.imp[0] = ni;
+                    SYNC();
+                } else {
+                    float nimp = r.imp[0];
+                    if (!(nimp > 0.f)) continue;
+                    float lo = -r.fric * nimp, hi = r.fric * nimp;
+                    for (int k = 1; k < 3; k++) {
+                        float dv = crow_dot(m, L, r, k);
+                        float delta = r.rhs[k] - dv * r.inv[k];
+                        float sum = r.imp[k] + delta, ni;
+                        if (sum < lo) { delta = lo - r.imp[k]; ni = lo; }
+                        else if (sum > hi) { delta = hi - r.imp[k]; ni = hi; }
+                        else ni = sum;
+                        SYNC();
+                        crow_apply(m, L, r, k, delta, lane);
+                        if (lane == 0) r.imp[k] = ni;
+                        SYNC();
+                    }
+                }
+            }
+        }
+    }
+    // write back normal impulses to the manifold points (warm start + normalForce)
+    for (int i = lane; i < n_c; i += 64) {
+        CRow &r = L.u.s.cr[i];
+        L.st[AVR_S_CP + AVR_CP_WORDS * r.cp + AVR_CP_IMP] = r.imp[0];
+    }
+    SYNC();
+}
+
+// --------------------------------------------------------------------------- one sub-step
+AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
+    const int lane = lane_id();
+    robot_fk(m, L);
+    collide(m, L);
+    // unconstrained velocities
+    bool ok = robot_mass_matrix(m, L);
+    robot_bias(m, L);
+    {
+        float nh[MAXD], qdd[MAXD];
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) nh[d] = d < m.nd ? -L.h[d] : 0.f;
+        chol_solve(m, L, nh, qdd);
+        SYNC();
+        if (lane == 0) {
+#pragma unroll
+            for (int d = 0; d < MAXD; d++) L.qdd[d] = qdd[d];
+        }
+        SYNC();
+    }
+    const float vmax = m.max_vel;
+    if (lane < m.nd) {
+        float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
+        L.vq[lane] = clampf(v, -vmax, vmax);
+        L.dq[lane] = 0.f;
+    }
+    const float k1l = m.lin_damp, k1a = m.ang_damp;
+    if (lane < m.nf) {
+        int f = lane;
+        const float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * f;
+        v3 v = ld3(fb + 7), om = ld3(fb + 10);
+        qt q = ldq(fb + 3);
+        float mass = m.fb_mass[f];
+        v3 I = ld3(m.fb_inertia + 4 * f), g = ld3(m.fb_gravity + 4 * f);
+        v3 Iw = inertia_mul(q, I, om);
+        v3 F = sub(scl(g, mass), scl(v, mass * (k1l + k1l * len(v))));
+        v3 T = sub(scl(Iw, -(k1a + k1a * len(om))), crs(om, Iw));
+        v3 nv = add(v, scl(F, dt / mass));
+        v3 nw = add(om, scl(inertia_inv_mul(q, I, T), dt));
+        st3(L.fv[f], clamp3(nv, vmax));
+        st3(L.fw[f], clamp3(nw, vmax));
+        st3(L.dfv[f], V(0, 0, 0));
+        st3(L.dfw[f], V(0, 0, 0));
+        // world inverse inertia R diag(1/I) R^T
+        m3 R = qmat(q);
+        float inv[3] = {I.x > 0.f ? 1.f / I.x : 0.f, I.y > 0.f ? 1.f / I.y : 0.f, I.z > 0.f ? 1.f / I.z : 0.f};
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) L.Iinv[f][3 * a + b] = R.m[a][0] * inv[0] * R.m[b][0] + R.m[a][1] * inv[1] * R.m[b][1] + R.m[a][2] * inv[2] * R.m[b][2];
+    }
+    SYNC();
+    build_noncontact_rows(m, L, dt);
+    build_contact_rows(m, L, dt);
+    solve(m, L);
+    // integrate
+    if (lane < m.nd) {
+        float v = clampf(L.vq[lane] + L.dq[lane], -vmax, vmax);
+        L.st[AVR_S_QD + lane] = v;
+        L.st[AVR_S_Q + lane] += dt * v;
+    }
+    if (lane < m.nf) {
+        int f = lane;
+        float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * f;
+        v3 v = clamp3(add(ld3(L.fv[f]), ld3(L.dfv[f])), vmax);
+        v3 om = clamp3(add(ld3(L.fw[f]), ld3(L.dfw[f])), vmax);
+        st3(fb + 7, v);
+        st3(fb + 10, om);
+        st3(fb, add(ld3(fb), scl(v, dt)));
+        float ang = len(om);
+        if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = (0.5f * 1.5707963267948966f) / dt;
+        v3 ax;
+        if (ang < 0.001f) ax = scl(om, 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang);
+        else ax = scl(om, sinf(0.5f * ang * dt) / ang);
+        qt dq = Q(ax.x, ax.y, ax.z, cosf(ang * dt * 0.5f));
+        stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
+    }
+    SYNC();
+    return ok;
+}
+
+// --------------------------------------------------------------------------- task glue
+AVR_DI void mouth_target(const KModel &m, EnvLDS &L) {
+    tf t = ldtf(L.st + AVR_S_HUMAN + 7 * m.head_slot);
+    int g = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+    v3 p = tfpt(t, ld3(m.mouth[g]));
+    SYNC();
+    if (lane_id() == 0) st3(L.st + AVR_S_TASK + AVR_T_TARGET, p);
+    SYNC();
+}
+
+// sum of normalForce over contact points whose body pair satisfies `sel`, and their count
+// sel: 0 robot-human, 1 spoon-human, 2 body X vs body Y, 3 body X vs human
+AVR_DI float contact_sum(const KModel &m, const EnvLDS &L, int sel, int X, int Y, int &count) {
+    const int lane = lane_id();
+    int n = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    float s = 0.f;
+    int c = 0;
+    for (int i = lane; i < n; i += 64) {
+        const float *cp = L.st + AVR_S_CP + AVR_CP_WORDS * i;
+        int ba = m.shape_body[(int)cp[AVR_CP_SA]], bb = m.shape_body[(int)cp[AVR_CP_SB]];
+        int ka = m.body_kind[ba], kb = m.body_kind[bb];
+        bool hit;
+        if (sel == 0) hit = (ka == AVR_BODY_ROBOT && kb == AVR_BODY_HUMAN) || (kb == AVR_BODY_ROBOT && ka == AVR_BODY_HUMAN);
+        else if (sel == 1) hit = (ba == m.spoon_body && kb == AVR_BODY_HUMAN) || (bb == m.spoon_body && ka == AVR_BODY_HUMAN);
+        else if (sel == 2) hit = (ba == X && bb == Y) || (ba == Y && bb == X);
+        else hit = (ba == X && kb == AVR_BODY_HUMAN) || (bb == X && ka == AVR_BODY_HUMAN);
+        if (hit) { s += cp[AVR_CP_IMP] / m.time_step; c++; }
+    }
+    // deterministic reduction: sequential order over lanes via shuffles
+    float tot = 0.f;
+    int ctot = 0;
+    for (int k = 0; k < 64; k++) { tot += __shfl(s, k, 64); ctot += __shfl(c, k, 64); }
+    count = ctot;
+    return tot;
+}
+
+AVR_DI void observe(const KModel &m, EnvLDS &L, float spoon_force, float *obs_out) {
+    robot_fk(m, L);
+    if (lane_id() == 0) {
+        v3 torso = ld3(L.cm[m.torso_link]);
+        const float *sp = L.st + AVR_S_FREE + AVR_FB_WORDS * m.spoon_free;
+        v3 spos = ld3(sp);
+        v3 tgt = ld3(L.st + AVR_S_TASK + AVR_T_TARGET);
+        const float *h = L.st + AVR_S_HUMAN + 7 * m.head_slot;
+        int k = 0;
+        v3 a = sub(spos, torso);
+        obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
+        for (int i = 0; i < 4; i++) obs_out[k++] = sp[3 + i];
+        a = sub(spos, tgt);
+        obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
+        for (int i = 0; i < m.n_arm; i++) obs_out[k++] = L.st[AVR_S_Q + m.arm_dofs[i]];
+        a = sub(ld3(h), torso);
+        obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
+        for (int i = 0; i < 4; i++) obs_out[k++] = h[3 + i];
+        obs_out[k++] = spoon_force;
+    }
+}
+
+// Philox4x32-10 (Salmon et al. 2011): counter (env, step, j, 0), key (seed lo, seed hi)
+AVR_DI void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1) {
+    for (int r = 0; r < 10; r++) {
+        unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
+        unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
+        unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0;
+        unsigned h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+        unsigned n0 = h1 ^ c[1] ^ k0, n1 = l1, n2 = h0 ^ c[3] ^ k1, n3 = l0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j) {
+    unsigned c[4] = {(unsigned)env, (unsigned)t, (unsigned)(j >> 2), (unsigned)((unsigned long long)t >> 32)};
+    philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32));
+    unsigned x = c[j & 3];
+    return (float)(x >> 8) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
+}
+
+enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
+
+__global__ __launch_bounds__(64) void avr_step_kernel(KModel m, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
+                                                      float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
+                                                      int mode, long long t, int n_envs) {
+    __shared__ EnvLDS L;
+    const int env = blockIdx.x;
+    const int lane = lane_id();
+    if (env >= n_envs) return;
+    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    for (int i = lane; i < AVR_STATE_WORDS; i += 64) L.st[i] = gst[i];
+    if (lane == 0) { L.flags = 0; L.gender = 0; }
+    SYNC();
+    if (lane == 0) L.gender = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+    SYNC();
+    const int nsub = m.nsub > 0 ? m.nsub : 1;
+    const float dt = m.time_step / (float)nsub;
+    bool ok = true;
+    if (mode == MODE_SUBSTEP) {
+        ok = substep(m, L, *(const float *)&t);
+    } else if (mode == MODE_SETTLE) {
+        for (long long f = 0; f < t; f++)
+            for (int s = 0; s < nsub; s++) ok &= substep(m, L, dt);
+        mouth_target(m, L);
+        if (obs) observe(m, L, 0.f, obs + (size_t)env * AVR_OBS_DIM);
+    } else {
+        // ---- take_step (env.py:274-337)
+        float a_raw[AVR_ACT_DIM];
+#pragma unroll
+        for (int i = 0; i < AVR_ACT_DIM; i++)
+            a_raw[i] = i >= m.n_arm ? 0.f : mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * AVR_ACT_DIM + i];
+        float a[AVR_ACT_DIM], qn[AVR_ACT_DIM];
+#pragma unroll
+        for (int i = 0; i < AVR_ACT_DIM; i++) {
+            a[i] = clampf(a_raw[i], -1.f, 1.f) * 0.05f;
+            qn[i] = i < m.n_arm ? L.st[AVR_S_Q + m.arm_dofs[i]] : 0.f;
+        }
+        for (int it = 0; it < m.frame_skip; it++) {
+#pragma unroll
+            for (int i = 0; i < AVR_ACT_DIM; i++) {
+                if (qn[i] + a[i] < m.arm_lower[i]) a[i] = 0.f;
+                if (qn[i] + a[i] > m.arm_upper[i]) a[i] = 0.f;
+                qn[i] += a[i];
+            }
+        }
+        SYNC();
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < AVR_ACT_DIM; i++) {
+                if (i >= m.n_arm) break;
+                int d = m.arm_dofs[i];
+                L.st[AVR_S_QTGT + d] = qn[i];
+                L.st[AVR_S_KP + d] = m.robot_gain;
+                L.st[AVR_S_MAXIMP + d] = m.robot_force * m.time_step;
+            }
+        SYNC();
+        for (int fr = 0; fr < m.frame_skip; fr++) {
+            for (int s = 0; s < nsub; s++) ok &= substep(m, L, dt);
+            mouth_target(m, L);
+        }
+        if (lane == 0) L.st[AVR_S_TASK + AVR_T_ITER] += 1.f;
+        SYNC();
+        // ---- get_total_force (feeding.py:83-90)
+        int dummy;
+        float robot_force = contact_sum(m, L, 0, 0, 0, dummy);
+        float spoon_force = contact_sum(m, L, 1, 0, 0, dummy);
+        // ---- get_food_rewards (feeding.py:92-121), uniform
+        float food_reward = 0.f, hit_reward = 0.f, mouth_vel = 0.f;
+        int alive = (int)L.st[AVR_S_TASK + AVR_T_ALIVE], hit = (int)L.st[AVR_S_TASK + AVR_T_HIT];
+        float succ = L.st[AVR_S_TASK + AVR_T_SUCCESS];
+        v3 tgt = ld3(L.st + AVR_S_TASK + AVR_T_TARGET);
+        for (int k = 0; k < m.n_food; k++) {
+            if (!(alive >> k & 1)) continue;
+            float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * (m.food_free0 + k);
+            v3 fp = ld3(fb);
+            int fbody = m.food_body0 + k;
+            if (len(sub(tgt, fp)) < 0.02f) {
+                food_reward += 20.f;
+                succ += 1.f;
+                mouth_vel += len(ld3(fb + 7));
+                alive &= ~(1 << k);
+                SYNC();
+                if (lane == 0) st3(fb, V(1500.f + 10.f * k, 1500.f, 1500.f));
+                SYNC();
+                continue;
+            }
+            int ctab, cbowl, chum;
+            contact_sum(m, L, 2, fbody, m.table_body, ctab);
+            contact_sum(m, L, 2, fbody, m.bowl_body, cbowl);
+            if (fp.z < 0.5f || ctab > 0 || cbowl > 0) {
+                food_reward -= 5.f;
+                alive &= ~(1 << k);
+                continue;
+            }
+            contact_sum(m, L, 3, fbody, 0, chum);
+            if (chum > 0 && !(hit >> k & 1)) { hit |= 1 << k; hit_reward -= 1.f; }
+        }
+        SYNC();
+        if (lane == 0) {
+            L.st[AVR_S_TASK + AVR_T_ALIVE] = (float)alive;
+            L.st[AVR_S_TASK + AVR_T_HIT] = (float)hit;
+            L.st[AVR_S_TASK + AVR_T_SUCCESS] = succ;
+        }
+        SYNC();
+        const float *sp = L.st + AVR_S_FREE + AVR_FB_WORDS * m.spoon_free;
+        float ee_vel = len(ld3(sp + 7));
+        observe(m, L, spoon_force, obs + (size_t)env * AVR_OBS_DIM);
+        float prefs = m.w_velocity * (-ee_vel) + m.w_force_nontarget * (-robot_force) +
+                      m.w_high_forces * (spoon_force < 10.f ? 0.f : -spoon_force) + m.w_food_hit * hit_reward +
+                      m.w_food_velocities * (-mouth_vel);
+        float dist = len(sub(tgt, ld3(sp)));
+        float asq = 0.f;
+#pragma unroll
+        for (int i = 0; i < AVR_ACT_DIM; i++) asq += a_raw[i] * a_raw[i];
+        float r = m.w_distance * (-dist) + m.w_action * (-asq) + m.w_food * food_reward + prefs;
+        if (lane == 0) {
+            rew[env] = r;
+            int itn = (int)L.st[AVR_S_TASK + AVR_T_ITER];
+            done[env] = (unsigned char)(itn >= m.max_steps);
+            info[(size_t)env * AVR_INFO_DIM + 0] = robot_force + spoon_force;
+            info[(size_t)env * AVR_INFO_DIM + 1] = succ >= (float)m.n_food * m.task_success_threshold ? 1.f : 0.f;
+        }
+    }
+    SYNC();
+    // NaN guard + flags, then write the state back
+    bool bad = false;
+    for (int i = lane; i < AVR_STATE_WORDS; i += 64) bad |= !(L.st[i] == L.st[i]);
+    bad = __any(bad) || !ok;
+    if (lane == 0) {
+        int fl = (int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags | (bad ? 1 : 0);
+        L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)fl;
+    }
+    SYNC();
+    for (int i = lane; i < AVR_STATE_WORDS; i += 64) gst[i] = L.st[i];
+}
+
+__global__ void avr_random_actions_kernel(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_envs * AVR_ACT_DIM) return;
+    int e = i / AVR_ACT_DIM, j = i % AVR_ACT_DIM;
+    act[i] = j < n_arm ? philox_action(seed, env_offset + e, t, j) : 0.f;
+}
+
+// host-side launch helpers (used by avr_capi.hip)
+extern "C" hipError_t avr_launch_step(const KModel *m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
+                                      float *info, int mode, long long t, int n_envs, hipStream_t stream) {
+    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, *m, state, act, obs, rew, done, info, mode, t, n_envs);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
+                                                hipStream_t stream) {
+    int n = n_envs * AVR_ACT_DIM;
+    hipLaunchKernelGGL(avr_random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, seed, env_offset, t, act, n_envs, n_arm);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t avr_kernel_attrs(int *out4) {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, (const void *)avr_step_kernel);
+    if (e != hipSuccess) return e;
+    out4[0] = a.numRegs;
+    out4[1] = 0;
+    out4[2] = (int)a.sharedSizeBytes;
+    out4[3] = (int)a.localSizeBytes;
+    return hipSuccess;
+}
+
+extern "C" size_t avr_kmodel_size(void) { return sizeof(KModel); }

@@ -1,0 +1,58 @@
+// avr_kmodel.h -- device-side scene description (float copies of avr_model_desc) shared by the
+// step kernel and the C-ABI host code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../../include/avr_model.h"
+
+#define MAXL AVR_MAX_LINKS
+#define MAXD AVR_MAX_DOF
+#define MAXF AVR_MAX_FREE
+#define MAXB 64
+#define MAXSP 256
+#define MAXAP 256
+#define MAXNC 32
+#define MAXRS 64
+#define SMALL_NV 64
+#define GJK_MAX_IT 64
+#define GJK_REL_EPS 1e-6f
+#define EPA_MAX_IT 64
+#define EPA_MAX_V 64
+#define EPA_MAX_F 128
+#define EPA_EPS 1e-6f
+#define BT_BROADPHASE_EXPAND 0.02f
+#define BT_DENOM_EPS 1e-12f
+#define BT_ANGULAR_MOTION_THRESHOLD (0.5f * 1.5707963267948966f)
+#define BIGF 1e30f
+
+
+struct KModel {
+    int nl, nd, nf, nb, ns, np, nh;
+    const int *rl_parent, *rl_jtype, *rl_dof, *rl_has_limit;
+    const float *rl_jorig;    // [nl][8] p3 q4 pad
+    const float *rl_com;      // [nl][8]
+    const float *rl_axis;     // [nl][4]
+    const float *rl_inertia;  // [nl][4]
+    const float *rl_mass, *rl_lower, *rl_upper;
+    float base[8];
+    const float *fb_mass, *fb_inertia, *fb_gravity;   // [nf], [nf][4], [nf][4]
+    const float *st_pose;                             // [nst][8]
+    const int *body_kind, *body_index, *body_shape_start, *body_shape_count, *body_flags;
+    const float *body_friction, *body_threshold, *body_aabb;   // [nb][12]
+    const int *shape_kind, *shape_body, *shape_gender, *shape_hull;   // hull [ns][4]
+    const float *shape_pose, *shape_param, *shape_margin, *shape_aabb; // [ns][8] [ns][4] [ns] [ns][8]
+    const float4 *hull_verts;
+    const int *pair_a, *pair_b;
+    int n_arm, arm_dofs[8], n_finger, finger_dofs[4];
+    int tool_link, torso_link, head_slot, spoon_free, bowl_free, food_free0, n_food;
+    int table_body, bowl_body, spoon_body, food_body0, tool_body;
+    float tool_offset[8], mouth[2][4], arm_lower[8], arm_upper[8];
+    float time_step;
+    int nsub, frame_skip, iters, max_steps;
+    float erp, warmstart, lin_damp, ang_damp, max_vel, robot_gain, robot_force, fixed_max_imp;
+    float w_distance, w_action, w_food, w_velocity, w_force_nontarget, w_high_forces, w_food_hit,
+        w_food_velocities, task_success_threshold;
+    unsigned long long seed;
+    int env_offset;
+    int dof_link[MAXD];        // link owning each DoF
+    unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+};

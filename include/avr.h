@@ -1,0 +1,90 @@
+/* avr.h -- C-ABI of libavr.so, the MI355X-native replacement for the PyBullet calls on the
+ * Assistive Gym step path.
+ *
+ * The reference reaches its physics through the PyBullet module API, one DIRECT client per env
+ * (env.py:23).  One `env.step(a)` of FeedingJaco-v0 issues ~68 PyBullet calls:
+ *   p.getJointStates            env.py:320-321, 393; feeding.py:126
+ *   p.setJointMotorControlArray env.py:335-337
+ *   p.stepSimulation  x5        env.py:342        (2 Bullet sub-steps each, feeding.py:289)
+ *   p.getLinkState / multiplyTransforms / resetBasePositionAndOrientation
+ *                               feeding.py:345-349 (update_targets), 124, 134
+ *   p.getContactPoints          feeding.py:86-89, 111, 116
+ *   p.getBasePositionAndOrientation / getBaseVelocity
+ *                               feeding.py:59, 65, 100, 106, 125
+ * avr_step() replaces that whole sequence for a batch of envs with one call; the task glue
+ * (take_step env.py:274-351, get_total_force feeding.py:83-90, get_food_rewards :92-121,
+ * _get_obs :123-142, reward :56-77, human_preferences env.py:412-448) is fused into the same
+ * device launch.  The Python facade (assistive-vr-gym_amd/avr/env.py) keeps the gym
+ * reset/step/observation/reward contract on top of this ABI.
+ *
+ * Conventions: every function returns 0 on success and a negative code on error; the message is
+ * available from avr_last_error(sim).  A handle owns one HIP stream on one device and is not
+ * thread-safe.  Host-pointer calls block until outputs are on the host; *_device calls take
+ * device pointers and are asynchronous on avr_stream(sim).
+ */
+#ifndef AVR_H
+#define AVR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "avr_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVR_ABI_VERSION 1
+
+typedef struct avr_config {
+    int32_t n_envs;        /* envs owned by this handle (one GPU)                          */
+    int32_t device;        /* HIP device ordinal                                           */
+    int32_t env_offset;    /* global id of local env 0 (keys per-env RNG; sharding-stable)  */
+    int32_t flags;         /* reserved, 0                                                  */
+    uint64_t seed;         /* action RNG seed for avr_step_random (env.py:53 uses 1001)     */
+} avr_config;
+
+typedef struct avr_sim avr_sim;
+
+/* Create a handle: copies the compiled scene to the device.  (replaces p.connect + the
+ * loadURDF/createMultiBody/createConstraint scene build of world_creation.py:27-93) */
+int avr_create(const avr_config *cfg, const avr_model_desc *model, avr_sim **out);
+int avr_destroy(avr_sim *sim);
+
+/* Per-env state blocks (n_envs x AVR_STATE_WORDS floats, layout in avr_model.h).
+ * (replaces resetJointState / resetBasePositionAndOrientation of the reset path) */
+int avr_set_state(avr_sim *sim, const float *host_state);
+int avr_get_state(avr_sim *sim, float *host_state);
+/* Set the state of the envs whose mask byte is non-zero (auto-reset of finished episodes). */
+int avr_set_state_masked(avr_sim *sim, const uint8_t *env_mask, const float *host_state);
+
+/* n_frames x p.stepSimulation with the motors as they are, no task glue, then the reset
+ * observation (feeding.py:319-320, 325).  obs may be NULL. */
+int avr_settle(avr_sim *sim, int32_t n_frames, float *host_obs);
+
+/* One gym step for every env: act[n_envs*7] -> obs[n_envs*25], rew[n_envs],
+ * done[n_envs] (TimeLimit 200), info[n_envs*2] = {total_force_on_human, task_success}. */
+int avr_step(avr_sim *sim, const float *act, float *obs, float *rew, uint8_t *done, float *info);
+int avr_step_device(avr_sim *sim, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
+/* Same, with synthetic actions a[e,t] ~ U(-1,1)^7 drawn on the device from Philox4x32-10
+ * keyed by (seed, env_offset + e, t) -- examples/random_actions.py semantics. */
+int avr_step_random_device(avr_sim *sim, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
+/* Device actions for inspection: d_act[n_envs*7] for step t (same Philox stream). */
+int avr_random_actions_device(avr_sim *sim, int64_t t, float *d_act);
+
+/* One Bullet sub-step of length dt for every env, no task glue (known-answer tests). */
+int avr_substep(avr_sim *sim, float dt);
+
+int avr_sync(avr_sim *sim);
+void *avr_stream(avr_sim *sim);
+void *avr_state_device_ptr(avr_sim *sim);
+int32_t avr_n_envs(avr_sim *sim);
+int32_t avr_state_words(void);
+int32_t avr_abi_version(void);
+/* Kernel resource usage: [vgprs, sgprs, lds_bytes, scratch_bytes] of the step kernel. */
+int avr_kernel_info(avr_sim *sim, int32_t *out4);
+const char *avr_last_error(avr_sim *sim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
