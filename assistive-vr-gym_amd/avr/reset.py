@@ -259,3 +259,168 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='none'):
         S[k], m = feeding_reset_state(A, md, seed, e, gender=g, impairment=impairment)
         meta.append(m)
     return S, meta
+
+
+# ----------------------------------------------------------------------------- batched reset
+def _qmul(a, b):
+    ax, ay, az, aw = a[..., 0], a[..., 1], a[..., 2], a[..., 3]
+    bx, by, bz, bw = b[..., 0], b[..., 1], b[..., 2], b[..., 3]
+    return np.stack([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz], -1)
+
+
+def _cross(a, b):
+    return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1], a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
+                     a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
+
+
+def _qrot(q, v):
+    u = q[..., :3]
+    t = 2.0 * _cross(u, v)
+    return v + q[..., 3:4] * t + _cross(u, t)
+
+
+def _qaxis(axis, ang):
+    s = np.sin(0.5 * ang)[..., None]
+    return np.concatenate([axis * s, np.cos(0.5 * ang)[..., None]], -1)
+
+
+def robot_fk_batch(A, Q):
+    """Vectorised robot_fk over envs: Q (N, ndof) -> COM pos/quat, joint axes/origins (N, nl, .)."""
+    N = Q.shape[0]
+    nl = int(A['n_links'])
+    bp = np.broadcast_to(A['robot_base'][:3], (N, 3))
+    bq = np.broadcast_to(A['robot_base'][3:], (N, 4))
+    LP = np.zeros((N, nl, 3)); LQ = np.zeros((N, nl, 4))
+    CP = np.zeros((N, nl, 3)); CQ = np.zeros((N, nl, 4))
+    AX = np.zeros((N, nl, 3)); OR = np.zeros((N, nl, 3))
+    for i in range(nl):
+        p = A['rl_parent'][i]
+        pp, pq = (bp, bq) if p < 0 else (LP[:, p], LQ[:, p])
+        tp = pp + _qrot(pq, np.broadcast_to(A['rl_jpos'][i], (N, 3)))
+        tq = _qmul(pq, np.broadcast_to(A['rl_jquat'][i], (N, 4)))
+        OR[:, i] = tp
+        AX[:, i] = _qrot(tq, np.broadcast_to(A['rl_axis'][i], (N, 3)))
+        dof = A['rl_dof'][i]
+        if A['rl_jtype'][i] == 1:
+            tq = _qmul(tq, _qaxis(np.broadcast_to(A['rl_axis'][i], (N, 3)), Q[:, dof]))
+        LP[:, i], LQ[:, i] = tp, tq
+        CP[:, i] = tp + _qrot(tq, np.broadcast_to(A['rl_com_pos'][i], (N, 3)))
+        CQ[:, i] = _qmul(tq, np.broadcast_to(A['rl_com_quat'][i], (N, 4)))
+    return CP, CQ, AX, OR
+
+
+def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, restarts=40, tol=0.01):
+    """Vectorised DLS IK (same acceptance rule as `ik`), one random restart per round for every
+    env that has not converged yet."""
+    N = tpos.shape[0]
+    chain = _chain(A, link)
+    cols = []
+    for dof in arm_dofs:
+        l = [k for k in chain if A['rl_dof'][k] == dof]
+        cols.append(l[0] if l else -1)
+    done = np.zeros(N, bool)
+    Qout = np.repeat(q0[None], N, 0)
+    for r in range(restarts):
+        idx = np.nonzero(~done)[0]
+        if len(idx) == 0:
+            break
+        Q = np.repeat(q0[None], len(idx), 0)
+        Q[:, arm_dofs] = np.stack([rngs[i].uniform(lower, upper) for i in idx])
+        tp, tq = tpos[idx], tquat[idx]
+        for it in range(iters):
+            CP, CQ, AX, OR = robot_fk_batch(A, Q)
+            ep = tp - CP[:, link]
+            dq = _qmul(tq, CQ[:, link] * np.array([-1, -1, -1, 1.0]))
+            dq = np.where(dq[:, 3:4] < 0, -dq, dq)
+            s = np.linalg.norm(dq[:, :3], axis=1)
+            ang = 2.0 * np.arctan2(s, dq[:, 3])
+            er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
+            err = np.concatenate([ep, er], 1)
+            if it % 10 == 9 and np.all(np.linalg.norm(ep, axis=1) < 1e-5) and np.all(np.linalg.norm(er, axis=1) < 1e-4):
+                break
+            J = np.zeros((len(idx), 6, len(arm_dofs)))
+            for c, l in enumerate(cols):
+                if l < 0:
+                    continue
+                J[:, :3, c] = _cross(AX[:, l], CP[:, link] - OR[:, l])
+                J[:, 3:, c] = AX[:, l]
+            JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
+            step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, err[..., None])
+            Q[:, arm_dofs] = np.clip(Q[:, arm_dofs] + step[..., 0], lower, upper)
+        CP, CQ, _, _ = robot_fk_batch(A, Q)
+        pe = np.linalg.norm(tp - CP[:, link], axis=1)
+        qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))
+        for k, e in enumerate(idx):
+            if r == restarts - 1 and not done[e]:
+                Qout[e] = Q[k]
+            if pe[k] < tol and qe[k] < tol and table_clear(A, Q[k]):
+                Qout[e] = Q[k]
+                done[e] = True
+    return Qout, done
+
+
+def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none'):
+    """Vectorised equivalent of batch_reset_states (same per-env draws and acceptance rules,
+    IK batched across envs)."""
+    env_ids = list(env_ids)
+    N = len(env_ids)
+    rngs = [np.random.default_rng([int(seed), int(e)]) for e in env_ids]
+    S = np.zeros((N, ABI.STATE_WORDS))
+    gl, tpos, bowl = [], np.zeros((N, 3)), np.zeros((N, 3))
+    for k in range(N):
+        rng = rngs[k]
+        g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
+        gl.append(g)
+        ls = rng.uniform(0.5, 1.0) if impairment == 'limits' else 1.0
+        qh = human_joint_angles(A, g, rng, ls)
+        S[k, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, g, qh).ravel()
+        bowl[k] = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
+        tpos[k] = bowl[k] + np.array([0, -0.1, 0.4]) + rng.uniform(-0.05, 0.05, size=3)
+    tq = np.repeat(G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])[None], N, 0)
+    arm = md.arm_dofs
+    lower = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
+    upper = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
+    q0 = np.zeros(int(A['n_dof']))
+    for d in md.finger_dofs:
+        q0[d] = md.params['finger_target']
+    tool = int(A['task_tool_link'])
+    Q, ok = ik_batch(A, tool, tpos, tq, arm, lower, upper, rngs, q0)
+    CP, CQ, _, _ = robot_fk_batch(A, Q)
+    off = A['task_tool_offset']
+    meta = []
+    for k in range(N):
+        st = S[k]
+        st[ABI.S_Q:ABI.S_Q + Q.shape[1]] = Q[k]
+        for d in arm:
+            st[ABI.S_KP + d] = 0.0
+            st[ABI.S_QTGT + d] = 0.0
+            st[ABI.S_MAXIMP + d] = md.params['default_motor_impulse']
+        for d in md.finger_dofs:
+            st[ABI.S_KP + d] = md.params['finger_gain']
+            st[ABI.S_QTGT + d] = md.params['finger_target']
+            st[ABI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+        sp, sq = G.tf_mul(CP[k, tool], CQ[k, tool], off[:3], off[3:])
+        st[ABI.S_FREE:ABI.S_FREE + 3] = sp
+        st[ABI.S_FREE + 3:ABI.S_FREE + 7] = sq
+        b = ABI.S_FREE + ABI.FB_WORDS
+        st[b:b + 3] = bowl[k]
+        st[b + 3:b + 7] = G.quat_from_euler([np.pi / 2.0, 0, 0])
+        r = 0.005
+        n = 0
+        for i in range(2):
+            for j in range(2):
+                for kk in range(2):
+                    f = ABI.S_FREE + ABI.FB_WORDS * (2 + n)
+                    st[f:f + 3] = np.array([i * 2 * r - 0.005, j * 2 * r, kk * 2 * r + 0.02]) + sp
+                    st[f + 3:f + 7] = [0, 0, 0, 1]
+                    n += 1
+        t = ABI.S_TASK
+        gi = 0 if gl[k] == 'male' else 1
+        head = st[ABI.S_HUMAN + 7 * int(A['task_head_slot']):][:7]
+        mouth = A['task_mouth_male'] if gi == 0 else A['task_mouth_female']
+        st[t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
+        st[t + ABI.T_ALIVE] = (1 << 8) - 1
+        st[t + ABI.T_GENDER] = gi
+        meta.append(dict(gender=gl[k], ik_ok=bool(ok[k]), bowl_pos=bowl[k], target_pos=tpos[k]))
+    return S, meta

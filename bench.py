@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: FeedingJaco-v0 env-steps/s on MI355X (BASELINE.json configs[1]).
+
+One "step" = one gym step of every env (take_step + 5 x stepSimulation x 2 sub-steps + task
+glue) = one launch of the gfx950 step kernel.  Synthetic random actions are drawn on the device
+(Philox4x32-10 keyed by (seed=1001, global env id, step), examples/random_actions.py semantics).
+Inputs are resident in HBM before the timed region; host buffers are not touched inside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E_per_gpu]
+  torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Multi-GPU: envs shard across ranks (global env id = rank*E + e, independent units -> weak
+scaling); rollouts (obs, reward, done, info) are collected with an RCCL all-gather over xGMI
+every --gather-every steps (the only data-path collective).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd'))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes_per_env_step(ABI):
+    """Bytes the step must move per env per gym step: the per-env state block read once and
+    written once (it stays in LDS across the 10 sub-steps), plus the I/O (actions are generated
+    on the device; obs 25 f32, reward f32, done u8, info 2 f32 written)."""
+    state = ABI.STATE_WORDS * 4
+    io_out = (ABI.OBS_DIM + 1 + ABI.INFO_DIM) * 4 + 1
+    return 2 * state + io_out
+
+
+def cpu_baseline(md, A, RS, seconds, threads):
+    """Oracle (the CPU restatement, fp64) on the host cores; bounded sample."""
+    import numpy as np
+    from oracle.oracle import Oracle
+    from avr import _lib
+    n = max(threads * 2, 8)
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)))
+    o = Oracle(md, n)
+    o.set_threads(threads)
+    o.set_state(S)
+    o.settle(100)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        a = _lib.random_actions(1001, np.arange(n), steps)
+        o.step(a)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and steps >= 2:
+            break
+    return dict(value=n * steps / el, unit='env-steps/s', cores=threads, kind='port',
+                sample='FeedingJaco-v0, %d envs x %d gym steps (%.1f s) after a 100-frame settle; fp64 oracle, OpenMP over envs' % (n, steps, el))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    ap.add_argument('--settle', type=int, default=100)
+    ap.add_argument('--gather-every', type=int, default=16)
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--reset-pool', type=int, default=1024,
+                    help='distinct host reset states, tiled over the envs (IK is host-side)')
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from avr import _abi as ABI, reset as RS, _lib
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+
+    A = ABI.load_scene()
+    md = ABI.ModelDesc(A)
+    E = args.envs
+    # reset pool: distinct initial states for global env ids; tiled if pool < E
+    pool = min(args.reset_pool, E)
+    base_id = rank * E
+    S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)])
+    S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
+    sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
+    sim.set_state(S.astype(np.float32))
+    sim.settle(args.settle)
+
+    obs = torch.zeros(E, ABI.OBS_DIM, device=dev)
+    rew = torch.zeros(E, device=dev)
+    done = torch.zeros(E, dtype=torch.uint8, device=dev)
+    info = torch.zeros(E, ABI.INFO_DIM, device=dev)
+    ext = torch.cuda.ExternalStream(sim.stream(), device=dev)
+    G = args.gather_every
+    roll = torch.zeros(G, E, ABI.OBS_DIM + 1 + ABI.INFO_DIM + 1, device=dev)
+    gathered = torch.zeros(world * G * E * roll.shape[-1], device=dev) if world > 1 else None
+
+    def one_step(t, k):
+        sim.step_random_device(t, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr())
+        if world > 1:
+            with torch.cuda.stream(ext):
+                j = k % G
+                roll[j, :, :ABI.OBS_DIM] = obs
+                roll[j, :, ABI.OBS_DIM] = rew
+                roll[j, :, ABI.OBS_DIM + 1:ABI.OBS_DIM + 1 + ABI.INFO_DIM] = info
+                roll[j, :, -1] = done.float()
+                if j == G - 1:
+                    dist.all_gather_into_tensor(gathered, roll.reshape(-1))
+
+    for w in range(args.warmup):
+        one_step(w, w)
+    sim.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for k in range(args.steps):
+        one_step(args.warmup + k, k)
+    ev1.record(ext)
+    sim.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    St = sim.get_state()
+    flags = St[:, ABI.S_TASK + ABI.T_FLAGS].astype(np.int64)
+    value = world * E * args.steps / el
+    bpe = algorithmic_bytes_per_env_step(ABI)
+    achieved = bpe * E / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get('envs') == E:
+                traffic = tj.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    out = {
+        'metric': 'env-steps/sec at N parallel envs, 1/2/4/8 MI355X; max |dq| vs PyBullet',
+        'value': value,
+        'unit': 'env-steps/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': el / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the host IK path (%d distinct per GPU, tiled)' % pool,
+        'config': {'workload': 'FeedingJaco-v0, %d envs/GPU, rigid-only, random actions' % E, 'envs_per_gpu': E,
+                   'global_envs': world * E, 'substeps_per_env_step': 10, 'solver_iterations': 10,
+                   'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None},
+        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'bytes_per_env_step': bpe, 'kernel_ms': kern_ms},
+        'nan_or_overflow_envs': int(np.count_nonzero(flags)),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+        threads = max(1, min(threads, 16))
+        out['cpu_baseline'] = cpu_baseline(md, A, RS, args.cpu_seconds, threads)
+    elif rank == 0:
+        out['cpu_baseline'] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -21,6 +21,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/avr_model.h"
 
@@ -158,6 +161,7 @@ typedef struct {
     int nsp;
     int gender;
     real oldcp[AVR_MAX_CONTACTS * AVR_CP_WORDS];
+    long long stats_gjk, stats_epa, stats_rows;
 } ws_t;
 
 typedef struct avr_oracle {
@@ -166,7 +170,7 @@ typedef struct avr_oracle {
     real *state;         /* n_envs * AVR_STATE_WORDS */
     ws_t *ws;
     char err[256];
-    long long stats_gjk, stats_epa, stats_rows;
+    int threads;
 } avr_oracle;
 
 /* ---------------------------------------------------------------- kinematics */
@@ -610,7 +614,7 @@ static int epa(const wshape *A, const wshape *B, simplex *S, v3 *normal_out, rea
 
 /* ---------------------------------------------------------------- narrowphase */
 /* returns 1 and (normalOnB, pointOnB, distance) if a contact within `thr` exists */
-static int narrowphase(avr_oracle *o, const wshape *A, const wshape *B, real thr, v3 *nB, v3 *pB, real *dist) {
+static int narrowphase(ws_t *o, const wshape *A, const wshape *B, real thr, v3 *nB, v3 *pB, real *dist) {
     int ka = A->kind, kb = B->kind;
     if (ka == AVR_SPHERE && kb == AVR_SPHERE) {               /* btSphereSphereCollisionAlgorithm */
         v3 diff = sub(A->t.p, B->t.p);
@@ -1166,7 +1170,7 @@ static void collide(avr_oracle *o, real *st, ws_t *w) {
         wshape A = make_wshape(m, sa, w->body[ba]), B = make_wshape(m, sb, w->body[bb]);
         v3 nB, pB;
         real d;
-        if (narrowphase(o, &A, &B, thr, &nB, &pB, &d)) manifold_add(&M, sa, sb, p, w->body[ba], w->body[bb], nB, pB, d, thr);
+        if (narrowphase(w, &A, &B, thr, &nB, &pB, &d)) manifold_add(&M, sa, sb, p, w->body[ba], w->body[bb], nB, pB, d, thr);
         manifold_refresh(&M, w->body[ba], w->body[bb], thr);
         for (int k = 0; k < M.n; k++) {
             if (nnew >= AVR_MAX_CONTACTS) { st[AVR_S_TASK + AVR_T_FLAGS] = (real)((int)st[AVR_S_TASK + AVR_T_FLAGS] | 2); break; }
@@ -1214,7 +1218,7 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
     w->nrows = w->n_nc = w->n_nrm = w->n_fr = 0;
     build_noncontact_rows(m, st, w, dt);
     build_contact_rows(m, st, w, dt);
-    o->stats_rows += w->nrows;
+    w->stats_rows += w->nrows;
     solve(m, w);
     for (int j = 0; j < w->n_nrm; j++) {
         row_t *r = &w->rows[w->nrm_idx[j]];
@@ -1433,6 +1437,7 @@ EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **o
     for (int i = 0; i < 3 * d->n_hull_verts; i++) m->hv[i] = R(d->hull_verts[i]);
     m->hp = 0;
     o->n_envs = n_envs;
+    o->threads = 1;
     o->state = (real *)calloc((size_t)n_envs * AVR_STATE_WORDS, sizeof(real));
     o->ws = (ws_t *)calloc((size_t)n_envs, sizeof(ws_t));
     *out = o;
@@ -1491,11 +1496,15 @@ EXPORT int avr_oracle_settle(avr_oracle *o, int n_frames, float *obs) {
 }
 
 EXPORT int avr_oracle_step(avr_oracle *o, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
+    int bad = -1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(o->threads) if (o->threads > 1)
     for (int e = 0; e < o->n_envs; e++)
-        if (env_step(o, e, act + (size_t)e * AVR_ACT_DIM, obs + (size_t)e * AVR_OBS_DIM, rew + e, done + e, info + (size_t)e * AVR_INFO_DIM)) {
-            snprintf(o->err, sizeof(o->err), "env %d: mass matrix not positive definite", e);
-            return -1;
-        }
+        if (env_step(o, e, act + (size_t)e * AVR_ACT_DIM, obs + (size_t)e * AVR_OBS_DIM, rew + e, done + e, info + (size_t)e * AVR_INFO_DIM))
+            bad = e;
+    if (bad >= 0) {
+        snprintf(o->err, sizeof(o->err), "env %d: mass matrix not positive definite", bad);
+        return -1;
+    }
     return 0;
 }
 
@@ -1510,8 +1519,12 @@ EXPORT int avr_oracle_substep(avr_oracle *o, double dt) {
 }
 
 EXPORT void avr_oracle_stats(avr_oracle *o, long long *out3) {
-    out3[0] = o->stats_gjk; out3[1] = o->stats_epa; out3[2] = o->stats_rows;
+    out3[0] = out3[1] = out3[2] = 0;
+    for (int e = 0; e < o->n_envs; e++) { out3[0] += o->ws[e].stats_gjk; out3[1] += o->ws[e].stats_epa; out3[2] += o->ws[e].stats_rows; }
 }
+
+/* threads used by avr_oracle_step / avr_oracle_settle (OpenMP over envs; 1 = serial) */
+EXPORT void avr_oracle_set_threads(avr_oracle *o, int n) { o->threads = n > 0 ? n : 1; }
 
 /* geometry query for tests: narrowphase between shapes sa (on body pose pa[7]) and sb (pb[7]) */
 EXPORT int avr_oracle_narrowphase(avr_oracle *o, int sa, const double *pa, int sb, const double *pb, double thr, double *out7) {
@@ -1519,7 +1532,7 @@ EXPORT int avr_oracle_narrowphase(avr_oracle *o, int sa, const double *pa, int s
     wshape A = make_wshape(&o->m, sa, ta), B = make_wshape(&o->m, sb, tb);
     v3 n, p;
     real d;
-    int r = narrowphase(o, &A, &B, R(thr), &n, &p, &d);
+    int r = narrowphase(&o->ws[0], &A, &B, R(thr), &n, &p, &d);
     out7[0] = n.x; out7[1] = n.y; out7[2] = n.z; out7[3] = p.x; out7[4] = p.y; out7[5] = p.z; out7[6] = d;
     return r;
 }

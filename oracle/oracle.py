@@ -35,6 +35,7 @@ def _load(precision):
     lib.avr_oracle_stats.argtypes = [vp, vp]
     lib.avr_oracle_narrowphase.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_double, vp]
     lib.avr_oracle_robot_fk.argtypes = [vp, C.c_int, vp]
+    lib.avr_oracle_set_threads.argtypes = [vp, C.c_int]
     lib.avr_oracle_last_error.argtypes = [vp]
     lib.avr_oracle_last_error.restype = C.c_char_p
     lib.avr_oracle_state_words.restype = C.c_int
@@ -61,6 +62,9 @@ class Oracle:
             raise RuntimeError('avr_oracle_create failed: %d' % rc)
         self.h = h
         self.words = self.lib.avr_oracle_state_words()
+
+    def set_threads(self, n):
+        self.lib.avr_oracle_set_threads(self.h, int(n))
 
     def close(self):
         if self.h:
