@@ -35,6 +35,12 @@ def load(path=LIB_PATH):
         return _LIB
     if not os.path.exists(path):
         raise RuntimeError('libavr.so not built (%s); run __graft_entry__.build()' % path)
+    # One HIP runtime per process: if torch is importable, let it load its libamdhip64 first so
+    # libavr binds to the same runtime (device pointers from torch tensors stay valid here).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     lib = C.CDLL(path)
     vp = C.c_void_p
     lib.avr_create.argtypes = [C.POINTER(avr_config), vp, C.POINTER(vp)]

@@ -22,7 +22,8 @@ extern "C" hipError_t avr_kernel_attrs(int *out4);
 
 struct avr_sim {
     avr_config cfg;
-    KModel km;
+    KModel km;          // host copy
+    KModel *d_km;       // device copy (the kernel reads the scene description through it)
     hipStream_t stream;
     std::vector<void *> allocs;
     float *d_state;
@@ -188,6 +189,8 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int q = l; q >= 0; q = d->rl_parent[q]) mask |= 1u << q;
         k.anc_mask[l] = mask;
     }
+    HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
+    HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
     size_t E = (size_t)cfg->n_envs;
     HIPCHK(s, hipMalloc(&s->d_state, E * AVR_STATE_WORDS * sizeof(float)));
     HIPCHK(s, hipMemset(s->d_state, 0, E * AVR_STATE_WORDS * sizeof(float)));
@@ -204,6 +207,7 @@ extern "C" int avr_destroy(avr_sim *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void *p : s->allocs) (void)hipFree(p);
     if (s->d_state) (void)hipFree(s->d_state);
+    if (s->d_km) (void)hipFree(s->d_km);
     if (s->d_act) (void)hipFree(s->d_act);
     if (s->d_obs) (void)hipFree(s->d_obs);
     if (s->d_rew) (void)hipFree(s->d_rew);
@@ -247,7 +251,7 @@ extern "C" int avr_get_state(avr_sim *s, float *h) {
 
 extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 2, n_frames, s->cfg.n_envs, s->stream));
     if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
@@ -257,20 +261,20 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 3, t, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 3, t, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, 0, 0, s->cfg.n_envs, s->stream));
     return 0;
 }
 
 extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
                               d_info ? d_info : s->d_info, 1, t, s->cfg.n_envs, s->stream));
     return 0;
 }
@@ -285,7 +289,7 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
     HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, 0, 0, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));
@@ -297,6 +301,14 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
 extern "C" int avr_sync(avr_sim *s) {
     CHECK_SIM(s);
     HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+// Diagnostic builds (-DAVR_PROF): attach a device buffer [n_envs][16] of per-phase cycle counters.
+extern "C" int avr_set_profile_buffer(avr_sim *s, void *d_prof) {
+    CHECK_SIM(s);
+    s->km.prof = (unsigned long long *)d_prof;
+    HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
     return 0;
 }
 

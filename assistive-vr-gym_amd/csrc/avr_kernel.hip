@@ -57,6 +57,9 @@ struct EnvLDS {
     float h[MAXD], qdd[MAXD];
     float rn[6][MAXL][4];   // RNEA temporaries: omega, v_com, alpha, a_com, F, N
     int nsp, nap, n_nc, n_c, n_rs, flags, gender, pad;
+#ifdef AVR_PROF
+    unsigned long long prof[16];
+#endif
     union {
         struct {
             int sp_a[MAXSP], sp_b[MAXSP], sp_pair[MAXSP];
@@ -78,6 +81,16 @@ struct EnvLDS {
 };
 
 #define SYNC() __syncthreads()
+
+// Diagnostic phase timers (separate AVR_PROF build only; the shipped kernel has none).
+#ifdef AVR_PROF
+#define PROF_START(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_STOP(slot, v) \
+    do { unsigned long long _n = __builtin_amdgcn_s_memtime(); if (lane_id() == 0) L.prof[slot] += _n - (v); v = _n; } while (0)
+#else
+#define PROF_START(v) (void)0
+#define PROF_STOP(slot, v) (void)0
+#endif
 
 // --------------------------------------------------------------------------- kinematics
 // robot_fk: serial recursion over the (DFS-ordered) links on lane 0, frames published in LDS.
@@ -321,41 +334,76 @@ struct Simplex { v3 w[4], a[4], b[4]; int n; };
 
 AVR_DI void sx_copy(Simplex &S, int dst, int src) { S.w[dst] = S.w[src]; S.a[dst] = S.a[src]; S.b[dst] = S.b[src]; }
 
-AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]);
-
-AVR_DI int tri_closest(Simplex &S, v3 &vout, float lam[4]) {
-    v3 A = S.w[0], B = S.w[1], C = S.w[2];
+// Closest point of triangle ABC to the origin (Ericson 5.1.5).  used: bit mask of the vertices
+// spanning the closest feature (1=A 2=B 4=C); l*: barycentric weights.
+AVR_DI v3 tri_cp(v3 A, v3 B, v3 C, int &used, float &la, float &lb, float &lc) {
     v3 ab = sub(B, A), ac = sub(C, A), ap = scl(A, -1.f);
     float d1 = dot(ab, ap), d2 = dot(ac, ap);
-    if (d1 <= 0.f && d2 <= 0.f) { S.n = 1; lam[0] = 1.f; vout = A; return 0; }
+    la = lb = lc = 0.f;
+    if (d1 <= 0.f && d2 <= 0.f) { used = 1; la = 1.f; return A; }
     v3 bp = scl(B, -1.f);
     float d3 = dot(ab, bp), d4 = dot(ac, bp);
-    if (d3 >= 0.f && d4 <= d3) { sx_copy(S, 0, 1); S.n = 1; lam[0] = 1.f; vout = B; return 0; }
+    if (d3 >= 0.f && d4 <= d3) { used = 2; lb = 1.f; return B; }
     float vc = d1 * d4 - d3 * d2;
     if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
         float v = d1 / (d1 - d3);
-        S.n = 2; lam[0] = 1.f - v; lam[1] = v; vout = add(A, scl(ab, v)); return 0;
+        used = 3; la = 1.f - v; lb = v; return add(A, scl(ab, v));
     }
     v3 cp = scl(C, -1.f);
     float d5 = dot(ab, cp), d6 = dot(ac, cp);
-    if (d6 >= 0.f && d5 <= d6) { sx_copy(S, 0, 2); S.n = 1; lam[0] = 1.f; vout = C; return 0; }
+    if (d6 >= 0.f && d5 <= d6) { used = 4; lc = 1.f; return C; }
     float vb = d5 * d2 - d1 * d6;
     if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
         float wv = d2 / (d2 - d6);
-        sx_copy(S, 1, 2); S.n = 2;
-        lam[0] = 1.f - wv; lam[1] = wv; vout = add(A, scl(ac, wv)); return 0;
+        used = 5; la = 1.f - wv; lc = wv; return add(A, scl(ac, wv));
     }
     float va = d3 * d6 - d5 * d4;
     if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
         float wv = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        sx_copy(S, 0, 1); sx_copy(S, 1, 2); S.n = 2;
-        lam[0] = 1.f - wv; lam[1] = wv; vout = add(B, scl(sub(C, B), wv)); return 0;
+        used = 6; lb = 1.f - wv; lc = wv; return add(B, scl(sub(C, B), wv));
     }
     float den = 1.f / (va + vb + vc);
     float v = vb * den, wv = vc * den;
-    lam[0] = 1.f - v - wv; lam[1] = v; lam[2] = wv;
-    vout = add(A, add(scl(ab, v), scl(ac, wv)));
+    used = 7; la = 1.f - v - wv; lb = v; lc = wv;
+    return add(A, add(scl(ab, v), scl(ac, wv)));
+}
+
+// keep the vertices of slots 0..2 selected by `used`, compacted in order; lam in slot order
+AVR_DI void tri_compact(Simplex &S, int used, float la, float lb, float lc, float lam[4]) {
+    switch (used) {
+    case 1: S.n = 1; lam[0] = la; break;
+    case 2: sx_copy(S, 0, 1); S.n = 1; lam[0] = lb; break;
+    case 4: sx_copy(S, 0, 2); S.n = 1; lam[0] = lc; break;
+    case 3: S.n = 2; lam[0] = la; lam[1] = lb; break;
+    case 5: sx_copy(S, 1, 2); S.n = 2; lam[0] = la; lam[1] = lc; break;
+    case 6: sx_copy(S, 0, 1); sx_copy(S, 1, 2); S.n = 2; lam[0] = lb; lam[1] = lc; break;
+    default: S.n = 3; lam[0] = la; lam[1] = lb; lam[2] = lc; break;
+    }
+}
+
+AVR_DI int tri_closest(Simplex &S, v3 &vout, float lam[4]) {
+    int used;
+    float la, lb, lc;
+    vout = tri_cp(S.w[0], S.w[1], S.w[2], used, la, lb, lc);
+    tri_compact(S, used, la, lb, lc, lam);
     return 0;
+}
+
+// one face (i0,i1,i2) of the tetrahedron, opposite vertex i3 (literal indices at every call)
+AVR_DI void tetra_face(const Simplex &S, int f, int i0, int i1, int i2, int i3, bool &outside_any, float &best, int &bf, int &bused,
+                       float &bla, float &blb, float &blc, v3 &bestv) {
+    v3 A = S.w[i0], B = S.w[i1], C = S.w[i2], D = S.w[i3];
+    v3 n = crs(sub(B, A), sub(C, A));
+    float sp = dot(scl(A, -1.f), n), sd = dot(sub(D, A), n);
+    if (sd * sd < 1e-30f) return;
+    if (sp * sd < 0.f) {
+        outside_any = true;
+        int used;
+        float la, lb, lc;
+        v3 v = tri_cp(A, B, C, used, la, lb, lc);
+        float d2 = len2(v);
+        if (d2 < best) { best = d2; bf = f; bused = used; bla = la; blb = lb; blc = lc; bestv = v; }
+    }
 }
 
 AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
@@ -371,33 +419,30 @@ AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
         return 0;
     }
     if (S.n == 3) return tri_closest(S, vout, lam);
-    const int F[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
     float best = BIGF;
-    Simplex bestS;
-    bestS.n = 0;
-    float bestL[4] = {0, 0, 0, 0};
+    int bf = -1, bused = 0;
+    float bla = 0.f, blb = 0.f, blc = 0.f;
     v3 bestv = V(0, 0, 0);
     bool outside_any = false;
-    for (int f = 0; f < 4; f++) {
-        v3 A = S.w[F[f][0]], B = S.w[F[f][1]], C = S.w[F[f][2]], D = S.w[F[f][3]];
-        v3 n = crs(sub(B, A), sub(C, A));
-        float sp = dot(scl(A, -1.f), n), sd = dot(sub(D, A), n);
-        if (sd * sd < 1e-30f) continue;
-        if (sp * sd < 0.f) {
-            outside_any = true;
-            Simplex T;
-            for (int k = 0; k < 3; k++) { T.w[k] = S.w[F[f][k]]; T.a[k] = S.a[F[f][k]]; T.b[k] = S.b[F[f][k]]; }
-            T.n = 3;
-            float Lx[4] = {0, 0, 0, 0};
-            v3 v;
-            tri_closest(T, v, Lx);
-            float d2 = len2(v);
-            if (d2 < best) { best = d2; bestS = T; bestv = v; for (int k = 0; k < 4; k++) bestL[k] = Lx[k]; }
-        }
+    tetra_face(S, 0, 0, 1, 2, 3, outside_any, best, bf, bused, bla, blb, blc, bestv);
+    tetra_face(S, 1, 0, 3, 1, 2, outside_any, best, bf, bused, bla, blb, blc, bestv);
+    tetra_face(S, 2, 0, 2, 3, 1, outside_any, best, bf, bused, bla, blb, blc, bestv);
+    tetra_face(S, 3, 1, 3, 2, 0, outside_any, best, bf, bused, bla, blb, blc, bestv);
+    if (!outside_any || bf < 0) { lam[0] = lam[1] = lam[2] = lam[3] = 0.f; vout = V(0, 0, 0); return 1; }
+    // move the winning face's vertices to slots 0,1,2 (in face order), then compact
+    switch (bf) {
+    case 0: break;
+    case 1: {
+        v3 w1 = S.w[1], a1 = S.a[1], b1 = S.b[1];
+        sx_copy(S, 1, 3);
+        S.w[2] = w1; S.a[2] = a1; S.b[2] = b1;
+        break;
     }
-    if (!outside_any) { lam[0] = lam[1] = lam[2] = lam[3] = 0.f; vout = V(0, 0, 0); return 1; }
-    S = bestS;
-    for (int k = 0; k < 4; k++) lam[k] = bestL[k];
+    case 2: sx_copy(S, 1, 2); sx_copy(S, 2, 3); break;
+    default: sx_copy(S, 0, 1); sx_copy(S, 1, 3); break;
+    }
+    S.n = 3;
+    tri_compact(S, bused, bla, blb, blc, lam);
     vout = bestv;
     return 0;
 }
@@ -420,11 +465,15 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
         float vv = len2(v), vw = dot(v, wv);
         if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
         bool dup = false;
-        for (int k = 0; k < S.n; k++)
-            if (S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < S.n && S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
         if (dup && S.n > 0) break;
         if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) break;
-        S.w[S.n] = wv; S.a[S.n] = sa; S.b[S.n] = sb; S.n++;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k == S.n) { S.w[k] = wv; S.a[k] = sa; S.b[k] = sb; }
+        S.n++;
         v3 nv;
         if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; break; }
         float nvv = len2(nv);
@@ -435,7 +484,9 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     }
     if (status == GJK_PENETRATING) return GJK_PENETRATING;
     v3 a = V(0, 0, 0), b = V(0, 0, 0);
-    for (int k = 0; k < S.n; k++) { a = add(a, scl(S.a[k], lam[k])); b = add(b, scl(S.b[k], lam[k])); }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < S.n) { a = add(a, scl(S.a[k], lam[k])); b = add(b, scl(S.b[k], lam[k])); }
     pa = a; pb = b;
     dist = len(sub(a, b));
     return GJK_SEPARATED;
@@ -468,10 +519,12 @@ AVR_DI void epa_set_vert(EnvLDS &L, int vi, v3 w, v3 a, v3 b) {
 
 AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, const Simplex &S, v3 &normal_out, float &depth, v3 &pa, v3 &pb) {
     int nv = 0;
-    for (int k = 0; k < S.n; k++) epa_set_vert(L, nv++, S.w[k], S.a[k], S.b[k]);
-    const float dirs[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < S.n) { epa_set_vert(L, nv, S.w[k], S.a[k], S.b[k]); nv++; }
     for (int di = 0; di < 6 && nv < 4; di++) {
-        v3 d = V(dirs[di][0], dirs[di][1], dirs[di][2]);
+        float sg = (di & 1) ? -1.f : 1.f;
+        v3 d = V(di < 2 ? sg : 0.f, (di >> 1) == 1 ? sg : 0.f, di >= 4 ? sg : 0.f);
         if (nv == 2) {
             v3 e = sub(ld3(L.u.c.eW[1]), ld3(L.u.c.eW[0]));
             v3 c = crs(e, d);
@@ -599,8 +652,8 @@ AVR_DI int narrowphase(const KModel &m, EnvLDS &L, const WShape &A, const WShape
     }
     if ((ka == AVR_SPHERE && kb == AVR_BOX) || (ka == AVR_BOX && kb == AVR_SPHERE)) {
         bool swapped = ka == AVR_BOX;
-        const WShape &Sp = swapped ? B : A;
-        const WShape &X = swapped ? A : B;
+        const WShape Sp = swapped ? B : A;
+        const WShape X = swapped ? A : B;
         v3 rel = tfinvpt(X.t, Sp.t.p);
         v3 he = X.he;
         v3 cp = V(fminf(he.x, fmaxf(-he.x, rel.x)), fminf(he.y, fmaxf(-he.y, rel.y)), fminf(he.z, fmaxf(-he.z, rel.z)));
@@ -631,8 +684,8 @@ AVR_DI int narrowphase(const KModel &m, EnvLDS &L, const WShape &A, const WShape
     }
     if ((ka == AVR_SPHERE || ka == AVR_CAPSULE) && (kb == AVR_SPHERE || kb == AVR_CAPSULE) && !(ka == AVR_CAPSULE && kb == AVR_CAPSULE)) {
         bool swapped = ka == AVR_CAPSULE;
-        const WShape &Sp = swapped ? B : A;
-        const WShape &Cp = swapped ? A : B;
+        const WShape Sp = swapped ? B : A;
+        const WShape Cp = swapped ? A : B;
         v3 az = qrot(Cp.t.q, V(0, 0, 1));
         v3 p0 = sub(Cp.t.p, scl(az, Cp.he.y)), p1 = add(Cp.t.p, scl(az, Cp.he.y));
         v3 e = sub(p1, p0);
@@ -710,19 +763,40 @@ AVR_DI bool shape_enabled(const KModel &m, int s, int gender) {
 }
 
 // --------------------------------------------------------------------------- manifolds (one lane per shape pair)
-struct Manifold { float p[AVR_MANIFOLD_POINTS][AVR_CP_WORDS]; int n; };
+// A manifold is <= 4 points of the OLD contact pool (each point belongs to exactly one shape
+// pair, so lanes update disjoint LDS words in place) plus at most one NEW point held in
+// registers.  Slot order is kept as 8-bit indices packed in one register (255 = the new point).
+#define MF_NEW 255
+struct MfNew { float p[AVR_CP_WORDS]; };
 
-AVR_DI void mf_copy(float *dst, const float *src) {
-    for (int k = 0; k < AVR_CP_WORDS; k++) dst[k] = src[k];
+AVR_DI int mf_idx(unsigned pk, int j) { return (int)((pk >> (8 * j)) & 255u); }
+AVR_DI unsigned mf_set(unsigned pk, int j, int v) { return (pk & ~(255u << (8 * j))) | ((unsigned)v << (8 * j)); }
+AVR_DI float mf_rd(const float *cp, const MfNew &nw, int idx, int w) {
+    return idx == MF_NEW ? nw.p[w] : cp[AVR_CP_WORDS * idx + w];
+}
+AVR_DI v3 mf_rd3(const float *cp, const MfNew &nw, int idx, int w) {
+    return V(mf_rd(cp, nw, idx, w), mf_rd(cp, nw, idx, w + 1), mf_rd(cp, nw, idx, w + 2));
+}
+AVR_DI void mf_wr(float *cp, MfNew &nw, int idx, int w, float x) {
+    if (idx == MF_NEW) {
+#pragma unroll
+        for (int k = 0; k < AVR_CP_WORDS; k++)
+            if (k == w) nw.p[k] = x;
+    } else cp[AVR_CP_WORDS * idx + w] = x;
 }
 
-AVR_DI int sort_cached(const Manifold &M, v3 la_new, float d_new) {
+// btPersistentManifold::sortCachedPoints
+AVR_DI int sort_cached(const float *cp, const MfNew &nw, unsigned pk, v3 la_new, float d_new) {
     int maxi = -1;
     float maxpen = d_new;
-    for (int i = 0; i < 4; i++)
-        if (M.p[i][AVR_CP_DIST] < maxpen) { maxi = i; maxpen = M.p[i][AVR_CP_DIST]; }
     v3 p[4];
-    for (int i = 0; i < 4; i++) p[i] = ld3(M.p[i] + AVR_CP_LA);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int id = mf_idx(pk, i);
+        float d = mf_rd(cp, nw, id, AVR_CP_DIST);
+        if (d < maxpen) { maxi = i; maxpen = d; }
+        p[i] = mf_rd3(cp, nw, id, AVR_CP_LA);
+    }
     float res[4] = {0, 0, 0, 0};
     if (maxi != 0) res[0] = len2(crs(sub(la_new, p[1]), sub(p[3], p[2])));
     if (maxi != 1) res[1] = len2(crs(sub(la_new, p[0]), sub(p[3], p[2])));
@@ -730,56 +804,78 @@ AVR_DI int sort_cached(const Manifold &M, v3 la_new, float d_new) {
     if (maxi != 3) res[3] = len2(crs(sub(la_new, p[0]), sub(p[2], p[1])));
     int bi = 0;
     float bv = -1.f;
+#pragma unroll
     for (int i = 0; i < 4; i++)
         if (fabsf(res[i]) > bv) { bv = fabsf(res[i]); bi = i; }
     return bi;
 }
 
-AVR_DI void manifold_add(Manifold &M, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB, float dist, float thr) {
+// btManifoldResult::addContactPoint (getCacheEntry / replaceContactPoint / addManifoldPoint)
+AVR_DI void manifold_add(float *cp, MfNew &nw, unsigned &pk, int &n, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB,
+                         float dist, float thr) {
     if (dist > thr) return;
     v3 pA = add(pB, scl(nB, dist));
     v3 la = tfinvpt(ta, pA), lb = tfinvpt(tb, pB);
     float shortest = thr * thr;
     int near = -1;
-    for (int k = 0; k < M.n; k++) {
-        float d2 = len2(sub(ld3(M.p[k] + AVR_CP_LA), la));
-        if (d2 < shortest) { shortest = d2; near = k; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < n) {
+            float d2 = len2(sub(mf_rd3(cp, nw, mf_idx(pk, k), AVR_CP_LA), la));
+            if (d2 < shortest) { shortest = d2; near = k; }
+        }
     }
-    int slot;
-    if (near >= 0) slot = near;
-    else if (M.n == AVR_MANIFOLD_POINTS) {
-        slot = sort_cached(M, la, dist);
-        M.p[slot][AVR_CP_IMP] = 0.f; M.p[slot][AVR_CP_LIFE] = 0.f;
+    int id;
+    if (near >= 0) id = mf_idx(pk, near);
+    else if (n == AVR_MANIFOLD_POINTS) {
+        id = mf_idx(pk, sort_cached(cp, nw, pk, la, dist));
+        mf_wr(cp, nw, id, AVR_CP_IMP, 0.f);
+        mf_wr(cp, nw, id, AVR_CP_LIFE, 0.f);
     } else {
-        slot = M.n++;
-        M.p[slot][AVR_CP_IMP] = 0.f; M.p[slot][AVR_CP_LIFE] = 0.f;
+        id = MF_NEW;
+        pk = mf_set(pk, n, MF_NEW);
+        n++;
+        nw.p[AVR_CP_IMP] = 0.f;
+        nw.p[AVR_CP_LIFE] = 0.f;
     }
-    float *c = M.p[slot];
-    c[AVR_CP_SA] = (float)sa; c[AVR_CP_SB] = (float)sb; c[AVR_CP_PAIR] = (float)pair; c[AVR_CP_SLOT] = 0.f;
-    st3(c + AVR_CP_LA, la); st3(c + AVR_CP_LB, lb); st3(c + AVR_CP_N, nB);
-    c[AVR_CP_DIST] = dist;
+    mf_wr(cp, nw, id, AVR_CP_SA, (float)sa);
+    mf_wr(cp, nw, id, AVR_CP_SB, (float)sb);
+    mf_wr(cp, nw, id, AVR_CP_PAIR, (float)pair);
+    mf_wr(cp, nw, id, AVR_CP_SLOT, 0.f);
+    mf_wr(cp, nw, id, AVR_CP_LA + 0, la.x); mf_wr(cp, nw, id, AVR_CP_LA + 1, la.y); mf_wr(cp, nw, id, AVR_CP_LA + 2, la.z);
+    mf_wr(cp, nw, id, AVR_CP_LB + 0, lb.x); mf_wr(cp, nw, id, AVR_CP_LB + 1, lb.y); mf_wr(cp, nw, id, AVR_CP_LB + 2, lb.z);
+    mf_wr(cp, nw, id, AVR_CP_N + 0, nB.x); mf_wr(cp, nw, id, AVR_CP_N + 1, nB.y); mf_wr(cp, nw, id, AVR_CP_N + 2, nB.z);
+    mf_wr(cp, nw, id, AVR_CP_DIST, dist);
 }
 
-AVR_DI void manifold_refresh(Manifold &M, tf ta, tf tb, float thr) {
-    for (int k = M.n - 1; k >= 0; k--) {
-        float *c = M.p[k];
-        v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
-        c[AVR_CP_DIST] = dot(sub(pa, pb), ld3(c + AVR_CP_N));
-        c[AVR_CP_LIFE] += 1.f;
-    }
-    for (int k = M.n - 1; k >= 0; k--) {
-        float *c = M.p[k];
-        bool rm = false;
-        if (c[AVR_CP_DIST] > thr) rm = true;
-        else {
-            v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
-            v3 nrm = ld3(c + AVR_CP_N);
-            v3 dd = sub(pb, sub(pa, scl(nrm, c[AVR_CP_DIST])));
-            if (len2(dd) > thr * thr) rm = true;
+// btPersistentManifold::refreshContactPoints
+AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, tf tb, float thr) {
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        if (k < n) {
+            int id = mf_idx(pk, k);
+            v3 pa = tfpt(ta, mf_rd3(cp, nw, id, AVR_CP_LA)), pb = tfpt(tb, mf_rd3(cp, nw, id, AVR_CP_LB));
+            mf_wr(cp, nw, id, AVR_CP_DIST, dot(sub(pa, pb), mf_rd3(cp, nw, id, AVR_CP_N)));
+            mf_wr(cp, nw, id, AVR_CP_LIFE, mf_rd(cp, nw, id, AVR_CP_LIFE) + 1.f);
         }
-        if (rm) {
-            if (k != M.n - 1) mf_copy(c, M.p[M.n - 1]);
-            M.n--;
+    }
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        if (k < n) {
+            int id = mf_idx(pk, k);
+            float dd = mf_rd(cp, nw, id, AVR_CP_DIST);
+            bool rm = false;
+            if (dd > thr) rm = true;
+            else {
+                v3 pa = tfpt(ta, mf_rd3(cp, nw, id, AVR_CP_LA)), pb = tfpt(tb, mf_rd3(cp, nw, id, AVR_CP_LB));
+                v3 nrm = mf_rd3(cp, nw, id, AVR_CP_N);
+                v3 df = sub(pb, sub(pa, scl(nrm, dd)));
+                if (len2(df) > thr * thr) rm = true;
+            }
+            if (rm) {   // removeContactPoint: the last slot moves into slot k
+                pk = mf_set(pk, k, mf_idx(pk, n - 1));
+                n--;
+            }
         }
     }
 }
@@ -788,6 +884,7 @@ AVR_DI void manifold_refresh(Manifold &M, tf ta, tf tb, float thr) {
 AVR_DI void collide(const KModel &m, EnvLDS &L) {
     const int lane = lane_id();
     const int gender = L.gender;
+    PROF_START(pt);
     // body transforms + fattened AABBs
     for (int b = lane; b < m.nb; b += 64) {
         tf t = body_tf(m, L, b);
@@ -817,6 +914,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
     }
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
+    PROF_STOP(1, pt);
     // child-level shape pairs (compound culling), i-major / j-minor within each body pair
     int nsp = 0;
     for (int k = 0; k < nap; k++) {
@@ -856,6 +954,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
     }
     if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; nsp = MAXSP; }
     SYNC();
+    PROF_STOP(2, pt);
     // narrowphase pass A: one lane per small shape pair; big hulls and EPA deferred
     for (int q = lane; q < nsp; q += 64) {
         int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q];
@@ -871,6 +970,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         st3(r + 1, nB); st3(r + 4, pB); r[7] = d;
     }
     SYNC();
+    PROF_STOP(3, pt);
     // pass B: wave-cooperative narrowphase (big hulls, EPA), in pair order
     for (int q = 0; q < nsp; q++) {
         if (L.u.c.res[q][0] != 2.f) continue;
@@ -889,39 +989,49 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         }
         SYNC();
     }
+    PROF_STOP(4, pt);
     // pass C: rebuild the contact pool, one lane per manifold, order-preserving
     const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    float *oldcp = L.st + AVR_S_CP;
     int nnew = 0;
     for (int base = 0; base < nsp; base += 64) {
         int q = base + lane;
-        Manifold M;
-        M.n = 0;
-        int sa = 0, sb = 0, p = 0, ba = 0, bb = 0;
-        float thr = 0.f;
+        unsigned pk = 0u;
+        int n = 0;
+        MfNew nw;
+#pragma unroll
+        for (int k = 0; k < AVR_CP_WORDS; k++) nw.p[k] = 0.f;
         if (q < nsp) {
-            sa = L.u.c.sp_a[q]; sb = L.u.c.sp_b[q]; p = L.u.c.sp_pair[q];
-            ba = m.shape_body[sa]; bb = m.shape_body[sb];
-            thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-            for (int i = 0; i < nold && M.n < AVR_MANIFOLD_POINTS; i++) {
-                const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * i;
-                if ((int)c[AVR_CP_SA] == sa && (int)c[AVR_CP_SB] == sb) { mf_copy(M.p[M.n], c); M.n++; }
+            int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q], p = L.u.c.sp_pair[q];
+            int ba = m.shape_body[sa], bb = m.shape_body[sb];
+            float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+            for (int i = 0; i < nold && n < AVR_MANIFOLD_POINTS; i++) {
+                const float *c = oldcp + AVR_CP_WORDS * i;
+                if ((int)c[AVR_CP_SA] == sa && (int)c[AVR_CP_SB] == sb) { pk = mf_set(pk, n, i); n++; }
             }
             tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
             const float *r = L.u.c.res[q];
-            if (r[0] == 1.f) manifold_add(M, sa, sb, p, ta, tb, ld3(r + 1), ld3(r + 4), r[7], thr);
-            manifold_refresh(M, ta, tb, thr);
+            if (r[0] == 1.f) manifold_add(oldcp, nw, pk, n, sa, sb, p, ta, tb, ld3(r + 1), ld3(r + 4), r[7], thr);
+            manifold_refresh(oldcp, nw, pk, n, ta, tb, thr);
         }
         // exclusive prefix sum of survivor counts across lanes
-        int cnt = M.n, incl = cnt;
+        int incl = n;
         for (int o = 1; o < 64; o <<= 1) {
             int y = __shfl_up(incl, o, 64);
             if (lane >= o) incl += y;
         }
-        int excl = incl - cnt;
+        int excl = incl - n;
         int tot = __shfl(incl, 63, 64);
-        for (int k = 0; k < M.n; k++) {
-            int dst = nnew + excl + k;
-            if (dst < AVR_MAX_CONTACTS) mf_copy(L.u.c.newcp[dst], M.p[k]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (k < n) {
+                int dst = nnew + excl + k;
+                int id = mf_idx(pk, k);
+                if (dst < AVR_MAX_CONTACTS) {
+#pragma unroll
+                    for (int w = 0; w < AVR_CP_WORDS; w++) L.u.c.newcp[dst][w] = mf_rd(oldcp, nw, id, w);
+                }
+            }
         }
         nnew += tot;
     }
@@ -930,6 +1040,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
     for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) L.st[AVR_S_CP + i] = (&L.u.c.newcp[0][0])[i];
     if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
     SYNC();
+    PROF_STOP(5, pt);
 }
 
 // --------------------------------------------------------------------------- constraint rows
@@ -1065,7 +1176,8 @@ AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
                     jbl = scl(lin, -1.f);
                     jba = crs(sub(pivB, tb.p), jbl);
                 } else {
-                    an = V(FA.m[0][i - 3], FA.m[1][i - 3], FA.m[2][i - 3]);
+                    v3 c0 = V(FA.m[0][0], FA.m[1][0], FA.m[2][0]), c1 = V(FA.m[0][1], FA.m[1][1], FA.m[2][1]), c2 = V(FA.m[0][2], FA.m[1][2], FA.m[2][2]);
+                    an = i == 3 ? c0 : (i == 4 ? c1 : c2);
                     pos = i == 3 ? ang.x : i == 4 ? ang.y : ang.z;
                     robot_jac(m, L, link, pivA, V(0, 0, 0), an, JA);
                     jbl = V(0, 0, 0);
@@ -1206,112 +1318,153 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float dt) {
     SYNC();
 }
 
-// apply impulse of contact row k of contact c to the delta velocities (uniform, lane 0 writes)
-AVR_DI void crow_apply(const KModel &m, EnvLDS &L, const CRow &r, int k, float imp, int lane) {
-    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
-    int slot = r.rs + k * ((r.kA == 1) + (r.kB == 1));
-    if (r.kA == 1) {
-        if (lane < m.nd) L.dq[lane] += L.u.s.rsM[slot][lane] * imp;
-        slot++;
-    } else if (r.kA == 2) {
-        v3 ja = crs(ld3(r.rA), dir);
-        v3 dl = scl(dir, imp / m.fb_mass[r.iA]);
-        v3 da = scl(iinv_mul(L, r.iA, ja), imp);
-        if (lane == 0) { st3(L.dfv[r.iA], add(ld3(L.dfv[r.iA]), dl)); st3(L.dfw[r.iA], add(ld3(L.dfw[r.iA]), da)); }
+// ---------------------------------------------------------------------------- PGS solve
+// Delta velocities live in registers, distributed over lanes: lane d < nd holds the robot's
+// dq[d]; lane f < nf holds free body f's (dv, dw).  A row reads its endpoints' values with
+// v_readlane (uniform), reduces the robot dot product over lanes 0..15 with DPP, and only the
+// owning lanes update.  No barrier and no LDS round trip sits on the row-to-row dependency.
+struct DV { float rq, vx, vy, vz, wx, wy, wz; };
+
+AVR_DI float rdl(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+AVR_DI float unif(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+AVR_DI float dpp_shr(float x, int n) {
+    int v = __float_as_int(x);
+    int r;
+    switch (n) {
+    case 1: r = __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true); break;
+    case 2: r = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true); break;
+    case 4: r = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true); break;
+    default: r = __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true); break;
     }
-    if (r.kB == 1) {
-        if (lane < m.nd) L.dq[lane] += L.u.s.rsM[slot][lane] * imp;
-    } else if (r.kB == 2) {
-        v3 nd = scl(dir, -1.f);
-        v3 jb = crs(ld3(r.rB), nd);
-        v3 dl = scl(nd, imp / m.fb_mass[r.iB]);
-        v3 da = scl(iinv_mul(L, r.iB, jb), imp);
-        if (lane == 0) { st3(L.dfv[r.iB], add(ld3(L.dfv[r.iB]), dl)); st3(L.dfw[r.iB], add(ld3(L.dfw[r.iB]), da)); }
+    return __int_as_float(r);
+}
+// sum over lanes 0..15 (lanes >= 16 must pass 0), broadcast as a uniform value
+AVR_DI float robot_reduce(float x) {
+    x += dpp_shr(x, 1);
+    x += dpp_shr(x, 2);
+    x += dpp_shr(x, 4);
+    x += dpp_shr(x, 8);
+    return rdl(x, 15);
+}
+
+AVR_DI float free_dot_dv(const DV &d, int f, v3 jl, v3 ja) {
+    v3 v = V(rdl(d.vx, f), rdl(d.vy, f), rdl(d.vz, f));
+    v3 w = V(rdl(d.wx, f), rdl(d.wy, f), rdl(d.wz, f));
+    return dot(jl, v) + dot(ja, w);
+}
+
+AVR_DI void free_apply(DV &d, int f, v3 ml, v3 ma, float imp) {
+    if (lane_id() == f) {
+        d.vx += ml.x * imp; d.vy += ml.y * imp; d.vz += ml.z * imp;
+        d.wx += ma.x * imp; d.wy += ma.y * imp; d.wz += ma.z * imp;
     }
 }
 
-AVR_DI float crow_dot(const KModel &m, const EnvLDS &L, const CRow &r, int k) {
+AVR_DI v3 iinv_mul_u(const EnvLDS &L, int f, v3 a) { return iinv_mul(L, f, a); }
+
+// contact row k of contact r: dot with the current delta velocities
+AVR_DI float crow_dot(const KModel &m, const EnvLDS &L, const CRow &r, int k, int kA, int iA, int kB, int iB, int rs, const DV &d) {
+    const int lane = lane_id();
     v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
-    int slot = r.rs + k * ((r.kA == 1) + (r.kB == 1));
+    int nrob = (kA == 1) + (kB == 1);
+    int slot = rs + k * nrob;
     float s = 0.f;
-    if (r.kA == 1) { s += robot_dot(m, L, L.u.s.rsJ[slot], true); slot++; }
-    else if (r.kA == 2) s += free_dot(L, r.iA, dir, crs(ld3(r.rA), dir), true);
-    if (r.kB == 1) s += robot_dot(m, L, L.u.s.rsJ[slot], true);
-    else if (r.kB == 2) { v3 nd = scl(dir, -1.f); s += free_dot(L, r.iB, nd, crs(ld3(r.rB), nd), true); }
+    if (nrob) {
+        float p = 0.f;
+        if (kA == 1 && lane < MAXD) p += L.u.s.rsJ[slot][lane] * d.rq;
+        if (kB == 1 && lane < MAXD) p += L.u.s.rsJ[slot + (kA == 1)][lane] * d.rq;
+        s += robot_reduce(p);
+    }
+    if (kA == 2) s += free_dot_dv(d, iA, dir, crs(ld3(r.rA), dir));
+    if (kB == 2) { v3 nd = scl(dir, -1.f); s += free_dot_dv(d, iB, nd, crs(ld3(r.rB), nd)); }
     return s;
 }
 
-// Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order).
+AVR_DI void crow_apply(const KModel &m, const EnvLDS &L, const CRow &r, int k, int kA, int iA, int kB, int iB, int rs, DV &d, float imp) {
+    const int lane = lane_id();
+    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
+    int nrob = (kA == 1) + (kB == 1);
+    int slot = rs + k * nrob;
+    if (kA == 1 && lane < MAXD) d.rq += L.u.s.rsM[slot][lane] * imp;
+    if (kB == 1 && lane < MAXD) d.rq += L.u.s.rsM[slot + (kA == 1)][lane] * imp;
+    if (kA == 2) free_apply(d, iA, scl(dir, 1.f / m.fb_mass[iA]), iinv_mul(L, iA, crs(ld3(r.rA), dir)), imp);
+    if (kB == 2) {
+        v3 nd = scl(dir, -1.f);
+        free_apply(d, iB, scl(nd, 1.f / m.fb_mass[iB]), iinv_mul(L, iB, crs(ld3(r.rB), nd)), imp);
+    }
+}
+
+AVR_DI float clamp_imp(float imp, float delta, float lo, float hi, float &ni) {
+    float sum = imp + delta;
+    if (sum < lo) { ni = lo; return lo - imp; }
+    if (sum > hi) { ni = hi; return hi - imp; }
+    ni = sum;
+    return delta;
+}
+
+// Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order):
+// non-contact rows (alternating sweep direction), normal rows, friction rows.
 AVR_DI void solve(const KModel &m, EnvLDS &L) {
     const int lane = lane_id();
-    const int n_nc = L.n_nc, n_c = L.n_c;
+    const int n_nc = uni(L.n_nc), n_c = uni(L.n_c);
+    DV d;
+    d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
     // warm start, in contact order
     for (int i = 0; i < n_c; i++) {
-        CRow &r = L.u.s.cr[i];
-        if (r.rs < 0 && (r.kA == 1 || r.kB == 1)) continue;
-        float imp = r.imp[0];
-        if (imp != 0.f) crow_apply(m, L, r, 0, imp, lane);
-        SYNC();
+        const CRow &r = L.u.s.cr[i];
+        int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
+        if (rs < 0 && (kA == 1 || kB == 1)) continue;
+        float imp = unif(r.imp[0]);
+        if (imp != 0.f) crow_apply(m, L, r, 0, kA, iA, kB, iB, rs, d, imp);
     }
     for (int it = 0; it < m.iters; it++) {
         for (int j = 0; j < n_nc; j++) {
             int k = (it & 1) ? j : n_nc - 1 - j;
             NCRow &r = L.u.s.nc[k];
-            float dv = robot_dot(m, L, r.JA, true);
-            if (r.fb >= 0) dv += free_dot(L, r.fb, ld3(r.JB), ld3(r.JB + 3), true);
-            float delta = r.rhs - dv * r.inv;
-            float sum = r.imp + delta;
+            int fb = uni(r.fb);
+            float p = lane < MAXD ? r.JA[lane] * d.rq : 0.f;
+            float dv = robot_reduce(p);
+            if (fb >= 0) dv += free_dot_dv(d, fb, ld3(r.JB), ld3(r.JB + 3));
+            float inv = unif(r.inv), imp = unif(r.imp);
             float ni;
-            if (sum < r.lo) { delta = r.lo - r.imp; ni = r.lo; }
-            else if (sum > r.hi) { delta = r.hi - r.imp; ni = r.hi; }
-            else ni = sum;
-            SYNC();
-            if (lane < m.nd) L.dq[lane] += r.MA[lane] * delta;
-            if (lane == 0) {
-                r.imp = ni;
-                if (r.fb >= 0) {
-                    st3(L.dfv[r.fb], add(ld3(L.dfv[r.fb]), scl(ld3(r.MB), delta)));
-                    st3(L.dfw[r.fb], add(ld3(L.dfw[r.fb]), scl(ld3(r.MB + 3), delta)));
-                }
-            }
-            SYNC();
+            float delta = clamp_imp(imp, unif(r.rhs) - dv * inv, unif(r.lo), unif(r.hi), ni);
+            if (lane < MAXD) d.rq += r.MA[lane] * delta;
+            if (fb >= 0) free_apply(d, fb, ld3(r.MB), ld3(r.MB + 3), delta);
+            if (lane == 0) r.imp = ni;
         }
-        for (int pass = 0; pass < 3; pass++) {
-            // pass 0: normals; passes 1,2 interleaved friction rows (t1 then t2 per contact)
-            if (pass == 2) break;
-            for (int i = 0; i < n_c; i++) {
-                CRow &r = L.u.s.cr[i];
-                if (r.rs < 0 && (r.kA == 1 || r.kB == 1)) continue;
-                if (pass == 0) {
-                    float dv = crow_dot(m, L, r, 0);
-                    float delta = r.rhs[0] - dv * r.inv[0];
-                    float sum = r.imp[0] + delta, ni;
-                    if (sum < 0.f) { delta = -r.imp[0]; ni = 0.f; }
-                    else if (sum > 1e10f) { delta = 1e10f - r.imp[0]; ni = 1e10f; }
-                    else ni = sum;
-                    SYNC();
-                    crow_apply(m, L, r, 0, delta, lane);
-                    if (lane == 0) r.imp[0] = ni;
-                    SYNC();
-                } else {
-                    float nimp = r.imp[0];
-                    if (!(nimp > 0.f)) continue;
-                    float lo = -r.fric * nimp, hi = r.fric * nimp;
-                    for (int k = 1; k < 3; k++) {
-                        float dv = crow_dot(m, L, r, k);
-                        float delta = r.rhs[k] - dv * r.inv[k];
-                        float sum = r.imp[k] + delta, ni;
-                        if (sum < lo) { delta = lo - r.imp[k]; ni = lo; }
-                        else if (sum > hi) { delta = hi - r.imp[k]; ni = hi; }
-                        else ni = sum;
-                        SYNC();
-                        crow_apply(m, L, r, k, delta, lane);
-                        if (lane == 0) r.imp[k] = ni;
-                        SYNC();
-                    }
-                }
+        for (int i = 0; i < n_c; i++) {
+            CRow &r = L.u.s.cr[i];
+            int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
+            if (rs < 0 && (kA == 1 || kB == 1)) continue;
+            float dv = crow_dot(m, L, r, 0, kA, iA, kB, iB, rs, d);
+            float imp = unif(r.imp[0]), ni;
+            float delta = clamp_imp(imp, unif(r.rhs[0]) - dv * unif(r.inv[0]), 0.f, 1e10f, ni);
+            crow_apply(m, L, r, 0, kA, iA, kB, iB, rs, d, delta);
+            if (lane == 0) r.imp[0] = ni;
+        }
+        for (int i = 0; i < n_c; i++) {
+            CRow &r = L.u.s.cr[i];
+            int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
+            if (rs < 0 && (kA == 1 || kB == 1)) continue;
+            float nimp = unif(r.imp[0]);
+            if (!(nimp > 0.f)) continue;
+            float fr = unif(r.fric);
+            float lo = -fr * nimp, hi = fr * nimp;
+            for (int k = 1; k < 3; k++) {
+                float dv = crow_dot(m, L, r, k, kA, iA, kB, iB, rs, d);
+                float imp = unif(r.imp[k]), ni;
+                float delta = clamp_imp(imp, unif(r.rhs[k]) - dv * unif(r.inv[k]), lo, hi, ni);
+                crow_apply(m, L, r, k, kA, iA, kB, iB, rs, d, delta);
+                if (lane == 0) r.imp[k] = ni;
             }
         }
+    }
+    SYNC();
+    if (lane < MAXD) L.dq[lane] = d.rq;
+    if (lane < MAXF) {
+        L.dfv[lane][0] = d.vx; L.dfv[lane][1] = d.vy; L.dfv[lane][2] = d.vz;
+        L.dfw[lane][0] = d.wx; L.dfw[lane][1] = d.wy; L.dfw[lane][2] = d.wz;
     }
     // write back normal impulses to the manifold points (warm start + normalForce)
     for (int i = lane; i < n_c; i += 64) {
@@ -1324,8 +1477,11 @@ AVR_DI void solve(const KModel &m, EnvLDS &L) {
 // --------------------------------------------------------------------------- one sub-step
 AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
     const int lane = lane_id();
+    PROF_START(ps);
     robot_fk(m, L);
+    PROF_STOP(0, ps);
     collide(m, L);
+    PROF_STOP(13, ps);
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
     robot_bias(m, L);
@@ -1371,9 +1527,13 @@ AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
             for (int b = 0; b < 3; b++) L.Iinv[f][3 * a + b] = R.m[a][0] * inv[0] * R.m[b][0] + R.m[a][1] * inv[1] * R.m[b][1] + R.m[a][2] * inv[2] * R.m[b][2];
     }
     SYNC();
+    PROF_STOP(6, ps);
     build_noncontact_rows(m, L, dt);
+    PROF_STOP(7, ps);
     build_contact_rows(m, L, dt);
+    PROF_STOP(8, ps);
     solve(m, L);
+    PROF_STOP(9, ps);
     // integrate
     if (lane < m.nd) {
         float v = clampf(L.vq[lane] + L.dq[lane], -vmax, vmax);
@@ -1397,6 +1557,7 @@ AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
         stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
     }
     SYNC();
+    PROF_STOP(10, ps);
     return ok;
 }
 
@@ -1481,17 +1642,22 @@ AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j)
 
 enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 
-__global__ __launch_bounds__(64) void avr_step_kernel(KModel m, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
+__global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
                                                       float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
                                                       int mode, long long t, int n_envs) {
     __shared__ EnvLDS L;
+    const KModel &m = *mp;
     const int env = blockIdx.x;
     const int lane = lane_id();
     if (env >= n_envs) return;
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) L.st[i] = gst[i];
     if (lane == 0) { L.flags = 0; L.gender = 0; }
+#ifdef AVR_PROF
+    if (lane < 16) L.prof[lane] = 0;
+#endif
     SYNC();
+    PROF_START(ptot);
     if (lane == 0) L.gender = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
     SYNC();
     const int nsub = m.nsub > 0 ? m.nsub : 1;
@@ -1613,6 +1779,11 @@ __global__ __launch_bounds__(64) void avr_step_kernel(KModel m, float *__restric
     }
     SYNC();
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) gst[i] = L.st[i];
+#ifdef AVR_PROF
+    PROF_STOP(12, ptot);
+    SYNC();
+    if (m.prof && lane < 16) m.prof[(size_t)env * 16 + lane] = L.prof[lane];
+#endif
 }
 
 __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm) {
@@ -1623,9 +1794,9 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 }
 
 // host-side launch helpers (used by avr_capi.hip)
-extern "C" hipError_t avr_launch_step(const KModel *m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
+extern "C" hipError_t avr_launch_step(const KModel *d_m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
                                       float *info, int mode, long long t, int n_envs, hipStream_t stream) {
-    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, *m, state, act, obs, rew, done, info, mode, t, n_envs);
+    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mode, t, n_envs);
     return hipGetLastError();
 }
 

@@ -55,4 +55,5 @@ struct KModel {
     int env_offset;
     int dof_link[MAXD];        // link owning each DoF
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+    unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
 };
