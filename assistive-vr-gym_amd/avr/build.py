@@ -32,14 +32,19 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force=False, extra=()):
+def build_lib(force=False, extra=(), out=LIB):
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if not force and not _stale(out, deps):
+        return out
     cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result',
-           '-o', LIB] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
+           '-o', out] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
     subprocess.check_call(cmd)
-    return LIB
+    return out
+
+
+def build_prof(force=False):
+    """Diagnostic build with per-phase s_memtime counters (tools/prof_phases.py); never shipped."""
+    return build_lib(force=force, extra=('-DAVR_PROF',), out=os.path.join(HERE, 'libavr_prof.so'))
 
 
 def build_oracle():
@@ -53,4 +58,6 @@ def build_all(force=False):
 
 if __name__ == '__main__':
     build_all(force='--force' in sys.argv)
+    if '--prof' in sys.argv:
+        build_prof(force=True)
     print(LIB)

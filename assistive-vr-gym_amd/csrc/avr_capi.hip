@@ -189,9 +189,17 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int q = l; q >= 0; q = d->rl_parent[q]) mask |= 1u << q;
         k.anc_mask[l] = mask;
     }
+    size_t E = (size_t)cfg->n_envs;
+    // per-env constraint-row scratch (written and read inside each sub-step)
+    k.rowcap = MAXNC + 3 * AVR_MAX_CONTACTS;
+    {
+        float *rows = nullptr;
+        HIPCHK(s, hipMalloc(&rows, E * 2 * (size_t)k.rowcap * 32 * sizeof(float)));
+        s->allocs.push_back(rows);
+        k.rows = rows;
+    }
     HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
-    size_t E = (size_t)cfg->n_envs;
     HIPCHK(s, hipMalloc(&s->d_state, E * AVR_STATE_WORDS * sizeof(float)));
     HIPCHK(s, hipMemset(s->d_state, 0, E * AVR_STATE_WORDS * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_act, E * AVR_ACT_DIM * sizeof(float)));

@@ -30,22 +30,6 @@
 
 
 // --------------------------------------------------------------------------- LDS layout
-struct NCRow {                 // limit / motor / fixed-constraint row (robot endpoint A)
-    float JA[MAXD], MA[MAXD];  // robot part
-    float JB[6], MB[6];        // free-body part (fixed constraint) or zero
-    float inv, rhs, lo, hi, imp;
-    int fb;                    // free body index of endpoint B, -1 if none
-    int pad[2];
-};
-struct CRow {                  // one contact point = 1 normal + 2 friction rows
-    float n[3], t1[3], t2[3];
-    float rA[3], rB[3];        // lever arms from the free bodies' COM (if free)
-    float inv[3], rhs[3], imp[3];
-    float fric;
-    int kA, iA, kB, iB;        // endpoint kinds: 0 none, 1 robot, 2 free
-    int rs;                    // first robot slot (rows use rs, rs+1, rs+2 per robot endpoint)
-    int cp;                    // contact point index
-};
 struct EnvLDS {
     float st[AVR_STATE_WORDS];
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
@@ -56,7 +40,7 @@ struct EnvLDS {
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
     float h[MAXD], qdd[MAXD];
     float rn[6][MAXL][4];   // RNEA temporaries: omega, v_com, alpha, a_com, F, N
-    int nsp, nap, n_nc, n_c, n_rs, flags, gender, pad;
+    int nsp, nap, n_nc, n_c, flags, gender, pad, pad2;
 #ifdef AVR_PROF
     unsigned long long prof[16];
 #endif
@@ -71,12 +55,6 @@ struct EnvLDS {
             float eFn[EPA_MAX_F][4];       // normal + d
             int eEdge[EPA_MAX_F * 3][2];
         } c;
-        struct {
-            NCRow nc[MAXNC];
-            CRow cr[AVR_MAX_CONTACTS];
-            float rsJ[MAXRS][MAXD];
-            float rsM[MAXRS][MAXD];
-        } s;
     } u;
 };
 
@@ -1080,11 +1058,44 @@ AVR_DI float robot_dot(const KModel &m, const EnvLDS &L, const float *J, bool de
     return s;
 }
 
+// Constraint rows live in a per-env buffer in global memory (L2-resident working set), one
+// 32-word record per row, in solve order [non-contact][normals][frictions]:
+//   w0 info (iA | iB<<6 | robot<<12; 63 = endpoint is not a free body)   w1 friction coeff
+//   w2 inv   w3 rhs   w4 lo   w5 hi   w6 initial impulse   w7 -
+//   w8..13 free A Jacobian (lin, ang)   w14..19 free A  M^-1 J^T
+//   w20..25 free B Jacobian             w26..31 free B  M^-1 J^T
+// Rows with a robot endpoint also own a robot part at the same index in the second half of the
+// buffer: w0..11 J (A and B endpoints combined), w16..27 M^-1 J^T.  Everything a row resolve
+// needs is precomputed here, so the PGS chain (solve) is loads + register arithmetic only.
+#define RW 32
+#define RI_NONE 63
+#define RI_ROBOT (1 << 12)
+
+AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RW; }
+AVR_DI float *row_rob(const KModel &m, float *base, int r) { return base + (m.rowcap + r) * RW; }
+
+AVR_DI void put_free(float *w, v3 jl, v3 ja, v3 ml, v3 ma) {
+    w[0] = jl.x; w[1] = jl.y; w[2] = jl.z; w[3] = ja.x; w[4] = ja.y; w[5] = ja.z;
+    w[6] = ml.x; w[7] = ml.y; w[8] = ml.z; w[9] = ma.x; w[10] = ma.y; w[11] = ma.z;
+}
+AVR_DI void put_free_zero(float *w) {
+#pragma unroll
+    for (int k = 0; k < 12; k++) w[k] = 0.f;
+}
+AVR_DI void put_hdr(float *w, int info, float fric, float inv, float rhs, float lo, float hi, float imp0) {
+    w[0] = __int_as_float(info); w[1] = fric; w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = imp0; w[7] = 0.f;
+}
+AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) { w[d] = J[d]; w[16 + d] = MJ[d]; }
+}
+
 // Non-contact rows (limits, motors, fixed constraint); lanes build rows in parallel.
-AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
+// Row order restates btMultiBodyConstraintSolver's setup order: joint-limit rows
+// of violated limits (link order, lower then upper), motor rows (link order), fixed rows.
+AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float dt) {
     const int lane = lane_id();
     const float erp = m.erp;
-    // enumerate: violated limits (link order, lower then upper), motors (link order), fixed (6)
     int nrow = 0;
     // limits
     for (int i = 0; i < m.nl; i++) {
@@ -1095,18 +1106,18 @@ AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
             float pen = side == 0 ? q - m.rl_lower[i] : m.rl_upper[i] - q;
             if (pen > 0.f) continue;
             if (nrow < MAXNC && lane == (nrow & 63)) {
-                NCRow &r = L.u.s.nc[nrow];
-                for (int d = 0; d < MAXD; d++) r.JA[d] = 0.f;
-                r.JA[dof] = side == 0 ? 1.f : -1.f;
-                float MA[MAXD];
-                chol_solve(m, L, r.JA, MA);
-                float den = 0.f;
+                float JA[MAXD], MA[MAXD];
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { r.MA[d] = MA[d]; den += r.JA[d] * MA[d]; }
-                r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                float rel = robot_dot(m, L, r.JA, false);
-                r.rhs = (-pen * erp / dt - rel) * r.inv;
-                r.lo = 0.f; r.hi = 100.f; r.imp = 0.f; r.fb = -1;
+                for (int d = 0; d < MAXD; d++) JA[d] = d == dof ? (side == 0 ? 1.f : -1.f) : 0.f;
+                chol_solve(m, L, JA, MA);
+                float den = 0.f, rel = 0.f;
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
+                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+                float *w = row_rec(m, rows, nrow);
+                put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f);
+                put_free_zero(w + 8); put_free_zero(w + 20);
+                put_robot(row_rob(m, rows, nrow), JA, MA);
             }
             nrow++;
         }
@@ -1116,22 +1127,22 @@ AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
         int dof = m.rl_dof[i];
         if (dof < 0) continue;
         if (nrow < MAXNC && lane == (nrow & 63)) {
-            NCRow &r = L.u.s.nc[nrow];
-            for (int d = 0; d < MAXD; d++) r.JA[d] = 0.f;
-            r.JA[dof] = 1.f;
-            float MA[MAXD];
-            chol_solve(m, L, r.JA, MA);
-            float den = 0.f;
+            float JA[MAXD], MA[MAXD];
 #pragma unroll
-            for (int d = 0; d < MAXD; d++) { r.MA[d] = MA[d]; den += r.JA[d] * MA[d]; }
-            r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+            for (int d = 0; d < MAXD; d++) JA[d] = d == dof ? 1.f : 0.f;
+            chol_solve(m, L, JA, MA);
+            float den = 0.f, rel = 0.f;
+#pragma unroll
+            for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
+            float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
             float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
             float kp = L.st[AVR_S_KP + dof], kd = 1.f;
             float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
-            float rel = robot_dot(m, L, r.JA, false);
-            r.rhs = (desired - rel) * r.inv;
             float mi = L.st[AVR_S_MAXIMP + dof];
-            r.lo = -mi; r.hi = mi; r.imp = 0.f; r.fb = -1;
+            float *w = row_rec(m, rows, nrow);
+            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f);
+            put_free_zero(w + 8); put_free_zero(w + 20);
+            put_robot(row_rob(m, rows, nrow), JA, MA);
         }
         nrow++;
     }
@@ -1164,7 +1175,6 @@ AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
         for (int i = 0; i < 6; i++) {
             int row = nrow + i;
             if (row < MAXNC && lane == (row & 63)) {
-                NCRow &r = L.u.s.nc[row];
                 v3 lin = V(0, 0, 0), an = V(0, 0, 0);
                 float pos;
                 float JA[MAXD];
@@ -1185,24 +1195,26 @@ AVR_DI void build_noncontact_rows(const KModel &m, EnvLDS &L, float dt) {
                 }
                 float MA[MAXD];
                 chol_solve(m, L, JA, MA);
-                float den = 0.f;
+                float den = 0.f, rel = 0.f;
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { r.JA[d] = JA[d]; r.MA[d] = MA[d]; den += JA[d] * MA[d]; }
+                for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
                 float im = 1.f / m.fb_mass[fb];
                 v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
-                st3(r.JB, jbl); st3(r.JB + 3, jba); st3(r.MB, mbl); st3(r.MB + 3, mba);
                 den += dot(jbl, mbl) + dot(jba, mba);
-                r.inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                float rel = robot_dot(m, L, r.JA, false) + free_dot(L, fb, jbl, jba, false);
-                r.rhs = (-pos * erp / dt - rel) * r.inv;
-                r.lo = -mi; r.hi = mi; r.imp = 0.f; r.fb = fb;
+                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+                rel += free_dot(L, fb, jbl, jba, false);
+                float *w = row_rec(m, rows, row);
+                put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f);
+                put_free_zero(w + 8);
+                put_free(w + 20, jbl, jba, mbl, mba);
+                put_robot(row_rob(m, rows, row), JA, MA);
             }
         }
         nrow += 6;
     }
     if (nrow > MAXNC) { if (lane == 0) L.flags |= 16; nrow = MAXNC; }
     if (lane == 0) L.n_nc = nrow;
-    SYNC();
+    return nrow;
 }
 
 AVR_DI void plane_space(v3 n, v3 &p, v3 &q) {
@@ -1224,105 +1236,86 @@ AVR_DI void body_endpoint(const KModel &m, int b, int &kind, int &idx) {
     else { kind = 0; idx = 0; }
 }
 
-// Contact rows: one lane per contact point.  Robot endpoints take robot slots (prefix sum).
-AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float dt) {
+// Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal) and
+// n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions).
+AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
     const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
     const float erp = m.erp;
-    int rs_base = 0;
-    for (int base = 0; base < ncp; base += 64) {
-        int i = base + lane;
-        bool valid = i < ncp;
+    for (int i = lane; i < ncp; i += 64) {
         int kA = 0, iA = 0, kB = 0, iB = 0;
-        const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * (valid ? i : 0);
+        const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * i;
         int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
         body_endpoint(m, ba, kA, iA);
         body_endpoint(m, bb, kB, iB);
-        int need = valid ? 3 * ((kA == 1) + (kB == 1)) : 0;
-        int incl = need;
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        int myrs = rs_base + incl - need;
-        int tot = __shfl(incl, 63, 64);
-        if (valid) {
-            CRow &r = L.u.s.cr[i];
-            tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
-            v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
-            v3 n = ld3(c + AVR_CP_N);
-            v3 t1, t2;
-            plane_space(n, t1, t2);
-            st3(r.n, n); st3(r.t1, t1); st3(r.t2, t2);
-            v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
-            st3(r.rA, rA); st3(r.rB, rB);
-            float fr = m.body_friction[ba] * m.body_friction[bb];
-            r.fric = fminf(fr, 10.f);
-            r.kA = kA; r.iA = iA; r.kB = kB; r.iB = iB;
-            r.cp = i;
-            bool fits = myrs + need <= MAXRS;
-            r.rs = fits ? myrs : -1;
-            int slot = myrs;
-            for (int k = 0; k < 3; k++) {
-                v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
-                float den = 0.f, rel = 0.f;
-                if (kA == 1) {
-                    if (fits) {
-                        float J[MAXD], MJ[MAXD];
-                        robot_jac(m, L, iA, pa, dir, V(0, 0, 0), J);
-                        chol_solve(m, L, J, MJ);
+        tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+        v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
+        v3 n = ld3(c + AVR_CP_N);
+        v3 t1, t2;
+        plane_space(n, t1, t2);
+        v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
+        float fric = fminf(m.body_friction[ba] * m.body_friction[bb], 10.f);
+        bool rob = kA == 1 || kB == 1;
+        int info = (kA == 2 ? iA : RI_NONE) | ((kB == 2 ? iB : RI_NONE) << 6) | (rob ? RI_ROBOT : 0);
+        float imA = kA == 2 ? 1.f / m.fb_mass[iA] : 0.f, imB = kB == 2 ? 1.f / m.fb_mass[iB] : 0.f;
+        for (int k = 0; k < 3; k++) {
+            v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
+            int row = k == 0 ? n_nc + i : n_nc + ncp + 2 * i + (k - 1);
+            float *w = row_rec(m, rows, row);
+            float den = 0.f, rel = 0.f;
+            float J[MAXD], MJ[MAXD];
 #pragma unroll
-                        for (int d = 0; d < MAXD; d++) { L.u.s.rsJ[slot][d] = J[d]; L.u.s.rsM[slot][d] = MJ[d]; den += J[d] * MJ[d]; rel += J[d] * L.vq[d]; }
-                    }
-                    slot++;
-                } else if (kA == 2) {
-                    v3 ja = crs(rA, dir);
-                    den += dot(dir, dir) / m.fb_mass[iA] + dot(ja, iinv_mul(L, iA, ja));
-                    rel += free_dot(L, iA, dir, ja, false);
-                }
-                v3 nd = scl(dir, -1.f);
-                if (kB == 1) {
-                    if (fits) {
-                        float J[MAXD], MJ[MAXD];
-                        robot_jac(m, L, iB, pb, nd, V(0, 0, 0), J);
-                        chol_solve(m, L, J, MJ);
+            for (int d = 0; d < MAXD; d++) { J[d] = 0.f; MJ[d] = 0.f; }
+            if (kA == 1) {
+                float Ja[MAXD], Ma[MAXD];
+                robot_jac(m, L, iA, pa, dir, V(0, 0, 0), Ja);
+                chol_solve(m, L, Ja, Ma);
 #pragma unroll
-                        for (int d = 0; d < MAXD; d++) { L.u.s.rsJ[slot][d] = J[d]; L.u.s.rsM[slot][d] = MJ[d]; den += J[d] * MJ[d]; rel += J[d] * L.vq[d]; }
-                    }
-                    slot++;
-                } else if (kB == 2) {
-                    v3 jb = crs(rB, nd);
-                    den += dot(nd, nd) / m.fb_mass[iB] + dot(jb, iinv_mul(L, iB, jb));
-                    rel += free_dot(L, iB, nd, jb, false);
-                }
-                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                r.inv[k] = inv;
-                if (k == 0) {
-                    float pen = c[AVR_CP_DIST];
-                    float velerr = -rel, poserr = 0.f;
-                    if (pen > 0.f) velerr -= pen / dt;
-                    else poserr = -pen * erp / dt;
-                    r.rhs[0] = (poserr + velerr) * inv;
-                    r.imp[0] = c[AVR_CP_IMP] * m.warmstart;
-                } else {
-                    r.rhs[k] = -rel * inv;
-                    r.imp[k] = 0.f;
-                }
+                for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; J[d] += Ja[d]; MJ[d] += Ma[d]; }
+                put_free_zero(w + 8);
+            } else if (kA == 2) {
+                v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
+                den += dot(dir, ml) + dot(ja, ma);
+                rel += free_dot(L, iA, dir, ja, false);
+                put_free(w + 8, dir, ja, ml, ma);
+            } else put_free_zero(w + 8);
+            v3 nd = scl(dir, -1.f);
+            if (kB == 1) {
+                float Jb[MAXD], Mb[MAXD];
+                robot_jac(m, L, iB, pb, nd, V(0, 0, 0), Jb);
+                chol_solve(m, L, Jb, Mb);
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; J[d] += Jb[d]; MJ[d] += Mb[d]; }
+                put_free_zero(w + 20);
+            } else if (kB == 2) {
+                v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
+                den += dot(nd, ml) + dot(jb, mb);
+                rel += free_dot(L, iB, nd, jb, false);
+                put_free(w + 20, nd, jb, ml, mb);
+            } else put_free_zero(w + 20);
+            if (rob) put_robot(row_rob(m, rows, row), J, MJ);
+            float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+            if (k == 0) {
+                float pen = c[AVR_CP_DIST];
+                float velerr = -rel, poserr = 0.f;
+                if (pen > 0.f) velerr -= pen / dt;
+                else poserr = -pen * erp / dt;
+                put_hdr(w, info, fric, inv, (poserr + velerr) * inv, 0.f, 1e10f, c[AVR_CP_IMP] * m.warmstart);
+            } else {
+                put_hdr(w, info, fric, inv, -rel * inv, 0.f, 0.f, 0.f);
             }
         }
-        rs_base += tot;
     }
-    if (rs_base > MAXRS && lane == 0) L.flags |= 32;
     if (lane == 0) L.n_c = ncp;
-    SYNC();
 }
 
 // ---------------------------------------------------------------------------- PGS solve
 // Delta velocities live in registers, distributed over lanes: lane d < nd holds the robot's
-// dq[d]; lane f < nf holds free body f's (dv, dw).  A row reads its endpoints' values with
-// v_readlane (uniform), reduces the robot dot product over lanes 0..15 with DPP, and only the
-// owning lanes update.  No barrier and no LDS round trip sits on the row-to-row dependency.
+// dq[d]; lane f < nf holds free body f's (dv, dw).  A row's uniform data (header, free-body
+// Jacobians) arrives through the scalar cache (s_load into SGPRs); each endpoint's owner lane
+// forms its partial J.dv against its own registers, one 16-lane DPP reduction sums them, and
+// the owner lanes apply M^-1 J^T delta.  No LDS access and no barrier on the row-to-row chain.
 struct DV { float rq, vx, vy, vz, wx, wy, wz; };
 
 AVR_DI float rdl(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
@@ -1348,129 +1341,142 @@ AVR_DI float robot_reduce(float x) {
     return rdl(x, 15);
 }
 
-AVR_DI float free_dot_dv(const DV &d, int f, v3 jl, v3 ja) {
-    v3 v = V(rdl(d.vx, f), rdl(d.vy, f), rdl(d.vz, f));
-    v3 w = V(rdl(d.wx, f), rdl(d.wy, f), rdl(d.wz, f));
-    return dot(jl, v) + dot(ja, w);
-}
+// scalar-cache view of the row buffer (the rows are written by this wave's vector stores
+// before each solve; solve() invalidates the scalar cache after the stores have completed)
+typedef float f8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef const __attribute__((address_space(4))) f8 *cf8p;
+typedef const __attribute__((address_space(4))) f16v *cf16p;
+typedef const __attribute__((address_space(1))) float *gfp;
 
-AVR_DI void free_apply(DV &d, int f, v3 ml, v3 ma, float imp) {
-    if (lane_id() == f) {
-        d.vx += ml.x * imp; d.vy += ml.y * imp; d.vz += ml.z * imp;
-        d.wx += ma.x * imp; d.wy += ma.y * imp; d.wz += ma.z * imp;
-    }
-}
+struct RowS { f8 h; f16v a; f8 b; float jr, mr; };   // header, free A + B(J) , B(MJ), robot parts
 
-AVR_DI v3 iinv_mul_u(const EnvLDS &L, int f, v3 a) { return iinv_mul(L, f, a); }
-
-// contact row k of contact r: dot with the current delta velocities
-AVR_DI float crow_dot(const KModel &m, const EnvLDS &L, const CRow &r, int k, int kA, int iA, int kB, int iB, int rs, const DV &d) {
+AVR_DI void load_row(RowS &R, const float *rec, const float *rob, bool robot) {
+    R.h = *(cf8p)(rec);
+    R.a = *(cf16p)(rec + 8);
+    R.b = *(cf8p)(rec + 24);
     const int lane = lane_id();
-    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
-    int nrob = (kA == 1) + (kB == 1);
-    int slot = rs + k * nrob;
-    float s = 0.f;
-    if (nrob) {
-        float p = 0.f;
-        if (kA == 1 && lane < MAXD) p += L.u.s.rsJ[slot][lane] * d.rq;
-        if (kB == 1 && lane < MAXD) p += L.u.s.rsJ[slot + (kA == 1)][lane] * d.rq;
-        s += robot_reduce(p);
-    }
-    if (kA == 2) s += free_dot_dv(d, iA, dir, crs(ld3(r.rA), dir));
-    if (kB == 2) { v3 nd = scl(dir, -1.f); s += free_dot_dv(d, iB, nd, crs(ld3(r.rB), nd)); }
-    return s;
+    R.jr = 0.f; R.mr = 0.f;
+    if (robot && lane < MAXD) { R.jr = ((gfp)rob)[lane]; R.mr = ((gfp)rob)[16 + lane]; }
 }
 
-AVR_DI void crow_apply(const KModel &m, const EnvLDS &L, const CRow &r, int k, int kA, int iA, int kB, int iB, int rs, DV &d, float imp) {
+// one row: returns the clamped impulse increment and applies it
+AVR_DI float row_go(const RowS &R, DV &d, float imp, float lo, float hi, bool robot) {
     const int lane = lane_id();
-    v3 dir = k == 0 ? ld3(r.n) : (k == 1 ? ld3(r.t1) : ld3(r.t2));
-    int nrob = (kA == 1) + (kB == 1);
-    int slot = rs + k * nrob;
-    if (kA == 1 && lane < MAXD) d.rq += L.u.s.rsM[slot][lane] * imp;
-    if (kB == 1 && lane < MAXD) d.rq += L.u.s.rsM[slot + (kA == 1)][lane] * imp;
-    if (kA == 2) free_apply(d, iA, scl(dir, 1.f / m.fb_mass[iA]), iinv_mul(L, iA, crs(ld3(r.rA), dir)), imp);
-    if (kB == 2) {
-        v3 nd = scl(dir, -1.f);
-        free_apply(d, iB, scl(nd, 1.f / m.fb_mass[iB]), iinv_mul(L, iB, crs(ld3(r.rB), nd)), imp);
-    }
-}
-
-AVR_DI float clamp_imp(float imp, float delta, float lo, float hi, float &ni) {
-    float sum = imp + delta;
-    if (sum < lo) { ni = lo; return lo - imp; }
-    if (sum > hi) { ni = hi; return hi - imp; }
-    ni = sum;
-    return delta;
+    const int info = __float_as_int(R.h[0]);
+    const int iA = info & 63, iB = (info >> 6) & 63;
+    // A: J = a[0..5], MJ = a[6..11]; B: J = a[12..15] b[0..1], MJ = b[2..7]
+    float pA = R.a[0] * d.vx + R.a[1] * d.vy + R.a[2] * d.vz + R.a[3] * d.wx + R.a[4] * d.wy + R.a[5] * d.wz;
+    float pB = R.a[12] * d.vx + R.a[13] * d.vy + R.a[14] * d.vz + R.a[15] * d.wx + R.b[0] * d.wy + R.b[1] * d.wz;
+    float p = (lane == iA ? pA : 0.f) + (lane == iB ? pB : 0.f);
+    if (robot) p += R.jr * d.rq;
+    float dv = robot_reduce(p);
+    float inv = R.h[2], rhs = R.h[3];
+    float sum = imp + (rhs - dv * inv);
+    float ni = fminf(fmaxf(sum, lo), hi);
+    float delta = ni - imp;
+    float cA = lane == iA ? delta : 0.f, cB = lane == iB ? delta : 0.f;
+    d.vx += R.a[6] * cA + R.b[2] * cB;
+    d.vy += R.a[7] * cA + R.b[3] * cB;
+    d.vz += R.a[8] * cA + R.b[4] * cB;
+    d.wx += R.a[9] * cA + R.b[5] * cB;
+    d.wy += R.a[10] * cA + R.b[6] * cB;
+    d.wz += R.a[11] * cA + R.b[7] * cB;
+    if (robot) d.rq += R.mr * delta;
+    return ni;
 }
 
 // Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order):
-// non-contact rows (alternating sweep direction), normal rows, friction rows.
-AVR_DI void solve(const KModel &m, EnvLDS &L) {
+// non-contact rows (alternating sweep direction), normal rows, friction rows.  Impulses are
+// lane-distributed registers: nc row j -> lane j of inc; normal c -> lane c&63 of in0/in1;
+// friction row f -> lane f&63 of if0/if1/if2.
+AVR_DI void solve(const KModel &m, EnvLDS &L, float *rows) {
     const int lane = lane_id();
     const int n_nc = uni(L.n_nc), n_c = uni(L.n_c);
+    // row records were written by vector stores of this wave: wait for them to reach L2 and
+    // drop any stale scalar-cache lines from the previous sub-step before reading them.
+    // s_dcache_inv is itself a scalar-memory op: wait for it before the first row s_load, or
+    // that load can still hit a stale line from the previous sub-step's rows.
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("s_dcache_inv\n\ts_waitcnt lgkmcnt(0)" : "+s"(rows) :: "memory");
     DV d;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
-    // warm start, in contact order
-    for (int i = 0; i < n_c; i++) {
-        const CRow &r = L.u.s.cr[i];
-        int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
-        if (rs < 0 && (kA == 1 || kB == 1)) continue;
-        float imp = unif(r.imp[0]);
-        if (imp != 0.f) crow_apply(m, L, r, 0, kA, iA, kB, iB, rs, d, imp);
+    float inc = 0.f, in0 = 0.f, in1 = 0.f, if0 = 0.f, if1 = 0.f, if2 = 0.f;
+    // warm start (normal rows, contact order): impulse = cached * warmstart factor
+    for (int c = 0; c < n_c; c++) {
+        const float *rec = row_rec(m, rows, n_nc + c);
+        RowS R;
+        float imp0 = (*(cf8p)rec)[6];
+        if (lane == (c & 63)) { if (c < 64) in0 = imp0; else in1 = imp0; }
+        if (imp0 == 0.f) continue;
+        bool robot = (__float_as_int((*(cf8p)rec)[0]) & RI_ROBOT) != 0;
+        load_row(R, rec, row_rob(m, rows, n_nc + c), robot);
+        // apply M^-1 J^T imp0 (row_go with imp fixed: lo = hi = imp0 around 0 -> delta = imp0)
+        (void)row_go(R, d, 0.f, imp0, imp0, robot);
     }
-    for (int it = 0; it < m.iters; it++) {
-        for (int j = 0; j < n_nc; j++) {
-            int k = (it & 1) ? j : n_nc - 1 - j;
-            NCRow &r = L.u.s.nc[k];
-            int fb = uni(r.fb);
-            float p = lane < MAXD ? r.JA[lane] * d.rq : 0.f;
-            float dv = robot_reduce(p);
-            if (fb >= 0) dv += free_dot_dv(d, fb, ld3(r.JB), ld3(r.JB + 3));
-            float inv = unif(r.inv), imp = unif(r.imp);
-            float ni;
-            float delta = clamp_imp(imp, unif(r.rhs) - dv * inv, unif(r.lo), unif(r.hi), ni);
-            if (lane < MAXD) d.rq += r.MA[lane] * delta;
-            if (fb >= 0) free_apply(d, fb, ld3(r.MB), ld3(r.MB + 3), delta);
-            if (lane == 0) r.imp = ni;
+    // One flat sweep over (iteration, position); position p < n_nc: non-contact rows (sweep
+    // direction alternates), then n_c normal rows, then 2 n_c friction rows.  The next row's
+    // loads are issued while the current row resolves; the empty asm makes the prefetch address
+    // depend on the current row's header so its s_load is issued after the current data landed
+    // (s_load returns out of order, so any wait on the scalar counter is a wait for all).
+    const int T = n_nc + 3 * n_c;
+    const int G = m.iters * T, iters = m.iters;
+    const float *robs = row_rob(m, rows, 0);
+    RowS cur;
+    if (G > 0) load_row(cur, row_rec(m, rows, n_nc - 1), robs + (n_nc - 1) * RW, true);
+    int it = 0, p = 0;
+    for (int g = 0; g < G; g++) {
+        int p1 = p + 1, it1 = it;
+        if (p1 == T) { p1 = 0; it1++; }
+        int rn = p1 < n_nc ? ((it1 & 1) ? p1 : n_nc - 1 - p1) : p1;
+        if (it1 == iters) rn = 0;
+#ifdef AVR_NO_PREFETCH
+        {
+            int rc = p < n_nc ? ((it & 1) ? p : n_nc - 1 - p) : p;
+            load_row(cur, row_rec(m, rows, rc), robs + rc * RW, true);
         }
-        for (int i = 0; i < n_c; i++) {
-            CRow &r = L.u.s.cr[i];
-            int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
-            if (rs < 0 && (kA == 1 || kB == 1)) continue;
-            float dv = crow_dot(m, L, r, 0, kA, iA, kB, iB, rs, d);
-            float imp = unif(r.imp[0]), ni;
-            float delta = clamp_imp(imp, unif(r.rhs[0]) - dv * unif(r.inv[0]), 0.f, 1e10f, ni);
-            crow_apply(m, L, r, 0, kA, iA, kB, iB, rs, d, delta);
-            if (lane == 0) r.imp[0] = ni;
-        }
-        for (int i = 0; i < n_c; i++) {
-            CRow &r = L.u.s.cr[i];
-            int kA = uni(r.kA), kB = uni(r.kB), iA = uni(r.iA), iB = uni(r.iB), rs = uni(r.rs);
-            if (rs < 0 && (kA == 1 || kB == 1)) continue;
-            float nimp = unif(r.imp[0]);
-            if (!(nimp > 0.f)) continue;
-            float fr = unif(r.fric);
-            float lo = -fr * nimp, hi = fr * nimp;
-            for (int k = 1; k < 3; k++) {
-                float dv = crow_dot(m, L, r, k, kA, iA, kB, iB, rs, d);
-                float imp = unif(r.imp[k]), ni;
-                float delta = clamp_imp(imp, unif(r.rhs[k]) - dv * unif(r.inv[k]), lo, hi, ni);
-                crow_apply(m, L, r, k, kA, iA, kB, iB, rs, d, delta);
-                if (lane == 0) r.imp[k] = ni;
+        RowS nxt = cur;
+#else
+        const float *recn = row_rec(m, rows, rn);
+        asm volatile("" : "+s"(recn) : "s"(cur.h[0]));
+        RowS nxt;
+        load_row(nxt, recn, robs + rn * RW, true);
+#endif
+        if (p < n_nc) {
+            const int k = (it & 1) ? p : n_nc - 1 - p;
+            float imp = rdl(inc, k);
+            float ni = row_go(cur, d, imp, cur.h[4], cur.h[5], true);
+            if (lane == k) inc = ni;
+        } else if (p < n_nc + n_c) {
+            const int c = p - n_nc;
+            const bool robot = (__float_as_int(cur.h[0]) & RI_ROBOT) != 0;
+            float imp = rdl(c < 64 ? in0 : in1, c & 63);
+            float ni = row_go(cur, d, imp, 0.f, 1e10f, robot);
+            if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
+        } else {
+            const int f = p - n_nc - n_c, c = f >> 1;
+            float nimp = rdl(c < 64 ? in0 : in1, c & 63);
+            if (nimp > 0.f) {
+                const bool robot = (__float_as_int(cur.h[0]) & RI_ROBOT) != 0;
+                float fr = cur.h[1];
+                const int s = f >> 6;
+                float imp = rdl(s == 0 ? if0 : (s == 1 ? if1 : if2), f & 63);
+                float ni = row_go(cur, d, imp, -fr * nimp, fr * nimp, robot);
+                if (lane == (f & 63)) { if (s == 0) if0 = ni; else if (s == 1) if1 = ni; else if2 = ni; }
             }
         }
+        cur = nxt;
+        p = p1; it = it1;
     }
-    SYNC();
     if (lane < MAXD) L.dq[lane] = d.rq;
     if (lane < MAXF) {
         L.dfv[lane][0] = d.vx; L.dfv[lane][1] = d.vy; L.dfv[lane][2] = d.vz;
         L.dfw[lane][0] = d.wx; L.dfw[lane][1] = d.wy; L.dfw[lane][2] = d.wz;
     }
-    // write back normal impulses to the manifold points (warm start + normalForce)
-    for (int i = lane; i < n_c; i += 64) {
-        CRow &r = L.u.s.cr[i];
-        L.st[AVR_S_CP + AVR_CP_WORDS * r.cp + AVR_CP_IMP] = r.imp[0];
-    }
+    // normal impulses back to the manifold points (warm start + normalForce); rows are in
+    // contact order, so contact c is manifold point c
+    if (lane < n_c) L.st[AVR_S_CP + AVR_CP_WORDS * lane + AVR_CP_IMP] = in0;
+    if (lane + 64 < n_c) L.st[AVR_S_CP + AVR_CP_WORDS * (lane + 64) + AVR_CP_IMP] = in1;
     SYNC();
 }
 
@@ -1528,11 +1534,13 @@ AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
     }
     SYNC();
     PROF_STOP(6, ps);
-    build_noncontact_rows(m, L, dt);
+    float *rows = m.rows + (size_t)blockIdx.x * (size_t)(2 * m.rowcap * RW);
+    const int n_nc = build_noncontact_rows(m, L, rows, dt);
     PROF_STOP(7, ps);
-    build_contact_rows(m, L, dt);
+    build_contact_rows(m, L, rows, n_nc, dt);
+    SYNC();
     PROF_STOP(8, ps);
-    solve(m, L);
+    solve(m, L, rows);
     PROF_STOP(9, ps);
     // integrate
     if (lane < m.nd) {

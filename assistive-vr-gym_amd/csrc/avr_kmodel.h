@@ -11,7 +11,6 @@
 #define MAXSP 256
 #define MAXAP 256
 #define MAXNC 32
-#define MAXRS 64
 #define SMALL_NV 64
 #define GJK_MAX_IT 64
 #define GJK_REL_EPS 1e-6f
@@ -55,5 +54,7 @@ struct KModel {
     int env_offset;
     int dof_link[MAXD];        // link owning each DoF
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+    float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
+    int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
 };

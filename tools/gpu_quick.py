@@ -5,6 +5,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd')); sys.path.insert(0, ROOT)
 from avr import _abi as ABI, reset as RS, _lib
 from oracle.oracle import Oracle
+if len(sys.argv) > 3:
+    _lib.LIB_PATH = os.path.join(ROOT, 'assistive-vr-gym_amd', 'avr', sys.argv[3]); _lib.load(_lib.LIB_PATH)
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
