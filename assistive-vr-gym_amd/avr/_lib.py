@@ -17,7 +17,7 @@ EXPORTS = [
     'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',
     'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_state_words', 'avr_abi_version',
-    'avr_kernel_info', 'avr_last_error', 'avr_substep',
+    'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset',
 ]
 
 
@@ -65,6 +65,7 @@ def load(path=LIB_PATH):
     lib.avr_last_error.argtypes = [vp]
     lib.avr_last_error.restype = C.c_char_p
     lib.avr_substep.argtypes = [vp, C.c_float]
+    lib.avr_reset.argtypes = [vp, vp, vp, C.c_int32, vp]
     _LIB = lib
     return lib
 
@@ -120,6 +121,16 @@ class Sim:
     def settle(self, frames=100):
         obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
         self._chk(self.lib.avr_settle(self.h, frames, obs.ctypes.data))
+        return obs
+
+    def reset(self, mask, S, frames=100, obs=None):
+        """Masked episode reset (include/avr.h avr_reset): rows of S for mask!=0, settle, obs."""
+        S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.n)
+        if obs is None:
+            obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.shape == (self.n, ABI.OBS_DIM)
+        self._chk(self.lib.avr_reset(self.h, None if m is None else m.ctypes.data, S.ctypes.data, int(frames), obs.ctypes.data))
         return obs
 
     def substep(self, dt):

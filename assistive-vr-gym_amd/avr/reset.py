@@ -192,7 +192,7 @@ def human_slot_poses(A, gender, q):
 # ----------------------------------------------------------------------------- full reset
 def feeding_reset_state(A, md, seed, env_id, gender=None, impairment='none'):
     """One env's initial state block (float64[STATE_WORDS]) before the settle frames."""
-    rng = np.random.default_rng([int(seed), int(env_id)])
+    rng = _rng(seed, env_id)
     if gender is None:
         gender = 'male' if rng.integers(2) == 0 else 'female'     # feeding.py:169
     limit_scale = rng.uniform(0.5, 1.0) if impairment == 'limits' else 1.0   # world_creation.py:71
@@ -360,12 +360,19 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, r
     return Qout, done
 
 
-def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none'):
+def _rng(seed, env_id, episode=0):
+    """Per-env, per-episode reset stream: independent of batch composition and GPU count."""
+    key = [int(seed), int(env_id)] if not episode else [int(seed), int(env_id), int(episode)]
+    return np.random.default_rng(key)
+
+
+def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none', episodes=None):
     """Vectorised equivalent of batch_reset_states (same per-env draws and acceptance rules,
-    IK batched across envs)."""
+    IK batched across envs).  episodes[k] selects the k-th env's episode stream (default 0)."""
     env_ids = list(env_ids)
     N = len(env_ids)
-    rngs = [np.random.default_rng([int(seed), int(e)]) for e in env_ids]
+    eps = [0] * N if episodes is None else list(episodes)
+    rngs = [_rng(seed, e, ep) for e, ep in zip(env_ids, eps)]
     S = np.zeros((N, ABI.STATE_WORDS))
     gl, tpos, bowl = [], np.zeros((N, 3)), np.zeros((N, 3))
     for k in range(N):

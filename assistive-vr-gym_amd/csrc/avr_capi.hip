@@ -15,7 +15,8 @@
 #include "avr_kmodel.h"
 
 extern "C" hipError_t avr_launch_step(const KModel *m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
-                                      float *info, int mode, long long t, int n_envs, hipStream_t stream);
+                                      float *info, const unsigned char *mask, int mode, long long t, int n_envs, hipStream_t stream);
+extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
 extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream);
 extern "C" hipError_t avr_kernel_attrs(int *out4);
@@ -27,6 +28,8 @@ struct avr_sim {
     hipStream_t stream;
     std::vector<void *> allocs;
     float *d_state;
+    float *d_stage;     // [n_envs][STATE_WORDS] host-upload staging (masked resets)
+    uint8_t *d_mask;    // [n_envs]
     float *d_act, *d_obs, *d_rew, *d_info;
     unsigned char *d_done;
     char err[512];
@@ -207,6 +210,8 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     HIPCHK(s, hipMalloc(&s->d_rew, E * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_done, E));
     HIPCHK(s, hipMalloc(&s->d_info, E * AVR_INFO_DIM * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_stage, E * AVR_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_mask, E));
     return 0;
 }
 
@@ -221,6 +226,8 @@ extern "C" int avr_destroy(avr_sim *s) {
     if (s->d_rew) (void)hipFree(s->d_rew);
     if (s->d_done) (void)hipFree(s->d_done);
     if (s->d_info) (void)hipFree(s->d_info);
+    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->d_mask) (void)hipFree(s->d_mask);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return 0;
@@ -241,11 +248,40 @@ extern "C" int avr_set_state(avr_sim *s, const float *h) {
     return 0;
 }
 
+// Masked upload: the whole host array and the mask go up once, a copy kernel moves the
+// selected env rows (one transfer instead of one per env).
+static int upload_masked(avr_sim *s, const uint8_t *mask, const float *h) {
+    const size_t E = (size_t)s->cfg.n_envs;
+    HIPCHK(s, hipMemcpyAsync(s->d_stage, h, E * AVR_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(s->d_mask, mask, E, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, avr_launch_copy_masked(s->d_state, s->d_stage, s->d_mask, s->cfg.n_envs, s->stream));
+    return 0;
+}
+
 extern "C" int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float *h) {
     CHECK_SIM(s);
-    const size_t W = AVR_STATE_WORDS * sizeof(float);
-    for (int e = 0; e < s->cfg.n_envs; e++)
-        if (!mask || mask[e]) HIPCHK(s, hipMemcpyAsync(s->d_state + (size_t)e * AVR_STATE_WORDS, h + (size_t)e * AVR_STATE_WORDS, W, hipMemcpyHostToDevice, s->stream));
+    if (!mask) return avr_set_state(s, h);
+    if (upload_masked(s, mask, h)) return -2;
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_t n_frames, float *host_obs) {
+    CHECK_SIM(s);
+    const size_t E = (size_t)s->cfg.n_envs;
+    std::vector<uint8_t> all;
+    if (!mask) { all.assign(E, 1); mask = all.data(); }
+    if (!h) return fail(s, -1, "avr_reset: host_state is NULL");
+    if (n_frames < 0) return fail(s, -1, "avr_reset: n_frames < 0");
+    if (upload_masked(s, mask, h)) return -2;
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream));
+    if (host_obs) {
+        std::vector<float> o(E * AVR_OBS_DIM);
+        HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(s, hipStreamSynchronize(s->stream));
+        for (size_t e = 0; e < E; e++)
+            if (mask[e]) memcpy(host_obs + e * AVR_OBS_DIM, o.data() + e * AVR_OBS_DIM, AVR_OBS_DIM * sizeof(float));
+    }
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
@@ -259,7 +295,7 @@ extern "C" int avr_get_state(avr_sim *s, float *h) {
 
 extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream));
     if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
@@ -269,21 +305,21 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, 3, t, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
     return 0;
 }
 
 extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
     HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
-                              d_info ? d_info : s->d_info, 1, t, s->cfg.n_envs, s->stream));
+                              d_info ? d_info : s->d_info, nullptr, 1, t, s->cfg.n_envs, s->stream));
     return 0;
 }
 
@@ -297,7 +333,7 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
     HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));

@@ -1652,12 +1652,13 @@ enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 
 __global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
                                                       float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
-                                                      int mode, long long t, int n_envs) {
+                                                      const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
     __shared__ EnvLDS L;
     const KModel &m = *mp;
     const int env = blockIdx.x;
     const int lane = lane_id();
     if (env >= n_envs) return;
+    if (mask && !mask[env]) return;   // masked launches (reset/settle of a subset) leave the rest untouched
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) L.st[i] = gst[i];
     if (lane == 0) { L.flags = 0; L.gender = 0; }
@@ -1794,6 +1795,18 @@ __global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__
 #endif
 }
 
+// state[e] = src[e] for the envs whose mask byte is set (masked reset upload)
+__global__ void avr_copy_masked_kernel(float *state, const float *src, const unsigned char *mask, int n_envs) {
+    const int e = blockIdx.x;
+    if (e >= n_envs || !mask[e]) return;
+    for (int i = threadIdx.x; i < AVR_STATE_WORDS; i += blockDim.x) state[(size_t)e * AVR_STATE_WORDS + i] = src[(size_t)e * AVR_STATE_WORDS + i];
+}
+extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st) {
+    if (n_envs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_copy_masked_kernel, dim3(n_envs), dim3(256), 0, st, state, src, mask, n_envs);
+    return hipGetLastError();
+}
+
 __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_envs * AVR_ACT_DIM) return;
@@ -1803,8 +1816,9 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 
 // host-side launch helpers (used by avr_capi.hip)
 extern "C" hipError_t avr_launch_step(const KModel *d_m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
-                                      float *info, int mode, long long t, int n_envs, hipStream_t stream) {
-    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mode, t, n_envs);
+                                      float *info, const unsigned char *mask, int mode, long long t, int n_envs, hipStream_t stream) {
+    if (n_envs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mask, mode, t, n_envs);
     return hipGetLastError();
 }
 

@@ -76,6 +76,7 @@ def main():
     import numpy as np
     import torch
     from avr import _abi as ABI, reset as RS, _lib
+    from avr import dist as D
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -92,7 +93,7 @@ def main():
     E = args.envs
     # reset pool: distinct initial states for global env ids; tiled if pool < E
     pool = min(args.reset_pool, E)
-    base_id = rank * E
+    base_id, _ = D.shard(E, rank)
     S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)])
     S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
     sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
@@ -105,20 +106,17 @@ def main():
     info = torch.zeros(E, ABI.INFO_DIM, device=dev)
     ext = torch.cuda.ExternalStream(sim.stream(), device=dev)
     G = args.gather_every
-    roll = torch.zeros(G, E, ABI.OBS_DIM + 1 + ABI.INFO_DIM + 1, device=dev)
-    gathered = torch.zeros(world * G * E * roll.shape[-1], device=dev) if world > 1 else None
+    roll = torch.zeros(G, E, D.ROLL_WIDTH, device=dev)
+    gathered = torch.zeros(world * G * E * D.ROLL_WIDTH, device=dev) if world > 1 else None
 
     def one_step(t, k):
         sim.step_random_device(t, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr())
         if world > 1:
             with torch.cuda.stream(ext):
                 j = k % G
-                roll[j, :, :ABI.OBS_DIM] = obs
-                roll[j, :, ABI.OBS_DIM] = rew
-                roll[j, :, ABI.OBS_DIM + 1:ABI.OBS_DIM + 1 + ABI.INFO_DIM] = info
-                roll[j, :, -1] = done.float()
+                D.pack_rollout(roll, j, obs, rew, info, done)
                 if j == G - 1:
-                    dist.all_gather_into_tensor(gathered, roll.reshape(-1))
+                    D.gather_rollouts(roll, out=gathered)
 
     for w in range(args.warmup):
         one_step(w, w)

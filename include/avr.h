@@ -61,6 +61,13 @@ int avr_set_state_masked(avr_sim *sim, const uint8_t *env_mask, const float *hos
  * observation (feeding.py:319-320, 325).  obs may be NULL. */
 int avr_settle(avr_sim *sim, int32_t n_frames, float *host_obs);
 
+/* Episode reset of the envs whose mask byte is non-zero (mask NULL = all): their state rows
+ * are taken from host_state[n_envs*STATE_WORDS] (the host reset path: scene randomisation and
+ * IK, feeding.py:144-307), then n_frames x stepSimulation drop the food into the spoon
+ * (feeding.py:318-320) and their reset observation goes to host_obs rows (feeding.py:325).
+ * Unmasked envs and their host_obs rows are left untouched.  Replaces FeedingEnv.reset(). */
+int avr_reset(avr_sim *sim, const uint8_t *env_mask, const float *host_state, int32_t n_frames, float *host_obs);
+
 /* One gym step for every env: act[n_envs*7] -> obs[n_envs*25], rew[n_envs],
  * done[n_envs] (TimeLimit 200), info[n_envs*2] = {total_force_on_human, task_success}. */
 int avr_step(avr_sim *sim, const float *act, float *obs, float *rew, uint8_t *done, float *info);
@@ -83,6 +90,10 @@ int32_t avr_abi_version(void);
 /* Kernel resource usage: [vgprs, sgprs, lds_bytes, scratch_bytes] of the step kernel. */
 int avr_kernel_info(avr_sim *sim, int32_t *out4);
 const char *avr_last_error(avr_sim *sim);
+
+/* Diagnostics (phase-timer builds only, -DAVR_PROF): attach a device buffer of
+ * [n_envs][16] uint64 cycle counters.  A no-op for the shipped kernel. */
+int avr_set_profile_buffer(avr_sim *sim, void *d_prof);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,41 @@
+"""Host side of the gym facade (no GPU): registry mirrors the reference's ids, spaces, errors."""
+import re
+
+import numpy as np
+import pytest
+
+from avr import env as E
+from avr import _abi as ABI
+
+
+def test_registry_has_every_reference_id():
+    # ids registered by assistive_gym/__init__.py (49 ids: 4 tasks x {PR2, Jaco} x 6 variants + HumanTesting)
+    assert len(E.REGISTRY) == 49
+    assert E.REGISTRY['FeedingJaco-v0'] == ('feeding', 'jaco', True)
+    assert sum(v[2] for v in E.REGISTRY.values()) == 1
+    for k in E.REGISTRY:
+        assert re.match(r'^[A-Za-z0-9]+-v0$', k)
+
+
+def test_unbuilt_ids_raise_not_implemented():
+    with pytest.raises(NotImplementedError):
+        E.AVRVecEnv('ScratchItchPR2-v0', 4)
+    with pytest.raises(KeyError):
+        E.AVRVecEnv('NoSuchEnv-v0', 4)
+
+
+def test_spaces():
+    b = E.Box(-1.0, 1.0, (ABI.ACT_DIM,))
+    x = b.sample(np.random.default_rng(0))
+    assert x.shape == (7,) and x.dtype == np.float32 and b.contains(x)
+    assert not b.contains(np.full(7, 2.0, np.float32))
+    assert ABI.OBS_DIM == 25 and ABI.ACT_DIM == 7 and ABI.INFO_DIM == 2
+
+
+def test_constants_follow_reference():
+    assert E.MAX_EPISODE_STEPS == 200      # TimeLimit in assistive_gym/__init__.py
+    assert E.SETTLE_FRAMES == 100          # feeding.py:318-320
+    P = ABI.FEEDING_PARAMS
+    assert P['num_sub_steps'] == 2 and P['solver_iterations'] == 10    # feeding.py:289
+    assert P['time_step'] == 0.02                                      # world_creation.py:75
+    assert P['frame_skip'] == 5
