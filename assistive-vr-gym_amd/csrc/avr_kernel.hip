@@ -1650,10 +1650,13 @@ AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j)
 
 enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 
-__global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
-                                                      float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
-                                                      const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
-    __shared__ EnvLDS L;
+// One body, two kernels: TASK = gym step (take_step + frames + task glue; modes STEP,
+// STEP_RANDOM), !TASK = physics only (SETTLE frames, single SUBSTEP).  Separate symbols keep the
+// settle launch out of the step kernel's profile.
+template <bool TASK>
+AVR_DI void env_kernel_body(EnvLDS &L, const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
+                            float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
+                            const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
     const KModel &m = *mp;
     const int env = blockIdx.x;
     const int lane = lane_id();
@@ -1672,9 +1675,9 @@ __global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__
     const int nsub = m.nsub > 0 ? m.nsub : 1;
     const float dt = m.time_step / (float)nsub;
     bool ok = true;
-    if (mode == MODE_SUBSTEP) {
+    if (!TASK && mode == MODE_SUBSTEP) {
         ok = substep(m, L, *(const float *)&t);
-    } else if (mode == MODE_SETTLE) {
+    } else if (!TASK) {
         for (long long f = 0; f < t; f++)
             for (int s = 0; s < nsub; s++) ok &= substep(m, L, dt);
         mouth_target(m, L);
@@ -1795,6 +1798,19 @@ __global__ __launch_bounds__(64) void avr_step_kernel(const KModel *__restrict__
 #endif
 }
 
+__global__ __launch_bounds__(64) void avr_env_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
+                                                          float *__restrict__ obs, float *__restrict__ rew, unsigned char *__restrict__ done,
+                                                          float *__restrict__ info, const unsigned char *__restrict__ mask, int mode, long long t,
+                                                          int n_envs) {
+    __shared__ EnvLDS L;
+    env_kernel_body<true>(L, mp, state, act, obs, rew, done, info, mask, mode, t, n_envs);
+}
+__global__ __launch_bounds__(64) void avr_physics_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ obs,
+                                                         const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
+    __shared__ EnvLDS L;
+    env_kernel_body<false>(L, mp, state, nullptr, obs, nullptr, nullptr, nullptr, mask, mode, t, n_envs);
+}
+
 // state[e] = src[e] for the envs whose mask byte is set (masked reset upload)
 __global__ void avr_copy_masked_kernel(float *state, const float *src, const unsigned char *mask, int n_envs) {
     const int e = blockIdx.x;
@@ -1818,7 +1834,10 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 extern "C" hipError_t avr_launch_step(const KModel *d_m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
                                       float *info, const unsigned char *mask, int mode, long long t, int n_envs, hipStream_t stream) {
     if (n_envs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(avr_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mask, mode, t, n_envs);
+    if (mode == MODE_SETTLE || mode == MODE_SUBSTEP)
+        hipLaunchKernelGGL(avr_physics_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, mask, mode, t, n_envs);
+    else
+        hipLaunchKernelGGL(avr_env_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mask, mode, t, n_envs);
     return hipGetLastError();
 }
 
@@ -1831,7 +1850,7 @@ extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env
 
 extern "C" hipError_t avr_kernel_attrs(int *out4) {
     hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, (const void *)avr_step_kernel);
+    hipError_t e = hipFuncGetAttributes(&a, (const void *)avr_env_step_kernel);
     if (e != hipSuccess) return e;
     out4[0] = a.numRegs;
     out4[1] = 0;

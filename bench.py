@@ -26,13 +26,16 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def algorithmic_bytes_per_env_step(ABI):
-    """Bytes the step must move per env per gym step: the per-env state block read once and
-    written once (it stays in LDS across the 10 sub-steps), plus the I/O (actions are generated
-    on the device; obs 25 f32, reward f32, done u8, info 2 f32 written)."""
-    state = ABI.STATE_WORDS * 4
-    io_out = (ABI.OBS_DIM + 1 + ABI.INFO_DIM) * 4 + 1
-    return 2 * state + io_out
+# algorithmic bytes per FeedingJaco env-step = persistent state read + written once
+# (605 words, 2420 B each way) + read-only per-env params (144 B) + action in (28 B) + obs,
+# reward, done, info out (116 B).
+ALGO_BYTES_PER_ENV_STEP = 2420 * 2 + 144 + 28 + 116      # 5128
+
+
+def layout_bytes_per_env_step(ABI):
+    """What this build's state layout actually moves per env-step (state block in and out once,
+    it stays in LDS across the 10 sub-steps; actions are generated on the device)."""
+    return 2 * ABI.STATE_WORDS * 4 + (ABI.OBS_DIM + 1 + ABI.INFO_DIM) * 4 + 1
 
 
 def cpu_baseline(md, A, RS, seconds, threads):
@@ -144,7 +147,7 @@ def main():
     St = sim.get_state()
     flags = St[:, ABI.S_TASK + ABI.T_FLAGS].astype(np.int64)
     value = world * E * args.steps / el
-    bpe = algorithmic_bytes_per_env_step(ABI)
+    bpe = ALGO_BYTES_PER_ENV_STEP
     achieved = bpe * E / (kern_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
@@ -173,7 +176,8 @@ def main():
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'bytes_per_env_step': bpe, 'kernel_ms': kern_ms},
+                     'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(ABI),
+                     'kernel': 'avr_env_step_kernel', 'kernel_ms': kern_ms},
         'nan_or_overflow_envs': int(np.count_nonzero(flags)),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,86 @@
+"""Summarise rocprofv3 rocpd databases (ROCm 7.2 default output) into profiles/.
+
+    python tools/rocpd_summary.py <prof_dir> <round_tag> [envs]
+
+<prof_dir>/kt/*.db     --kernel-trace --stats run  -> profiles/<tag>_kernel_stats.csv
+<prof_dir>/fetch/*.db  --pmc FETCH_SIZE            -> } profiles/pmc_traffic.json and
+<prof_dir>/write/*.db  --pmc WRITE_SIZE            -> } profiles/<tag>_pmc.json
+<prof_dir>/sq/*.db     --pmc SQ_* instruction mix  -> }
+FETCH_SIZE is doubled (gfx950: it reports half the bytes of 128-B requests, MI355X_MICROARCH.md
+HBM section); WRITE_SIZE is taken as is.  Counter values are per dispatch, in KiB.
+"""
+import glob
+import json
+import os
+import sqlite3
+import sys
+
+import numpy as np
+
+STEP = 'avr_env_step_kernel'
+
+
+def db(d):
+    f = sorted(glob.glob(os.path.join(d, '*.db')))
+    return sqlite3.connect(f[0]) if f else None
+
+
+def kernel_stats(c):
+    rows = c.execute('select name, duration from kernels').fetchall()
+    by = {}
+    for n, d in rows:
+        by.setdefault(n.split('(')[0], []).append(d)
+    out = []
+    tot = sum(sum(v) for v in by.values())
+    for n, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        v = np.array(v, float)
+        out.append((n, len(v), v.sum(), v.mean(), np.median(v), v.min(), v.max(), 100 * v.sum() / tot))
+    return out
+
+
+def counters(c, names):
+    res = {}
+    for n in names:
+        v = [r[0] for r in c.execute("select value from counters_collection where counter_name=? and kernel_name like ?", (n, STEP + '%'))]
+        if v:
+            res[n] = float(np.median(v))
+    return res
+
+
+def main(pdir, tag, envs=4096):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, 'profiles')
+    os.makedirs(prof, exist_ok=True)
+    c = db(os.path.join(pdir, 'kt'))
+    if c:
+        st = kernel_stats(c)
+        with open(os.path.join(prof, '%s_kernel_stats.csv' % tag), 'w') as f:
+            f.write('kernel,calls,total_ns,avg_ns,median_ns,min_ns,max_ns,pct\n')
+            for r in st:
+                f.write('%s,%d,%.0f,%.1f,%.1f,%.0f,%.0f,%.2f\n' % r)
+        for r in st:
+            print('%-28s calls %4d avg %10.3f ms  median %10.3f ms  %5.1f%%' % (r[0], r[1], r[3] / 1e6, r[4] / 1e6, r[7]))
+    out = {'kernel': STEP, 'envs': envs}
+    cf, cw, cs = db(os.path.join(pdir, 'fetch')), db(os.path.join(pdir, 'write')), db(os.path.join(pdir, 'sq'))
+    if cf:
+        out['FETCH_SIZE_KiB_raw'] = counters(cf, ['FETCH_SIZE']).get('FETCH_SIZE')
+    if cw:
+        out['WRITE_SIZE_KiB'] = counters(cw, ['WRITE_SIZE']).get('WRITE_SIZE')
+    if cs:
+        out['sq'] = counters(cs, ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_INSTS_LDS', 'SQ_WAIT_ANY',
+                                  'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES'])
+    if out.get('FETCH_SIZE_KiB_raw') is not None and out.get('WRITE_SIZE_KiB') is not None:
+        fb = 2 * out['FETCH_SIZE_KiB_raw'] * 1024
+        wb = out['WRITE_SIZE_KiB'] * 1024
+        out['hbm_read_bytes_per_launch'] = fb
+        out['hbm_write_bytes_per_launch'] = wb
+        out['hbm_bytes_per_launch'] = fb + wb
+        out['hbm_bytes_per_env_step'] = (fb + wb) / envs
+        out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median over step-kernel dispatches'
+        json.dump(out, open(os.path.join(prof, 'pmc_traffic.json'), 'w'), indent=1)
+    json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4096)
