@@ -162,9 +162,10 @@ class Sim:
         return self.lib.avr_stream(self.h)
 
     def kernel_info(self):
-        out = np.zeros(4, np.int32)
+        out = np.zeros(8, np.int32)
         self._chk(self.lib.avr_kernel_info(self.h, out.ctypes.data))
-        return dict(vgprs=int(out[0]), lds_bytes=int(out[2]), scratch_bytes=int(out[3]))
+        return dict(vgprs=int(out[0]), lds_bytes=int(out[2]), scratch_bytes=int(out[3]),
+                    b_vgprs=int(out[4]), b_lds_bytes=int(out[6]), b_scratch_bytes=int(out[7]))
 
 
 # ---------------------------------------------------------------- Philox4x32-10 (host mirror)

@@ -14,12 +14,13 @@
 #define AVR_KMODEL_ONLY
 #include "avr_kmodel.h"
 
-extern "C" hipError_t avr_launch_step(const KModel *m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
-                                      float *info, const unsigned char *mask, int mode, long long t, int n_envs, hipStream_t stream);
+extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
+                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
+                                      hipStream_t stream);
 extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
 extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream);
-extern "C" hipError_t avr_kernel_attrs(int *out4);
+extern "C" hipError_t avr_kernel_attrs(int *out8);
 
 struct avr_sim {
     avr_config cfg;
@@ -200,6 +201,11 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         HIPCHK(s, hipMalloc(&rows, E * 2 * (size_t)k.rowcap * 32 * sizeof(float)));
         s->allocs.push_back(rows);
         k.rows = rows;
+        float *ws = nullptr;
+        HIPCHK(s, hipMalloc(&ws, E * 128 * sizeof(float)));
+        HIPCHK(s, hipMemset(ws, 0, E * 128 * sizeof(float)));
+        s->allocs.push_back(ws);
+        k.ws = ws;
     }
     HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
@@ -274,7 +280,7 @@ extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_
     if (!h) return fail(s, -1, "avr_reset: host_state is NULL");
     if (n_frames < 0) return fail(s, -1, "avr_reset: n_frames < 0");
     if (upload_masked(s, mask, h)) return -2;
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream));
     if (host_obs) {
         std::vector<float> o(E * AVR_OBS_DIM);
         HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
@@ -295,7 +301,7 @@ extern "C" int avr_get_state(avr_sim *s, float *h) {
 
 extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream));
     if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
@@ -305,20 +311,20 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
     return 0;
 }
 
 extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
                               d_info ? d_info : s->d_info, nullptr, 1, t, s->cfg.n_envs, s->stream));
     return 0;
 }
@@ -333,7 +339,7 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
     HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
-    HIPCHK(s, avr_launch_step(s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
     HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));
@@ -356,8 +362,8 @@ extern "C" int avr_set_profile_buffer(avr_sim *s, void *d_prof) {
     return 0;
 }
 
-extern "C" int avr_kernel_info(avr_sim *s, int32_t *out4) {
+extern "C" int avr_kernel_info(avr_sim *s, int32_t *out8) {
     (void)s;
-    hipError_t e = avr_kernel_attrs(out4);
+    hipError_t e = avr_kernel_attrs(out8);
     return e == hipSuccess ? 0 : -3;
 }

@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "../../include/avr.h"
+#include <cstring>
 #include "avr_math.h"
 
 #include "avr_kmodel.h"
@@ -903,6 +904,9 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         int nitems = na * nb;
+#ifdef AVR_PROF
+        if (lane == 0) L.prof[11] += nitems;
+#endif
         for (int base = 0; base < nitems; base += 64) {
             int it = base + lane;
             bool act = false;
@@ -931,6 +935,9 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         }
     }
     if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; nsp = MAXSP; }
+#ifdef AVR_PROF
+    if (lane == 0) { L.prof[14] += nsp; L.prof[15] += nap; }
+#endif
     SYNC();
     PROF_STOP(2, pt);
     // narrowphase pass A: one lane per small shape pair; big hulls and EPA deferred
@@ -1068,6 +1075,14 @@ AVR_DI float robot_dot(const KModel &m, const EnvLDS &L, const float *J, bool de
 // buffer: w0..11 J (A and B endpoints combined), w16..27 M^-1 J^T.  Everything a row resolve
 // needs is precomputed here, so the PGS chain (solve) is loads + register arithmetic only.
 #define RW 32
+// per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
+#define WS_WORDS 128
+#define WS_NNC 0     // int bits: non-contact rows
+#define WS_NC 1      // int bits: contact points (rows n_nc .. n_nc + 3 n_c)
+#define WS_ASQ 2     // sum of squared caller actions (take_step -> task glue)
+#define WS_VQ 16     // [MAXD] unconstrained robot velocities
+#define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
+#define WS_FW 72     // [MAXF][4] angular
 #define RI_NONE 63
 #define RI_ROBOT (1 << 12)
 
@@ -1387,101 +1402,71 @@ AVR_DI float row_go(const RowS &R, DV &d, float imp, float lo, float hi, bool ro
 }
 
 // Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order):
-// non-contact rows (alternating sweep direction), normal rows, friction rows.  Impulses are
-// lane-distributed registers: nc row j -> lane j of inc; normal c -> lane c&63 of in0/in1;
-// friction row f -> lane f&63 of if0/if1/if2.
-AVR_DI void solve(const KModel &m, EnvLDS &L, float *rows) {
+// non-contact rows (sweep direction alternates per iteration), normal rows, friction rows.
+// Impulses are lane-distributed registers: nc row j -> lane j of inc; normal c -> lane c&63 of
+// in0/in1; friction row f -> lane f&63 of if0/if1/if2.  Returns the delta velocities in d and
+// the normal impulses in in0/in1 (contact c at lane c&63).
+AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV &d, float &in0, float &in1) {
     const int lane = lane_id();
-    const int n_nc = uni(L.n_nc), n_c = uni(L.n_c);
-    // row records were written by vector stores of this wave: wait for them to reach L2 and
-    // drop any stale scalar-cache lines from the previous sub-step before reading them.
-    // s_dcache_inv is itself a scalar-memory op: wait for it before the first row s_load, or
-    // that load can still hit a stale line from the previous sub-step's rows.
-    __builtin_amdgcn_s_waitcnt(0);
+    // row records were written by vector stores of the previous kernel; the scalar cache may
+    // still hold lines of the previous sub-step's rows: invalidate it and wait for the
+    // invalidation (an SMEM op itself) before the first row s_load.
     asm volatile("s_dcache_inv\n\ts_waitcnt lgkmcnt(0)" : "+s"(rows) :: "memory");
-    DV d;
+    const float *robs = rows + m.rowcap * RW;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
-    float inc = 0.f, in0 = 0.f, in1 = 0.f, if0 = 0.f, if1 = 0.f, if2 = 0.f;
+    float inc = 0.f, if0 = 0.f, if1 = 0.f, if2 = 0.f;
+    in0 = 0.f; in1 = 0.f;
     // warm start (normal rows, contact order): impulse = cached * warmstart factor
     for (int c = 0; c < n_c; c++) {
-        const float *rec = row_rec(m, rows, n_nc + c);
-        RowS R;
-        float imp0 = (*(cf8p)rec)[6];
+        const float *rec = rows + (n_nc + c) * RW;
+        const f8 h = *(cf8p)rec;
+        const float imp0 = h[6];
         if (lane == (c & 63)) { if (c < 64) in0 = imp0; else in1 = imp0; }
         if (imp0 == 0.f) continue;
-        bool robot = (__float_as_int((*(cf8p)rec)[0]) & RI_ROBOT) != 0;
-        load_row(R, rec, row_rob(m, rows, n_nc + c), robot);
-        // apply M^-1 J^T imp0 (row_go with imp fixed: lo = hi = imp0 around 0 -> delta = imp0)
-        (void)row_go(R, d, 0.f, imp0, imp0, robot);
+        const bool robot = (__float_as_int(h[0]) & RI_ROBOT) != 0;
+        RowS R;
+        load_row(R, rec, robs + (n_nc + c) * RW, robot);
+        (void)row_go(R, d, 0.f, imp0, imp0, robot);     // delta = imp0
     }
-    // One flat sweep over (iteration, position); position p < n_nc: non-contact rows (sweep
-    // direction alternates), then n_c normal rows, then 2 n_c friction rows.  The next row's
-    // loads are issued while the current row resolves; the empty asm makes the prefetch address
-    // depend on the current row's header so its s_load is issued after the current data landed
-    // (s_load returns out of order, so any wait on the scalar counter is a wait for all).
-    const int T = n_nc + 3 * n_c;
-    const int G = m.iters * T, iters = m.iters;
-    const float *robs = row_rob(m, rows, 0);
-    RowS cur;
-    if (G > 0) load_row(cur, row_rec(m, rows, n_nc - 1), robs + (n_nc - 1) * RW, true);
-    int it = 0, p = 0;
-    for (int g = 0; g < G; g++) {
-        int p1 = p + 1, it1 = it;
-        if (p1 == T) { p1 = 0; it1++; }
-        int rn = p1 < n_nc ? ((it1 & 1) ? p1 : n_nc - 1 - p1) : p1;
-        if (it1 == iters) rn = 0;
-#ifdef AVR_NO_PREFETCH
-        {
-            int rc = p < n_nc ? ((it & 1) ? p : n_nc - 1 - p) : p;
-            load_row(cur, row_rec(m, rows, rc), robs + rc * RW, true);
-        }
-        RowS nxt = cur;
-#else
-        const float *recn = row_rec(m, rows, rn);
-        asm volatile("" : "+s"(recn) : "s"(cur.h[0]));
-        RowS nxt;
-        load_row(nxt, recn, robs + rn * RW, true);
-#endif
-        if (p < n_nc) {
-            const int k = (it & 1) ? p : n_nc - 1 - p;
-            float imp = rdl(inc, k);
-            float ni = row_go(cur, d, imp, cur.h[4], cur.h[5], true);
+    for (int it = 0; it < m.iters; it++) {
+        for (int j = 0; j < n_nc; j++) {
+            const int k = (it & 1) ? j : n_nc - 1 - j;
+            RowS R;
+            load_row(R, rows + k * RW, robs + k * RW, true);
+            float ni = row_go(R, d, rdl(inc, k), R.h[4], R.h[5], true);
             if (lane == k) inc = ni;
-        } else if (p < n_nc + n_c) {
-            const int c = p - n_nc;
-            const bool robot = (__float_as_int(cur.h[0]) & RI_ROBOT) != 0;
-            float imp = rdl(c < 64 ? in0 : in1, c & 63);
-            float ni = row_go(cur, d, imp, 0.f, 1e10f, robot);
-            if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
-        } else {
-            const int f = p - n_nc - n_c, c = f >> 1;
-            float nimp = rdl(c < 64 ? in0 : in1, c & 63);
-            if (nimp > 0.f) {
-                const bool robot = (__float_as_int(cur.h[0]) & RI_ROBOT) != 0;
-                float fr = cur.h[1];
-                const int s = f >> 6;
-                float imp = rdl(s == 0 ? if0 : (s == 1 ? if1 : if2), f & 63);
-                float ni = row_go(cur, d, imp, -fr * nimp, fr * nimp, robot);
-                if (lane == (f & 63)) { if (s == 0) if0 = ni; else if (s == 1) if1 = ni; else if2 = ni; }
-            }
         }
-        cur = nxt;
-        p = p1; it = it1;
+        for (int c = 0; c < n_c; c++) {
+            const float *rec = rows + (n_nc + c) * RW;
+            RowS R;
+            R.h = *(cf8p)rec;
+            const bool robot = (__float_as_int(R.h[0]) & RI_ROBOT) != 0;
+            load_row(R, rec, robs + (n_nc + c) * RW, robot);
+            float ni = row_go(R, d, rdl(c < 64 ? in0 : in1, c & 63), 0.f, 1e10f, robot);
+            if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
+        }
+        for (int f = 0; f < 2 * n_c; f++) {
+            const int c = f >> 1;
+            const float nimp = rdl(c < 64 ? in0 : in1, c & 63);
+            if (!(nimp > 0.f)) continue;
+            const float *rec = rows + (n_nc + n_c + f) * RW;
+            RowS R;
+            R.h = *(cf8p)rec;
+            const bool robot = (__float_as_int(R.h[0]) & RI_ROBOT) != 0;
+            load_row(R, rec, robs + (n_nc + n_c + f) * RW, robot);
+            const float fr = R.h[1];
+            const int s = f >> 6;
+            float ni = row_go(R, d, rdl(s == 0 ? if0 : (s == 1 ? if1 : if2), f & 63), -fr * nimp, fr * nimp, robot);
+            if (lane == (f & 63)) { if (s == 0) if0 = ni; else if (s == 1) if1 = ni; else if2 = ni; }
+        }
     }
-    if (lane < MAXD) L.dq[lane] = d.rq;
-    if (lane < MAXF) {
-        L.dfv[lane][0] = d.vx; L.dfv[lane][1] = d.vy; L.dfv[lane][2] = d.vz;
-        L.dfw[lane][0] = d.wx; L.dfw[lane][1] = d.wy; L.dfw[lane][2] = d.wz;
-    }
-    // normal impulses back to the manifold points (warm start + normalForce); rows are in
-    // contact order, so contact c is manifold point c
-    if (lane < n_c) L.st[AVR_S_CP + AVR_CP_WORDS * lane + AVR_CP_IMP] = in0;
-    if (lane + 64 < n_c) L.st[AVR_S_CP + AVR_CP_WORDS * (lane + 64) + AVR_CP_IMP] = in1;
-    SYNC();
 }
 
 // --------------------------------------------------------------------------- one sub-step
-AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
+// Sub-step part A (kernel avr_substep_a): forward kinematics, collision, unconstrained
+// velocities, constraint rows.  Part B (avr_substep_b): PGS + integration.  What crosses the
+// kernel boundary goes through the per-env workspace (m.ws) and the row buffer (m.rows).
+AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *ws, float *rows) {
     const int lane = lane_id();
     PROF_START(ps);
     robot_fk(m, L);
@@ -1534,38 +1519,18 @@ AVR_DI bool substep(const KModel &m, EnvLDS &L, float dt) {
     }
     SYNC();
     PROF_STOP(6, ps);
-    float *rows = m.rows + (size_t)blockIdx.x * (size_t)(2 * m.rowcap * RW);
     const int n_nc = build_noncontact_rows(m, L, rows, dt);
     PROF_STOP(7, ps);
     build_contact_rows(m, L, rows, n_nc, dt);
     SYNC();
     PROF_STOP(8, ps);
-    solve(m, L, rows);
-    PROF_STOP(9, ps);
-    // integrate
-    if (lane < m.nd) {
-        float v = clampf(L.vq[lane] + L.dq[lane], -vmax, vmax);
-        L.st[AVR_S_QD + lane] = v;
-        L.st[AVR_S_Q + lane] += dt * v;
-    }
+    // hand-over to part B
+    if (lane == 0) { ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); }
+    if (lane < MAXD) ws[WS_VQ + lane] = lane < m.nd ? L.vq[lane] : 0.f;
     if (lane < m.nf) {
-        int f = lane;
-        float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * f;
-        v3 v = clamp3(add(ld3(L.fv[f]), ld3(L.dfv[f])), vmax);
-        v3 om = clamp3(add(ld3(L.fw[f]), ld3(L.dfw[f])), vmax);
-        st3(fb + 7, v);
-        st3(fb + 10, om);
-        st3(fb, add(ld3(fb), scl(v, dt)));
-        float ang = len(om);
-        if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = (0.5f * 1.5707963267948966f) / dt;
-        v3 ax;
-        if (ang < 0.001f) ax = scl(om, 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang);
-        else ax = scl(om, sinf(0.5f * ang * dt) / ang);
-        qt dq = Q(ax.x, ax.y, ax.z, cosf(ang * dt * 0.5f));
-        stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
+        st3(ws + WS_FV + 4 * lane, ld3(L.fv[lane]));
+        st3(ws + WS_FW + 4 * lane, ld3(L.fw[lane]));
     }
-    SYNC();
-    PROF_STOP(10, ps);
     return ok;
 }
 
@@ -1650,80 +1615,159 @@ AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j)
 
 enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 
-// One body, two kernels: TASK = gym step (take_step + frames + task glue; modes STEP,
-// STEP_RANDOM), !TASK = physics only (SETTLE frames, single SUBSTEP).  Separate symbols keep the
-// settle launch out of the step kernel's profile.
-template <bool TASK>
-AVR_DI void env_kernel_body(EnvLDS &L, const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act, float *__restrict__ obs,
-                            float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
-                            const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
-    const KModel &m = *mp;
-    const int env = blockIdx.x;
+// Occupancy request: waves per SIMD the register allocator must leave room for.
+#ifndef AVR_WAVES_PER_EU
+#define AVR_WAVES_PER_EU 1
+#endif
+#define AVR_KATTR __attribute__((amdgpu_waves_per_eu(AVR_WAVES_PER_EU)))
+
+#define AVR_ENV_GUARD()                      \
+    const int env = blockIdx.x;              \
+    if (env >= n_envs) return;               \
+    if (mask && !mask[env]) return;          \
+    const KModel &m = *mp;                   \
+    (void)m
+
+AVR_DI float *env_ws(const KModel &m, int env) { return m.ws + (size_t)env * WS_WORDS; }
+AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)(2 * m.rowcap * RW); }
+
+AVR_DI void load_state(EnvLDS &L, const float *gst) {
     const int lane = lane_id();
-    if (env >= n_envs) return;
-    if (mask && !mask[env]) return;   // masked launches (reset/settle of a subset) leave the rest untouched
-    float *gst = state + (size_t)env * AVR_STATE_WORDS;
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) L.st[i] = gst[i];
-    if (lane == 0) { L.flags = 0; L.gender = 0; }
+    if (lane == 0) { L.flags = 0; L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER]; }
 #ifdef AVR_PROF
     if (lane < 16) L.prof[lane] = 0;
 #endif
     SYNC();
-    PROF_START(ptot);
-    if (lane == 0) L.gender = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+}
+
+AVR_DI void prof_flush(const KModel &m, EnvLDS &L, int env) {
+#ifdef AVR_PROF
     SYNC();
-    const int nsub = m.nsub > 0 ? m.nsub : 1;
-    const float dt = m.time_step / (float)nsub;
-    bool ok = true;
-    if (!TASK && mode == MODE_SUBSTEP) {
-        ok = substep(m, L, *(const float *)&t);
-    } else if (!TASK) {
-        for (long long f = 0; f < t; f++)
-            for (int s = 0; s < nsub; s++) ok &= substep(m, L, dt);
-        mouth_target(m, L);
-        if (obs) observe(m, L, 0.f, obs + (size_t)env * AVR_OBS_DIM);
-    } else {
-        // ---- take_step (env.py:274-337)
-        float a_raw[AVR_ACT_DIM];
-#pragma unroll
-        for (int i = 0; i < AVR_ACT_DIM; i++)
-            a_raw[i] = i >= m.n_arm ? 0.f : mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * AVR_ACT_DIM + i];
-        float a[AVR_ACT_DIM], qn[AVR_ACT_DIM];
-#pragma unroll
-        for (int i = 0; i < AVR_ACT_DIM; i++) {
-            a[i] = clampf(a_raw[i], -1.f, 1.f) * 0.05f;
-            qn[i] = i < m.n_arm ? L.st[AVR_S_Q + m.arm_dofs[i]] : 0.f;
-        }
+    if (m.prof && lane_id() < 16) m.prof[(size_t)env * 16 + lane_id()] += L.prof[lane_id()];
+#else
+    (void)m; (void)L; (void)env;
+#endif
+}
+
+// take_step (env.py:274-337): clip, scale, 5x limit-respecting accumulation, motor targets.
+// One thread per env.
+__global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
+                                                           const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const KModel &m = *mp;
+    float *st = state + (size_t)env * AVR_STATE_WORDS;
+    float *ws = env_ws(m, env);
+    float asq = 0.f;
+    for (int i = 0; i < m.n_arm; i++) {
+        float a_raw = mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * AVR_ACT_DIM + i];
+        asq += a_raw * a_raw;                    // reward_action uses the caller's action (feeding.py:69)
+        float a = clampf(a_raw, -1.f, 1.f) * 0.05f;
+        const int d = m.arm_dofs[i];
+        float qn = st[AVR_S_Q + d];
         for (int it = 0; it < m.frame_skip; it++) {
-#pragma unroll
-            for (int i = 0; i < AVR_ACT_DIM; i++) {
-                if (qn[i] + a[i] < m.arm_lower[i]) a[i] = 0.f;
-                if (qn[i] + a[i] > m.arm_upper[i]) a[i] = 0.f;
-                qn[i] += a[i];
-            }
+            if (qn + a < m.arm_lower[i]) a = 0.f;
+            if (qn + a > m.arm_upper[i]) a = 0.f;
+            qn += a;
         }
-        SYNC();
-        if (lane == 0)
-#pragma unroll
-            for (int i = 0; i < AVR_ACT_DIM; i++) {
-                if (i >= m.n_arm) break;
-                int d = m.arm_dofs[i];
-                L.st[AVR_S_QTGT + d] = qn[i];
-                L.st[AVR_S_KP + d] = m.robot_gain;
-                L.st[AVR_S_MAXIMP + d] = m.robot_force * m.time_step;
-            }
-        SYNC();
-        for (int fr = 0; fr < m.frame_skip; fr++) {
-            for (int s = 0; s < nsub; s++) ok &= substep(m, L, dt);
-            mouth_target(m, L);
-        }
+        st[AVR_S_QTGT + d] = qn;
+        st[AVR_S_KP + d] = m.robot_gain;
+        st[AVR_S_MAXIMP + d] = m.robot_force * m.time_step;
+    }
+    ws[WS_ASQ] = asq;
+}
+
+// Sub-step part A: one 64-lane block per env, state staged in LDS.
+__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                                     const unsigned char *__restrict__ mask, float dt, int n_envs) {
+    __shared__ EnvLDS L;
+    AVR_ENV_GUARD();
+    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    load_state(L, gst);
+    bool ok = substep_a(m, L, dt, env_ws(m, env), env_rows(m, env));
+    if (lane_id() == 0 && !ok) L.flags |= 1;
+    SYNC();
+    if (lane_id() == 0) L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)((int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags);
+    SYNC();
+    // write back what part A changes: the contact cache (+ count, flags)
+    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    for (int i = lane_id(); i < ncp * AVR_CP_WORDS; i += 64) gst[AVR_S_CP + i] = L.st[AVR_S_CP + i];
+    if (lane_id() < 16) gst[AVR_S_TASK + lane_id()] = L.st[AVR_S_TASK + lane_id()];
+    prof_flush(m, L, env);
+}
+
+// Sub-step part B: PGS over the row buffer, then semi-implicit Euler (A.1) with the
+// quaternion exp-map update of btTransformUtil::integrateTransform for the free bodies.
+// No LDS: velocities and impulses stay in registers.
+__global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                           const unsigned char *__restrict__ mask, float dt, int n_envs) {
+    AVR_ENV_GUARD();
+    const int lane = lane_id();
+#ifdef AVR_PROF
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    const float *ws = env_ws(m, env);
+    float *st = state + (size_t)env * AVR_STATE_WORDS;
+    const int n_nc = uni(__float_as_int(ws[WS_NNC])), n_c = uni(__float_as_int(ws[WS_NC]));
+    DV d;
+    float in0, in1;
+    pgs_solve(m, env_rows(m, env), n_nc, n_c, d, in0, in1);
+#ifdef AVR_PROF
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
+    const float vmax = m.max_vel;
+    if (lane < m.nd) {
+        float v = clampf(ws[WS_VQ + lane] + d.rq, -vmax, vmax);
+        st[AVR_S_QD + lane] = v;
+        st[AVR_S_Q + lane] += dt * v;
+    }
+    if (lane < m.nf) {
+        float *fb = st + AVR_S_FREE + AVR_FB_WORDS * lane;
+        v3 v = clamp3(add(ld3(ws + WS_FV + 4 * lane), V(d.vx, d.vy, d.vz)), vmax);
+        v3 om = clamp3(add(ld3(ws + WS_FW + 4 * lane), V(d.wx, d.wy, d.wz)), vmax);
+        st3(fb + 7, v);
+        st3(fb + 10, om);
+        st3(fb, add(ld3(fb), scl(v, dt)));
+        float ang = len(om);
+        if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = (0.5f * 1.5707963267948966f) / dt;
+        v3 ax;
+        if (ang < 0.001f) ax = scl(om, 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang);
+        else ax = scl(om, sinf(0.5f * ang * dt) / ang);
+        qt dq = Q(ax.x, ax.y, ax.z, cosf(ang * dt * 0.5f));
+        stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
+    }
+    // normal impulses back to the manifold points (warm start + normalForce); rows are in
+    // contact order, so contact c is manifold point c
+    if (lane < n_c) st[AVR_S_CP + AVR_CP_WORDS * lane + AVR_CP_IMP] = in0;
+    if (lane + 64 < n_c) st[AVR_S_CP + AVR_CP_WORDS * (lane + 64) + AVR_CP_IMP] = in1;
+#ifdef AVR_PROF
+    unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    if (m.prof && lane == 0) { m.prof[(size_t)env * 16 + 9] += t1 - t0; m.prof[(size_t)env * 16 + 10] += t2 - t1; }
+#endif
+}
+
+// Task glue after the frames: update_targets (feeding.py:345-349), iteration count,
+// get_total_force (83-90), get_food_rewards (92-121), _get_obs (123-142), reward (56-77),
+// TimeLimit; SETTLE mode: target + reset observation only.  NaN guard for every mode.
+__global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ obs,
+                                                      float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
+                                                      const unsigned char *__restrict__ mask, int mode, int n_envs) {
+    __shared__ EnvLDS L;
+    AVR_ENV_GUARD();
+    const int lane = lane_id();
+    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    load_state(L, gst);
+    PROF_START(ptask);
+    mouth_target(m, L);
+    if (mode == MODE_SETTLE) {
+        if (obs) observe(m, L, 0.f, obs + (size_t)env * AVR_OBS_DIM);
+    } else if (mode == MODE_STEP || mode == MODE_STEP_RANDOM) {
         if (lane == 0) L.st[AVR_S_TASK + AVR_T_ITER] += 1.f;
         SYNC();
-        // ---- get_total_force (feeding.py:83-90)
         int dummy;
         float robot_force = contact_sum(m, L, 0, 0, 0, dummy);
         float spoon_force = contact_sum(m, L, 1, 0, 0, dummy);
-        // ---- get_food_rewards (feeding.py:92-121), uniform
         float food_reward = 0.f, hit_reward = 0.f, mouth_vel = 0.f;
         int alive = (int)L.st[AVR_S_TASK + AVR_T_ALIVE], hit = (int)L.st[AVR_S_TASK + AVR_T_HIT];
         float succ = L.st[AVR_S_TASK + AVR_T_SUCCESS];
@@ -1768,9 +1812,7 @@ AVR_DI void env_kernel_body(EnvLDS &L, const KModel *__restrict__ mp, float *__r
                       m.w_high_forces * (spoon_force < 10.f ? 0.f : -spoon_force) + m.w_food_hit * hit_reward +
                       m.w_food_velocities * (-mouth_vel);
         float dist = len(sub(tgt, ld3(sp)));
-        float asq = 0.f;
-#pragma unroll
-        for (int i = 0; i < AVR_ACT_DIM; i++) asq += a_raw[i] * a_raw[i];
+        float asq = env_ws(m, env)[WS_ASQ];
         float r = m.w_distance * (-dist) + m.w_action * (-asq) + m.w_food * food_reward + prefs;
         if (lane == 0) {
             rew[env] = r;
@@ -1784,31 +1826,15 @@ AVR_DI void env_kernel_body(EnvLDS &L, const KModel *__restrict__ mp, float *__r
     // NaN guard + flags, then write the state back
     bool bad = false;
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) bad |= !(L.st[i] == L.st[i]);
-    bad = __any(bad) || !ok;
+    bad = __any(bad);
     if (lane == 0) {
         int fl = (int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags | (bad ? 1 : 0);
         L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)fl;
     }
     SYNC();
     for (int i = lane; i < AVR_STATE_WORDS; i += 64) gst[i] = L.st[i];
-#ifdef AVR_PROF
-    PROF_STOP(12, ptot);
-    SYNC();
-    if (m.prof && lane < 16) m.prof[(size_t)env * 16 + lane] = L.prof[lane];
-#endif
-}
-
-__global__ __launch_bounds__(64) void avr_env_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
-                                                          float *__restrict__ obs, float *__restrict__ rew, unsigned char *__restrict__ done,
-                                                          float *__restrict__ info, const unsigned char *__restrict__ mask, int mode, long long t,
-                                                          int n_envs) {
-    __shared__ EnvLDS L;
-    env_kernel_body<true>(L, mp, state, act, obs, rew, done, info, mask, mode, t, n_envs);
-}
-__global__ __launch_bounds__(64) void avr_physics_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ obs,
-                                                         const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
-    __shared__ EnvLDS L;
-    env_kernel_body<false>(L, mp, state, nullptr, obs, nullptr, nullptr, nullptr, mask, mode, t, n_envs);
+    PROF_STOP(12, ptask);
+    prof_flush(m, L, env);
 }
 
 // state[e] = src[e] for the envs whose mask byte is set (masked reset upload)
@@ -1831,13 +1857,35 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 }
 
 // host-side launch helpers (used by avr_capi.hip)
-extern "C" hipError_t avr_launch_step(const KModel *d_m, float *state, const float *act, float *obs, float *rew, unsigned char *done,
-                                      float *info, const unsigned char *mask, int mode, long long t, int n_envs, hipStream_t stream) {
+// One gym step / settle / single sub-step as a sequence of kernels on `stream`:
+//   take_step -> frame_skip x nsub x (substep_a, substep_b) -> task      (STEP, STEP_RANDOM)
+//   t frames x nsub x (substep_a, substep_b) -> task (settle obs)        (SETTLE)
+//   substep_a, substep_b with dt = bit-cast(t)                           (SUBSTEP)
+extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
+                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
+                                      hipStream_t stream) {
     if (n_envs <= 0) return hipSuccess;
-    if (mode == MODE_SETTLE || mode == MODE_SUBSTEP)
-        hipLaunchKernelGGL(avr_physics_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, mask, mode, t, n_envs);
-    else
-        hipLaunchKernelGGL(avr_env_step_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, act, obs, rew, done, info, mask, mode, t, n_envs);
+    const int nsub = h_m->nsub > 0 ? h_m->nsub : 1;
+    const float dt = h_m->time_step / (float)nsub;
+    auto sub = [&](float h) {
+        hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
+        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
+    };
+    if (mode == MODE_SUBSTEP) {
+        float h;
+        std::memcpy(&h, &t, sizeof(float));
+        sub(h);
+        return hipGetLastError();
+    }
+    if (mode == MODE_SETTLE) {
+        for (long long f = 0; f < t; f++)
+            for (int k = 0; k < nsub; k++) sub(dt);
+    } else {
+        hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, n_envs);
+        for (int f = 0; f < h_m->frame_skip; f++)
+            for (int k = 0; k < nsub; k++) sub(dt);
+    }
+    hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, n_envs);
     return hipGetLastError();
 }
 
@@ -1848,14 +1896,18 @@ extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env
     return hipGetLastError();
 }
 
-extern "C" hipError_t avr_kernel_attrs(int *out4) {
-    hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, (const void *)avr_env_step_kernel);
-    if (e != hipSuccess) return e;
-    out4[0] = a.numRegs;
-    out4[1] = 0;
-    out4[2] = (int)a.sharedSizeBytes;
-    out4[3] = (int)a.localSizeBytes;
+// [vgprs, 0, lds bytes, scratch bytes] of substep_a, then of substep_b
+extern "C" hipError_t avr_kernel_attrs(int *out8) {
+    const void *k[2] = {(const void *)avr_substep_a_kernel, (const void *)avr_substep_b_kernel};
+    for (int i = 0; i < 2; i++) {
+        hipFuncAttributes a;
+        hipError_t e = hipFuncGetAttributes(&a, k[i]);
+        if (e != hipSuccess) return e;
+        out8[4 * i + 0] = a.numRegs;
+        out8[4 * i + 1] = 0;
+        out8[4 * i + 2] = (int)a.sharedSizeBytes;
+        out8[4 * i + 3] = (int)a.localSizeBytes;
+    }
     return hipSuccess;
 }
 

@@ -56,5 +56,6 @@ struct KModel {
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
     int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
+    float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
 };

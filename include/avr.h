@@ -87,8 +87,9 @@ void *avr_state_device_ptr(avr_sim *sim);
 int32_t avr_n_envs(avr_sim *sim);
 int32_t avr_state_words(void);
 int32_t avr_abi_version(void);
-/* Kernel resource usage: [vgprs, sgprs, lds_bytes, scratch_bytes] of the step kernel. */
-int avr_kernel_info(avr_sim *sim, int32_t *out4);
+/* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of the sub-step kernel A
+ * (kinematics, collision, rows), then the same four for kernel B (PGS + integration). */
+int avr_kernel_info(avr_sim *sim, int32_t *out8);
 const char *avr_last_error(avr_sim *sim);
 
 /* Diagnostics (phase-timer builds only, -DAVR_PROF): attach a device buffer of

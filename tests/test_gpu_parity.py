@@ -48,8 +48,8 @@ def test_kernel_resources(lib_and_scene):
     A, md = lib_and_scene
     sim = make_sim(md, 4)
     ki = sim.kernel_info()
-    assert ki['scratch_bytes'] == 0          # no spills to scratch on gfx950
-    assert ki['lds_bytes'] <= 64 * 1024
+    assert ki['scratch_bytes'] == 0 and ki['b_scratch_bytes'] == 0     # no spills to scratch on gfx950
+    assert ki['lds_bytes'] <= 64 * 1024 and ki['b_lds_bytes'] == 0
     sim.close()
 
 

@@ -4,7 +4,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd')); sys.path.insert(0, ROOT)
 from avr import _abi as ABI, reset as RS, _lib
-so = os.path.join(ROOT, 'assistive-vr-gym_amd', 'avr', 'libavr_prof.so')
+so = os.path.join(ROOT, 'assistive-vr-gym_amd', 'avr', sys.argv[2] if len(sys.argv) > 2 else 'libavr_prof.so')
 _lib.LIB_PATH = so
 lib = _lib.load(so)
 lib.avr_set_profile_buffer.argtypes = [C.c_void_p, C.c_void_p]
@@ -17,15 +17,17 @@ sim = _lib.Sim(md, N)
 prof = torch.zeros(N * 16, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
-names = ['fk', 'bodies+broad', 'childpairs', 'passA', 'passB', 'passC', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '-', 'TOTAL', 'collide']
-for t in range(3):
+names = ['fk', 'bodies+broad', 'childpairs', 'passA', 'passB', 'passC', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#childitems', 'task', 'collide', '#shapepairs', '#bodypairs']
+for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
     p = prof.cpu().numpy().reshape(N, 16).astype(np.float64)
-    tot = p[:, 12].mean()
+    tot = p[:, [0, 13, 6, 7, 8, 9, 10, 12]].sum(1).mean()
     print('step %d wall %.1f ms, mean cycles/env %.3g' % (t, el * 1e3, tot))
     for k, nm in enumerate(names):
-        if nm == '-': continue
+        if nm.startswith('#'):
+            print('  %-13s per env-step mean %.1f (per substep %.1f)' % (nm, p[:, k].mean(), p[:, k].mean() / 10))
+            continue
         print('  %-13s %6.2f%%  mean %.3g  max %.3g' % (nm, 100 * p[:, k].mean() / tot, p[:, k].mean(), p[:, k].max()))
 St = sim.get_state()
 print('ncp mean', St[:, ABI.S_TASK + ABI.T_NCP].mean(), 'flags', np.unique(St[:, ABI.S_TASK + ABI.T_FLAGS]))
