@@ -17,7 +17,7 @@ EXPORTS = [
     'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',
     'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_state_words', 'avr_abi_version',
-    'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset',
+    'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
 ]
 
 
@@ -66,6 +66,8 @@ def load(path=LIB_PATH):
     lib.avr_last_error.restype = C.c_char_p
     lib.avr_substep.argtypes = [vp, C.c_float]
     lib.avr_reset.argtypes = [vp, vp, vp, C.c_int32, vp]
+    lib.avr_profile_kernels.argtypes = [vp, C.c_int32]
+    lib.avr_kernel_times.argtypes = [vp, vp, vp]
     _LIB = lib
     return lib
 
@@ -160,6 +162,18 @@ class Sim:
 
     def stream(self):
         return self.lib.avr_stream(self.h)
+
+    KERNEL_KINDS = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b_kernel', 'avr_task_kernel')
+
+    def profile_kernels(self, enable=True):
+        self._chk(self.lib.avr_profile_kernels(self.h, int(bool(enable))))
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} accumulated since profile_kernels(True)."""
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.int64)
+        self._chk(self.lib.avr_kernel_times(self.h, ms.ctypes.data, n.ctypes.data))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_KINDS)}
 
     def kernel_info(self):
         out = np.zeros(8, np.int32)

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <vector>
+#include <cmath>
 
 #include "../../include/avr.h"
 
@@ -16,7 +17,7 @@
 
 extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
                                       unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
-                                      hipStream_t stream);
+                                      hipStream_t stream, avr_evlog *log);
 extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
 extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream);
@@ -34,6 +35,11 @@ struct avr_sim {
     float *d_act, *d_obs, *d_rew, *d_info;
     unsigned char *d_done;
     char err[512];
+    avr_evlog evlog;                       // per-kernel timing (avr_profile_kernels)
+    std::vector<hipEvent_t> ev;
+    std::vector<int> evkind;
+    double kt_ms[AVR_K_KINDS];
+    long long kt_n[AVR_K_KINDS];
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -77,6 +83,40 @@ static std::vector<float> cvt(const double *p, size_t n, int stride_in = 1, int 
 
 static std::vector<int> ivec(const int32_t *p, size_t n) { return std::vector<int>(p, p + n); }
 
+// host (double) transform helpers for precomputed static geometry; quaternions are x y z w
+static void hq_mul(const double *a, const double *b, double *o) {
+    double r[4] = {a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1], a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
+                   a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3], a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
+    for (int i = 0; i < 4; i++) o[i] = r[i];
+}
+static void hq_mat(const double *q, double R[3][3]) {
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - z * w); R[0][2] = 2 * (x * z + y * w);
+    R[1][0] = 2 * (x * y + z * w); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - x * w);
+    R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
+}
+
+// world AABB of shape s on a static body: aabb_of(body * shape_pose, center, half) as in the kernel
+static void static_shape_aabb(const avr_model_desc *d, int s, float *out8) {
+    const int b = d->shape_body[s];
+    const double *bp = d->st_pose + 7 * d->body_index[b];
+    const double *sp = d->shape_pose + 7 * s;
+    double R[3][3], q[4], p[3];
+    hq_mat(bp + 3, R);
+    for (int i = 0; i < 3; i++) p[i] = bp[i] + R[i][0] * sp[0] + R[i][1] * sp[1] + R[i][2] * sp[2];
+    hq_mul(bp + 3, sp + 3, q);
+    double T[3][3];
+    hq_mat(q, T);
+    const double *c = d->shape_aabb + 6 * s, *h = c + 3;
+    for (int i = 0; i < 3; i++) {
+        double cw = p[i] + T[i][0] * c[0] + T[i][1] * c[1] + T[i][2] * c[2];
+        double hw = fabs(T[i][0]) * h[0] + fabs(T[i][1]) * h[1] + fabs(T[i][2]) * h[2];
+        out8[i] = (float)(cw - hw);
+        out8[4 + i] = (float)(cw + hw);
+    }
+    out8[3] = out8[7] = 0.f;
+}
+
 // pose arrays: [n][pos3 + quat4] -> [n][8]
 static std::vector<float> poses(const double *pos, const double *quat, int n) {
     std::vector<float> v((size_t)n * 8, 0.f);
@@ -98,7 +138,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     s->cfg = *cfg;
     if (cfg->n_envs <= 0) { int r = fail(s, -1, "n_envs must be > 0"); *out = s; return r; }
     if (d->n_links > AVR_MAX_LINKS || d->n_dof > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
-        d->n_bodies > 64 || d->n_arm > AVR_ACT_DIM) {
+        d->n_bodies > MAXB || d->n_arm > AVR_ACT_DIM) {
         int r = fail(s, -2, "model exceeds compiled capacities");
         *out = s;
         return r;
@@ -159,6 +199,19 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int i = 0; i < d->n_hull_verts; i++)
             hv[i] = make_float4((float)d->hull_verts[3 * i], (float)d->hull_verts[3 * i + 1], (float)d->hull_verts[3 * i + 2], 0.f);
         if ((r = upload(s, hv, &k.hull_verts))) return r;
+    }
+    {
+        // child AABB cache slots for the non-static shapes; static shapes get host-computed AABBs
+        std::vector<int> cidx(ns, -1);
+        std::vector<float> saabb((size_t)ns * 8, 0.f);
+        int nc = 0;
+        for (int i = 0; i < ns; i++) {
+            if (d->body_kind[d->shape_body[i]] == AVR_BODY_STATIC) static_shape_aabb(d, i, &saabb[8 * (size_t)i]);
+            else cidx[i] = nc++;
+        }
+        if (nc > MAXCC) return fail(s, -2, "model has %d non-static shapes > MAXCC %d", nc, MAXCC);
+        if ((r = upload(s, cidx, &k.shape_cidx))) return r;
+        if ((r = upload(s, saabb, &k.static_saabb))) return r;
     }
     if ((r = upload(s, ivec(d->pair_a, d->n_pairs), &k.pair_a))) return r;
     if ((r = upload(s, ivec(d->pair_b, d->n_pairs), &k.pair_b))) return r;
@@ -234,6 +287,7 @@ extern "C" int avr_destroy(avr_sim *s) {
     if (s->d_info) (void)hipFree(s->d_info);
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->d_mask) (void)hipFree(s->d_mask);
+    for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return 0;
@@ -280,7 +334,7 @@ extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_
     if (!h) return fail(s, -1, "avr_reset: host_state is NULL");
     if (n_frames < 0) return fail(s, -1, "avr_reset: n_frames < 0");
     if (upload_masked(s, mask, h)) return -2;
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     if (host_obs) {
         std::vector<float> o(E * AVR_OBS_DIM);
         HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
@@ -301,7 +355,7 @@ extern "C" int avr_get_state(avr_sim *s, float *h) {
 
 extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
@@ -311,21 +365,21 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     return 0;
 }
 
 extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
     HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
-                              d_info ? d_info : s->d_info, nullptr, 1, t, s->cfg.n_envs, s->stream));
+                              d_info ? d_info : s->d_info, nullptr, 1, t, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     return 0;
 }
 
@@ -339,7 +393,7 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
     HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream));
+    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
     HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));
@@ -366,4 +420,44 @@ extern "C" int avr_kernel_info(avr_sim *s, int32_t *out8) {
     (void)s;
     hipError_t e = avr_kernel_attrs(out8);
     return e == hipSuccess ? 0 : -3;
+}
+
+// ------------------------------------------------------------------ per-kernel timing
+// Fold the logged events into per-kind totals (synchronises the stream).
+static int drain_evlog(avr_sim *s) {
+    if (!s->evlog.cap || !s->evlog.n) return 0;
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    for (int i = 0; i + 1 < s->evlog.n; i++) {
+        int k = s->evlog.kind[i];
+        if (k < 0) continue;
+        float ms = 0.f;
+        HIPCHK(s, hipEventElapsedTime(&ms, s->evlog.ev[i], s->evlog.ev[i + 1]));
+        s->kt_ms[k] += ms;
+        s->kt_n[k] += 1;
+    }
+    s->evlog.n = 0;
+    return 0;
+}
+
+extern "C" int avr_profile_kernels(avr_sim *s, int32_t enable) {
+    CHECK_SIM(s);
+    if (drain_evlog(s)) return -3;
+    for (int k = 0; k < AVR_K_KINDS; k++) { s->kt_ms[k] = 0; s->kt_n[k] = 0; }
+    if (enable && s->ev.empty()) {
+        s->ev.resize(4096);
+        s->evkind.resize(4096);
+        for (auto &e : s->ev) HIPCHK(s, hipEventCreate(&e));
+    }
+    s->evlog.ev = s->ev.data();
+    s->evlog.kind = s->evkind.data();
+    s->evlog.n = 0;
+    s->evlog.cap = enable ? (int)s->ev.size() : 0;
+    return 0;
+}
+
+extern "C" int avr_kernel_times(avr_sim *s, double *ms4, int64_t *count4) {
+    CHECK_SIM(s);
+    if (drain_evlog(s)) return -3;
+    for (int k = 0; k < AVR_K_KINDS; k++) { ms4[k] = s->kt_ms[k]; count4[k] = s->kt_n[k]; }
+    return 0;
 }

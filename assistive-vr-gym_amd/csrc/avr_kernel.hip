@@ -32,30 +32,29 @@
 
 // --------------------------------------------------------------------------- LDS layout
 struct EnvLDS {
-    float st[AVR_STATE_WORDS];
+    float st[AVR_S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
-    float btf[MAXB][8], bmin[MAXB][4], bmax[MAXB][4];
+    float btf[MAXB][8];
     float Mi[MAXD][MAXD];
-    float vq[MAXD], dq[MAXD];
-    float fv[MAXF][4], fw[MAXF][4], dfv[MAXF][4], dfw[MAXF][4];
+    float vq[MAXD];
+    float fv[MAXF][4], fw[MAXF][4];
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
     float h[MAXD], qdd[MAXD];
-    float rn[6][MAXL][4];   // RNEA temporaries: omega, v_com, alpha, a_com, F, N
     int nsp, nap, n_nc, n_c, flags, gender, pad, pad2;
 #ifdef AVR_PROF
     unsigned long long prof[16];
 #endif
     union {
-        struct {
-            int sp_a[MAXSP], sp_b[MAXSP], sp_pair[MAXSP];
-            float res[MAXSP][8];           // flag, n3, p3, d
-            int apair[MAXAP];
-            float newcp[AVR_MAX_CONTACTS][AVR_CP_WORDS];
-            float eW[EPA_MAX_V][9];        // minkowski vertex + support on A + support on B
-            int eFi[EPA_MAX_F][4];         // i j k alive
-            float eFn[EPA_MAX_F][4];       // normal + d
-            int eEdge[EPA_MAX_F * 3][2];
+        struct {                           // collision detection
+            float bmin[MAXB][4], bmax[MAXB][4];
+            int apair[MAXAP];              // active body pairs (broadphase output, in pair order)
+            int okey[AVR_MAX_CONTACTS];    // (sa | sb << 16) of the previous contact pool
+            int qk[128], qp[128];          // shape-pair queue: (sa | sb << 16), body pair
+            float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
         } c;
+        struct {
+            float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
+        } d;
     } u;
 };
 
@@ -182,7 +181,7 @@ AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *
 // temporaries in LDS; result in L.h.
 AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
     if (lane_id() == 0) {
-        float (*OM)[4] = L.rn[0], (*VC)[4] = L.rn[1], (*AL)[4] = L.rn[2], (*AC)[4] = L.rn[3], (*FF)[4] = L.rn[4], (*NN)[4] = L.rn[5];
+        float (*OM)[4] = L.u.d.rn[0], (*VC)[4] = L.u.d.rn[1], (*AL)[4] = L.u.d.rn[2], (*AC)[4] = L.u.d.rn[3], (*FF)[4] = L.u.d.rn[4], (*NN)[4] = L.u.d.rn[5];
         const float k1l = m.lin_damp, k1a = m.ang_damp;
         tf base = ldtf(m.base);
         for (int i = 0; i < m.nl; i++) {
@@ -471,32 +470,40 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     return GJK_SEPARATED;
 }
 
-// --------------------------------------------------------------------------- EPA (wave-cooperative; polytope in LDS)
-AVR_DI int epa_add_face(EnvLDS &L, int &nf, int i, int j, int k) {
+// --------------------------------------------------------------------------- EPA (wave-cooperative)
+// The polytope lives in a per-env global scratch buffer (EPA runs only when shape cores
+// overlap, which is rare; keeping it out of LDS buys occupancy for everything else).
+struct EpaBuf {
+    float eW[EPA_MAX_V][9];        // minkowski vertex + support on A + support on B
+    int eFi[EPA_MAX_F][4];         // i j k alive
+    float eFn[EPA_MAX_F][4];       // normal + d
+    int eEdge[EPA_MAX_F * 3][2];
+};
+AVR_DI int epa_add_face(EpaBuf &L, int &nf, int i, int j, int k) {
     if (nf >= EPA_MAX_F) return -1;
-    v3 Wi = ld3(L.u.c.eW[i]), Wj = ld3(L.u.c.eW[j]), Wk = ld3(L.u.c.eW[k]);
+    v3 Wi = ld3(L.eW[i]), Wj = ld3(L.eW[j]), Wk = ld3(L.eW[k]);
     v3 n = crs(sub(Wj, Wi), sub(Wk, Wi));
     float l = len(n);
     if (l < 1e-18f) return -2;
     n = scl(n, 1.f / l);
     SYNC();
     if (lane_id() == 0) {
-        L.u.c.eFi[nf][0] = i; L.u.c.eFi[nf][1] = j; L.u.c.eFi[nf][2] = k; L.u.c.eFi[nf][3] = 1;
-        st3(L.u.c.eFn[nf], n);
-        L.u.c.eFn[nf][3] = dot(n, Wi);
+        L.eFi[nf][0] = i; L.eFi[nf][1] = j; L.eFi[nf][2] = k; L.eFi[nf][3] = 1;
+        st3(L.eFn[nf], n);
+        L.eFn[nf][3] = dot(n, Wi);
     }
     SYNC();
     nf++;
     return 0;
 }
 
-AVR_DI void epa_set_vert(EnvLDS &L, int vi, v3 w, v3 a, v3 b) {
+AVR_DI void epa_set_vert(EpaBuf &L, int vi, v3 w, v3 a, v3 b) {
     SYNC();
-    if (lane_id() == 0) { st3(L.u.c.eW[vi], w); st3(L.u.c.eW[vi] + 3, a); st3(L.u.c.eW[vi] + 6, b); }
+    if (lane_id() == 0) { st3(L.eW[vi], w); st3(L.eW[vi] + 3, a); st3(L.eW[vi] + 6, b); }
     SYNC();
 }
 
-AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, const Simplex &S, v3 &normal_out, float &depth, v3 &pa, v3 &pb) {
+AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, const Simplex &S, v3 &normal_out, float &depth, v3 &pa, v3 &pb) {
     int nv = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++)
@@ -505,13 +512,13 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
         float sg = (di & 1) ? -1.f : 1.f;
         v3 d = V(di < 2 ? sg : 0.f, (di >> 1) == 1 ? sg : 0.f, di >= 4 ? sg : 0.f);
         if (nv == 2) {
-            v3 e = sub(ld3(L.u.c.eW[1]), ld3(L.u.c.eW[0]));
+            v3 e = sub(ld3(L.eW[1]), ld3(L.eW[0]));
             v3 c = crs(e, d);
             if (len2(c) < 1e-12f) continue;
             d = c;
         } else if (nv == 3) {
-            v3 W0 = ld3(L.u.c.eW[0]);
-            d = crs(sub(ld3(L.u.c.eW[1]), W0), sub(ld3(L.u.c.eW[2]), W0));
+            v3 W0 = ld3(L.eW[0]);
+            d = crs(sub(ld3(L.eW[1]), W0), sub(ld3(L.eW[2]), W0));
             if (di & 1) d = scl(d, -1.f);
             if (len2(d) < 1e-24f) continue;
         }
@@ -519,19 +526,19 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
         v3 wv = sub(sa, sb);
         bool dup = false;
         for (int k = 0; k < nv; k++)
-            if (len2(sub(ld3(L.u.c.eW[k]), wv)) < 1e-20f) dup = true;
+            if (len2(sub(ld3(L.eW[k]), wv)) < 1e-20f) dup = true;
         if (dup) continue;
         epa_set_vert(L, nv++, wv, sa, sb);
     }
     if (nv < 4) return -1;
     {
-        v3 W0 = ld3(L.u.c.eW[0]), W1 = ld3(L.u.c.eW[1]), W2 = ld3(L.u.c.eW[2]), W3 = ld3(L.u.c.eW[3]);
+        v3 W0 = ld3(L.eW[0]), W1 = ld3(L.eW[1]), W2 = ld3(L.eW[2]), W3 = ld3(L.eW[3]);
         if (dot(crs(sub(W1, W0), sub(W2, W0)), sub(W3, W0)) > 0.f) {
             float t1[9], t2[9];
-            for (int k = 0; k < 9; k++) { t1[k] = L.u.c.eW[1][k]; t2[k] = L.u.c.eW[2][k]; }
+            for (int k = 0; k < 9; k++) { t1[k] = L.eW[1][k]; t2[k] = L.eW[2][k]; }
             SYNC();
             if (lane_id() == 0)
-                for (int k = 0; k < 9; k++) { L.u.c.eW[1][k] = t2[k]; L.u.c.eW[2][k] = t1[k]; }
+                for (int k = 0; k < 9; k++) { L.eW[1][k] = t2[k]; L.eW[2][k] = t1[k]; }
             SYNC();
         }
     }
@@ -542,33 +549,33 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
         best = -1;
         float bd = BIGF;
         for (int f = 0; f < nf; f++)
-            if (L.u.c.eFi[f][3] && L.u.c.eFn[f][3] < bd) { bd = L.u.c.eFn[f][3]; best = f; }
+            if (L.eFi[f][3] && L.eFn[f][3] < bd) { bd = L.eFn[f][3]; best = f; }
         if (best < 0) return -1;
-        v3 n = ld3(L.u.c.eFn[best]);
+        v3 n = ld3(L.eFn[best]);
         v3 sa = support<true>(m, A, n), sb = support<true>(m, B, scl(n, -1.f));
         v3 wv = sub(sa, sb);
         float dist = dot(wv, n);
-        if (dist - L.u.c.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
+        if (dist - L.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
         int vi = nv++;
         epa_set_vert(L, vi, wv, sa, sb);
         int ne = 0;
         for (int f = 0; f < nf; f++) {
-            if (!L.u.c.eFi[f][3]) continue;
-            if (dot(ld3(L.u.c.eFn[f]), sub(wv, ld3(L.u.c.eW[L.u.c.eFi[f][0]]))) > 0.f) {
-                int fi = L.u.c.eFi[f][0], fj = L.u.c.eFi[f][1], fk = L.u.c.eFi[f][2];
+            if (!L.eFi[f][3]) continue;
+            if (dot(ld3(L.eFn[f]), sub(wv, ld3(L.eW[L.eFi[f][0]]))) > 0.f) {
+                int fi = L.eFi[f][0], fj = L.eFi[f][1], fk = L.eFi[f][2];
                 SYNC();
-                if (lane_id() == 0) L.u.c.eFi[f][3] = 0;
+                if (lane_id() == 0) L.eFi[f][3] = 0;
                 SYNC();
                 int e3[3][2] = {{fi, fj}, {fj, fk}, {fk, fi}};
                 for (int e = 0; e < 3; e++) {
                     int found = -1;
                     for (int q = 0; q < ne; q++)
-                        if (L.u.c.eEdge[q][0] == e3[e][1] && L.u.c.eEdge[q][1] == e3[e][0]) { found = q; break; }
-                    int n0 = L.u.c.eEdge[ne - 1 < 0 ? 0 : ne - 1][0], n1 = L.u.c.eEdge[ne - 1 < 0 ? 0 : ne - 1][1];
+                        if (L.eEdge[q][0] == e3[e][1] && L.eEdge[q][1] == e3[e][0]) { found = q; break; }
+                    int n0 = L.eEdge[ne - 1 < 0 ? 0 : ne - 1][0], n1 = L.eEdge[ne - 1 < 0 ? 0 : ne - 1][1];
                     SYNC();
                     if (lane_id() == 0) {
-                        if (found >= 0) { L.u.c.eEdge[found][0] = n0; L.u.c.eEdge[found][1] = n1; }
-                        else { L.u.c.eEdge[ne][0] = e3[e][0]; L.u.c.eEdge[ne][1] = e3[e][1]; }
+                        if (found >= 0) { L.eEdge[found][0] = n0; L.eEdge[found][1] = n1; }
+                        else { L.eEdge[ne][0] = e3[e][0]; L.eEdge[ne][1] = e3[e][1]; }
                     }
                     SYNC();
                     if (found >= 0) ne--; else ne++;
@@ -578,14 +585,14 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
         // compact dead faces (uniform read, lane 0 writes in order)
         int k = 0;
         for (int f = 0; f < nf; f++) {
-            int alive = L.u.c.eFi[f][3];
+            int alive = L.eFi[f][3];
             if (alive) {
-                int a0 = L.u.c.eFi[f][0], a1 = L.u.c.eFi[f][1], a2 = L.u.c.eFi[f][2];
-                float n0 = L.u.c.eFn[f][0], n1 = L.u.c.eFn[f][1], n2 = L.u.c.eFn[f][2], n3 = L.u.c.eFn[f][3];
+                int a0 = L.eFi[f][0], a1 = L.eFi[f][1], a2 = L.eFi[f][2];
+                float n0 = L.eFn[f][0], n1 = L.eFn[f][1], n2 = L.eFn[f][2], n3 = L.eFn[f][3];
                 SYNC();
                 if (lane_id() == 0) {
-                    L.u.c.eFi[k][0] = a0; L.u.c.eFi[k][1] = a1; L.u.c.eFi[k][2] = a2; L.u.c.eFi[k][3] = 1;
-                    L.u.c.eFn[k][0] = n0; L.u.c.eFn[k][1] = n1; L.u.c.eFn[k][2] = n2; L.u.c.eFn[k][3] = n3;
+                    L.eFi[k][0] = a0; L.eFi[k][1] = a1; L.eFi[k][2] = a2; L.eFi[k][3] = 1;
+                    L.eFn[k][0] = n0; L.eFn[k][1] = n1; L.eFn[k][2] = n2; L.eFn[k][3] = n3;
                 }
                 SYNC();
                 k++;
@@ -593,22 +600,22 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
         }
         nf = k;
         for (int e = 0; e < ne; e++)
-            if (epa_add_face(L, nf, L.u.c.eEdge[e][0], L.u.c.eEdge[e][1], vi) == -1) return -1;
+            if (epa_add_face(L, nf, L.eEdge[e][0], L.eEdge[e][1], vi) == -1) return -1;
     }
     if (best < 0) return -1;
-    v3 n = ld3(L.u.c.eFn[best]);
-    float fd = L.u.c.eFn[best][3];
+    v3 n = ld3(L.eFn[best]);
+    float fd = L.eFn[best][3];
     v3 p = scl(n, fd);
-    int fi = L.u.c.eFi[best][0], fj = L.u.c.eFi[best][1], fk = L.u.c.eFi[best][2];
-    v3 a = ld3(L.u.c.eW[fi]), b = ld3(L.u.c.eW[fj]), c = ld3(L.u.c.eW[fk]);
+    int fi = L.eFi[best][0], fj = L.eFi[best][1], fk = L.eFi[best][2];
+    v3 a = ld3(L.eW[fi]), b = ld3(L.eW[fj]), c = ld3(L.eW[fk]);
     v3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
     float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
     float den = d00 * d11 - d01 * d01;
     float lv = 0.f, lw = 0.f;
     if (fabsf(den) > 1e-30f) { lv = (d11 * d20 - d01 * d21) / den; lw = (d00 * d21 - d01 * d20) / den; }
     float lu = 1.f - lv - lw;
-    pa = add(add(scl(ld3(L.u.c.eW[fi] + 3), lu), scl(ld3(L.u.c.eW[fj] + 3), lv)), scl(ld3(L.u.c.eW[fk] + 3), lw));
-    pb = add(add(scl(ld3(L.u.c.eW[fi] + 6), lu), scl(ld3(L.u.c.eW[fj] + 6), lv)), scl(ld3(L.u.c.eW[fk] + 6), lw));
+    pa = add(add(scl(ld3(L.eW[fi] + 3), lu), scl(ld3(L.eW[fj] + 3), lv)), scl(ld3(L.eW[fk] + 3), lw));
+    pb = add(add(scl(ld3(L.eW[fi] + 6), lu), scl(ld3(L.eW[fj] + 6), lv)), scl(ld3(L.eW[fk] + 6), lw));
     normal_out = n;
     depth = fd;
     return 0;
@@ -617,7 +624,7 @@ AVR_DI int epa(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, con
 // --------------------------------------------------------------------------- narrowphase
 // returns: 0 no contact, 1 contact (nB, pB, dist), 2 needs the cooperative path
 template <bool COOP>
-AVR_DI int narrowphase(const KModel &m, EnvLDS &L, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist) {
+AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist) {
     int ka = A.kind, kb = B.kind;
     if (ka == AVR_SPHERE && kb == AVR_SPHERE) {
         v3 diff = sub(A.t.p, B.t.p);
@@ -696,7 +703,7 @@ AVR_DI int narrowphase(const KModel &m, EnvLDS &L, const WShape &A, const WShape
         if (!COOP) return 2;
         float depth;
         v3 en;
-        if (epa(m, L, A, B, S, en, depth, pa, pb)) return 0;
+        if (epa(m, E, A, B, S, en, depth, pa, pb)) return 0;
         n = scl(en, -1.f);
         d = -depth - ma - mb;
     }
@@ -860,9 +867,117 @@ AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, 
 }
 
 // --------------------------------------------------------------------------- collision detection
-AVR_DI void collide(const KModel &m, EnvLDS &L) {
+// Per sub-step (btCollisionWorld::performDiscreteCollisionDetection restated):
+//   1. body transforms and fattened AABBs (btDbvtBroadphase, margin 0.02);
+//   2. broadphase over the compiled candidate body pairs, order-preserving compaction;
+//   3. world AABBs of every non-static child shape, cached in LDS (static ones are precomputed
+//      on the host, m.static_saabb);
+//   4. child shape pairs (compound culling, i-major / j-minor within a body pair) stream through
+//      a 128-entry LDS queue; every 64 pairs form a batch that is finished right away:
+//      narrowphase one lane per pair (small shapes), wave-cooperative narrowphase for big hulls
+//      and EPA (in pair order), then the persistent-manifold update one lane per pair with an
+//      order-preserving append of the surviving points to the new contact pool.
+// The previous contact pool stays in the env's global state (read, and updated in place by the
+// single lane that owns each point); the new pool is appended to global scratch and copied
+// over the old one at the end.
+#define SCR_EPA 0                                   // EpaBuf
+#define SCR_NEWCP 2560                              // new contact pool [AVR_MAX_CONTACTS][16]
+
+AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, v3 &mn, v3 &mx) {
+    const int c = m.shape_cidx[s];
+    if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
+    else { const float *a = m.static_saabb + 8 * s; mn = ld3(a); mx = ld3(a + 4); }
+}
+
+// narrowphase + manifold update for the nq (<= 64) queued pairs, lane q <-> queue entry q
+AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int nold, float *newcp, int &nnew, EpaBuf &E) {
     const int lane = lane_id();
     const int gender = L.gender;
+    (void)gender;
+    int sa = 0, sb = 0, p = 0;
+    if (lane < nq) { int k = L.u.c.qk[lane]; sa = k & 0xffff; sb = k >> 16; p = L.u.c.qp[lane]; }
+    int rc = 0;
+    v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+    float d = 0.f;
+    bool coop = false;
+    if (lane < nq) {
+        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
+        if (A.nv > SMALL_NV || B.nv > SMALL_NV) coop = true;
+        else {
+            rc = narrowphase<false>(m, E, A, B, thr, nB, pB, d);
+            if (rc == 2) coop = true;
+        }
+    }
+    // wave-cooperative narrowphase, in pair order
+    unsigned long long cm = __ballot(coop);
+    while (cm) {
+        const int j = __ffsll((long long)cm) - 1;
+        cm &= cm - 1;
+        const int sj = __shfl(sa, j, 64), tj = __shfl(sb, j, 64);
+        int ba = m.shape_body[sj], bb = m.shape_body[tj];
+        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        WShape A = make_wshape(m, sj, ldtf(L.btf[ba])), B = make_wshape(m, tj, ldtf(L.btf[bb]));
+        v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
+        float d2 = 0.f;
+        int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2);
+        if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
+    }
+    // manifold update (one lane per pair)
+    unsigned pk = 0u;
+    int n = 0;
+    MfNew nw;
+#pragma unroll
+    for (int k = 0; k < AVR_CP_WORDS; k++) nw.p[k] = 0.f;
+    if (lane < nq) {
+        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        const int key = sa | (sb << 16);
+        for (int i = 0; i < nold && n < AVR_MANIFOLD_POINTS; i++)
+            if (L.u.c.okey[i] == key) { pk = mf_set(pk, n, i); n++; }
+        tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+        if (rc == 1) manifold_add(oldcp, nw, pk, n, sa, sb, p, ta, tb, nB, pB, d, thr);
+        manifold_refresh(oldcp, nw, pk, n, ta, tb, thr);
+    }
+    int incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - n;
+    const int tot = __shfl(incl, 63, 64);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < n) {
+            int dst = nnew + excl + k;
+            int id = mf_idx(pk, k);
+            if (dst < AVR_MAX_CONTACTS) {
+                // 16-word point record: the new point from registers or an old one from memory
+                float4 *o = (float4 *)(newcp + AVR_CP_WORDS * dst);
+                if (id == MF_NEW) {
+                    o[0] = make_float4(nw.p[0], nw.p[1], nw.p[2], nw.p[3]);
+                    o[1] = make_float4(nw.p[4], nw.p[5], nw.p[6], nw.p[7]);
+                    o[2] = make_float4(nw.p[8], nw.p[9], nw.p[10], nw.p[11]);
+                    o[3] = make_float4(nw.p[12], nw.p[13], nw.p[14], nw.p[15]);
+                } else {
+                    const float *q = oldcp + AVR_CP_WORDS * id;     // state rows are only 4-byte aligned
+                    o[0] = make_float4(q[0], q[1], q[2], q[3]);
+                    o[1] = make_float4(q[4], q[5], q[6], q[7]);
+                    o[2] = make_float4(q[8], q[9], q[10], q[11]);
+                    o[3] = make_float4(q[12], q[13], q[14], q[15]);
+                }
+            }
+        }
+    }
+    nnew += tot;
+}
+
+AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
+    const int lane = lane_id();
+    const int gender = L.gender;
+    EpaBuf &E = *(EpaBuf *)(scratch + SCR_EPA);
+    float *newcp = scratch + SCR_NEWCP;
     PROF_START(pt);
     // body transforms + fattened AABBs
     for (int b = lane; b < m.nb; b += 64) {
@@ -873,10 +988,24 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         aabb_of(t, ld3(a), ld3(a + 3), mn, mx);
         v3 e = V(BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND);
         sttf(L.btf[b], t);
-        st3(L.bmin[b], sub(mn, e));
-        st3(L.bmax[b], add(mx, e));
+        st3(L.u.c.bmin[b], sub(mn, e));
+        st3(L.u.c.bmax[b], add(mx, e));
     }
+    // keys of the previous contact pool (matching in the manifold update)
+    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    for (int i = lane; i < nold; i += 64)
+        L.u.c.okey[i] = (int)gcp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gcp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     SYNC();
+    // world AABBs of the non-static child shapes
+    for (int s = lane; s < m.ns; s += 64) {
+        const int c = m.shape_cidx[s];
+        if (c >= 0) {
+            v3 mn, mx;
+            shape_aabb(m, s, ldtf(L.btf[m.shape_body[s]]), mn, mx);
+            st3(L.u.c.caabb[c], mn);
+            st3(L.u.c.caabb[c] + 3, mx);
+        }
+    }
     // broadphase over the candidate pair list, order-preserving compaction
     int nap = 0;
     for (int base = 0; base < m.np; base += 64) {
@@ -884,7 +1013,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
         bool act = false;
         if (p < m.np) {
             int ba = m.pair_a[p], bb = m.pair_b[p];
-            act = overlap(ld3(L.bmin[ba]), ld3(L.bmax[ba]), ld3(L.bmin[bb]), ld3(L.bmax[bb]));
+            act = overlap(ld3(L.u.c.bmin[ba]), ld3(L.u.c.bmax[ba]), ld3(L.u.c.bmin[bb]), ld3(L.u.c.bmax[bb]));
         }
         int tot;
         int pre = ballot_prefix(act, &tot);
@@ -894,135 +1023,69 @@ AVR_DI void collide(const KModel &m, EnvLDS &L) {
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
     PROF_STOP(1, pt);
-    // child-level shape pairs (compound culling), i-major / j-minor within each body pair
-    int nsp = 0;
+    // child shape pairs -> queue -> batches of 64
+    int nq = 0, nsp = 0, nnew = 0;
     for (int k = 0; k < nap; k++) {
-        int p = L.u.c.apair[k];
-        int ba = m.pair_a[p], bb = m.pair_b[p];
-        int sa0 = m.body_shape_start[ba], na = m.body_shape_count[ba];
-        int sb0 = m.body_shape_start[bb], nb = m.body_shape_count[bb];
-        bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
-        tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
-        int nitems = na * nb;
+        const int p = L.u.c.apair[k];
+        const int ba = m.pair_a[p], bb = m.pair_b[p];
+        const int sa0 = m.body_shape_start[ba], na = m.body_shape_count[ba];
+        const int sb0 = m.body_shape_start[bb], nb = m.body_shape_count[bb];
+        const bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
+        const int nitems = na * nb;
 #ifdef AVR_PROF
         if (lane == 0) L.prof[11] += nitems;
 #endif
         for (int base = 0; base < nitems; base += 64) {
-            int it = base + lane;
+            const int it = base + lane;
             bool act = false;
             int sa = 0, sb = 0;
             if (it < nitems) {
-                sa = sa0 + it / nb;
-                sb = sb0 + it % nb;
+                const int i = it / nb;
+                sa = sa0 + i;
+                sb = sb0 + (it - i * nb);
                 if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
                     if (bare) act = true;
                     else {
                         v3 a0, a1, b0, b1;
-                        shape_aabb(m, sa, ta, a0, a1);
-                        shape_aabb(m, sb, tb, b0, b1);
+                        child_aabb(m, L, sa, a0, a1);
+                        child_aabb(m, L, sb, b0, b1);
                         act = overlap(a0, a1, b0, b1);
                     }
                 }
             }
             int tot;
             int pre = ballot_prefix(act, &tot);
-            if (act && nsp + pre < MAXSP) {
-                L.u.c.sp_a[nsp + pre] = sa;
-                L.u.c.sp_b[nsp + pre] = sb;
-                L.u.c.sp_pair[nsp + pre] = p;
-            }
+            // the restated pipeline keeps at most MAXSP shape pairs per sub-step (flag 8)
+            if (act && nsp + pre < MAXSP) { L.u.c.qk[nq + pre] = sa | (sb << 16); L.u.c.qp[nq + pre] = p; }
+            const int add = nsp + tot <= MAXSP ? tot : (nsp < MAXSP ? MAXSP - nsp : 0);
             nsp += tot;
+            nq += add;
+            if (nq >= 64) {
+                SYNC();
+                PROF_STOP(2, pt);
+                collide_batch(m, L, 64, gcp, nold, newcp, nnew, E);
+                PROF_STOP(3, pt);
+                SYNC();
+                if (lane < nq - 64) { L.u.c.qk[lane] = L.u.c.qk[64 + lane]; L.u.c.qp[lane] = L.u.c.qp[64 + lane]; }
+                nq -= 64;
+                SYNC();
+            }
         }
     }
-    if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; nsp = MAXSP; }
+    if (nq > 0) {
+        SYNC();
+        PROF_STOP(2, pt);
+        collide_batch(m, L, nq, gcp, nold, newcp, nnew, E);
+        PROF_STOP(3, pt);
+    }
+    if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; }
 #ifdef AVR_PROF
-    if (lane == 0) { L.prof[14] += nsp; L.prof[15] += nap; }
+    if (lane == 0) { L.prof[14] += nsp < MAXSP ? nsp : MAXSP; L.prof[15] += nap; }
 #endif
-    SYNC();
-    PROF_STOP(2, pt);
-    // narrowphase pass A: one lane per small shape pair; big hulls and EPA deferred
-    for (int q = lane; q < nsp; q += 64) {
-        int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q];
-        int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
-        float *r = L.u.c.res[q];
-        if (A.nv > SMALL_NV || B.nv > SMALL_NV) { r[0] = 2.f; continue; }
-        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
-        float d = 0.f;
-        int rc = narrowphase<false>(m, L, A, B, thr, nB, pB, d);
-        r[0] = (float)rc;
-        st3(r + 1, nB); st3(r + 4, pB); r[7] = d;
-    }
-    SYNC();
-    PROF_STOP(3, pt);
-    // pass B: wave-cooperative narrowphase (big hulls, EPA), in pair order
-    for (int q = 0; q < nsp; q++) {
-        if (L.u.c.res[q][0] != 2.f) continue;
-        int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q];
-        int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
-        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
-        float d = 0.f;
-        int rc = narrowphase<true>(m, L, A, B, thr, nB, pB, d);
-        SYNC();
-        if (lane == 0) {
-            float *r = L.u.c.res[q];
-            r[0] = (float)rc;
-            st3(r + 1, nB); st3(r + 4, pB); r[7] = d;
-        }
-        SYNC();
-    }
-    PROF_STOP(4, pt);
-    // pass C: rebuild the contact pool, one lane per manifold, order-preserving
-    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
-    float *oldcp = L.st + AVR_S_CP;
-    int nnew = 0;
-    for (int base = 0; base < nsp; base += 64) {
-        int q = base + lane;
-        unsigned pk = 0u;
-        int n = 0;
-        MfNew nw;
-#pragma unroll
-        for (int k = 0; k < AVR_CP_WORDS; k++) nw.p[k] = 0.f;
-        if (q < nsp) {
-            int sa = L.u.c.sp_a[q], sb = L.u.c.sp_b[q], p = L.u.c.sp_pair[q];
-            int ba = m.shape_body[sa], bb = m.shape_body[sb];
-            float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-            for (int i = 0; i < nold && n < AVR_MANIFOLD_POINTS; i++) {
-                const float *c = oldcp + AVR_CP_WORDS * i;
-                if ((int)c[AVR_CP_SA] == sa && (int)c[AVR_CP_SB] == sb) { pk = mf_set(pk, n, i); n++; }
-            }
-            tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
-            const float *r = L.u.c.res[q];
-            if (r[0] == 1.f) manifold_add(oldcp, nw, pk, n, sa, sb, p, ta, tb, ld3(r + 1), ld3(r + 4), r[7], thr);
-            manifold_refresh(oldcp, nw, pk, n, ta, tb, thr);
-        }
-        // exclusive prefix sum of survivor counts across lanes
-        int incl = n;
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        int excl = incl - n;
-        int tot = __shfl(incl, 63, 64);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (k < n) {
-                int dst = nnew + excl + k;
-                int id = mf_idx(pk, k);
-                if (dst < AVR_MAX_CONTACTS) {
-#pragma unroll
-                    for (int w = 0; w < AVR_CP_WORDS; w++) L.u.c.newcp[dst][w] = mf_rd(oldcp, nw, id, w);
-                }
-            }
-        }
-        nnew += tot;
-    }
     if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
     SYNC();
-    for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) L.st[AVR_S_CP + i] = (&L.u.c.newcp[0][0])[i];
+    // the new pool replaces the old one
+    for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) gcp[i] = newcp[i];
     if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
     SYNC();
     PROF_STOP(5, pt);
@@ -1046,10 +1109,8 @@ AVR_DI void robot_jac(const KModel &m, const EnvLDS &L, int link, v3 p, v3 lin, 
     }
 }
 
-AVR_DI float free_dot(const EnvLDS &L, int f, v3 lin, v3 ang, bool delta) {
-    v3 v = delta ? ld3(L.dfv[f]) : ld3(L.fv[f]);
-    v3 w = delta ? ld3(L.dfw[f]) : ld3(L.fw[f]);
-    return dot(lin, v) + dot(ang, w);
+AVR_DI float free_dot(const EnvLDS &L, int f, v3 lin, v3 ang) {
+    return dot(lin, ld3(L.fv[f])) + dot(ang, ld3(L.fw[f]));
 }
 
 AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
@@ -1057,13 +1118,6 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
     return V(I[0] * a.x + I[1] * a.y + I[2] * a.z, I[3] * a.x + I[4] * a.y + I[5] * a.z, I[6] * a.x + I[7] * a.y + I[8] * a.z);
 }
 
-AVR_DI float robot_dot(const KModel &m, const EnvLDS &L, const float *J, bool delta) {
-    (void)m;
-    float s = 0.f;
-#pragma unroll
-    for (int d = 0; d < MAXD; d++) s += J[d] * (delta ? L.dq[d] : L.vq[d]);
-    return s;
-}
 
 // Constraint rows live in a per-env buffer in global memory (L2-resident working set), one
 // 32-word record per row, in solve order [non-contact][normals][frictions]:
@@ -1217,7 +1271,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
                 v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
                 den += dot(jbl, mbl) + dot(jba, mba);
                 float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                rel += free_dot(L, fb, jbl, jba, false);
+                rel += free_dot(L, fb, jbl, jba);
                 float *w = row_rec(m, rows, row);
                 put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f);
                 put_free_zero(w + 8);
@@ -1253,13 +1307,13 @@ AVR_DI void body_endpoint(const KModel &m, int b, int &kind, int &idx) {
 
 // Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal) and
 // n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions).
-AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float *rows, int n_nc, float dt) {
+AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
     const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
     const float erp = m.erp;
     for (int i = lane; i < ncp; i += 64) {
         int kA = 0, iA = 0, kB = 0, iB = 0;
-        const float *c = L.st + AVR_S_CP + AVR_CP_WORDS * i;
+        const float *c = gcp + AVR_CP_WORDS * i;
         int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
         body_endpoint(m, ba, kA, iA);
@@ -1292,7 +1346,7 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float *rows, int n_nc
             } else if (kA == 2) {
                 v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
                 den += dot(dir, ml) + dot(ja, ma);
-                rel += free_dot(L, iA, dir, ja, false);
+                rel += free_dot(L, iA, dir, ja);
                 put_free(w + 8, dir, ja, ml, ma);
             } else put_free_zero(w + 8);
             v3 nd = scl(dir, -1.f);
@@ -1306,7 +1360,7 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, float *rows, int n_nc
             } else if (kB == 2) {
                 v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
                 den += dot(nd, ml) + dot(jb, mb);
-                rel += free_dot(L, iB, nd, jb, false);
+                rel += free_dot(L, iB, nd, jb);
                 put_free(w + 20, nd, jb, ml, mb);
             } else put_free_zero(w + 20);
             if (rob) put_robot(row_rob(m, rows, row), J, MJ);
@@ -1466,12 +1520,12 @@ AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV 
 // Sub-step part A (kernel avr_substep_a): forward kinematics, collision, unconstrained
 // velocities, constraint rows.  Part B (avr_substep_b): PGS + integration.  What crosses the
 // kernel boundary goes through the per-env workspace (m.ws) and the row buffer (m.rows).
-AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *ws, float *rows) {
+AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows) {
     const int lane = lane_id();
     PROF_START(ps);
     robot_fk(m, L);
     PROF_STOP(0, ps);
-    collide(m, L);
+    collide(m, L, gst + AVR_S_CP, rows);
     PROF_STOP(13, ps);
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
@@ -1492,7 +1546,6 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *ws, float *ro
     if (lane < m.nd) {
         float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
         L.vq[lane] = clampf(v, -vmax, vmax);
-        L.dq[lane] = 0.f;
     }
     const float k1l = m.lin_damp, k1a = m.ang_damp;
     if (lane < m.nf) {
@@ -1509,8 +1562,6 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *ws, float *ro
         v3 nw = add(om, scl(inertia_inv_mul(q, I, T), dt));
         st3(L.fv[f], clamp3(nv, vmax));
         st3(L.fw[f], clamp3(nw, vmax));
-        st3(L.dfv[f], V(0, 0, 0));
-        st3(L.dfw[f], V(0, 0, 0));
         // world inverse inertia R diag(1/I) R^T
         m3 R = qmat(q);
         float inv[3] = {I.x > 0.f ? 1.f / I.x : 0.f, I.y > 0.f ? 1.f / I.y : 0.f, I.z > 0.f ? 1.f / I.z : 0.f};
@@ -1521,7 +1572,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *ws, float *ro
     PROF_STOP(6, ps);
     const int n_nc = build_noncontact_rows(m, L, rows, dt);
     PROF_STOP(7, ps);
-    build_contact_rows(m, L, rows, n_nc, dt);
+    build_contact_rows(m, L, gst + AVR_S_CP, rows, n_nc, dt);
     SYNC();
     PROF_STOP(8, ps);
     // hand-over to part B
@@ -1546,13 +1597,13 @@ AVR_DI void mouth_target(const KModel &m, EnvLDS &L) {
 
 // sum of normalForce over contact points whose body pair satisfies `sel`, and their count
 // sel: 0 robot-human, 1 spoon-human, 2 body X vs body Y, 3 body X vs human
-AVR_DI float contact_sum(const KModel &m, const EnvLDS &L, int sel, int X, int Y, int &count) {
+AVR_DI float contact_sum(const KModel &m, const EnvLDS &L, const float *gcp, int sel, int X, int Y, int &count) {
     const int lane = lane_id();
     int n = (int)L.st[AVR_S_TASK + AVR_T_NCP];
     float s = 0.f;
     int c = 0;
     for (int i = lane; i < n; i += 64) {
-        const float *cp = L.st + AVR_S_CP + AVR_CP_WORDS * i;
+        const float *cp = gcp + AVR_CP_WORDS * i;
         int ba = m.shape_body[(int)cp[AVR_CP_SA]], bb = m.shape_body[(int)cp[AVR_CP_SB]];
         int ka = m.body_kind[ba], kb = m.body_kind[bb];
         bool hit;
@@ -1633,7 +1684,7 @@ AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env *
 
 AVR_DI void load_state(EnvLDS &L, const float *gst) {
     const int lane = lane_id();
-    for (int i = lane; i < AVR_STATE_WORDS; i += 64) L.st[i] = gst[i];
+    for (int i = lane; i < AVR_S_CP; i += 64) L.st[i] = gst[i];
     if (lane == 0) { L.flags = 0; L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER]; }
 #ifdef AVR_PROF
     if (lane < 16) L.prof[lane] = 0;
@@ -1685,14 +1736,13 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     AVR_ENV_GUARD();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     load_state(L, gst);
-    bool ok = substep_a(m, L, dt, env_ws(m, env), env_rows(m, env));
+    bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env));
     if (lane_id() == 0 && !ok) L.flags |= 1;
     SYNC();
     if (lane_id() == 0) L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)((int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags);
     SYNC();
-    // write back what part A changes: the contact cache (+ count, flags)
-    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
-    for (int i = lane_id(); i < ncp * AVR_CP_WORDS; i += 64) gst[AVR_S_CP + i] = L.st[AVR_S_CP + i];
+    // write back what part A changes in LDS: contact count and flags (the pool itself was
+    // written to global memory by collide)
     if (lane_id() < 16) gst[AVR_S_TASK + lane_id()] = L.st[AVR_S_TASK + lane_id()];
     prof_flush(m, L, env);
 }
@@ -1757,6 +1807,7 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     AVR_ENV_GUARD();
     const int lane = lane_id();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    const float *gcp = gst + AVR_S_CP;
     load_state(L, gst);
     PROF_START(ptask);
     mouth_target(m, L);
@@ -1766,8 +1817,8 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
         if (lane == 0) L.st[AVR_S_TASK + AVR_T_ITER] += 1.f;
         SYNC();
         int dummy;
-        float robot_force = contact_sum(m, L, 0, 0, 0, dummy);
-        float spoon_force = contact_sum(m, L, 1, 0, 0, dummy);
+        float robot_force = contact_sum(m, L, gcp, 0, 0, 0, dummy);
+        float spoon_force = contact_sum(m, L, gcp, 1, 0, 0, dummy);
         float food_reward = 0.f, hit_reward = 0.f, mouth_vel = 0.f;
         int alive = (int)L.st[AVR_S_TASK + AVR_T_ALIVE], hit = (int)L.st[AVR_S_TASK + AVR_T_HIT];
         float succ = L.st[AVR_S_TASK + AVR_T_SUCCESS];
@@ -1788,14 +1839,14 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
                 continue;
             }
             int ctab, cbowl, chum;
-            contact_sum(m, L, 2, fbody, m.table_body, ctab);
-            contact_sum(m, L, 2, fbody, m.bowl_body, cbowl);
+            contact_sum(m, L, gcp, 2, fbody, m.table_body, ctab);
+            contact_sum(m, L, gcp, 2, fbody, m.bowl_body, cbowl);
             if (fp.z < 0.5f || ctab > 0 || cbowl > 0) {
                 food_reward -= 5.f;
                 alive &= ~(1 << k);
                 continue;
             }
-            contact_sum(m, L, 3, fbody, 0, chum);
+            contact_sum(m, L, gcp, 3, fbody, 0, chum);
             if (chum > 0 && !(hit >> k & 1)) { hit |= 1 << k; hit_reward -= 1.f; }
         }
         SYNC();
@@ -1825,14 +1876,16 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     SYNC();
     // NaN guard + flags, then write the state back
     bool bad = false;
-    for (int i = lane; i < AVR_STATE_WORDS; i += 64) bad |= !(L.st[i] == L.st[i]);
+    for (int i = lane; i < AVR_S_CP; i += 64) bad |= !(L.st[i] == L.st[i]);
+    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    for (int i = lane; i < ncp * AVR_CP_WORDS; i += 64) bad |= !(gcp[i] == gcp[i]);
     bad = __any(bad);
     if (lane == 0) {
         int fl = (int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags | (bad ? 1 : 0);
         L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)fl;
     }
     SYNC();
-    for (int i = lane; i < AVR_STATE_WORDS; i += 64) gst[i] = L.st[i];
+    for (int i = lane; i < AVR_S_CP; i += 64) gst[i] = L.st[i];
     PROF_STOP(12, ptask);
     prof_flush(m, L, env);
 }
@@ -1863,29 +1916,38 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 //   substep_a, substep_b with dt = bit-cast(t)                           (SUBSTEP)
 extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
                                       unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
-                                      hipStream_t stream) {
+                                      hipStream_t stream, avr_evlog *log) {
     if (n_envs <= 0) return hipSuccess;
     const int nsub = h_m->nsub > 0 ? h_m->nsub : 1;
     const float dt = h_m->time_step / (float)nsub;
+    auto mark = [&](int kind) {
+        if (log && log->n < log->cap && hipEventRecord(log->ev[log->n], stream) == hipSuccess) log->kind[log->n++] = kind;
+    };
     auto sub = [&](float h) {
+        mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
+        mark(AVR_K_B);
         hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
     };
     if (mode == MODE_SUBSTEP) {
         float h;
         std::memcpy(&h, &t, sizeof(float));
         sub(h);
+        mark(-1);
         return hipGetLastError();
     }
     if (mode == MODE_SETTLE) {
         for (long long f = 0; f < t; f++)
             for (int k = 0; k < nsub; k++) sub(dt);
     } else {
+        mark(AVR_K_TAKE);
         hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, n_envs);
         for (int f = 0; f < h_m->frame_skip; f++)
             for (int k = 0; k < nsub; k++) sub(dt);
     }
+    mark(AVR_K_TASK);
     hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, n_envs);
+    mark(-1);
     return hipGetLastError();
 }
 

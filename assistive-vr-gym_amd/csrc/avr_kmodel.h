@@ -7,7 +7,8 @@
 #define MAXL AVR_MAX_LINKS
 #define MAXD AVR_MAX_DOF
 #define MAXF AVR_MAX_FREE
-#define MAXB 64
+#define MAXB 48
+#define MAXCC 224      // non-static child shapes whose world AABBs are cached per sub-step
 #define MAXSP 256
 #define MAXAP 256
 #define MAXNC 32
@@ -40,6 +41,8 @@ struct KModel {
     const int *shape_kind, *shape_body, *shape_gender, *shape_hull;   // hull [ns][4]
     const float *shape_pose, *shape_param, *shape_margin, *shape_aabb; // [ns][8] [ns][4] [ns] [ns][8]
     const float4 *hull_verts;
+    const int *shape_cidx;      // [ns] index into the per-sub-step child AABB cache, -1 for static shapes
+    const float *static_saabb;  // [ns][8] world AABB (min3, pad, max3, pad) of static shapes (host-computed)
     const int *pair_a, *pair_b;
     int n_arm, arm_dofs[8], n_finger, finger_dofs[4];
     int tool_link, torso_link, head_slot, spoon_free, bowl_free, food_free0, n_food;
@@ -58,4 +61,13 @@ struct KModel {
     int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
+};
+
+// Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):
+// an event is recorded before every launch (kind = AVR_K_*) and after the last one (kind -1).
+enum { AVR_K_TAKE = 0, AVR_K_A = 1, AVR_K_B = 2, AVR_K_TASK = 3, AVR_K_KINDS = 4 };
+struct avr_evlog {
+    hipEvent_t *ev;
+    int *kind;
+    int n, cap;
 };

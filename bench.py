@@ -144,18 +144,29 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    # per-kernel launch durations (HIP events between the launches of a step, on the sim
+    # stream), from a separate short pass so the timed loop above carries no event overhead
+    P = min(10, args.steps)
+    sim.profile_kernels(True)
+    for k in range(P):
+        one_step(args.warmup + args.steps + k, k)
+    kt = sim.kernel_times()
+    sim.profile_kernels(False)
+    kernels = {k: {'avg_ms': v[0] / max(v[1], 1), 'launches_per_step': v[1] / P, 'ms_per_step': v[0] / P} for k, v in kt.items()}
+    step_kernel_ms = sum(v['ms_per_step'] for v in kernels.values())
+    dominant = max(kernels, key=lambda k: kernels[k]['ms_per_step'])
     St = sim.get_state()
     flags = St[:, ABI.S_TASK + ABI.T_FLAGS].astype(np.int64)
     value = world * E * args.steps / el
     bpe = ALGO_BYTES_PER_ENV_STEP
-    achieved = bpe * E / (kern_ms * 1e-3) / 1e9
+    achieved = bpe * E / (step_kernel_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get('envs') == E:
-                traffic = tj.get('hbm_bytes_per_launch')
+                traffic = tj.get('hbm_bytes_per_step')
         except Exception:
             traffic = None
     out = {
@@ -176,8 +187,11 @@ def main():
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'scope': 'one env-step = 1 take_step + 10 x (substep_a, substep_b) + 1 task launch; '
+                              'achieved = algorithmic bytes of the step / summed launch durations',
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(ABI),
-                     'kernel': 'avr_env_step_kernel', 'kernel_ms': kern_ms},
+                     'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
+                     'dominant_kernel': dominant, 'kernels': kernels},
         'nan_or_overflow_envs': int(np.count_nonzero(flags)),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -92,6 +92,13 @@ int32_t avr_abi_version(void);
 int avr_kernel_info(avr_sim *sim, int32_t *out8);
 const char *avr_last_error(avr_sim *sim);
 
+/* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
+ * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times
+ * returns the accumulated milliseconds and launch counts per kernel kind
+ * [take_step, substep_a, substep_b, task] since enabling (synchronises the stream). */
+int avr_profile_kernels(avr_sim *sim, int32_t enable);
+int avr_kernel_times(avr_sim *sim, double *ms4, int64_t *count4);
+
 /* Diagnostics (phase-timer builds only, -DAVR_PROF): attach a device buffer of
  * [n_envs][16] uint64 cycle counters.  A no-op for the shipped kernel. */
 int avr_set_profile_buffer(avr_sim *sim, void *d_prof);

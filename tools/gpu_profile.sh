@@ -3,12 +3,14 @@
 set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/prof
 B="bench.py --steps 20 --warmup 3 --no-cpu-baseline"
+(rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_before.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt -- python3 $B > gpurun_out/prof/kt_bench.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/fetch.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/write.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/prof/sq -o sq -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/sq.log 2>&1 && \
 timeout -k 10 600 python3 bench.py > gpurun_out/prof/bench_full.log 2>&1
 rc=$?
+(rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_after.txt
 find gpurun_out/prof -name "*.csv" | head -20
 tail -1 gpurun_out/prof/bench_full.log
 echo rc=$rc

@@ -17,7 +17,7 @@ import sys
 
 import numpy as np
 
-STEP = 'avr_env_step_kernel'
+STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_a_kernel': 10, 'avr_substep_b_kernel': 10, 'avr_task_kernel': 1}
 
 
 def db(d):
@@ -39,12 +39,21 @@ def kernel_stats(c):
 
 
 def counters(c, names):
+    """{kernel: {counter: median per-dispatch value}} for the step's kernels."""
     res = {}
-    for n in names:
-        v = [r[0] for r in c.execute("select value from counters_collection where counter_name=? and kernel_name like ?", (n, STEP + '%'))]
-        if v:
-            res[n] = float(np.median(v))
+    for k in STEP_KERNELS:
+        for n in names:
+            v = [r[0] for r in c.execute("select value from counters_collection where counter_name=? and kernel_name like ?", (n, k + '%'))]
+            if v:
+                res.setdefault(k, {})[n] = float(np.median(v))
     return res
+
+
+def per_step(cnt, name):
+    """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS)."""
+    if not cnt or any(name not in cnt.get(k, {}) for k in STEP_KERNELS):
+        return None
+    return sum(cnt[k][name] * m for k, m in STEP_KERNELS.items())
 
 
 def main(pdir, tag, envs=4096):
@@ -60,23 +69,23 @@ def main(pdir, tag, envs=4096):
                 f.write('%s,%d,%.0f,%.1f,%.1f,%.0f,%.0f,%.2f\n' % r)
         for r in st:
             print('%-28s calls %4d avg %10.3f ms  median %10.3f ms  %5.1f%%' % (r[0], r[1], r[3] / 1e6, r[4] / 1e6, r[7]))
-    out = {'kernel': STEP, 'envs': envs}
+    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs}
     cf, cw, cs = db(os.path.join(pdir, 'fetch')), db(os.path.join(pdir, 'write')), db(os.path.join(pdir, 'sq'))
-    if cf:
-        out['FETCH_SIZE_KiB_raw'] = counters(cf, ['FETCH_SIZE']).get('FETCH_SIZE')
-    if cw:
-        out['WRITE_SIZE_KiB'] = counters(cw, ['WRITE_SIZE']).get('WRITE_SIZE')
+    fetch = counters(cf, ['FETCH_SIZE']) if cf else {}
+    write = counters(cw, ['WRITE_SIZE']) if cw else {}
+    out['FETCH_SIZE_KiB_raw_per_launch'] = {k: v['FETCH_SIZE'] for k, v in fetch.items()}
+    out['WRITE_SIZE_KiB_per_launch'] = {k: v['WRITE_SIZE'] for k, v in write.items()}
     if cs:
-        out['sq'] = counters(cs, ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_INSTS_LDS', 'SQ_WAIT_ANY',
-                                  'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES'])
-    if out.get('FETCH_SIZE_KiB_raw') is not None and out.get('WRITE_SIZE_KiB') is not None:
-        fb = 2 * out['FETCH_SIZE_KiB_raw'] * 1024
-        wb = out['WRITE_SIZE_KiB'] * 1024
-        out['hbm_read_bytes_per_launch'] = fb
-        out['hbm_write_bytes_per_launch'] = wb
-        out['hbm_bytes_per_launch'] = fb + wb
+        out['sq_per_launch'] = counters(cs, ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_INSTS_LDS', 'SQ_WAIT_ANY',
+                                             'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES'])
+    f_step, w_step = per_step(fetch, 'FETCH_SIZE'), per_step(write, 'WRITE_SIZE')
+    if f_step is not None and w_step is not None:
+        fb, wb = 2 * f_step * 1024, w_step * 1024
+        out['hbm_read_bytes_per_step'] = fb
+        out['hbm_write_bytes_per_step'] = wb
+        out['hbm_bytes_per_step'] = fb + wb
         out['hbm_bytes_per_env_step'] = (fb + wb) / envs
-        out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median over step-kernel dispatches'
+        out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x launches per step'
         json.dump(out, open(os.path.join(prof, 'pmc_traffic.json'), 'w'), indent=1)
     json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
     print(json.dumps(out, indent=1))
