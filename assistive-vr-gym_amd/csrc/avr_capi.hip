@@ -16,12 +16,14 @@
 #include "avr_kmodel.h"
 
 extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
-                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
-                                      hipStream_t stream, avr_evlog *log);
+                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int env0,
+                                      int env1, hipStream_t stream, avr_evlog *log);
 extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
 extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream);
 extern "C" hipError_t avr_kernel_attrs(int *out8);
+
+#define AVR_MAX_GROUPS 8
 
 struct avr_sim {
     avr_config cfg;
@@ -35,6 +37,13 @@ struct avr_sim {
     float *d_act, *d_obs, *d_rew, *d_info;
     unsigned char *d_done;
     char err[512];
+    // env groups on their own streams: group g's launch sequence runs concurrently with the
+    // others', so latency-bound PGS waves of one group share the CUs with compute-bound
+    // collision waves of another (envs are independent; fork/join events keep the handle's
+    // stream the single point of ordering for callers)
+    int ngroups;
+    hipStream_t gstream[AVR_MAX_GROUPS];
+    hipEvent_t fork_ev, join_ev[AVR_MAX_GROUPS];
     avr_evlog evlog;                       // per-kernel timing (avr_profile_kernels)
     std::vector<hipEvent_t> ev;
     std::vector<int> evkind;
@@ -150,6 +159,19 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     *out = s;
     HIPCHK(s, hipSetDevice(cfg->device));
     HIPCHK(s, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    {
+        const char *g = getenv("AVR_ENV_GROUPS");
+        int ng = g ? atoi(g) : 2;
+        if (ng < 1) ng = 1;
+        if (ng > AVR_MAX_GROUPS) ng = AVR_MAX_GROUPS;
+        if (ng > cfg->n_envs) ng = cfg->n_envs;
+        s->ngroups = ng;
+        HIPCHK(s, hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
+        for (int i = 0; i < ng; i++) {
+            HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));
+            HIPCHK(s, hipEventCreateWithFlags(&s->join_ev[i], hipEventDisableTiming));
+        }
+    }
     KModel &k = s->km;
     memset(&k, 0, sizeof(k));
     int nl = d->n_links, nb = d->n_bodies, ns = d->n_shapes;
@@ -274,6 +296,28 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     return 0;
 }
 
+
+// one launch sequence over all envs: on the handle's stream (1 group, or while per-kernel
+// timing is on), else forked over the group streams and joined back
+static hipError_t run_step(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
+                           const unsigned char *mask, int mode, long long t) {
+    const int E = s->cfg.n_envs;
+    if (s->ngroups <= 1 || s->evlog.cap)
+        return avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, 0, E, s->stream,
+                               s->evlog.cap ? &s->evlog : nullptr);
+    hipError_t e = hipEventRecord(s->fork_ev, s->stream);
+    if (e != hipSuccess) return e;
+    for (int g = 0; g < s->ngroups; g++) {
+        const int e0 = (int)((long long)E * g / s->ngroups), e1 = (int)((long long)E * (g + 1) / s->ngroups);
+        if ((e = hipStreamWaitEvent(s->gstream[g], s->fork_ev, 0)) != hipSuccess) return e;
+        if ((e = avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, e0, e1, s->gstream[g], nullptr)) != hipSuccess)
+            return e;
+        if ((e = hipEventRecord(s->join_ev[g], s->gstream[g])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s->stream, s->join_ev[g], 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 extern "C" int avr_destroy(avr_sim *s) {
     if (!s) return -1;
     if (s->stream) (void)hipStreamSynchronize(s->stream);
@@ -288,6 +332,11 @@ extern "C" int avr_destroy(avr_sim *s) {
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->d_mask) (void)hipFree(s->d_mask);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    for (int i = 0; i < s->ngroups; i++) {
+        if (s->gstream[i]) (void)hipStreamDestroy(s->gstream[i]);
+        if (s->join_ev[i]) (void)hipEventDestroy(s->join_ev[i]);
+    }
+    if (s->fork_ev) (void)hipEventDestroy(s->fork_ev);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return 0;
@@ -334,7 +383,7 @@ extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_
     if (!h) return fail(s, -1, "avr_reset: host_state is NULL");
     if (n_frames < 0) return fail(s, -1, "avr_reset: n_frames < 0");
     if (upload_masked(s, mask, h)) return -2;
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames));
     if (host_obs) {
         std::vector<float> o(E * AVR_OBS_DIM);
         HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
@@ -355,7 +404,7 @@ extern "C" int avr_get_state(avr_sim *s, float *h) {
 
 extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames));
     if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
@@ -365,21 +414,21 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 3, t));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0));
     return 0;
 }
 
 extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
-                              d_info ? d_info : s->d_info, nullptr, 1, t, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
+                              d_info ? d_info : s->d_info, nullptr, 1, t));
     return 0;
 }
 
@@ -393,7 +442,7 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
     HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
-    HIPCHK(s, avr_launch_step(&s->km, s->d_km, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0, s->cfg.n_envs, s->stream, s->evlog.cap ? &s->evlog : nullptr));
+    HIPCHK(s, run_step(s, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0));
     HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));

@@ -50,6 +50,7 @@ struct EnvLDS {
             int apair[MAXAP];              // active body pairs (broadphase output, in pair order)
             int okey[AVR_MAX_CONTACTS];    // (sa | sb << 16) of the previous contact pool
             int qk[128], qp[128];          // shape-pair queue: (sa | sb << 16), body pair
+            int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
             float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
         } c;
         struct {
@@ -912,6 +913,10 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
     }
     // wave-cooperative narrowphase, in pair order
     unsigned long long cm = __ballot(coop);
+#ifdef AVR_PROF
+    unsigned long long tcoop = __builtin_amdgcn_s_memtime();
+    if (lane == 0) L.prof[11] += __popcll(cm);
+#endif
     while (cm) {
         const int j = __ffsll((long long)cm) - 1;
         cm &= cm - 1;
@@ -924,6 +929,9 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2);
         if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
     }
+#ifdef AVR_PROF
+    if (lane == 0) L.prof[5] += __builtin_amdgcn_s_memtime() - tcoop;
+#endif
     // manifold update (one lane per pair)
     unsigned pk = 0u;
     int n = 0;
@@ -1023,7 +1031,10 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
     PROF_STOP(1, pt);
-    // child shape pairs -> queue -> batches of 64
+    // child shape pairs -> queue -> batches of 64.  A child's world AABB lies inside its body's
+    // fattened AABB, so children of A that miss B's body AABB cannot meet any child of B: the
+    // child lists are culled against the other body first, which leaves the set of overlapping
+    // child pairs and its i-major / j-minor order unchanged.
     int nq = 0, nsp = 0, nnew = 0;
     for (int k = 0; k < nap; k++) {
         const int p = L.u.c.apair[k];
@@ -1031,25 +1042,71 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
         const int sa0 = m.body_shape_start[ba], na = m.body_shape_count[ba];
         const int sb0 = m.body_shape_start[bb], nb = m.body_shape_count[bb];
         const bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
-        const int nitems = na * nb;
+        int ncA = na, ncB = nb;
+        const bool cull = !bare && na * nb > 1;
+        if (cull) {
+            const v3 bAmn = ld3(L.u.c.bmin[ba]), bAmx = ld3(L.u.c.bmax[ba]);
+            const v3 bBmn = ld3(L.u.c.bmin[bb]), bBmx = ld3(L.u.c.bmax[bb]);
+            ncA = 0;
+            for (int base = 0; base < na; base += 64) {
+                const int i = base + lane;
+                bool act = false;
+                if (i < na && shape_enabled(m, sa0 + i, gender)) {
+                    v3 a0, a1;
+                    child_aabb(m, L, sa0 + i, a0, a1);
+                    act = overlap(a0, a1, bBmn, bBmx);
+                }
+                int tot;
+                int pre = ballot_prefix(act, &tot);
+                if (act) L.u.c.candA[ncA + pre] = sa0 + i;
+                ncA += tot;
+            }
+            ncB = 0;
+            for (int base = 0; base < nb; base += 64) {
+                const int j = base + lane;
+                bool act = false;
+                if (j < nb && shape_enabled(m, sb0 + j, gender)) {
+                    v3 b0, b1;
+                    child_aabb(m, L, sb0 + j, b0, b1);
+                    act = overlap(b0, b1, bAmn, bAmx);
+                }
+                int tot;
+                int pre = ballot_prefix(act, &tot);
+                if (act) L.u.c.candB[ncB + pre] = sb0 + j;
+                ncB += tot;
+            }
+            SYNC();
+        }
+        const int nitems = ncA * ncB;
 #ifdef AVR_PROF
-        if (lane == 0) L.prof[11] += nitems;
+        if (lane == 0) L.prof[4] += nitems;
 #endif
+        const float rcpB = 1.f / (float)(ncB > 0 ? ncB : 1);
         for (int base = 0; base < nitems; base += 64) {
             const int it = base + lane;
             bool act = false;
             int sa = 0, sb = 0;
             if (it < nitems) {
-                const int i = it / nb;
-                sa = sa0 + i;
-                sb = sb0 + (it - i * nb);
-                if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
-                    if (bare) act = true;
-                    else {
-                        v3 a0, a1, b0, b1;
-                        child_aabb(m, L, sa, a0, a1);
-                        child_aabb(m, L, sb, b0, b1);
-                        act = overlap(a0, a1, b0, b1);
+                const int i = (int)(((float)it + 0.5f) * rcpB);     // exact: it < 2^14, ncB <= 128
+                const int j = it - i * ncB;
+                if (cull) {
+                    sa = L.u.c.candA[i];
+                    sb = L.u.c.candB[j];
+                    v3 a0, a1, b0, b1;
+                    child_aabb(m, L, sa, a0, a1);
+                    child_aabb(m, L, sb, b0, b1);
+                    act = overlap(a0, a1, b0, b1);
+                } else {
+                    sa = sa0 + i;
+                    sb = sb0 + j;
+                    if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
+                        if (bare) act = true;
+                        else {
+                            v3 a0, a1, b0, b1;
+                            child_aabb(m, L, sa, a0, a1);
+                            child_aabb(m, L, sb, b0, b1);
+                            act = overlap(a0, a1, b0, b1);
+                        }
                     }
                 }
             }
@@ -1071,6 +1128,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                 SYNC();
             }
         }
+        if (cull) SYNC();
     }
     if (nq > 0) {
         SYNC();
@@ -1088,7 +1146,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) gcp[i] = newcp[i];
     if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
     SYNC();
-    PROF_STOP(5, pt);
+    PROF_STOP(2, pt);
 }
 
 // --------------------------------------------------------------------------- constraint rows
@@ -1673,7 +1731,7 @@ enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 #define AVR_KATTR __attribute__((amdgpu_waves_per_eu(AVR_WAVES_PER_EU)))
 
 #define AVR_ENV_GUARD()                      \
-    const int env = blockIdx.x;              \
+    const int env = env0 + blockIdx.x;       \
     if (env >= n_envs) return;               \
     if (mask && !mask[env]) return;          \
     const KModel &m = *mp;                   \
@@ -1704,8 +1762,8 @@ AVR_DI void prof_flush(const KModel &m, EnvLDS &L, int env) {
 // take_step (env.py:274-337): clip, scale, 5x limit-respecting accumulation, motor targets.
 // One thread per env.
 __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
-                                                           const unsigned char *__restrict__ mask, int mode, long long t, int n_envs) {
-    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+                                                           const unsigned char *__restrict__ mask, int mode, long long t, int env0, int n_envs) {
+    const int env = env0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
     float *st = state + (size_t)env * AVR_STATE_WORDS;
@@ -1731,7 +1789,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
 
 // Sub-step part A: one 64-lane block per env, state staged in LDS.
 __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                                     const unsigned char *__restrict__ mask, float dt, int n_envs) {
+                                                                     const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
@@ -1751,7 +1809,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 // quaternion exp-map update of btTransformUtil::integrateTransform for the free bodies.
 // No LDS: velocities and impulses stay in registers.
 __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                           const unsigned char *__restrict__ mask, float dt, int n_envs) {
+                                                           const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
     AVR_ENV_GUARD();
     const int lane = lane_id();
 #ifdef AVR_PROF
@@ -1802,7 +1860,7 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
 // TimeLimit; SETTLE mode: target + reset observation only.  NaN guard for every mode.
 __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ obs,
                                                       float *__restrict__ rew, unsigned char *__restrict__ done, float *__restrict__ info,
-                                                      const unsigned char *__restrict__ mask, int mode, int n_envs) {
+                                                      const unsigned char *__restrict__ mask, int mode, int env0, int n_envs) {
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     const int lane = lane_id();
@@ -1914,9 +1972,11 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 //   take_step -> frame_skip x nsub x (substep_a, substep_b) -> task      (STEP, STEP_RANDOM)
 //   t frames x nsub x (substep_a, substep_b) -> task (settle obs)        (SETTLE)
 //   substep_a, substep_b with dt = bit-cast(t)                           (SUBSTEP)
+// envs [env0, env1) of the handle; n_envs arguments of the kernels are the end bound env1
 extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
-                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int n_envs,
-                                      hipStream_t stream, avr_evlog *log) {
+                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int env0,
+                                      int env1, hipStream_t stream, avr_evlog *log) {
+    const int n_envs = env1 - env0;
     if (n_envs <= 0) return hipSuccess;
     const int nsub = h_m->nsub > 0 ? h_m->nsub : 1;
     const float dt = h_m->time_step / (float)nsub;
@@ -1925,9 +1985,9 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     };
     auto sub = [&](float h) {
         mark(AVR_K_A);
-        hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
+        hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
-        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, n_envs);
+        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
     };
     if (mode == MODE_SUBSTEP) {
         float h;
@@ -1941,12 +2001,12 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
             for (int k = 0; k < nsub; k++) sub(dt);
     } else {
         mark(AVR_K_TAKE);
-        hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, n_envs);
+        hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, env0, env1);
         for (int f = 0; f < h_m->frame_skip; f++)
             for (int k = 0; k < nsub; k++) sub(dt);
     }
     mark(AVR_K_TASK);
-    hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, n_envs);
+    hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, env0, env1);
     mark(-1);
     return hipGetLastError();
 }

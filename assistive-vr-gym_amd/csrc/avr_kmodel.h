@@ -12,7 +12,9 @@
 #define MAXSP 256
 #define MAXAP 256
 #define MAXNC 32
-#define SMALL_NV 64
+#ifndef SMALL_NV
+#define SMALL_NV 64     // hulls with more vertices take the wave-cooperative narrowphase
+#endif
 #define GJK_MAX_IT 64
 #define GJK_REL_EPS 1e-6f
 #define EPA_MAX_IT 64

@@ -17,12 +17,12 @@ sim = _lib.Sim(md, N)
 prof = torch.zeros(N * 16, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
-names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '-', 'poolcopy', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#childitems', 'task', 'collide', '#shapepairs', '#bodypairs']
+names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '(coop part)', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
     p = prof.cpu().numpy().reshape(N, 16).astype(np.float64)
-    tot = p[:, [0, 13, 6, 7, 8, 9, 10, 12]].sum(1).mean()
+    tot = p[:, [0, 13, 6, 7, 8, 9, 10, 12]].sum(1).mean()   # (coop part) is inside narrow+mf
     print('step %d wall %.1f ms, mean cycles/env %.3g' % (t, el * 1e3, tot))
     for k, nm in enumerate(names):
         if nm == '-':
