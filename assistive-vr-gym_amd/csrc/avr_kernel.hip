@@ -23,6 +23,7 @@
 
 #include "../../include/avr.h"
 #include <cstring>
+#include <cstdlib>
 #include "avr_math.h"
 
 #include "avr_kmodel.h"
@@ -35,7 +36,8 @@ struct EnvLDS {
     float st[AVR_S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
     float btf[MAXB][8];
-    float Mi[MAXD][MAXD];
+    float Mi[MAXD][MAXD];   // Cholesky factor of the mass matrix (lower)
+    float Minv[MAXD][MAXD]; // its inverse
     float vq[MAXD];
     float fv[MAXF][4], fw[MAXF][4];
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
@@ -110,6 +112,8 @@ AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &
 
 // Mass matrix: one lane per lower-triangle entry (a,b); Cholesky on lane 0 in LDS.  Rows and
 // columns beyond nd are padded with the identity so M^-1 solves run over MAXD unrolled.
+AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x);
+
 AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
     const int nd = m.nd;
     const int lane = lane_id();
@@ -138,24 +142,46 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         if (a != b) L.Mi[b][a] = 0.f;
     }
     SYNC();
+    // column Cholesky, rows of each column in parallel (one lane per row)
     int ok = 1;
-    if (lane == 0) {
-        for (int j = 0; j < MAXD; j++) {
-            float s = L.Mi[j][j];
-            for (int k = 0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
-            if (s <= 0.f) ok = 0;
-            float d = sqrtf(fmaxf(s, 1e-30f));
-            L.Mi[j][j] = d;
-            for (int i = j + 1; i < MAXD; i++) {
-                float t = L.Mi[i][j];
-                for (int k = 0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
-                L.Mi[i][j] = t / d;
-            }
+    for (int j = 0; j < MAXD; j++) {
+        float s = L.Mi[j][j];
+        for (int k = 0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
+        if (s <= 0.f) ok = 0;
+        const float d = sqrtf(fmaxf(s, 1e-30f));
+        float t = 0.f;
+        const int i = lane;
+        if (i > j && i < MAXD) {
+            t = L.Mi[i][j];
+            for (int k = 0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
         }
-        L.pad = ok;
+        SYNC();
+        if (i > j && i < MAXD) L.Mi[i][j] = t / d;
+        if (i == j) L.Mi[j][j] = d;
+        SYNC();
+    }
+    // columns of M^-1 (one lane per DoF): every robot row gets M^-1 J^T from these
+    if (lane < MAXD) {
+        float e[MAXD], x[MAXD];
+#pragma unroll
+        for (int k = 0; k < MAXD; k++) e[k] = k == lane ? 1.f : 0.f;
+        chol_solve(m, L, e, x);
+#pragma unroll
+        for (int k = 0; k < MAXD; k++) L.Minv[k][lane] = x[k];
     }
     SYNC();
-    return L.pad != 0;
+    return ok != 0;
+}
+
+// y = M^-1 x (padding DoFs have identity rows)
+AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < MAXD; k++) s += L.Minv[i][k] * x[k];
+        y[i] = s;
+    }
 }
 
 // x = M^-1 b with the Cholesky factor in LDS; fixed-size, fully unrolled (register arrays)
@@ -1217,127 +1243,114 @@ AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
     for (int d = 0; d < MAXD; d++) { w[d] = J[d]; w[16 + d] = MJ[d]; }
 }
 
-// Non-contact rows (limits, motors, fixed constraint); lanes build rows in parallel.
+// Non-contact rows (limits, motors, fixed constraint), one lane per row.
 // Row order restates btMultiBodyConstraintSolver's setup order: joint-limit rows
 // of violated limits (link order, lower then upper), motor rows (link order), fixed rows.
 AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float dt) {
     const int lane = lane_id();
     const float erp = m.erp;
-    int nrow = 0;
-    // limits
+    // enumerate (uniform loop); each lane keeps the description of its own row
+    int nrow = 0, kind = -1, dof = 0, fix = 0;
+    float pen = 0.f;
     for (int i = 0; i < m.nl; i++) {
         if (!m.rl_has_limit[i]) continue;
-        int dof = m.rl_dof[i];
-        float q = L.st[AVR_S_Q + dof];
+        const int d = m.rl_dof[i];
+        const float q = L.st[AVR_S_Q + d];
         for (int side = 0; side < 2; side++) {
-            float pen = side == 0 ? q - m.rl_lower[i] : m.rl_upper[i] - q;
-            if (pen > 0.f) continue;
-            if (nrow < MAXNC && lane == (nrow & 63)) {
-                float JA[MAXD], MA[MAXD];
-#pragma unroll
-                for (int d = 0; d < MAXD; d++) JA[d] = d == dof ? (side == 0 ? 1.f : -1.f) : 0.f;
-                chol_solve(m, L, JA, MA);
-                float den = 0.f, rel = 0.f;
-#pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
-                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                float *w = row_rec(m, rows, nrow);
-                put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f);
-                put_free_zero(w + 8); put_free_zero(w + 20);
-                put_robot(row_rob(m, rows, nrow), JA, MA);
-            }
+            const float pn = side == 0 ? q - m.rl_lower[i] : m.rl_upper[i] - q;
+            if (pn > 0.f) continue;
+            if (lane == nrow) { kind = side; dof = d; pen = pn; }
             nrow++;
         }
     }
-    // motors
     for (int i = 0; i < m.nl; i++) {
-        int dof = m.rl_dof[i];
-        if (dof < 0) continue;
-        if (nrow < MAXNC && lane == (nrow & 63)) {
-            float JA[MAXD], MA[MAXD];
-#pragma unroll
-            for (int d = 0; d < MAXD; d++) JA[d] = d == dof ? 1.f : 0.f;
-            chol_solve(m, L, JA, MA);
-            float den = 0.f, rel = 0.f;
-#pragma unroll
-            for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
-            float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-            float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
-            float kp = L.st[AVR_S_KP + dof], kd = 1.f;
-            float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
-            float mi = L.st[AVR_S_MAXIMP + dof];
-            float *w = row_rec(m, rows, nrow);
-            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f);
-            put_free_zero(w + 8); put_free_zero(w + 20);
-            put_robot(row_rob(m, rows, nrow), JA, MA);
-        }
+        const int d = m.rl_dof[i];
+        if (d < 0) continue;
+        if (lane == nrow) { kind = 2; dof = d; }
         nrow++;
     }
-    // fixed constraint robot tool link <-> spoon
-    {
-        int link = m.tool_link, fb = m.spoon_free;
-        tf ta = ldtf(L.cm[link]);
-        tf off = ldtf(m.tool_offset);
-        v3 pivA = tfpt(ta, off.p);
-        qt frA = qmul(ta.q, off.q);
-        tf tb = ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * fb);
-        v3 pivB = tb.p;
-        m3 FA = qmat(frA), FB = qmat(tb.q);
-        m3 rr;
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) {
-                float s = 0.f;
-                for (int k = 0; k < 3; k++) s += FA.m[k][a] * FB.m[k][b];
-                rr.m[a][b] = s;
-            }
-#define ME(i) rr.m[(i) % 3][(i) / 3]
-        v3 ang;
-        float fi = ME(2);
-        if (fi < 1.f) {
-            if (fi > -1.f) ang = V(atan2f(-ME(5), ME(8)), asinf(ME(2)), atan2f(-ME(1), ME(0)));
-            else ang = V(-atan2f(ME(3), ME(4)), -1.5707963267948966f, 0.f);
-        } else ang = V(atan2f(ME(3), ME(4)), 1.5707963267948966f, 0.f);
-#undef ME
-        float mi = m.fixed_max_imp;
-        for (int i = 0; i < 6; i++) {
-            int row = nrow + i;
-            if (row < MAXNC && lane == (row & 63)) {
-                v3 lin = V(0, 0, 0), an = V(0, 0, 0);
-                float pos;
-                float JA[MAXD];
-                v3 jbl, jba;
-                if (i < 3) {
-                    if (i == 0) lin.x = 1.f; else if (i == 1) lin.y = 1.f; else lin.z = 1.f;
-                    pos = dot(sub(pivA, pivB), lin);
-                    robot_jac(m, L, link, pivA, lin, V(0, 0, 0), JA);
-                    jbl = scl(lin, -1.f);
-                    jba = crs(sub(pivB, tb.p), jbl);
-                } else {
-                    v3 c0 = V(FA.m[0][0], FA.m[1][0], FA.m[2][0]), c1 = V(FA.m[0][1], FA.m[1][1], FA.m[2][1]), c2 = V(FA.m[0][2], FA.m[1][2], FA.m[2][2]);
-                    an = i == 3 ? c0 : (i == 4 ? c1 : c2);
-                    pos = i == 3 ? ang.x : i == 4 ? ang.y : ang.z;
-                    robot_jac(m, L, link, pivA, V(0, 0, 0), an, JA);
-                    jbl = V(0, 0, 0);
-                    jba = scl(an, -1.f);
-                }
-                float MA[MAXD];
-                chol_solve(m, L, JA, MA);
-                float den = 0.f, rel = 0.f;
+    if (lane >= nrow && lane < nrow + 6) { kind = 3; fix = lane - nrow; }
+    nrow += 6;
+    if (lane >= MAXNC) kind = -1;
+    // fixed constraint robot tool link <-> spoon (uniform geometry)
+    const int link = m.tool_link, fb = m.spoon_free;
+    const tf ta = ldtf(L.cm[link]);
+    const tf off = ldtf(m.tool_offset);
+    const v3 pivA = tfpt(ta, off.p);
+    const qt frA = qmul(ta.q, off.q);
+    const tf tb = ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * fb);
+    const v3 pivB = tb.p;
+    const m3 FA = qmat(frA), FB = qmat(tb.q);
+    if (kind == 0 || kind == 1 || kind == 2) {
+        // J = +-e_dof: M^-1 J^T is a signed column of M^-1
+        const float sg = kind == 1 ? -1.f : 1.f;
+        float J[MAXD], MJ[MAXD];
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
-                float im = 1.f / m.fb_mass[fb];
-                v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
-                den += dot(jbl, mbl) + dot(jba, mba);
-                float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
-                rel += free_dot(L, fb, jbl, jba);
-                float *w = row_rec(m, rows, row);
-                put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f);
-                put_free_zero(w + 8);
-                put_free(w + 20, jbl, jba, mbl, mba);
-                put_robot(row_rob(m, rows, row), JA, MA);
-            }
+        for (int d = 0; d < MAXD; d++) { J[d] = d == dof ? sg : 0.f; MJ[d] = sg * L.Minv[d][dof]; }
+        const float den = L.Minv[dof][dof];
+        const float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+        const float rel = sg * L.vq[dof];
+        float *w = row_rec(m, rows, lane);
+        if (kind < 2) {
+            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f);
+        } else {
+            const float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
+            const float kp = L.st[AVR_S_KP + dof], kd = 1.f;
+            const float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
+            const float mi = L.st[AVR_S_MAXIMP + dof];
+            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f);
         }
-        nrow += 6;
+        put_free_zero(w + 8); put_free_zero(w + 20);
+        put_robot(row_rob(m, rows, lane), J, MJ);
+    } else if (kind == 3) {
+        v3 lin = V(0, 0, 0);
+        float pos;
+        float JA[MAXD], MA[MAXD];
+        v3 jbl, jba;
+        if (fix < 3) {
+            if (fix == 0) lin.x = 1.f; else if (fix == 1) lin.y = 1.f; else lin.z = 1.f;
+            pos = dot(sub(pivA, pivB), lin);
+            robot_jac(m, L, link, pivA, lin, V(0, 0, 0), JA);
+            jbl = scl(lin, -1.f);
+            jba = crs(sub(pivB, tb.p), jbl);
+        } else {
+            m3 rr;
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) {
+                    float t = 0.f;
+                    for (int k = 0; k < 3; k++) t += FA.m[k][a] * FB.m[k][b];
+                    rr.m[a][b] = t;
+                }
+#define ME(i) rr.m[(i) % 3][(i) / 3]
+            v3 ang;
+            const float fi = ME(2);
+            if (fi < 1.f) {
+                if (fi > -1.f) ang = V(atan2f(-ME(5), ME(8)), asinf(ME(2)), atan2f(-ME(1), ME(0)));
+                else ang = V(-atan2f(ME(3), ME(4)), -1.5707963267948966f, 0.f);
+            } else ang = V(atan2f(ME(3), ME(4)), 1.5707963267948966f, 0.f);
+#undef ME
+            const v3 c0 = V(FA.m[0][0], FA.m[1][0], FA.m[2][0]), c1 = V(FA.m[0][1], FA.m[1][1], FA.m[2][1]), c2 = V(FA.m[0][2], FA.m[1][2], FA.m[2][2]);
+            const v3 an = fix == 3 ? c0 : (fix == 4 ? c1 : c2);
+            pos = fix == 3 ? ang.x : fix == 4 ? ang.y : ang.z;
+            robot_jac(m, L, link, pivA, V(0, 0, 0), an, JA);
+            jbl = V(0, 0, 0);
+            jba = scl(an, -1.f);
+        }
+        minv_mul(L, JA, MA);
+        float den = 0.f, rel = 0.f;
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
+        const float im = 1.f / m.fb_mass[fb];
+        const v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
+        den += dot(jbl, mbl) + dot(jba, mba);
+        const float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+        rel += free_dot(L, fb, jbl, jba);
+        const float mi = m.fixed_max_imp;
+        float *w = row_rec(m, rows, lane);
+        put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f);
+        put_free_zero(w + 8);
+        put_free(w + 20, jbl, jba, mbl, mba);
+        put_robot(row_rob(m, rows, lane), JA, MA);
     }
     if (nrow > MAXNC) { if (lane == 0) L.flags |= 16; nrow = MAXNC; }
     if (lane == 0) L.n_nc = nrow;
@@ -1397,7 +1410,7 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
             if (kA == 1) {
                 float Ja[MAXD], Ma[MAXD];
                 robot_jac(m, L, iA, pa, dir, V(0, 0, 0), Ja);
-                chol_solve(m, L, Ja, Ma);
+                minv_mul(L, Ja, Ma);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; J[d] += Ja[d]; MJ[d] += Ma[d]; }
                 put_free_zero(w + 8);
@@ -1411,7 +1424,7 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
             if (kB == 1) {
                 float Jb[MAXD], Mb[MAXD];
                 robot_jac(m, L, iB, pb, nd, V(0, 0, 0), Jb);
-                chol_solve(m, L, Jb, Mb);
+                minv_mul(L, Jb, Mb);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; J[d] += Jb[d]; MJ[d] += Mb[d]; }
                 put_free_zero(w + 20);
@@ -1588,18 +1601,12 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
     robot_bias(m, L);
-    {
-        float nh[MAXD], qdd[MAXD];
-#pragma unroll
-        for (int d = 0; d < MAXD; d++) nh[d] = d < m.nd ? -L.h[d] : 0.f;
-        chol_solve(m, L, nh, qdd);
-        SYNC();
-        if (lane == 0) {
-#pragma unroll
-            for (int d = 0; d < MAXD; d++) L.qdd[d] = qdd[d];
-        }
-        SYNC();
+    if (lane < MAXD) {                      // qdd = -M^-1 h, one lane per DoF
+        float s = 0.f;
+        for (int k = 0; k < m.nd; k++) s -= L.Minv[lane][k] * L.h[k];
+        L.qdd[lane] = s;
     }
+    SYNC();
     const float vmax = m.max_vel;
     if (lane < m.nd) {
         float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
