@@ -195,6 +195,7 @@ def feeding_reset_state(A, md, seed, env_id, gender=None, impairment='none'):
     rng = _rng(seed, env_id)
     if gender is None:
         gender = 'male' if rng.integers(2) == 0 else 'female'     # feeding.py:169
+    impairment = _impairment(rng, impairment)
     limit_scale = rng.uniform(0.5, 1.0) if impairment == 'limits' else 1.0   # world_creation.py:71
     st = np.zeros(ABI.STATE_WORDS)
     qh = human_joint_angles(A, gender, rng, limit_scale)
@@ -360,6 +361,22 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, r
     return Qout, done
 
 
+IMPAIRMENTS = ('none', 'limits', 'weakness')   # world_creation.py:65-72 without 'tremor'
+
+
+def _impairment(rng, impairment):
+    """Resolve the impairment of one env (world_creation.py:66-69).  'tremor' drives the head/neck
+    with motors (env.py:327-337) and is not built: the human is static for the other three
+    (feeding.py:244 passes no controllable joints, world_creation.py:157-159 zeroes the masses)."""
+    if impairment == 'no_tremor':
+        return IMPAIRMENTS[int(rng.integers(3))]
+    if impairment in IMPAIRMENTS:
+        return impairment
+    if impairment in ('tremor', 'random'):
+        raise NotImplementedError("impairment %r: the tremor-driven head/neck is not built (use 'no_tremor')" % impairment)
+    raise ValueError('unknown impairment %r' % impairment)
+
+
 def _rng(seed, env_id, episode=0):
     """Per-env, per-episode reset stream: independent of batch composition and GPU count."""
     key = [int(seed), int(env_id)] if not episode else [int(seed), int(env_id), int(episode)]
@@ -379,7 +396,8 @@ def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none
         rng = rngs[k]
         g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
         gl.append(g)
-        ls = rng.uniform(0.5, 1.0) if impairment == 'limits' else 1.0
+        imp = _impairment(rng, impairment)
+        ls = rng.uniform(0.5, 1.0) if imp == 'limits' else 1.0
         qh = human_joint_angles(A, g, rng, ls)
         S[k, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, g, qh).ravel()
         bowl[k] = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
