@@ -299,6 +299,18 @@ AVR_DI WShape make_wshape(const KModel &m, int s, tf body) {
 }
 
 // support point of the CORE in world direction d; COOP: the whole wave scans a big hull
+// read-only float4 array accessed through the global address space (global_load, not flat)
+struct GlobalF4 {
+    const float4 *p;
+    AVR_DI float4 operator[](int i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return ((const __attribute__((address_space(1))) float4 *)p)[i];
+#else
+        return p[i];
+#endif
+    }
+};
+
 template <bool COOP>
 AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
     v3 l = qrot(qconj(s.t.q), d);
@@ -307,28 +319,50 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
     else if (s.kind == AVR_CAPSULE) r = V(0, 0, l.z >= 0.f ? s.he.y : -s.he.y);
     else if (s.kind == AVR_BOX) r = V(l.x >= 0.f ? s.he.x : -s.he.x, l.y >= 0.f ? s.he.y : -s.he.y, l.z >= 0.f ? s.he.z : -s.he.z);
     else {
-        const float4 *hv = m.hull_verts + s.vs;
+        // vertices through the global address space, several loads in flight per pass; the
+        // first vertex with the strictly largest projection wins (index order), as before
+        const GlobalF4 hv{m.hull_verts + s.vs};
         if (COOP) {
             float best = -BIGF;
             int bi = 0x7fffffff;
-            for (int i = lane_id(); i < s.nv; i += 64) {
-                float4 v = hv[i];
-                float dd = l.x * v.x + l.y * v.y + l.z * v.z;
+            int i = lane_id();
+            for (; i + 192 < s.nv; i += 256) {
+                const float4 v0 = hv[i], v1 = hv[i + 64], v2 = hv[i + 128], v3_ = hv[i + 192];
+                float d0 = l.x * v0.x + l.y * v0.y + l.z * v0.z, d1 = l.x * v1.x + l.y * v1.y + l.z * v1.z;
+                float d2 = l.x * v2.x + l.y * v2.y + l.z * v2.z, d3 = l.x * v3_.x + l.y * v3_.y + l.z * v3_.z;
+                if (d0 > best) { best = d0; bi = i; }
+                if (d1 > best) { best = d1; bi = i + 64; }
+                if (d2 > best) { best = d2; bi = i + 128; }
+                if (d3 > best) { best = d3; bi = i + 192; }
+            }
+            for (; i < s.nv; i += 64) {
+                const float4 v = hv[i];
+                const float dd = l.x * v.x + l.y * v.y + l.z * v.z;
                 if (dd > best) { best = dd; bi = i; }
             }
             bi = wave_argmax(best, bi);
-            float4 v = hv[bi];
+            const float4 v = hv[bi];
             r = V(v.x, v.y, v.z);
         } else {
             float best = -BIGF;
-            int bi = 0;
-            for (int i = 0; i < s.nv; i++) {
-                float4 v = hv[i];
-                float dd = l.x * v.x + l.y * v.y + l.z * v.z;
-                if (dd > best) { best = dd; bi = i; }
+            float4 bv = hv[0];
+            int i = 0;
+            for (; i + 8 <= s.nv; i += 8) {
+                float4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = hv[i + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const float dd = l.x * v[k].x + l.y * v[k].y + l.z * v[k].z;
+                    if (dd > best) { best = dd; bv = v[k]; }
+                }
             }
-            float4 v = hv[bi];
-            r = V(v.x, v.y, v.z);
+            for (; i < s.nv; i++) {
+                const float4 v = hv[i];
+                const float dd = l.x * v.x + l.y * v.y + l.z * v.z;
+                if (dd > best) { best = dd; bv = v; }
+            }
+            r = V(bv.x, bv.y, bv.z);
         }
     }
     return tfpt(s.t, r);
