@@ -1567,9 +1567,11 @@ AVR_DI float row_go(const RowS &R, DV &d, float imp, float lo, float hi, bool ro
 // the normal impulses in in0/in1 (contact c at lane c&63).
 AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV &d, float &in0, float &in1) {
     const int lane = lane_id();
-    // row records were written by vector stores of the previous kernel; the scalar cache may
-    // still hold lines of the previous sub-step's rows: invalidate it and wait for the
-    // invalidation (an SMEM op itself) before the first row s_load.
+    // Row records were written by the previous kernel (substep_a) with vector stores, and the
+    // scalar cache can still hold this env's rows from the previous sub-step: the launch-time
+    // acquire does NOT reliably clear it (measured: without this invalidate, 7 % of 4096 envs
+    // read stale rows).  Invalidate it and wait for the invalidation (an SMEM op itself)
+    // before the first row s_load.
     asm volatile("s_dcache_inv\n\ts_waitcnt lgkmcnt(0)" : "+s"(rows) :: "memory");
     const float *robs = rows + m.rowcap * RW;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
@@ -1595,28 +1597,51 @@ AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV 
             float ni = row_go(R, d, rdl(inc, k), R.h[4], R.h[5], true);
             if (lane == k) inc = ni;
         }
-        for (int c = 0; c < n_c; c++) {
+        // rows are fetched two at a time (one scalar round trip for consecutive records)
+        for (int c = 0; c < n_c; c += 2) {
             const float *rec = rows + (n_nc + c) * RW;
-            RowS R;
-            R.h = *(cf8p)rec;
-            const bool robot = (__float_as_int(R.h[0]) & RI_ROBOT) != 0;
-            load_row(R, rec, robs + (n_nc + c) * RW, robot);
-            float ni = row_go(R, d, rdl(c < 64 ? in0 : in1, c & 63), 0.f, 1e10f, robot);
+            RowS R0, R1;
+            const bool two = c + 1 < n_c;
+            R0.h = *(cf8p)rec; R0.a = *(cf16p)(rec + 8); R0.b = *(cf8p)(rec + 24);
+            R1.h = *(cf8p)(rec + RW); R1.a = *(cf16p)(rec + RW + 8); R1.b = *(cf8p)(rec + RW + 24);
+            const bool rb0 = (__float_as_int(R0.h[0]) & RI_ROBOT) != 0;
+            R0.jr = 0.f; R0.mr = 0.f;
+            if (rb0 && lane < MAXD) { R0.jr = ((gfp)(robs + (n_nc + c) * RW))[lane]; R0.mr = ((gfp)(robs + (n_nc + c) * RW))[16 + lane]; }
+            float ni = row_go(R0, d, rdl(c < 64 ? in0 : in1, c & 63), 0.f, 1e10f, rb0);
             if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
+            if (two) {
+                const int c1 = c + 1;
+                const bool rb1 = (__float_as_int(R1.h[0]) & RI_ROBOT) != 0;
+                R1.jr = 0.f; R1.mr = 0.f;
+                if (rb1 && lane < MAXD) { R1.jr = ((gfp)(robs + (n_nc + c1) * RW))[lane]; R1.mr = ((gfp)(robs + (n_nc + c1) * RW))[16 + lane]; }
+                ni = row_go(R1, d, rdl(c1 < 64 ? in0 : in1, c1 & 63), 0.f, 1e10f, rb1);
+                if (lane == (c1 & 63)) { if (c1 < 64) in0 = ni; else in1 = ni; }
+            }
         }
-        for (int f = 0; f < 2 * n_c; f++) {
-            const int c = f >> 1;
+        for (int c = 0; c < n_c; c++) {
             const float nimp = rdl(c < 64 ? in0 : in1, c & 63);
             if (!(nimp > 0.f)) continue;
+            // the contact's two friction rows are adjacent records
+            const int f = 2 * c;
             const float *rec = rows + (n_nc + n_c + f) * RW;
-            RowS R;
-            R.h = *(cf8p)rec;
-            const bool robot = (__float_as_int(R.h[0]) & RI_ROBOT) != 0;
-            load_row(R, rec, robs + (n_nc + n_c + f) * RW, robot);
-            const float fr = R.h[1];
-            const int s = f >> 6;
-            float ni = row_go(R, d, rdl(s == 0 ? if0 : (s == 1 ? if1 : if2), f & 63), -fr * nimp, fr * nimp, robot);
-            if (lane == (f & 63)) { if (s == 0) if0 = ni; else if (s == 1) if1 = ni; else if2 = ni; }
+            RowS R0, R1;
+            R0.h = *(cf8p)rec; R0.a = *(cf16p)(rec + 8); R0.b = *(cf8p)(rec + 24);
+            R1.h = *(cf8p)(rec + RW); R1.a = *(cf16p)(rec + RW + 8); R1.b = *(cf8p)(rec + RW + 24);
+            const bool robot = (__float_as_int(R0.h[0]) & RI_ROBOT) != 0;    // same endpoints for both
+            R0.jr = R0.mr = R1.jr = R1.mr = 0.f;
+            if (robot && lane < MAXD) {
+                const float *q0 = robs + (n_nc + n_c + f) * RW;
+                R0.jr = ((gfp)q0)[lane]; R0.mr = ((gfp)q0)[16 + lane];
+                R1.jr = ((gfp)q0)[RW + lane]; R1.mr = ((gfp)q0)[RW + 16 + lane];
+            }
+            const float fr = R0.h[1];
+            const int s = f >> 6;           // f and f + 1 share the impulse register (f even)
+            float fimp = s == 0 ? if0 : (s == 1 ? if1 : if2);
+            float ni = row_go(R0, d, rdl(fimp, f & 63), -fr * nimp, fr * nimp, robot);
+            if (lane == (f & 63)) fimp = ni;
+            ni = row_go(R1, d, rdl(fimp, (f + 1) & 63), -fr * nimp, fr * nimp, robot);
+            if (lane == ((f + 1) & 63)) fimp = ni;
+            if (s == 0) if0 = fimp; else if (s == 1) if1 = fimp; else if2 = fimp;
         }
     }
 }
