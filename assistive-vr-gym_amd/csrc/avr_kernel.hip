@@ -489,6 +489,13 @@ AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
 #define GJK_SEPARATED 0
 #define GJK_FAR 1
 #define GJK_PENETRATING 2
+#define GJK_UNFINISHED 3        // lane path only: iteration cap hit, finish on the cooperative path
+// The lane-per-pair path runs at the pace of its slowest lane: pairs that have not converged
+// after GJK_LANE_IT iterations are handed to the wave-cooperative path, which reruns the same
+// GJK (same support tie-break, same arithmetic) to completion -- identical results.
+#ifndef GJK_LANE_IT
+#define GJK_LANE_IT GJK_MAX_IT     // measured: a cap of 4..16 does not pay on this scene
+#endif
 
 template <bool COOP>
 AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S) {
@@ -498,7 +505,9 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     float lam[4] = {1, 0, 0, 0};
     float prev = BIGF;
     int status = GJK_SEPARATED;
-    for (int it = 0; it < GJK_MAX_IT; it++) {
+    const int max_it = COOP ? GJK_MAX_IT : GJK_LANE_IT;
+    bool converged = false;
+    for (int it = 0; it < max_it; it++) {
         v3 sa = support<COOP>(m, A, scl(v, -1.f)), sb = support<COOP>(m, B, v);
         v3 wv = sub(sa, sb);
         float vv = len2(v), vw = dot(v, wv);
@@ -507,20 +516,21 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
 #pragma unroll
         for (int k = 0; k < 4; k++)
             if (k < S.n && S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
-        if (dup && S.n > 0) break;
-        if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) break;
+        if (dup && S.n > 0) { converged = true; break; }
+        if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) { converged = true; break; }
 #pragma unroll
         for (int k = 0; k < 4; k++)
             if (k == S.n) { S.w[k] = wv; S.a[k] = sa; S.b[k] = sb; }
         S.n++;
         v3 nv;
-        if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; break; }
+        if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; converged = true; break; }
         float nvv = len2(nv);
-        if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; break; }
-        if (nvv >= prev) { v = nv; break; }
+        if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; converged = true; break; }
+        if (nvv >= prev) { v = nv; converged = true; break; }
         prev = nvv;
         v = nv;
     }
+    if (!COOP && !converged) return GJK_UNFINISHED;
     if (status == GJK_PENETRATING) return GJK_PENETRATING;
     v3 a = V(0, 0, 0), b = V(0, 0, 0);
 #pragma unroll
@@ -755,6 +765,7 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
     Simplex S;
     int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S);
     if (st == GJK_FAR) return 0;
+    if (st == GJK_UNFINISHED) return 2;
     v3 n;
     float d;
     if (st == GJK_SEPARATED && cd > 1e-9f) {
@@ -974,7 +985,6 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
     // wave-cooperative narrowphase, in pair order
     unsigned long long cm = __ballot(coop);
 #ifdef AVR_PROF
-    unsigned long long tcoop = __builtin_amdgcn_s_memtime();
     if (lane == 0) L.prof[11] += __popcll(cm);
 #endif
     while (cm) {
@@ -989,9 +999,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2);
         if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
     }
-#ifdef AVR_PROF
-    if (lane == 0) L.prof[5] += __builtin_amdgcn_s_memtime() - tcoop;
-#endif
+
     // manifold update (one lane per pair)
     unsigned pk = 0u;
     int n = 0;
@@ -1252,6 +1260,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_NNC 0     // int bits: non-contact rows
 #define WS_NC 1      // int bits: contact points (rows n_nc .. n_nc + 3 n_c)
 #define WS_ASQ 2     // sum of squared caller actions (take_step -> task glue)
+#define WS_XCC 3     // diagnostic builds: XCD that ran part A
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW 72     // [MAXF][4] angular
@@ -1803,6 +1812,12 @@ enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
     const KModel &m = *mp;                   \
     (void)m
 
+#ifdef AVR_PROF
+AVR_DI int xcc_id() {   // XCD of the executing CU (HW_REG_XCC_ID, id 20, bits 3:0)
+    return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xf);
+}
+#endif
+
 AVR_DI float *env_ws(const KModel &m, int env) { return m.ws + (size_t)env * WS_WORDS; }
 AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)(2 * m.rowcap * RW); }
 
@@ -1861,6 +1876,9 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     load_state(L, gst);
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env));
+#ifdef AVR_PROF
+    if (lane_id() == 0) env_ws(m, env)[WS_XCC] = __int_as_float(xcc_id());
+#endif
     if (lane_id() == 0 && !ok) L.flags |= 1;
     SYNC();
     if (lane_id() == 0) L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)((int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags);
@@ -1917,7 +1935,11 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
     if (lane + 64 < n_c) st[AVR_S_CP + AVR_CP_WORDS * (lane + 64) + AVR_CP_IMP] = in1;
 #ifdef AVR_PROF
     unsigned long long t2 = __builtin_amdgcn_s_memtime();
-    if (m.prof && lane == 0) { m.prof[(size_t)env * 16 + 9] += t1 - t0; m.prof[(size_t)env * 16 + 10] += t2 - t1; }
+    if (m.prof && lane == 0) {
+        m.prof[(size_t)env * 16 + 9] += t1 - t0;
+        m.prof[(size_t)env * 16 + 10] += t2 - t1;
+        m.prof[(size_t)env * 16 + 5] += __float_as_int(ws[WS_XCC]) != xcc_id() ? 1 : 0;   // A/B on different XCDs
+    }
 #endif
 }
 

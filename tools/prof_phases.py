@@ -17,7 +17,7 @@ sim = _lib.Sim(md, N)
 prof = torch.zeros(N * 16, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
-names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '(coop part)', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs']
+names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
