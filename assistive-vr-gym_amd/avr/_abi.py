@@ -11,7 +11,8 @@ import numpy as np
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # ---- capacities / offsets (must match include/avr_model.h) ----
-MAX_LINKS, MAX_DOF, MAX_FREE, MAX_HUMAN, MAX_CONTACTS = 16, 12, 10, 20, 96
+ABI_VERSION = 2
+MAX_LINKS, MAX_DOF, MAX_FREE, MAX_HUMAN, MAX_CONTACTS, HC_N = 20, 14, 10, 20, 96, 4
 MAX_FOOD, ACT_DIM, OBS_DIM, INFO_DIM = 8, 7, 25, 2
 FB_WORDS, CP_WORDS = 13, 16
 S_Q = 0
@@ -21,9 +22,10 @@ S_KP = S_QTGT + MAX_DOF
 S_MAXIMP = S_KP + MAX_DOF
 S_FREE = S_MAXIMP + MAX_DOF
 S_TASK = S_FREE + MAX_FREE * FB_WORDS
-T_TARGET, T_ITER, T_SUCCESS, T_ALIVE, T_HIT, T_GENDER, T_FLAGS, T_NCP, T_WORDS = 0, 3, 4, 5, 6, 7, 8, 9, 16
+T_TARGET, T_ITER, T_SUCCESS, T_ALIVE, T_HIT, T_GENDER, T_FLAGS, T_NCP, T_HDYN, T_WORDS = 0, 3, 4, 5, 6, 7, 8, 9, 10, 16
 S_HUMAN = S_TASK + T_WORDS
-S_CP = S_HUMAN + MAX_HUMAN * 7
+S_HCH = S_HUMAN + MAX_HUMAN * 7          # [HC_N] target_human_joint_positions, [HC_N] human_tremors
+S_CP = S_HCH + 2 * HC_N
 STATE_WORDS = S_CP + MAX_CONTACTS * CP_WORDS
 CP_SA, CP_SB, CP_LA, CP_LB, CP_N, CP_DIST, CP_IMP, CP_LIFE, CP_PAIR = 0, 1, 2, 5, 8, 11, 12, 13, 14
 
@@ -77,6 +79,14 @@ class avr_model_desc(C.Structure):
         ('w_distance', C.c_double), ('w_action', C.c_double), ('w_food', C.c_double),
         ('w_velocity', C.c_double), ('w_force_nontarget', C.c_double), ('w_high_forces', C.c_double),
         ('w_food_hit', C.c_double), ('w_food_velocities', C.c_double), ('task_success_threshold', C.c_double),
+        ('hc_n', C.c_int32), ('hc_parent_slot', C.c_int32),
+        ('hc_slot', C.c_int32 * HC_N), ('hc_body', C.c_int32 * HC_N),
+        ('hc_jpos', ((C.c_double * 3) * HC_N) * 2),
+        ('hc_axis', (C.c_double * 3) * HC_N),
+        ('hc_mass', (C.c_double * HC_N) * 2), ('hc_inertia', ((C.c_double * 3) * HC_N) * 2),
+        ('hc_lower', C.c_double * HC_N), ('hc_upper', C.c_double * HC_N),
+        ('human_gain', C.c_double), ('human_force', C.c_double),
+        ('n_pairs_base', C.c_int32),
     ]
 
 
@@ -104,6 +114,8 @@ FEEDING_PARAMS = dict(
     w_velocity=0.25, w_force_nontarget=0.01, w_high_forces=0.05,     # config.ini:37-39
     w_food_hit=1.0, w_food_velocities=1.0,                           # config.ini:40-41
     task_success_threshold=0.75,                                     # config.ini:26
+    human_gain=0.005,            # feeding.py:48 take_step(..., human_gains=0.005)
+    human_force=1.0,             # feeding.py:17 human_forces (x human_strength, 1.0 unless 'weakness')
 )
 
 
@@ -158,6 +170,7 @@ class ModelDesc:
         self.A['hull_planes'] = np.zeros(4)
         d.hull_planes = self.A['hull_planes'].ctypes.data_as(PF64)
         d.n_pairs = len(A['pair_a'])
+        d.n_pairs_base = int(A['n_pairs_base']) if 'n_pairs_base' in A else d.n_pairs
         d.pair_a = arr('pair_a', np.int32)
         d.pair_b = arr('pair_b', np.int32)
         arm = [int(x) for x in A['task_arm_dofs']]
@@ -194,6 +207,21 @@ class ModelDesc:
                 d.arm_lower[i], d.arm_upper[i] = float(A['rl_lower'][l]), float(A['rl_upper'][l])
             else:
                 d.arm_lower[i], d.arm_upper[i] = -1e10, 1e10
+        if 'hc_slot' in A:                 # tremor head/neck chain (model_compiler.head_chain)
+            d.hc_n = HC_N
+            d.hc_parent_slot = int(A['hc_parent_slot'])
+            for k in range(HC_N):
+                d.hc_slot[k] = int(A['hc_slot'][k])
+                d.hc_body[k] = int(A['hc_body'][k])
+                d.hc_lower[k] = float(A['hc_lower'][k])
+                d.hc_upper[k] = float(A['hc_upper'][k])
+                for i in range(3):
+                    d.hc_axis[k][i] = float(A['hc_axis'][k][i])
+                for g in range(2):
+                    d.hc_mass[g][k] = float(A['hc_mass'][g][k])
+                    for i in range(3):
+                        d.hc_jpos[g][k][i] = float(A['hc_jpos'][g][k][i])
+                        d.hc_inertia[g][k][i] = float(A['hc_inertia'][g][k][i])
         for k, v in P.items():
             setattr(d, k, v)
         self.desc = d

@@ -68,6 +68,9 @@ def load(path=LIB_PATH):
     lib.avr_reset.argtypes = [vp, vp, vp, C.c_int32, vp]
     lib.avr_profile_kernels.argtypes = [vp, C.c_int32]
     lib.avr_kernel_times.argtypes = [vp, vp, vp]
+    if lib.avr_abi_version() != ABI.ABI_VERSION or lib.avr_state_words() != ABI.STATE_WORDS:
+        raise RuntimeError('%s: ABI %d / %d state words, this package expects ABI %d / %d (rebuild)'
+                           % (path, lib.avr_abi_version(), lib.avr_state_words(), ABI.ABI_VERSION, ABI.STATE_WORDS))
     _LIB = lib
     return lib
 

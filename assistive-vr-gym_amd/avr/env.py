@@ -114,10 +114,13 @@ class AVRVecEnv:
     env_offset: global id of env 0 (multi-GPU sharding: rank * n_envs); reset randomness and the
     synthetic action stream are keyed by the global env id, so results do not depend on how
     envs are split over GPUs.
+
+    impairment: 'random' (FeedingJaco-v0's own setting, feeding.py:175: none / limits /
+    weakness / tremor, one draw per episode), a fixed one of those four, or 'no_tremor'.
     """
 
     def __init__(self, env_id='FeedingJaco-v0', n_envs=1, device=0, seed=1001, env_offset=0, auto_reset=True,
-                 impairment='none'):
+                 impairment='random'):
         if env_id not in REGISTRY:
             raise KeyError('unknown env id %r' % env_id)
         task, robot, ok = REGISTRY[env_id]
@@ -193,8 +196,8 @@ class AVRVecEnv:
 class AVREnv:
     """Single-env view with the reference's gym.Env signatures."""
 
-    def __init__(self, env_id='FeedingJaco-v0', device=0, seed=1001):
-        self.v = AVRVecEnv(env_id, 1, device=device, seed=seed, auto_reset=False)
+    def __init__(self, env_id='FeedingJaco-v0', device=0, seed=1001, impairment='random'):
+        self.v = AVRVecEnv(env_id, 1, device=device, seed=seed, auto_reset=False, impairment=impairment)
         self.observation_space = self.v.observation_space
         self.action_space = self.v.action_space
 

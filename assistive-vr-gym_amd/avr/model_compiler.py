@@ -381,6 +381,37 @@ def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
     return [hips], links
 
 
+HEAD_CHAIN = (24, 25, 26, 27)    # human joints driven under 'tremor' (feeding.py:219, env.py:307-337)
+
+
+def head_chain(S):
+    """Arrays of the tremor head/neck chain (include/avr_model.h hc_*): joint origins, axes,
+    masses and inertias per gender (human_creation.py:195-207; inertia from the collision
+    shapes' compound AABB as for every other link), limits (limit_scale 1: 'tremor' is not
+    'limits', world_creation.py:71), and the human slot / collision body of each link."""
+    out = dict(hc_jpos=np.zeros((2, 4, 3)), hc_axis=np.zeros((4, 3)), hc_mass=np.zeros((2, 4)),
+               hc_inertia=np.zeros((2, 4, 3)), hc_lower=np.zeros(4), hc_upper=np.zeros(4),
+               hc_slot=np.full(4, -1, np.int32), hc_body=np.full(4, -1, np.int32))
+    for g, gender in enumerate(('male', 'female')):
+        hl = S.human[gender][1]
+        for k, li in enumerate(HEAD_CHAIN):
+            L = hl[li]
+            assert L['jtype'] == J_REVOLUTE and L['parent'] == (hl[HEAD_CHAIN[0]]['parent'] if k == 0 else li - 1)
+            out['hc_jpos'][g, k] = L['pos']
+            out['hc_mass'][g, k] = L['mass']
+            if L['shapes'] and L['mass'] > 0:
+                lo, hi = compound_aabb(L['shapes'])
+                out['hc_inertia'][g, k] = box_inertia(L['mass'], lo, hi)
+            out['hc_axis'][k] = L['axis']
+            out['hc_lower'][k], out['hc_upper'][k] = L['lower'], L['upper']
+    out['hc_parent_slot'] = np.int32(S.human_slots.index(S.human['male'][1][HEAD_CHAIN[0]]['parent']))
+    for k, li in enumerate(HEAD_CHAIN):
+        if li in S.human_slots:
+            out['hc_slot'][k] = S.human_slots.index(li)
+            out['hc_body'][k] = S.human_body[li]
+    return out
+
+
 def human_fk(links, base_pos, base_quat, q):
     """World poses of the human link frames (== COM frames) for joint angles q[42]."""
     n = len(links)
@@ -548,6 +579,14 @@ def compile_feeding_jaco():
             pairs.append((free_body[i], free_body[j]))
         for sb in stat:
             pairs.append((free_body[i], sb))
+    # impairment 'tremor' makes the head/neck links dynamic (world_creation.py:157-159 keeps the
+    # masses of controllable joints): they then also collide with the static bodies.  These
+    # pairs come last and are skipped in the other envs (n_pairs_base).
+    S.n_pairs_base = len(pairs)
+    for li in HEAD_CHAIN:
+        if li in human_body:
+            for sb in static_body:
+                pairs.append((human_body[li], sb))
     S.pairs = pairs
     S.robot_body = robot_body
     S.table_body = static_body[2]
@@ -664,6 +703,8 @@ def compile_all(out_dir=DATA_DIR):
         A['human_%s_lower' % gender] = np.array([L['lower'] for L in hl])
         A['human_%s_upper' % gender] = np.array([L['upper'] for L in hl])
     A['human_slot_link'] = np.array(S.human_slots, np.int32)
+    A['n_pairs_base'] = np.int32(S.n_pairs_base)
+    A.update(head_chain(S))
     t = S.task
     A['task_arm_dofs'] = np.array(t['arm_dofs'], np.int32)
     A['task_finger_dofs'] = np.array(t['finger_dofs'], np.int32)

@@ -3,7 +3,8 @@
 It produces the initial per-env state block that the device step consumes:
   * human pose: setup_human_joints + enforce_joint_limits (world_creation.py:135-179,110-133)
     with the Feeding joint targets (feeding.py:242-245) -> per-env world poses of the human's
-    collision links (the human is fully static unless the impairment is 'tremor');
+    collision links (the human is fully static unless the impairment is 'tremor', whose head/neck
+    chain, joints 24..27, is simulated on the device: _tremor_state);
   * bowl position jitter (feeding.py:184), IK of the Jaco tool link to the spoon-above-bowl
     target (feeding.py:276-278; util.py:34-105 -- restated as damped least squares with random
     restarts, because p.calculateInverseKinematics is a Bullet internal);
@@ -21,6 +22,7 @@ from . import _abi as ABI
 from . import geom as G
 
 HUMAN_SCALED = set(range(7, 14)) | set(range(17, 24)) | set(range(24, 28))   # limit_scale joints
+HEAD_CHAIN = (24, 25, 26, 27)          # controllable joints under 'tremor' (feeding.py:219)
 
 
 # ----------------------------------------------------------------------------- Jaco FK / IK
@@ -200,6 +202,8 @@ def feeding_reset_state(A, md, seed, env_id, gender=None, impairment='none'):
     st = np.zeros(ABI.STATE_WORDS)
     qh = human_joint_angles(A, gender, rng, limit_scale)
     st[ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, gender, qh).ravel()
+    if impairment == 'tremor':
+        _tremor_state(st, md, qh, rng)
     bowl_pos = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
     target_pos = bowl_pos + np.array([0, -0.1, 0.4]) + rng.uniform(-0.05, 0.05, size=3)
     target_quat = G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])
@@ -249,7 +253,7 @@ def feeding_reset_state(A, md, seed, env_id, gender=None, impairment='none'):
     st[t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
     st[t + ABI.T_ALIVE] = (1 << 8) - 1
     st[t + ABI.T_GENDER] = gi
-    return st, dict(gender=gender, ik_ok=ok, bowl_pos=bowl_pos, target_pos=target_pos)
+    return st, dict(gender=gender, impairment=impairment, ik_ok=ok, bowl_pos=bowl_pos, target_pos=target_pos)
 
 
 def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='none'):
@@ -361,20 +365,34 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, r
     return Qout, done
 
 
-IMPAIRMENTS = ('none', 'limits', 'weakness')   # world_creation.py:65-72 without 'tremor'
+IMPAIRMENTS = ('none', 'limits', 'weakness', 'tremor')   # world_creation.py:65-72
 
 
 def _impairment(rng, impairment):
-    """Resolve the impairment of one env (world_creation.py:66-69).  'tremor' drives the head/neck
-    with motors (env.py:327-337) and is not built: the human is static for the other three
-    (feeding.py:244 passes no controllable joints, world_creation.py:157-159 zeroes the masses)."""
+    """Resolve the impairment of one env (world_creation.py:66-69; FeedingJaco-v0 itself asks
+    for 'random', feeding.py:175).  The human is static for none / limits / weakness
+    (feeding.py:244 passes no controllable joints, world_creation.py:157-159 zeroes the masses);
+    'tremor' keeps the head/neck chain's masses and drives it with motors (env.py:327-337)."""
+    if impairment == 'random':
+        return IMPAIRMENTS[int(rng.integers(4))]
     if impairment == 'no_tremor':
         return IMPAIRMENTS[int(rng.integers(3))]
     if impairment in IMPAIRMENTS:
         return impairment
-    if impairment in ('tremor', 'random'):
-        raise NotImplementedError("impairment %r: the tremor-driven head/neck is not built (use 'no_tremor')" % impairment)
     raise ValueError('unknown impairment %r' % impairment)
+
+
+def _tremor_state(st, md, qh, rng):
+    """Head-chain state of a 'tremor' env: human_tremors ~ U(+-20 deg) for the 4 controllable
+    joints (world_creation.py:136-139), target_human_joint_positions = the chain's angles after
+    setup (feeding.py:246-248), chain DoFs after the robot's, at rest.  Its motors stay off
+    (VELOCITY_CONTROL, force 0: world_creation.py:162-168) until the first take_step."""
+    nd = md.n_dof
+    for k, j in enumerate(HEAD_CHAIN):
+        st[ABI.S_Q + nd + k] = qh[j]
+        st[ABI.S_HCH + k] = qh[j]
+    st[ABI.S_HCH + ABI.HC_N:ABI.S_HCH + 2 * ABI.HC_N] = rng.uniform(np.deg2rad(-20), np.deg2rad(20), size=ABI.HC_N)
+    st[ABI.S_TASK + ABI.T_HDYN] = 1.0
 
 
 def _rng(seed, env_id, episode=0):
@@ -391,15 +409,18 @@ def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none
     eps = [0] * N if episodes is None else list(episodes)
     rngs = [_rng(seed, e, ep) for e, ep in zip(env_ids, eps)]
     S = np.zeros((N, ABI.STATE_WORDS))
-    gl, tpos, bowl = [], np.zeros((N, 3)), np.zeros((N, 3))
+    gl, il, tpos, bowl = [], [], np.zeros((N, 3)), np.zeros((N, 3))
     for k in range(N):
         rng = rngs[k]
         g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
         gl.append(g)
         imp = _impairment(rng, impairment)
+        il.append(imp)
         ls = rng.uniform(0.5, 1.0) if imp == 'limits' else 1.0
         qh = human_joint_angles(A, g, rng, ls)
         S[k, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, g, qh).ravel()
+        if imp == 'tremor':
+            _tremor_state(S[k], md, qh, rng)
         bowl[k] = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
         tpos[k] = bowl[k] + np.array([0, -0.1, 0.4]) + rng.uniform(-0.05, 0.05, size=3)
     tq = np.repeat(G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])[None], N, 0)
@@ -447,5 +468,5 @@ def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none
         st[t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
         st[t + ABI.T_ALIVE] = (1 << 8) - 1
         st[t + ABI.T_GENDER] = gi
-        meta.append(dict(gender=gl[k], ik_ok=bool(ok[k]), bowl_pos=bowl[k], target_pos=tpos[k]))
+        meta.append(dict(gender=gl[k], impairment=il[k], ik_ok=bool(ok[k]), bowl_pos=bowl[k], target_pos=tpos[k]))
     return S, meta

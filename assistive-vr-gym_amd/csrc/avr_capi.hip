@@ -146,8 +146,9 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     memset(s->err, 0, sizeof(s->err));
     s->cfg = *cfg;
     if (cfg->n_envs <= 0) { int r = fail(s, -1, "n_envs must be > 0"); *out = s; return r; }
-    if (d->n_links > AVR_MAX_LINKS || d->n_dof > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
-        d->n_bodies > MAXB || d->n_arm > AVR_ACT_DIM) {
+    const int hc = d->hc_n > 0 ? d->hc_n : 0;
+    if (d->n_links + hc > AVR_MAX_LINKS || d->n_dof + hc > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
+        d->n_bodies > MAXB || d->n_arm > AVR_ACT_DIM || hc > AVR_HC_N) {
         int r = fail(s, -2, "model exceeds compiled capacities");
         *out = s;
         return r;
@@ -178,18 +179,62 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     memset(&k, 0, sizeof(k));
     int nl = d->n_links, nb = d->n_bodies, ns = d->n_shapes;
     k.nl = nl; k.nd = d->n_dof; k.nf = d->n_free; k.nb = nb; k.ns = ns; k.np = d->n_pairs; k.nh = d->n_human;
+    // articulated link tables: robot links, then the tremor head/neck chain (avr_kmodel.h)
+    const int nla = nl + hc;
+    k.nla = nla; k.hc_n = hc; k.np_base = hc > 0 ? d->n_pairs_base : d->n_pairs;
+    std::vector<int> par(nla), jt(nla), dofv(nla), hasl(nla);
+    std::vector<float> jorig((size_t)2 * nla * 8, 0.f), com((size_t)2 * nla * 8, 0.f), axis((size_t)nla * 4, 0.f),
+        inert((size_t)2 * nla * 4, 0.f), mass((size_t)2 * nla, 0.f), lo(nla), hi(nla);
+    for (int i = 0; i < nl; i++) {
+        par[i] = d->rl_parent[i]; jt[i] = d->rl_jtype[i]; dofv[i] = d->rl_dof[i]; hasl[i] = d->rl_has_limit[i];
+        lo[i] = (float)d->rl_lower[i]; hi[i] = (float)d->rl_upper[i];
+        for (int q = 0; q < 3; q++) axis[4 * i + q] = (float)d->rl_axis[3 * i + q];
+        for (int g = 0; g < 2; g++) {
+            const size_t o = (size_t)g * nla + i;
+            for (int q = 0; q < 3; q++) {
+                jorig[8 * o + q] = (float)d->rl_jpos[3 * i + q];
+                com[8 * o + q] = (float)d->rl_com_pos[3 * i + q];
+                inert[4 * o + q] = (float)d->rl_inertia[3 * i + q];
+            }
+            for (int q = 0; q < 4; q++) {
+                jorig[8 * o + 3 + q] = (float)d->rl_jquat[4 * i + q];
+                com[8 * o + 3 + q] = (float)d->rl_com_quat[4 * i + q];
+            }
+            mass[o] = (float)d->rl_mass[i];
+        }
+    }
+    for (int c = 0; c < hc; c++) {
+        const int i = nl + c;
+        par[i] = c == 0 ? -2 : i - 1; jt[i] = AVR_J_REVOLUTE; dofv[i] = d->n_dof + c; hasl[i] = 1;
+        lo[i] = (float)d->hc_lower[c]; hi[i] = (float)d->hc_upper[c];
+        for (int q = 0; q < 3; q++) axis[4 * i + q] = (float)d->hc_axis[c][q];
+        for (int g = 0; g < 2; g++) {
+            const size_t o = (size_t)g * nla + i;
+            for (int q = 0; q < 3; q++) {
+                jorig[8 * o + q] = (float)d->hc_jpos[g][c][q];
+                inert[4 * o + q] = (float)d->hc_inertia[g][c][q];
+            }
+            jorig[8 * o + 6] = 1.f;   // identity joint frame rotation
+            com[8 * o + 6] = 1.f;     // COM frame == link frame (human_creation.py: inertial offsets 0)
+            mass[o] = (float)d->hc_mass[g][c];
+        }
+        k.hc_slot[c] = d->hc_slot[c]; k.hc_body[c] = d->hc_body[c];
+        k.hc_lower[c] = lo[i]; k.hc_upper[c] = hi[i];
+    }
+    k.hc_parent_slot = d->hc_parent_slot;
+    k.human_gain = (float)d->human_gain; k.human_force = (float)d->human_force;
     int r;
-    if ((r = upload(s, ivec(d->rl_parent, nl), &k.rl_parent))) return r;
-    if ((r = upload(s, ivec(d->rl_jtype, nl), &k.rl_jtype))) return r;
-    if ((r = upload(s, ivec(d->rl_dof, nl), &k.rl_dof))) return r;
-    if ((r = upload(s, ivec(d->rl_has_limit, nl), &k.rl_has_limit))) return r;
-    if ((r = upload(s, poses(d->rl_jpos, d->rl_jquat, nl), &k.rl_jorig))) return r;
-    if ((r = upload(s, poses(d->rl_com_pos, d->rl_com_quat, nl), &k.rl_com))) return r;
-    if ((r = upload(s, cvt(d->rl_axis, 0, 3, 4, nl), &k.rl_axis))) return r;
-    if ((r = upload(s, cvt(d->rl_inertia, 0, 3, 4, nl), &k.rl_inertia))) return r;
-    if ((r = upload(s, cvt(d->rl_mass, nl), &k.rl_mass))) return r;
-    if ((r = upload(s, cvt(d->rl_lower, nl), &k.rl_lower))) return r;
-    if ((r = upload(s, cvt(d->rl_upper, nl), &k.rl_upper))) return r;
+    if ((r = upload(s, par, &k.rl_parent))) return r;
+    if ((r = upload(s, jt, &k.rl_jtype))) return r;
+    if ((r = upload(s, dofv, &k.rl_dof))) return r;
+    if ((r = upload(s, hasl, &k.rl_has_limit))) return r;
+    if ((r = upload(s, jorig, &k.rl_jorig))) return r;
+    if ((r = upload(s, com, &k.rl_com))) return r;
+    if ((r = upload(s, axis, &k.rl_axis))) return r;
+    if ((r = upload(s, inert, &k.rl_inertia))) return r;
+    if ((r = upload(s, mass, &k.rl_mass))) return r;
+    if ((r = upload(s, lo, &k.rl_lower))) return r;
+    if ((r = upload(s, hi, &k.rl_upper))) return r;
     for (int i = 0; i < 7; i++) k.base[i] = (float)d->robot_base[i];
     if ((r = upload(s, cvt(d->fb_mass, d->n_free), &k.fb_mass))) return r;
     if ((r = upload(s, cvt(d->fb_inertia, 0, 3, 4, d->n_free), &k.fb_inertia))) return r;
@@ -263,11 +308,11 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     k.seed = cfg->seed;
     k.env_offset = cfg->env_offset;
     for (int i = 0; i < AVR_MAX_DOF; i++) k.dof_link[i] = 0;
-    for (int l = 0; l < nl; l++)
-        if (d->rl_dof[l] >= 0) k.dof_link[d->rl_dof[l]] = l;
-    for (int l = 0; l < nl; l++) {
+    for (int l = 0; l < nla; l++)
+        if (dofv[l] >= 0) k.dof_link[dofv[l]] = l;
+    for (int l = 0; l < nla; l++) {
         unsigned mask = 0;
-        for (int q = l; q >= 0; q = d->rl_parent[q]) mask |= 1u << q;
+        for (int q = l; q >= 0; q = par[q]) mask |= 1u << q;
         k.anc_mask[l] = mask;
     }
     size_t E = (size_t)cfg->n_envs;

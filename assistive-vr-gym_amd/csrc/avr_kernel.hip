@@ -42,7 +42,8 @@ struct EnvLDS {
     float fv[MAXF][4], fw[MAXF][4];
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
     float h[MAXD], qdd[MAXD];
-    int nsp, nap, n_nc, n_c, flags, gender, pad, pad2;
+    int nsp, nap, n_nc, n_c, flags, gender;
+    int nla, nda;           // articulated links / DoFs of this env (the head chain counts under 'tremor')
 #ifdef AVR_PROF
     unsigned long long prof[16];
 #endif
@@ -75,13 +76,19 @@ struct EnvLDS {
 
 // --------------------------------------------------------------------------- kinematics
 // robot_fk: serial recursion over the (DFS-ordered) links on lane 0, frames published in LDS.
+// Under 'tremor' the head chain follows the robot's links: its root hangs off the static chest
+// slot (parent -2) and its link frames (== COM frames) are published into the human slot poses,
+// where collision and the task glue (getLinkState(human, 27), feeding.py:134,254) read them.
+AVR_DI int lgo(const EnvLDS &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
+
 AVR_DI void robot_fk(const KModel &m, EnvLDS &L) {
     if (lane_id() == 0) {
         tf base = ldtf(m.base);
-        for (int i = 0; i < m.nl; i++) {
+        const int go = lgo(L, m);
+        for (int i = 0; i < L.nla; i++) {
             int p = m.rl_parent[i];
-            tf par = p < 0 ? base : ldtf(L.lk[p]);
-            tf t = tfmul(par, ldtf(m.rl_jorig + 8 * i));
+            tf par = p == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : p < 0 ? base : ldtf(L.lk[p]);
+            tf t = tfmul(par, ldtf(m.rl_jorig + 8 * (go + i)));
             v3 axl = ld3(m.rl_axis + 4 * i);
             v3 axw = qrot(t.q, axl);
             int dof = m.rl_dof[i];
@@ -91,7 +98,14 @@ AVR_DI void robot_fk(const KModel &m, EnvLDS &L) {
             if (jt == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(axl, L.st[AVR_S_Q + dof]));
             else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(axw, L.st[AVR_S_Q + dof]));
             sttf(L.lk[i], t);
-            sttf(L.cm[i], tfmul(t, ldtf(m.rl_com + 8 * i)));
+            sttf(L.cm[i], tfmul(t, ldtf(m.rl_com + 8 * (go + i))));
+        }
+        for (int c = 0; c < L.nla - m.nl; c++) {
+            const int slot = m.hc_slot[c];
+            if (slot < 0) continue;
+            float *h = L.st + AVR_S_HUMAN + 7 * slot;
+            st3(h, ld3(L.cm[m.nl + c]));
+            stq(h + 3, ldq(L.cm[m.nl + c] + 3));
         }
     }
     SYNC();
@@ -115,7 +129,8 @@ AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &
 AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x);
 
 AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
-    const int nd = m.nd;
+    const int nd = L.nda;
+    const int go = lgo(L, m);
     const int lane = lane_id();
     const int ne = MAXD * (MAXD + 1) / 2;
     for (int e = lane; e < ne; e += 64) {
@@ -125,8 +140,8 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         float s = 0.f;
         if (a < nd && b < nd) {
             int la = m.dof_link[a], lb = m.dof_link[b];
-            for (int i = 0; i < m.nl; i++) {
-                float mi = m.rl_mass[i];
+            for (int i = 0; i < L.nla; i++) {
+                float mi = m.rl_mass[go + i];
                 if (mi <= 0.f) continue;
                 if (!is_ancestor(m, i, la) || !is_ancestor(m, i, lb)) continue;
                 v3 c = ld3(L.cm[i]);
@@ -134,7 +149,7 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
                 v3 lina, anga, linb, angb;
                 dof_col(m, L, la, c, lina, anga);
                 dof_col(m, L, lb, c, linb, angb);
-                v3 Ia = inertia_mul(q, ld3(m.rl_inertia + 4 * i), anga);
+                v3 Ia = inertia_mul(q, ld3(m.rl_inertia + 4 * (go + i)), anga);
                 s += mi * dot(lina, linb) + dot(Ia, angb);
             }
         } else if (a == b) s = 1.f;
@@ -210,9 +225,10 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
     if (lane_id() == 0) {
         float (*OM)[4] = L.u.d.rn[0], (*VC)[4] = L.u.d.rn[1], (*AL)[4] = L.u.d.rn[2], (*AC)[4] = L.u.d.rn[3], (*FF)[4] = L.u.d.rn[4], (*NN)[4] = L.u.d.rn[5];
         const float k1l = m.lin_damp, k1a = m.ang_damp;
+        const int go = lgo(L, m);
         tf base = ldtf(m.base);
-        for (int i = 0; i < m.nl; i++) {
-            int p = m.rl_parent[i];
+        for (int i = 0; i < L.nla; i++) {
+            int p = m.rl_parent[i];          // < 0: fixed robot base or (-2) the static chest slot
             v3 omp = p < 0 ? V(0, 0, 0) : ld3(OM[p]);
             v3 vp = p < 0 ? V(0, 0, 0) : ld3(VC[p]);
             v3 alp = p < 0 ? V(0, 0, 0) : ld3(AL[p]);
@@ -245,9 +261,9 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
                 vc = add(vo, crs(om, roc));
                 ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
             }
-            float mi = m.rl_mass[i];
+            float mi = m.rl_mass[go + i];
             qt q = ldq(L.cm[i] + 3);
-            v3 I = ld3(m.rl_inertia + 4 * i);
+            v3 I = ld3(m.rl_inertia + 4 * (go + i));
             v3 Iw = inertia_mul(q, I, om);
             float vn = len(vc), wn = len(om);
             v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
@@ -257,7 +273,7 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
             st3(NN[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
         }
         for (int d = 0; d < MAXD; d++) L.h[d] = 0.f;
-        for (int i = m.nl - 1; i >= 0; i--) {
+        for (int i = L.nla - 1; i >= 0; i--) {
             int dof = m.rl_dof[i];
             v3 o = ld3(L.org[i]), c = ld3(L.cm[i]);
             v3 axw = ld3(L.ax[i]);
@@ -1084,10 +1100,11 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     }
     // broadphase over the candidate pair list, order-preserving compaction
     int nap = 0;
-    for (int base = 0; base < m.np; base += 64) {
+    const int npe = L.nla > m.nl ? m.np : m.np_base;   // chain-vs-static pairs: 'tremor' envs only
+    for (int base = 0; base < npe; base += 64) {
         int p = base + lane;
         bool act = false;
-        if (p < m.np) {
+        if (p < npe) {
             int ba = m.pair_a[p], bb = m.pair_b[p];
             act = overlap(ld3(L.u.c.bmin[ba]), ld3(L.u.c.bmax[ba]), ld3(L.u.c.bmin[bb]), ld3(L.u.c.bmax[bb]));
         }
@@ -1223,7 +1240,7 @@ AVR_DI void robot_jac(const KModel &m, const EnvLDS &L, int link, v3 p, v3 lin, 
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
         float v = 0.f;
-        if (d < m.nd) {
+        if (d < m.nd + m.hc_n) {           // chain DoFs are never ancestors of a robot link
             int k = m.dof_link[d];
             if ((am >> k) & 1u) {
                 v3 cl, ca;
@@ -1295,7 +1312,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     // enumerate (uniform loop); each lane keeps the description of its own row
     int nrow = 0, kind = -1, dof = 0, fix = 0;
     float pen = 0.f;
-    for (int i = 0; i < m.nl; i++) {
+    for (int i = 0; i < L.nla; i++) {
         if (!m.rl_has_limit[i]) continue;
         const int d = m.rl_dof[i];
         const float q = L.st[AVR_S_Q + d];
@@ -1306,7 +1323,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
             nrow++;
         }
     }
-    for (int i = 0; i < m.nl; i++) {
+    for (int i = 0; i < L.nla; i++) {
         const int d = m.rl_dof[i];
         if (d < 0) continue;
         if (lane == nrow) { kind = 2; dof = d; }
@@ -1412,11 +1429,15 @@ AVR_DI void plane_space(v3 n, v3 &p, v3 &q) {
     }
 }
 
-AVR_DI void body_endpoint(const KModel &m, int b, int &kind, int &idx) {
+AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, int &idx) {
     int k = m.body_kind[b];
+    kind = 0; idx = 0;
     if (k == AVR_BODY_ROBOT) { kind = 1; idx = m.body_index[b]; }
     else if (k == AVR_BODY_FREE) { kind = 2; idx = m.body_index[b]; }
-    else { kind = 0; idx = 0; }
+    else if (k == AVR_BODY_HUMAN) {
+        for (int c = 0; c < L.nla - m.nl; c++)     // head-chain link under 'tremor'
+            if (m.hc_body[c] == b) { kind = 1; idx = m.nl + c; }
+    }
 }
 
 // Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal) and
@@ -1430,8 +1451,8 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
         const float *c = gcp + AVR_CP_WORDS * i;
         int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        body_endpoint(m, ba, kA, iA);
-        body_endpoint(m, bb, kB, iB);
+        body_endpoint(m, L, ba, kA, iA);
+        body_endpoint(m, L, bb, kB, iB);
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
         v3 n = ld3(c + AVR_CP_N);
@@ -1671,12 +1692,12 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     robot_bias(m, L);
     if (lane < MAXD) {                      // qdd = -M^-1 h, one lane per DoF
         float s = 0.f;
-        for (int k = 0; k < m.nd; k++) s -= L.Minv[lane][k] * L.h[k];
+        for (int k = 0; k < L.nda; k++) s -= L.Minv[lane][k] * L.h[k];
         L.qdd[lane] = s;
     }
     SYNC();
     const float vmax = m.max_vel;
-    if (lane < m.nd) {
+    if (lane < L.nda) {
         float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
         L.vq[lane] = clampf(v, -vmax, vmax);
     }
@@ -1710,7 +1731,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     PROF_STOP(8, ps);
     // hand-over to part B
     if (lane == 0) { ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); }
-    if (lane < MAXD) ws[WS_VQ + lane] = lane < m.nd ? L.vq[lane] : 0.f;
+    if (lane < MAXD) ws[WS_VQ + lane] = lane < L.nda ? L.vq[lane] : 0.f;
     if (lane < m.nf) {
         st3(ws + WS_FV + 4 * lane, ld3(L.fv[lane]));
         st3(ws + WS_FW + 4 * lane, ld3(L.fw[lane]));
@@ -1821,10 +1842,18 @@ AVR_DI int xcc_id() {   // XCD of the executing CU (HW_REG_XCC_ID, id 20, bits 3
 AVR_DI float *env_ws(const KModel &m, int env) { return m.ws + (size_t)env * WS_WORDS; }
 AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)(2 * m.rowcap * RW); }
 
-AVR_DI void load_state(EnvLDS &L, const float *gst) {
+AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[AVR_S_TASK + AVR_T_HDYN] != 0.f; }
+
+AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
     const int lane = lane_id();
     for (int i = lane; i < AVR_S_CP; i += 64) L.st[i] = gst[i];
-    if (lane == 0) { L.flags = 0; L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER]; }
+    if (lane == 0) {
+        L.flags = 0;
+        L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER];
+        const bool hd = env_hdyn(m, gst);
+        L.nla = hd ? m.nla : m.nl;
+        L.nda = hd ? m.nd + m.hc_n : m.nd;
+    }
 #ifdef AVR_PROF
     if (lane < 16) L.prof[lane] = 0;
 #endif
@@ -1865,6 +1894,18 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
         st[AVR_S_KP + d] = m.robot_gain;
         st[AVR_S_MAXIMP + d] = m.robot_force * m.time_step;
     }
+    if (env_hdyn(m, st)) {
+        // tremor (env.py:327-337): targets target_human_joint_positions + human_tremors with the
+        // tremor's sign alternating with self.iteration, gains human_gains, forces human_forces
+        // (x human_strength = 1: 'tremor' is not 'weakness')
+        const float sg = ((int)st[AVR_S_TASK + AVR_T_ITER] & 1) ? -1.f : 1.f;
+        for (int c = 0; c < m.hc_n; c++) {
+            const int d = m.nd + c;
+            st[AVR_S_QTGT + d] = st[AVR_S_HCH + c] + st[AVR_S_HCH + AVR_HC_N + c] * sg;
+            st[AVR_S_KP + d] = m.human_gain;
+            st[AVR_S_MAXIMP + d] = m.human_force * m.time_step;
+        }
+    }
     ws[WS_ASQ] = asq;
 }
 
@@ -1874,7 +1915,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
-    load_state(L, gst);
+    load_state(m, L, gst);
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env));
 #ifdef AVR_PROF
     if (lane_id() == 0) env_ws(m, env)[WS_XCC] = __int_as_float(xcc_id());
@@ -1893,7 +1934,8 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 // quaternion exp-map update of btTransformUtil::integrateTransform for the free bodies.
 // No LDS: velocities and impulses stay in registers.
 __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                           const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
+                                                           const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
+                                                           int n_envs) {
     AVR_ENV_GUARD();
     const int lane = lane_id();
 #ifdef AVR_PROF
@@ -1909,10 +1951,18 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
     const float vmax = m.max_vel;
-    if (lane < m.nd) {
+    const int nda = env_hdyn(m, st) ? m.nd + m.hc_n : m.nd;
+    if (lane < nda) {
         float v = clampf(ws[WS_VQ + lane] + d.rq, -vmax, vmax);
+        float q = st[AVR_S_Q + lane] + dt * v;
+        if (frame_end && lane >= m.nd) {
+            // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
+            const float lo = m.hc_lower[lane - m.nd], hi = m.hc_upper[lane - m.nd];
+            if (q < lo) { q = lo; v = 0.f; }
+            else if (q > hi) { q = hi; v = 0.f; }
+        }
         st[AVR_S_QD + lane] = v;
-        st[AVR_S_Q + lane] += dt * v;
+        st[AVR_S_Q + lane] = q;
     }
     if (lane < m.nf) {
         float *fb = st + AVR_S_FREE + AVR_FB_WORDS * lane;
@@ -1954,8 +2004,9 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     const int lane = lane_id();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     const float *gcp = gst + AVR_S_CP;
-    load_state(L, gst);
+    load_state(m, L, gst);
     PROF_START(ptask);
+    if (L.nla > m.nl) robot_fk(m, L);    // head pose after the last sub-step (update_targets)
     mouth_target(m, L);
     if (mode == MODE_SETTLE) {
         if (obs) observe(m, L, 0.f, obs + (size_t)env * AVR_OBS_DIM);
@@ -2071,27 +2122,29 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     auto mark = [&](int kind) {
         if (log && log->n < log->cap && hipEventRecord(log->ev[log->n], stream) == hipSuccess) log->kind[log->n++] = kind;
     };
-    auto sub = [&](float h) {
+    // frame_end: the sub-step closes a gym frame (stepSimulation) and B applies
+    // enforce_hard_human_joint_limits (env.py:342-343); the reset's settle frames do not
+    auto sub = [&](float h, int frame_end) {
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
-        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
+        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
     };
     if (mode == MODE_SUBSTEP) {
         float h;
         std::memcpy(&h, &t, sizeof(float));
-        sub(h);
+        sub(h, 0);
         mark(-1);
         return hipGetLastError();
     }
     if (mode == MODE_SETTLE) {
         for (long long f = 0; f < t; f++)
-            for (int k = 0; k < nsub; k++) sub(dt);
+            for (int k = 0; k < nsub; k++) sub(dt, 0);
     } else {
         mark(AVR_K_TAKE);
         hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, env0, env1);
         for (int f = 0; f < h_m->frame_skip; f++)
-            for (int k = 0; k < nsub; k++) sub(dt);
+            for (int k = 0; k < nsub; k++) sub(dt, k == nsub - 1);
     }
     mark(AVR_K_TASK);
     hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, env0, env1);

@@ -27,14 +27,20 @@
 #define BIGF 1e30f
 
 
+// Articulated links: the robot's nl links, then (impairment 'tremor') the head/neck chain's
+// hc_n links with DoFs nd .. nd + hc_n - 1; nla = nl + hc_n.  The chain root's parent is -2:
+// the static human slot hc_parent_slot.  Per-link tables are [nla]; the tables that differ by
+// gender (joint origins, COM frames, masses, inertias) are [2][nla] (male, female).
 struct KModel {
     int nl, nd, nf, nb, ns, np, nh;
-    const int *rl_parent, *rl_jtype, *rl_dof, *rl_has_limit;
-    const float *rl_jorig;    // [nl][8] p3 q4 pad
-    const float *rl_com;      // [nl][8]
-    const float *rl_axis;     // [nl][4]
-    const float *rl_inertia;  // [nl][4]
-    const float *rl_mass, *rl_lower, *rl_upper;
+    int nla, hc_n, np_base;   // np_base: pairs active in every env (the rest: tremor envs only)
+    const int *rl_parent, *rl_jtype, *rl_dof, *rl_has_limit;   // [nla]
+    const float *rl_jorig;    // [2][nla][8] p3 q4 pad
+    const float *rl_com;      // [2][nla][8]
+    const float *rl_axis;     // [nla][4]
+    const float *rl_inertia;  // [2][nla][4]
+    const float *rl_mass;     // [2][nla]
+    const float *rl_lower, *rl_upper;   // [nla]
     float base[8];
     const float *fb_mass, *fb_inertia, *fb_gravity;   // [nf], [nf][4], [nf][4]
     const float *st_pose;                             // [nst][8]
@@ -59,6 +65,8 @@ struct KModel {
     int env_offset;
     int dof_link[MAXD];        // link owning each DoF
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+    int hc_parent_slot, hc_slot[AVR_HC_N], hc_body[AVR_HC_N];
+    float hc_lower[AVR_HC_N], hc_upper[AVR_HC_N], human_gain, human_force;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
     int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]

@@ -38,13 +38,13 @@ def layout_bytes_per_env_step(ABI):
     return 2 * ABI.STATE_WORDS * 4 + (ABI.OBS_DIM + 1 + ABI.INFO_DIM) * 4 + 1
 
 
-def cpu_baseline(md, A, RS, seconds, threads):
+def cpu_baseline(md, A, RS, seconds, threads, impairment):
     """Oracle (the CPU restatement, fp64) on the host cores; bounded sample."""
     import numpy as np
     from oracle.oracle import Oracle
     from avr import _lib
     n = max(threads * 2, 8)
-    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)))
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)), impairment=impairment)
     o = Oracle(md, n)
     o.set_threads(threads)
     o.set_state(S)
@@ -74,6 +74,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--reset-pool', type=int, default=1024,
                     help='distinct host reset states, tiled over the envs (IK is host-side)')
+    ap.add_argument('--impairment', default='random',
+                    help="human impairment per env: 'random' is FeedingJaco-v0's own setting (feeding.py:175)")
     args = ap.parse_args()
 
     import numpy as np
@@ -97,7 +99,8 @@ def main():
     # reset pool: distinct initial states for global env ids; tiled if pool < E
     pool = min(args.reset_pool, E)
     base_id, _ = D.shard(E, rank)
-    S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)])
+    S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)], impairment=args.impairment)
+    n_tremor = sum(m['impairment'] == 'tremor' for m in meta)
     S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
     sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
     sim.set_state(S.astype(np.float32))
@@ -183,6 +186,7 @@ def main():
         'dtype': 'f32',
         'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the host IK path (%d distinct per GPU, tiled)' % pool,
         'config': {'workload': 'FeedingJaco-v0, %d envs/GPU, rigid-only, random actions' % E, 'envs_per_gpu': E,
+                   'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
                    'global_envs': world * E, 'substeps_per_env_step': 10, 'solver_iterations': 10,
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -197,7 +201,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
         threads = max(1, min(threads, 16))
-        out['cpu_baseline'] = cpu_baseline(md, A, RS, args.cpu_seconds, threads)
+        out['cpu_baseline'] = cpu_baseline(md, A, RS, args.cpu_seconds, threads, args.impairment)
     elif rank == 0:
         out['cpu_baseline'] = None
     if rank == 0:

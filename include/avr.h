@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 1
+#define AVR_ABI_VERSION 2
 
 typedef struct avr_config {
     int32_t n_envs;        /* envs owned by this handle (one GPU)                          */

@@ -18,8 +18,9 @@ extern "C" {
 #endif
 
 /* ---- capacities (compile-time; checked against the model at create time) ---- */
-#define AVR_MAX_LINKS 16        /* robot links (Jaco: 15)                           */
-#define AVR_MAX_DOF 12          /* robot DoF (Jaco: 10)                             */
+#define AVR_MAX_LINKS 20        /* articulated links: robot (Jaco: 15) + head chain  */
+#define AVR_MAX_DOF 14          /* robot DoF (Jaco: 10) + head chain DoF (4)        */
+#define AVR_HC_N 4              /* tremor head/neck chain: human joints 24..27      */
 #define AVR_MAX_FREE 10         /* free bodies (spoon, bowl, 8 food)                */
 #define AVR_MAX_HUMAN 20        /* per-env static human slots (19)                  */
 #define AVR_MAX_CONTACTS 96     /* persistent contact points per env                */
@@ -53,9 +54,11 @@ enum { AVR_J_FIXED = 0, AVR_J_REVOLUTE = 1, AVR_J_PRISMATIC = 2 };
 #define AVR_T_GENDER   7      /* 0 male, 1 female                                    */
 #define AVR_T_FLAGS    8      /* bit0: NaN guard tripped                             */
 #define AVR_T_NCP      9      /* number of live contact points                       */
+#define AVR_T_HDYN     10     /* 1: impairment 'tremor', the head/neck chain is articulated */
 #define AVR_T_WORDS    16
 #define AVR_S_HUMAN    (AVR_S_TASK + AVR_T_WORDS)          /* [AVR_MAX_HUMAN*7] slot poses */
-#define AVR_S_CP       (AVR_S_HUMAN + AVR_MAX_HUMAN * 7)    /* [AVR_MAX_CONTACTS*16]  */
+#define AVR_S_HCH      (AVR_S_HUMAN + AVR_MAX_HUMAN * 7)    /* head chain: [AVR_HC_N] target_human_joint_positions, [AVR_HC_N] human_tremors */
+#define AVR_S_CP       (AVR_S_HCH + 2 * AVR_HC_N)           /* [AVR_MAX_CONTACTS*16]  */
 #define AVR_STATE_WORDS (AVR_S_CP + AVR_MAX_CONTACTS * AVR_CP_WORDS)
 
 /* contact point words (one Bullet btManifoldPoint, in body COM frames) */
@@ -126,6 +129,21 @@ typedef struct avr_model_desc {
     /* reward weights (config.ini) */
     double w_distance, w_action, w_food, w_velocity, w_force_nontarget, w_high_forces,
            w_food_hit, w_food_velocities, task_success_threshold;
+    /* impairment 'tremor': the head/neck chain (human joints 24..27, human_creation.py:195-207)
+     * keeps its masses and is driven by position motors (world_creation.py:135-159,
+     * env.py:307-345).  Its DoFs follow the robot's (n_dof .. n_dof + hc_n - 1) and its links
+     * follow the robot's links; the chain hangs off the static human slot hc_parent_slot.
+     * hc_n = 0: no chain.  Per-gender arrays are [male, female]. */
+    int32_t hc_n, hc_parent_slot;
+    int32_t hc_slot[AVR_HC_N];             /* human slot of each chain link (-1: no shape)  */
+    int32_t hc_body[AVR_HC_N];             /* collision body of each chain link (-1: none)  */
+    double hc_jpos[2][AVR_HC_N][3];        /* joint origin in the parent link frame         */
+    double hc_axis[AVR_HC_N][3];
+    double hc_mass[2][AVR_HC_N], hc_inertia[2][AVR_HC_N][3];
+    double hc_lower[AVR_HC_N], hc_upper[AVR_HC_N];
+    double human_gain, human_force;        /* feeding.py:48 human_gains, feeding.py:17 human_forces */
+    int32_t n_pairs_base;                  /* pairs [n_pairs_base, n_pairs): chain bodies vs static
+                                              bodies, active in 'tremor' envs only              */
 } avr_model_desc;
 
 #ifdef __cplusplus

@@ -117,9 +117,19 @@ static inline v3 tfinvpt(tf a, v3 p) { return qrot(qconj(a.q), sub(p, a.p)); }
 static inline tf ldtf(const double *p) { tf r; r.p = ld3d(p); r.q = ldqd(p + 3); return r; }
 
 /* ---------------------------------------------------------------- model (converted) */
+/* A model view: the articulated system an env simulates.  View 0 is the robot alone (the
+ * human is static: impairments none / limits / weakness, feeding.py:244 passes no controllable
+ * joints); views 1 and 2 (male, female) append the tremor head/neck chain -- human joints
+ * 24..27 as links nl_robot.. with DoFs nd_robot.. hanging off the static chest slot
+ * (parent -2), plus the chain-vs-static body pairs (np = n_pairs). */
+#define MAX_BODIES 64
 typedef struct {
     avr_model_desc d;                 /* arrays point into the copies below */
     int nl, nd, nf, nb, ns, np;
+    int nl_robot, nd_robot, hc;       /* hc: this view articulates the head chain */
+    int parent[AVR_MAX_LINKS], jtype[AVR_MAX_LINKS], dof[AVR_MAX_LINKS], has_limit[AVR_MAX_LINKS];
+    real lower[AVR_MAX_LINKS], upper[AVR_MAX_LINKS];
+    int body_link[MAX_BODIES];        /* articulated link of a collision body, -1 if none */
     tf jorig[AVR_MAX_LINKS], com[AVR_MAX_LINKS];
     v3 axis[AVR_MAX_LINKS], inertia[AVR_MAX_LINKS];
     real mass[AVR_MAX_LINKS];
@@ -130,7 +140,6 @@ typedef struct {
 
 /* ---------------------------------------------------------------- per-env workspace */
 #define MAX_ROWS 512
-#define MAX_BODIES 64
 #define MAX_SHAPES 512
 #define MAX_SPAIRS 256
 
@@ -165,7 +174,8 @@ typedef struct {
 } ws_t;
 
 typedef struct avr_oracle {
-    model m;
+    model m;             /* view 0 (static human) */
+    model mv[2];         /* tremor views: male, female */
     int n_envs;
     real *state;         /* n_envs * AVR_STATE_WORDS */
     ws_t *ws;
@@ -173,31 +183,54 @@ typedef struct avr_oracle {
     int threads;
 } avr_oracle;
 
+/* the view an env simulates: T_HDYN (impairment 'tremor') selects the head-chain view */
+static const model *oview(const avr_oracle *o, const real *st) {
+    if (o->m.d.hc_n > 0 && st[AVR_S_TASK + AVR_T_HDYN] != 0) return &o->mv[(int)st[AVR_S_TASK + AVR_T_GENDER] ? 1 : 0];
+    return &o->m;
+}
+
 /* ---------------------------------------------------------------- kinematics */
-static void robot_fk(const model *m, const real *st, ws_t *w) {
+static tf slot_pose(const real *st, int slot) {
+    const real *h = st + AVR_S_HUMAN + 7 * slot;
+    tf t; t.p = ld3(h); t.q = ldq(h + 3);
+    return t;
+}
+
+/* Link frames of the view's articulated links.  The head chain's root hangs off the chest slot
+ * (parent -2); its link frames are its COM frames and are published into the human slot poses
+ * so that collision and the task glue (getLinkState(human, 27), feeding.py:134,254) see them. */
+static void robot_fk(const model *m, real *st, ws_t *w) {
     for (int i = 0; i < m->nl; i++) {
-        int p = m->d.rl_parent[i];
-        tf par = p < 0 ? m->base : w->lk[p];
+        int p = m->parent[i];
+        tf par = p == -2 ? slot_pose(st, m->d.hc_parent_slot) : p < 0 ? m->base : w->lk[p];
         tf t = tfmul(par, m->jorig[i]);
         w->org[i] = t.p;
         w->ax[i] = qrot(t.q, m->axis[i]);
-        int dof = m->d.rl_dof[i];
-        if (m->d.rl_jtype[i] == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(m->axis[i], st[AVR_S_Q + dof]));
-        else if (m->d.rl_jtype[i] == AVR_J_PRISMATIC) t.p = add(t.p, scl(w->ax[i], st[AVR_S_Q + dof]));
+        int dof = m->dof[i];
+        if (m->jtype[i] == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(m->axis[i], st[AVR_S_Q + dof]));
+        else if (m->jtype[i] == AVR_J_PRISMATIC) t.p = add(t.p, scl(w->ax[i], st[AVR_S_Q + dof]));
         w->lk[i] = t;
         w->cm[i] = tfmul(t, m->com[i]);
     }
+    if (m->hc)
+        for (int k = 0; k < m->d.hc_n; k++) {
+            int slot = m->d.hc_slot[k];
+            if (slot < 0) continue;
+            real *h = st + AVR_S_HUMAN + 7 * slot;
+            st3(h, w->cm[m->nl_robot + k].p);
+            stq(h + 3, w->cm[m->nl_robot + k].q);
+        }
 }
 
 static int is_ancestor_dof(const model *m, int link, int dof_link) {
-    for (int k = link; k >= 0; k = m->d.rl_parent[k])
+    for (int k = link; k >= 0; k = m->parent[k])
         if (k == dof_link) return 1;
     return 0;
 }
 
 /* Jacobian column of DoF owned by link j for a point p (world) on a body downstream. */
 static void dof_col(const model *m, const ws_t *w, int j, v3 p, v3 *lin, v3 *ang) {
-    if (m->d.rl_jtype[j] == AVR_J_REVOLUTE) {
+    if (m->jtype[j] == AVR_J_REVOLUTE) {
         *ang = w->ax[j];
         *lin = crs(w->ax[j], sub(p, w->org[j]));
     } else {
@@ -214,7 +247,7 @@ static int robot_mass_matrix(const model *m, ws_t *w) {
     memset(M, 0, sizeof(M));
     int dl[AVR_MAX_DOF];
     for (int j = 0; j < m->nl; j++)
-        if (m->d.rl_dof[j] >= 0) dl[m->d.rl_dof[j]] = j;
+        if (m->dof[j] >= 0) dl[m->dof[j]] = j;
     for (int i = 0; i < m->nl; i++) {
         real mi = m->mass[i];
         if (mi <= 0) continue;
@@ -274,25 +307,25 @@ static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
     v3 F[AVR_MAX_LINKS], N[AVR_MAX_LINKS];
     real k1l = R(m->d.linear_damping), k1a = R(m->d.angular_damping);
     for (int i = 0; i < nl; i++) {
-        int p = m->d.rl_parent[i];
+        int p = m->parent[i];
         v3 omp = p < 0 ? V(0, 0, 0) : om[p];
         v3 vp = p < 0 ? V(0, 0, 0) : vc[p];
         v3 alp = p < 0 ? V(0, 0, 0) : al[p];
         v3 acp = p < 0 ? V(0, 0, 0) : ac[p];
         v3 cp = p < 0 ? m->base.p : w->cm[p].p;
-        int dof = m->d.rl_dof[i];
+        int dof = m->dof[i];
         real qd = dof >= 0 ? st[AVR_S_QD + dof] : 0;
         v3 o = w->org[i], c = w->cm[i].p;
         v3 rpo = sub(o, cp), roc = sub(c, o);
         v3 vo = add(vp, crs(omp, rpo));                               /* joint point velocity */
         v3 ao = add(acp, add(crs(alp, rpo), crs(omp, crs(omp, rpo))));
-        if (m->d.rl_jtype[i] == AVR_J_REVOLUTE) {
+        if (m->jtype[i] == AVR_J_REVOLUTE) {
             v3 wj = scl(w->ax[i], qd);
             om[i] = add(omp, wj);
             al[i] = add(alp, crs(omp, wj));
             vc[i] = add(vo, crs(om[i], roc));
             ac[i] = add(ao, add(crs(al[i], roc), crs(om[i], crs(om[i], roc))));
-        } else if (m->d.rl_jtype[i] == AVR_J_PRISMATIC) {
+        } else if (m->jtype[i] == AVR_J_PRISMATIC) {
             v3 vj = scl(w->ax[i], qd);
             om[i] = omp;
             al[i] = alp;
@@ -315,13 +348,13 @@ static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
     }
     for (int d = 0; d < m->nd; d++) h[d] = 0;
     for (int i = nl - 1; i >= 0; i--) {
-        int dof = m->d.rl_dof[i];
+        int dof = m->dof[i];
         v3 o = w->org[i], c = w->cm[i].p;
         if (dof >= 0) {
-            if (m->d.rl_jtype[i] == AVR_J_REVOLUTE) h[dof] = dot(w->ax[i], add(N[i], crs(sub(c, o), F[i])));
+            if (m->jtype[i] == AVR_J_REVOLUTE) h[dof] = dot(w->ax[i], add(N[i], crs(sub(c, o), F[i])));
             else h[dof] = dot(w->ax[i], F[i]);
         }
-        int p = m->d.rl_parent[i];
+        int p = m->parent[i];
         if (p >= 0) {
             F[p] = add(F[p], F[i]);
             N[p] = add(N[p], add(N[i], crs(sub(c, w->cm[p].p), F[i])));
@@ -827,8 +860,8 @@ static void manifold_refresh(manifold_t *M, tf ta, tf tb, real thr) {
 static void add_endpoint_jac(const model *m, const ws_t *w, int link, v3 p, v3 lin, v3 ang, real *J) {
     /* J[d] = d(lin . v(p) + ang . omega)/dqd for dofs in the chain of `link` */
     for (int d = 0; d < m->nd; d++) J[d] = 0;
-    for (int k = link; k >= 0; k = m->d.rl_parent[k]) {
-        int dof = m->d.rl_dof[k];
+    for (int k = link; k >= 0; k = m->parent[k]) {
+        int dof = m->dof[k];
         if (dof < 0) continue;
         v3 cl, ca;
         dof_col(m, w, k, p, &cl, &ca);
@@ -842,7 +875,8 @@ static void row_endpoint(const model *m, const real *st, ws_t *w, row_t *r, int 
     int kind = m->d.body_kind[b], idx = m->d.body_index[b];
     int *pk = side ? &r->kindB : &r->kindA, *pi = side ? &r->idxB : &r->idxA;
     real *J = side ? r->JB : r->JA, *MJ = side ? r->MB : r->MA;
-    if (kind == AVR_BODY_ROBOT) {
+    if (m->body_link[b] >= 0) {      /* robot link, or head-chain link in a tremor view */
+        idx = m->body_link[b];
         *pk = 1; *pi = idx;
         add_endpoint_jac(m, w, idx, p, lin, ang, J);
         chol_solve(m, w, J, MJ);
@@ -913,11 +947,11 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
     real erp = R(m->d.erp);
     /* joint limits (created at URDF load, link order); a row exists only when violated */
     for (int i = 0; i < m->nl; i++) {
-        if (!m->d.rl_has_limit[i]) continue;
-        int dof = m->d.rl_dof[i];
+        if (!m->has_limit[i]) continue;
+        int dof = m->dof[i];
         real q = st[AVR_S_Q + dof];
         for (int side = 0; side < 2; side++) {
-            real pen = side == 0 ? q - R(m->d.rl_lower[i]) : R(m->d.rl_upper[i]) - q;
+            real pen = side == 0 ? q - m->lower[i] : m->upper[i] - q;
             if (pen > 0) continue;
             row_t *r = new_row(w);
             r->kindA = 1; r->idxA = i;
@@ -934,7 +968,7 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
     }
     /* joint motors (createJointMotors order = link order) */
     for (int i = 0; i < m->nl; i++) {
-        int dof = m->d.rl_dof[i];
+        int dof = m->dof[i];
         if (dof < 0) continue;
         row_t *r = new_row(w);
         r->kindA = 1; r->idxA = i;
@@ -1114,7 +1148,7 @@ static void solve(const model *m, ws_t *w) {
 
 /* ---------------------------------------------------------------- collision detection */
 static void collide(avr_oracle *o, real *st, ws_t *w) {
-    const model *m = &o->m;
+    const model *m = oview(o, st);
     int gender = w->gender;
     for (int b = 0; b < m->nb; b++) {
         w->body[b] = body_tf(m, st, w, b);
@@ -1182,7 +1216,7 @@ static void collide(avr_oracle *o, real *st, ws_t *w) {
 
 /* ---------------------------------------------------------------- one Bullet sub-step */
 static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
-    const model *m = &o->m;
+    const model *m = oview(o, st);
     robot_fk(m, st, w);
     collide(o, st, w);
     /* unconstrained velocities (btMultiBody::computeAccelerationsArticulatedBodyAlgorithmMultiDof) */
@@ -1300,9 +1334,20 @@ static void observe(const model *m, real *st, ws_t *w, float spoon_force, float 
     obs[k++] = spoon_force;
 }
 
+/* enforce_hard_human_joint_limits (env.py:389-410): after every stepSimulation a head-chain
+ * joint outside its limits is reset onto the limit with zero velocity (resetJointState). */
+static void hard_limits(const model *m, real *st) {
+    for (int k = 0; k < m->d.hc_n; k++) {
+        int d = m->nd_robot + k;
+        real lo = R(m->d.hc_lower[k]), hi = R(m->d.hc_upper[k]);
+        if (st[AVR_S_Q + d] < lo) { st[AVR_S_Q + d] = lo; st[AVR_S_QD + d] = 0; }
+        else if (st[AVR_S_Q + d] > hi) { st[AVR_S_Q + d] = hi; st[AVR_S_QD + d] = 0; }
+    }
+}
+
 static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
-    const model *m = &o->m;
     real *st = o->state + (size_t)e * AVR_STATE_WORDS;
+    const model *m = oview(o, st);
     ws_t *w = &o->ws[e];
     w->gender = (int)st[AVR_S_TASK + AVR_T_GENDER];
     real dt = R(m->d.time_step) / (m->d.num_sub_steps > 0 ? m->d.num_sub_steps : 1);
@@ -1327,11 +1372,27 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
         st[AVR_S_KP + d] = R(m->d.robot_gain);
         st[AVR_S_MAXIMP + d] = R(m->d.robot_force * m->d.time_step);
     }
+    if (m->hc) {
+        /* tremor (env.py:327-337): position targets target_human_joint_positions + human_tremors,
+           the tremor's sign alternating with self.iteration; gains human_gains, forces
+           human_forces * human_strength (strength 1: 'tremor' is not 'weakness') */
+        real sg = ((int)st[AVR_S_TASK + AVR_T_ITER] % 2 == 0) ? 1 : -1;
+        for (int k = 0; k < m->d.hc_n; k++) {
+            int d = m->nd_robot + k;
+            st[AVR_S_QTGT + d] = st[AVR_S_HCH + k] + st[AVR_S_HCH + AVR_HC_N + k] * sg;
+            st[AVR_S_KP + d] = R(m->d.human_gain);
+            st[AVR_S_MAXIMP + d] = R(m->d.human_force * m->d.time_step);
+        }
+    }
     for (int fr = 0; fr < m->d.frame_skip; fr++) {
         for (int s = 0; s < nsub; s++)
             if (substep(o, st, w, dt)) return -1;
-        /* enforce_hard_human_joint_limits: the human is static here (no-op);
-           update_targets (feeding.py:345-349) */
+        /* enforce_hard_human_joint_limits (a no-op while the human is static), then
+           update_targets (feeding.py:345-349) on the current head pose */
+        if (m->hc) {
+            hard_limits(m, st);
+            robot_fk(m, st, w);
+        }
         mouth_target(m, st, st + AVR_S_TASK + AVR_T_TARGET);
     }
     st[AVR_S_TASK + AVR_T_ITER] += 1;
@@ -1402,8 +1463,8 @@ static void *dupa(const void *p, size_t n) {
 
 EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **out) {
     if (!d || !out || n_envs <= 0) return -1;
-    if (d->n_links > AVR_MAX_LINKS || d->n_dof > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
-        d->n_bodies > MAX_BODIES || d->n_shapes > MAX_SHAPES)
+    if (d->n_links + d->hc_n > AVR_MAX_LINKS || d->n_dof + d->hc_n > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE ||
+        d->n_human > AVR_MAX_HUMAN || d->n_bodies > MAX_BODIES || d->n_shapes > MAX_SHAPES || d->hc_n > AVR_HC_N)
         return -2;
     avr_oracle *o = (avr_oracle *)calloc(1, sizeof(avr_oracle));
     model *m = &o->m;
@@ -1424,18 +1485,44 @@ EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **o
     CP(hull_verts, 3 * d->n_hull_verts, double); CP(hull_planes, 4 * d->n_hull_planes, double);
     CP(pair_a, d->n_pairs, int32_t); CP(pair_b, d->n_pairs, int32_t);
 #undef CP
-    m->nl = L; m->nd = d->n_dof; m->nf = d->n_free; m->nb = B; m->ns = S; m->np = d->n_pairs;
+    m->nl = L; m->nd = d->n_dof; m->nf = d->n_free; m->nb = B; m->ns = S;
+    m->np = d->hc_n > 0 ? d->n_pairs_base : d->n_pairs;
+    m->nl_robot = L; m->nd_robot = d->n_dof; m->hc = 0;
     for (int i = 0; i < L; i++) {
+        m->parent[i] = d->rl_parent[i]; m->jtype[i] = d->rl_jtype[i]; m->dof[i] = d->rl_dof[i];
+        m->has_limit[i] = d->rl_has_limit[i]; m->lower[i] = R(d->rl_lower[i]); m->upper[i] = R(d->rl_upper[i]);
         m->jorig[i].p = ld3d(d->rl_jpos + 3 * i); m->jorig[i].q = ldqd(d->rl_jquat + 4 * i);
         m->com[i].p = ld3d(d->rl_com_pos + 3 * i); m->com[i].q = ldqd(d->rl_com_quat + 4 * i);
         m->axis[i] = ld3d(d->rl_axis + 3 * i);
         m->inertia[i] = ld3d(d->rl_inertia + 3 * i);
         m->mass[i] = R(d->rl_mass[i]);
     }
+    for (int b = 0; b < B; b++) m->body_link[b] = d->body_kind[b] == AVR_BODY_ROBOT ? d->body_index[b] : -1;
     m->base = ldtf(d->robot_base);
     m->hv = (real *)malloc(sizeof(real) * 3 * (size_t)(d->n_hull_verts + 1));
     for (int i = 0; i < 3 * d->n_hull_verts; i++) m->hv[i] = R(d->hull_verts[i]);
     m->hp = 0;
+    /* tremor views: the head chain appended to the robot (links nl.., DoFs nd..) */
+    for (int g = 0; g < 2; g++) {
+        model *v = &o->mv[g];
+        *v = *m;
+        if (d->hc_n <= 0) continue;
+        v->hc = 1;
+        v->np = d->n_pairs;
+        for (int k = 0; k < d->hc_n; k++) {
+            int i = L + k;
+            v->parent[i] = k == 0 ? -2 : i - 1;
+            v->jtype[i] = AVR_J_REVOLUTE; v->dof[i] = d->n_dof + k; v->has_limit[i] = 1;
+            v->lower[i] = R(d->hc_lower[k]); v->upper[i] = R(d->hc_upper[k]);
+            v->jorig[i].p = ld3d(d->hc_jpos[g][k]); v->jorig[i].q = Q(0, 0, 0, 1);
+            v->com[i].p = V(0, 0, 0); v->com[i].q = Q(0, 0, 0, 1);
+            v->axis[i] = ld3d(d->hc_axis[k]);
+            v->inertia[i] = ld3d(d->hc_inertia[g][k]);
+            v->mass[i] = R(d->hc_mass[g][k]);
+            if (d->hc_body[k] >= 0) v->body_link[d->hc_body[k]] = i;
+        }
+        v->nl = L + d->hc_n; v->nd = d->n_dof + d->hc_n;
+    }
     o->n_envs = n_envs;
     o->threads = 1;
     o->state = (real *)calloc((size_t)n_envs * AVR_STATE_WORDS, sizeof(real));
@@ -1479,16 +1566,19 @@ EXPORT int avr_oracle_get_state(avr_oracle *o, double *state) {
 /* reset-path settle: n_frames x stepSimulation with the current motor settings, no task glue
  * (feeding.py:319-320), then the reset observation (feeding.py:325). */
 EXPORT int avr_oracle_settle(avr_oracle *o, int n_frames, float *obs) {
-    const model *m = &o->m;
-    real dt = R(m->d.time_step) / (m->d.num_sub_steps > 0 ? m->d.num_sub_steps : 1);
-    int nsub = m->d.num_sub_steps > 0 ? m->d.num_sub_steps : 1;
+    const model *m0 = &o->m;
+    real dt = R(m0->d.time_step) / (m0->d.num_sub_steps > 0 ? m0->d.num_sub_steps : 1);
+    int nsub = m0->d.num_sub_steps > 0 ? m0->d.num_sub_steps : 1;
     for (int e = 0; e < o->n_envs; e++) {
         real *st = o->state + (size_t)e * AVR_STATE_WORDS;
+        const model *m = oview(o, st);
         ws_t *w = &o->ws[e];
         w->gender = (int)st[AVR_S_TASK + AVR_T_GENDER];
         for (int f = 0; f < n_frames; f++)
             for (int s = 0; s < nsub; s++)
                 if (substep(o, st, w, dt)) return -1;
+        /* reset drops the food with plain stepSimulation calls: no hard human limits here */
+        robot_fk(m, st, w);
         mouth_target(m, st, st + AVR_S_TASK + AVR_T_TARGET);
         if (obs) observe(m, st, w, 0.0f, obs + (size_t)e * AVR_OBS_DIM);
     }
@@ -1540,8 +1630,9 @@ EXPORT int avr_oracle_narrowphase(avr_oracle *o, int sa, const double *pa, int s
 /* forward kinematics for tests: COM frames of robot links -> out[n_links*7] */
 EXPORT int avr_oracle_robot_fk(avr_oracle *o, int env, double *out) {
     ws_t *w = &o->ws[env];
-    robot_fk(&o->m, o->state + (size_t)env * AVR_STATE_WORDS, w);
-    for (int i = 0; i < o->m.nl; i++) {
+    real *st = o->state + (size_t)env * AVR_STATE_WORDS;
+    robot_fk(oview(o, st), st, w);
+    for (int i = 0; i < o->m.nl_robot; i++) {
         out[7 * i + 0] = w->cm[i].p.x; out[7 * i + 1] = w->cm[i].p.y; out[7 * i + 2] = w->cm[i].p.z;
         out[7 * i + 3] = w->cm[i].q.x; out[7 * i + 4] = w->cm[i].q.y; out[7 * i + 5] = w->cm[i].q.z; out[7 * i + 6] = w->cm[i].q.w;
     }

@@ -39,7 +39,10 @@ def test_golden_inputs_are_the_reset_path_and_philox(scene, golden):
     from avr import reset as RS, _lib
     A, md = scene
     g = golden
-    S0, _ = RS.batch_reset_states_fast(A, md, int(g['seed']), list(g['env_ids']))
+    ids, trem = list(g['env_ids']), g['tremor']
+    S_a, _ = RS.batch_reset_states_fast(A, md, int(g['seed']), [e for e, t in zip(ids, trem) if not t])
+    S_b, _ = RS.batch_reset_states_fast(A, md, int(g['seed']), [e for e, t in zip(ids, trem) if t], impairment='tremor')
+    S0 = np.concatenate([S_a, S_b])
     assert np.allclose(S0.astype(np.float32).astype(np.float64), g['S0'], atol=1e-6)
     for t in range(g['actions'].shape[0]):
         assert np.array_equal(_lib.random_actions(int(g['seed']), g['env_ids'], t), g['actions'][t])

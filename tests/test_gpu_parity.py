@@ -38,10 +38,16 @@ def oracle(md, n):
     return o
 
 
-def reset_states(A, md, ids):
+def reset_states(A, md, ids, impairment='none'):
     from avr import reset as RS
-    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(ids))
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(ids), impairment=impairment)
     return S.astype(np.float32)
+
+
+def dofs(md):
+    """state columns of the articulated DoFs: robot, then the tremor head chain"""
+    from avr import _abi as ABI
+    return slice(0, md.n_dof + ABI.HC_N)
 
 
 def test_kernel_resources(lib_and_scene):
@@ -53,15 +59,18 @@ def test_kernel_resources(lib_and_scene):
     sim.close()
 
 
-def test_one_substep_matches_oracle(lib_and_scene):
+@pytest.mark.parametrize('impairment', ['none', 'tremor'])
+def test_one_substep_matches_oracle(lib_and_scene, impairment):
     from avr import _abi as ABI
     A, md = lib_and_scene
-    S = reset_states(A, md, range(8))
+    S = reset_states(A, md, range(8), impairment)
     sim, o = make_sim(md, 8), oracle(md, 8)
     sim.set_state(S); o.set_state(S)
     sim.substep(0.01); o.substep(0.01)
     G, C = sim.get_state(), o.get_state()
-    assert np.abs(G[:, :10] - C[:, :10]).max() < 1e-5
+    assert np.abs(G[:, dofs(md)] - C[:, dofs(md)]).max() < 1e-5
+    h = slice(ABI.S_HUMAN, ABI.S_HCH)
+    assert np.abs(G[:, h] - C[:, h]).max() < 1e-5
     fb = slice(ABI.S_FREE, ABI.S_FREE + ABI.MAX_FREE * ABI.FB_WORDS)
     assert np.abs(G[:, fb] - C[:, fb]).max() < 1e-4
     sim.close()
@@ -76,10 +85,12 @@ def test_golden_fixture_within_chaos_envelope(lib_and_scene):
     obs0 = sim.settle(100)
     assert np.abs(obs0 - g['obs0']).max() < 3e-3
     worst = 0.0
+    hc = slice(md.n_dof, md.n_dof + 4)
     for t in range(g['actions'].shape[0]):
         ob, r, d, i = sim.step(g['actions'][t])
         St = sim.get_state()
         worst = max(worst, np.abs(St[:, :7] - g['states'][t][:, :7]).max())
+        worst = max(worst, np.abs(St[g['tremor'], hc] - g['states'][t][g['tremor'], hc]).max())
         assert np.array_equal(d, g['done'][t])
         assert np.abs(r - g['rew'][t]).max() < 5e-2
         assert np.array_equal(i[:, 1], g['info'][t][:, 1])     # task_success
@@ -99,11 +110,12 @@ def _remove_food_and_bowl(S):
     return S
 
 
-def test_free_space_200_steps_within_1e3(lib_and_scene):
+@pytest.mark.parametrize('impairment', ['none', 'tremor'])
+def test_free_space_200_steps_within_1e3(lib_and_scene, impairment):
     from avr import _lib
     A, md = lib_and_scene
     n = 4
-    S = _remove_food_and_bowl(reset_states(A, md, range(n)))
+    S = _remove_food_and_bowl(reset_states(A, md, range(n), impairment))
     sim, o = make_sim(md, n), oracle(md, n)
     sim.set_state(S); o.set_state(S.astype(np.float64))
     worst = 0.0
@@ -111,7 +123,7 @@ def test_free_space_200_steps_within_1e3(lib_and_scene):
         a = _lib.random_actions(1001, np.arange(n), t)
         sim.step(a); o.step(a)
         if t % 20 == 19 or t == 199:
-            worst = max(worst, np.abs(sim.get_state()[:, :7] - o.get_state()[:, :7]).max())
+            worst = max(worst, np.abs(sim.get_state()[:, dofs(md)] - o.get_state()[:, dofs(md)]).max())
     assert worst < 1e-3, worst
     sim.close()
 
@@ -150,7 +162,7 @@ def test_deterministic_and_batch_independent(lib_and_scene):
     from avr import _lib
     A, md = lib_and_scene
     n = 64
-    S = reset_states(A, md, range(16))
+    S = reset_states(A, md, range(16), 'random')
     S = np.tile(S, (4, 1))
     outs = []
     for _ in range(2):
@@ -203,3 +215,30 @@ def test_create_errors(lib_and_scene):
         _lib.Sim(md, 0)
     with pytest.raises(RuntimeError):
         _lib.Sim(md, 4, device=99)
+
+
+def test_tremor_targets_and_hard_limits_match_oracle(lib_and_scene):
+    """Tremor glue on the device: motor targets alternate with the iteration parity
+    (env.py:330-331) and a chain joint pushed past its limit is clamped at the frame end
+    (enforce_hard_human_joint_limits, env.py:389-410), as in the oracle."""
+    from avr import _abi as ABI, _lib
+    A, md = lib_and_scene
+    n, nd = 4, md.n_dof
+    S = reset_states(A, md, range(20, 20 + n), 'tremor')
+    up = A['hc_upper']
+    S[:, ABI.S_Q + nd] = up[0] + 0.05          # neck 0.05 rad past its upper limit
+    S[:, ABI.S_Q + nd + 3] = -up[3] - 0.05     # head yaw past its lower limit
+    sim, o = make_sim(md, n), oracle(md, n)
+    sim.set_state(S); o.set_state(S.astype(np.float64))
+    for t in range(2):
+        a = _lib.random_actions(1001, np.arange(n), t)
+        sim.step(a); o.step(a)
+        G, C = sim.get_state(), o.get_state()
+        sg = 1.0 if t % 2 == 0 else -1.0
+        want = S[:, ABI.S_HCH:ABI.S_HCH + 4] + sg * S[:, ABI.S_HCH + 4:ABI.S_HCH + 8]
+        assert np.allclose(G[:, ABI.S_QTGT + nd:ABI.S_QTGT + nd + 4], want, atol=1e-6)
+        q = G[:, nd:nd + 4]
+        assert np.all(q <= A['hc_upper'] + 1e-6) and np.all(q >= A['hc_lower'] - 1e-6)
+        assert np.abs(G[:, dofs(md)] - C[:, dofs(md)]).max() < 1e-4
+        assert np.abs(G[:, ABI.S_QD:ABI.S_QD + nd + 4] - C[:, ABI.S_QD:ABI.S_QD + nd + 4]).max() < 1e-3
+    sim.close()

@@ -248,3 +248,77 @@ def test_oracle_is_deterministic_and_thread_invariant(scene, oracle_built):
             o.step(_lib.random_actions(1001, np.arange(4), t))
         outs.append(o.get_state())
     assert np.array_equal(outs[0], outs[1])
+
+
+# ----------------------------------------------------------------------------- tremor head chain
+def test_tremor_head_chain_fk_matches_host_fk(scene, oracle_built):
+    """The oracle's head chain (4 links appended to the robot, root on the chest slot) publishes
+    the neck / head poses of the host's full 42-joint human FK (reset.human_slot_poses)."""
+    from oracle.oracle import Oracle
+    A, md = scene
+    env = 9
+    S, meta = RS.batch_reset_states_fast(A, md, 1001, [env], impairment='tremor')
+    g = meta[0]['gender']
+    rng = RS._rng(1001, env)
+    rng.integers(2)                                     # the gender draw
+    qh = RS.human_joint_angles(A, g, rng, 1.0)
+    assert np.allclose(S[0, md.n_dof:md.n_dof + 4], qh[24:28])
+    dq = np.array([0.05, -0.2, 0.15, 0.3])
+    qh[24:28] += dq
+    S[0, md.n_dof:md.n_dof + 4] += dq
+    o = Oracle(md, 1)
+    o.set_state(S)
+    o.robot_fk(0)
+    St = o.get_state()[0]
+    want = RS.human_slot_poses(A, g, qh)
+    checked = 0
+    for slot in A['hc_slot']:
+        if slot < 0:
+            continue
+        got = St[ABI.S_HUMAN + 7 * slot:ABI.S_HUMAN + 7 * slot + 7]
+        assert np.allclose(got[:3], want[slot][:3], atol=1e-12)
+        assert abs(abs(np.dot(got[3:], want[slot][3:])) - 1) < 1e-12
+        checked += 1
+    assert checked == 2                                 # neck capsule, head mesh
+
+
+def test_tremor_targets_alternate_and_hard_limits_hold(scene, oracle_built):
+    """take_step tremor targets (env.py:330-331) and enforce_hard_human_joint_limits
+    (env.py:389-410): a neck pushed 0.05 rad past its upper limit is back within limits after
+    the first frame and stays there."""
+    from oracle.oracle import Oracle
+    from avr import _lib
+    A, md = scene
+    nd = md.n_dof
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, [11, 12], impairment='tremor')
+    S[:, nd] = A['hc_upper'][0] + 0.05
+    o = Oracle(md, 2)
+    o.set_state(S)
+    moved = 0.0
+    for t in range(3):
+        o.step(_lib.random_actions(1001, np.arange(2), t))
+        St = o.get_state()
+        sg = 1.0 if t % 2 == 0 else -1.0
+        want = S[:, ABI.S_HCH:ABI.S_HCH + 4] + sg * S[:, ABI.S_HCH + 4:ABI.S_HCH + 8]
+        assert np.allclose(St[:, ABI.S_QTGT + nd:ABI.S_QTGT + nd + 4], want, atol=1e-12)
+        assert np.all(St[:, ABI.S_KP + nd:ABI.S_KP + nd + 4] == ABI.FEEDING_PARAMS['human_gain'])
+        q = St[:, nd:nd + 4]
+        assert np.all(q <= A['hc_upper'] + 1e-12) and np.all(q >= A['hc_lower'] - 1e-12)
+        moved = max(moved, np.abs(q[:, 1:] - S[:, nd + 1:nd + 4]).max())
+    assert moved > 1e-3                                 # the motors do shake the head
+
+
+def test_static_human_views_ignore_the_chain(scene, oracle_built):
+    """Without 'tremor' the chain DoFs, targets and head pose are untouched by a step."""
+    from oracle.oracle import Oracle
+    from avr import _lib
+    A, md = scene
+    nd = md.n_dof
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, [0, 1], impairment='weakness')
+    o = Oracle(md, 2)
+    o.set_state(S)
+    o.step(_lib.random_actions(1001, np.arange(2), 0))
+    St = o.get_state()
+    assert np.all(St[:, nd:nd + 4] == 0) and np.all(St[:, ABI.S_HCH:ABI.S_CP] == 0)
+    h = slice(ABI.S_HUMAN, ABI.S_HCH)
+    assert np.array_equal(St[:, h], S[:, h])

@@ -55,3 +55,29 @@ def test_reset_state_layout(scene):
     assert np.allclose(f0 - sp, [-0.005, 0, 0.02])
     q = S[:, ABI.S_FREE + 3:ABI.S_FREE + 7]
     assert np.allclose(np.linalg.norm(q, axis=1), 1)
+
+
+def test_tremor_reset_state(scene):
+    """'tremor': human_tremors ~ U(+-20 deg) (world_creation.py:136-139), targets = the chain's
+    starting angles (feeding.py:246-248), chain at rest with its motors off."""
+    A, md = scene
+    nd = md.n_dof
+    S, meta = RS.batch_reset_states_fast(A, md, 1001, list(range(8)), impairment='tremor')
+    assert all(m['impairment'] == 'tremor' for m in meta)
+    assert np.all(S[:, ABI.S_TASK + ABI.T_HDYN] == 1)
+    assert np.array_equal(S[:, ABI.S_HCH:ABI.S_HCH + 4], S[:, nd:nd + 4])
+    tr = S[:, ABI.S_HCH + 4:ABI.S_HCH + 8]
+    assert np.all(np.abs(tr) <= np.deg2rad(20)) and np.abs(tr).max() > np.deg2rad(5)
+    assert np.all(S[:, nd] == 0)                                   # the neck starts straight
+    assert np.all(np.abs(S[:, nd + 1:nd + 4]) <= np.deg2rad(30))   # head U(+-30 deg) (feeding.py:242)
+    assert np.all(S[:, ABI.S_QD + nd:ABI.S_QD + nd + 4] == 0)
+    assert np.all(S[:, ABI.S_MAXIMP + nd:ABI.S_MAXIMP + nd + 4] == 0)
+
+
+def test_random_impairment_draws_all_four(scene):
+    A, md = scene
+    S, meta = RS.batch_reset_states_fast(A, md, 1001, list(range(48)), impairment='random')
+    kinds = [m['impairment'] for m in meta]
+    assert set(kinds) == {'none', 'limits', 'weakness', 'tremor'}
+    tr = np.array([k == 'tremor' for k in kinds])
+    assert np.array_equal(S[:, ABI.S_TASK + ABI.T_HDYN] == 1, tr)
