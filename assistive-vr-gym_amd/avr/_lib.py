@@ -11,7 +11,7 @@ import numpy as np
 from . import _abi as ABI
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libavr.so')
+LIB_PATH = os.environ.get('AVR_LIB') or os.path.join(HERE, 'libavr.so')   # AVR_LIB: experiment builds
 
 EXPORTS = [
     'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',

@@ -1555,23 +1555,60 @@ typedef const __attribute__((address_space(1))) float *gfp;
 
 struct RowS { f8 h; f16v a; f8 b; float jr, mr; };   // header, free A + B(J) , B(MJ), robot parts
 
-AVR_DI void load_row(RowS &R, const float *rec, const float *rob, bool robot) {
+// A row's loads go out together: the record through the scalar cache and, speculatively, the
+// articulated part as two vector loads (lane & 15 keeps every lane in bounds).  Whether the row
+// has an articulated part is only known from its header, so the part is selected afterwards
+// (rows without one hold stale words there; a select, never arithmetic, discards them).
+#ifdef AVR_ROW_VLOAD
+// experiment: the record as wave-uniform vector loads (TA/L1 path) instead of the scalar cache
+typedef const __attribute__((address_space(1))) f8 *gf8p;
+typedef const __attribute__((address_space(1))) f16v *gf16p;
+#endif
+AVR_DI void issue_row(RowS &R, float &j, float &mj, const float *rec, const float *rob) {
+    const int l = lane_id() & 15;
+    j = ((gfp)rob)[l];
+    mj = ((gfp)rob)[16 + l];
+#ifdef AVR_ROW_VLOAD
+    R.h = *(gf8p)(rec);
+    R.a = *(gf16p)(rec + 8);
+    R.b = *(gf8p)(rec + 24);
+#else
     R.h = *(cf8p)(rec);
     R.a = *(cf16p)(rec + 8);
     R.b = *(cf8p)(rec + 24);
-    const int lane = lane_id();
-    R.jr = 0.f; R.mr = 0.f;
-    if (robot && lane < MAXD) { R.jr = ((gfp)rob)[lane]; R.mr = ((gfp)rob)[16 + lane]; }
+#endif
+}
+AVR_DI int row_info(const RowS &R) { return uni(__float_as_int(R.h[0])); }
+AVR_DI bool row_robot(const RowS &R) { return (row_info(R) & RI_ROBOT) != 0; }
+AVR_DI void finish_row(RowS &R, float j, float mj, bool robot) {
+    const bool own = robot && lane_id() < MAXD;
+    R.jr = own ? j : 0.f;
+    R.mr = own ? mj : 0.f;
+}
+// keep the scalar loads of a row pair ahead of the first row's arithmetic (the compiler would
+// otherwise sink the second row's loads below it: two round trips instead of one)
+#ifdef AVR_ROW_VLOAD
+#define ROW_PIN(R) (void)0
+#else
+#define ROW_PIN(R) asm volatile("" ::"s"(R.h), "s"(R.a), "s"(R.b))
+#endif
+
+AVR_DI void load_row(RowS &R, const float *rec, const float *rob, bool robot) {
+    float j, mj;
+    issue_row(R, j, mj, rec, rob);
+    finish_row(R, j, mj, robot);
 }
 
 // one row: returns the clamped impulse increment and applies it
 AVR_DI float row_go(const RowS &R, DV &d, float imp, float lo, float hi, bool robot) {
     const int lane = lane_id();
-    const int info = __float_as_int(R.h[0]);
+    const int info = row_info(R);
     const int iA = info & 63, iB = (info >> 6) & 63;
     // A: J = a[0..5], MJ = a[6..11]; B: J = a[12..15] b[0..1], MJ = b[2..7]
     float pA = R.a[0] * d.vx + R.a[1] * d.vy + R.a[2] * d.vz + R.a[3] * d.wx + R.a[4] * d.wy + R.a[5] * d.wz;
     float pB = R.a[12] * d.vx + R.a[13] * d.vy + R.a[14] * d.vz + R.a[15] * d.wx + R.b[0] * d.wy + R.b[1] * d.wz;
+    // (measured: reading the two owner lanes with v_readlane for rows without an articulated
+    // part is slower than this branch-free 16-lane DPP reduction)
     float p = (lane == iA ? pA : 0.f) + (lane == iB ? pB : 0.f);
     if (robot) p += R.jr * d.rq;
     float dv = robot_reduce(p);
@@ -1620,30 +1657,44 @@ AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV 
         (void)row_go(R, d, 0.f, imp0, imp0, robot);     // delta = imp0
     }
     for (int it = 0; it < m.iters; it++) {
-        for (int j = 0; j < n_nc; j++) {
-            const int k = (it & 1) ? j : n_nc - 1 - j;
-            RowS R;
-            load_row(R, rows + k * RW, robs + k * RW, true);
-            float ni = row_go(R, d, rdl(inc, k), R.h[4], R.h[5], true);
-            if (lane == k) inc = ni;
+        // two consecutive rows of the sweep per scalar round trip
+        for (int j = 0; j < n_nc; j += 2) {
+            const int k0 = (it & 1) ? j : n_nc - 1 - j;
+            const bool two = j + 1 < n_nc;
+            const int k1 = two ? ((it & 1) ? j + 1 : n_nc - 2 - j) : k0;
+            RowS R0, R1;
+            float j0, m0, j1, m1;
+            issue_row(R0, j0, m0, rows + k0 * RW, robs + k0 * RW);
+            issue_row(R1, j1, m1, rows + k1 * RW, robs + k1 * RW);
+            ROW_PIN(R0);
+            ROW_PIN(R1);
+            finish_row(R0, j0, m0, true);
+            float ni = row_go(R0, d, rdl(inc, k0), R0.h[4], R0.h[5], true);
+            if (lane == k0) inc = ni;
+            if (two) {
+                finish_row(R1, j1, m1, true);
+                ni = row_go(R1, d, rdl(inc, k1), R1.h[4], R1.h[5], true);
+                if (lane == k1) inc = ni;
+            }
         }
         // rows are fetched two at a time (one scalar round trip for consecutive records)
         for (int c = 0; c < n_c; c += 2) {
             const float *rec = rows + (n_nc + c) * RW;
             RowS R0, R1;
             const bool two = c + 1 < n_c;
-            R0.h = *(cf8p)rec; R0.a = *(cf16p)(rec + 8); R0.b = *(cf8p)(rec + 24);
-            R1.h = *(cf8p)(rec + RW); R1.a = *(cf16p)(rec + RW + 8); R1.b = *(cf8p)(rec + RW + 24);
-            const bool rb0 = (__float_as_int(R0.h[0]) & RI_ROBOT) != 0;
-            R0.jr = 0.f; R0.mr = 0.f;
-            if (rb0 && lane < MAXD) { R0.jr = ((gfp)(robs + (n_nc + c) * RW))[lane]; R0.mr = ((gfp)(robs + (n_nc + c) * RW))[16 + lane]; }
+            float j0, m0, j1, m1;
+            issue_row(R0, j0, m0, rec, robs + (n_nc + c) * RW);
+            issue_row(R1, j1, m1, rec + RW, robs + (n_nc + c + 1) * RW);
+            ROW_PIN(R0);
+            ROW_PIN(R1);
+            const bool rb0 = row_robot(R0);
+            finish_row(R0, j0, m0, rb0);
             float ni = row_go(R0, d, rdl(c < 64 ? in0 : in1, c & 63), 0.f, 1e10f, rb0);
             if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
             if (two) {
                 const int c1 = c + 1;
-                const bool rb1 = (__float_as_int(R1.h[0]) & RI_ROBOT) != 0;
-                R1.jr = 0.f; R1.mr = 0.f;
-                if (rb1 && lane < MAXD) { R1.jr = ((gfp)(robs + (n_nc + c1) * RW))[lane]; R1.mr = ((gfp)(robs + (n_nc + c1) * RW))[16 + lane]; }
+                const bool rb1 = row_robot(R1);
+                finish_row(R1, j1, m1, rb1);
                 ni = row_go(R1, d, rdl(c1 < 64 ? in0 : in1, c1 & 63), 0.f, 1e10f, rb1);
                 if (lane == (c1 & 63)) { if (c1 < 64) in0 = ni; else in1 = ni; }
             }
@@ -1655,15 +1706,15 @@ AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV 
             const int f = 2 * c;
             const float *rec = rows + (n_nc + n_c + f) * RW;
             RowS R0, R1;
-            R0.h = *(cf8p)rec; R0.a = *(cf16p)(rec + 8); R0.b = *(cf8p)(rec + 24);
-            R1.h = *(cf8p)(rec + RW); R1.a = *(cf16p)(rec + RW + 8); R1.b = *(cf8p)(rec + RW + 24);
-            const bool robot = (__float_as_int(R0.h[0]) & RI_ROBOT) != 0;    // same endpoints for both
-            R0.jr = R0.mr = R1.jr = R1.mr = 0.f;
-            if (robot && lane < MAXD) {
-                const float *q0 = robs + (n_nc + n_c + f) * RW;
-                R0.jr = ((gfp)q0)[lane]; R0.mr = ((gfp)q0)[16 + lane];
-                R1.jr = ((gfp)q0)[RW + lane]; R1.mr = ((gfp)q0)[RW + 16 + lane];
-            }
+            float j0, m0, j1, m1;
+            const float *q0 = robs + (n_nc + n_c + f) * RW;
+            issue_row(R0, j0, m0, rec, q0);
+            issue_row(R1, j1, m1, rec + RW, q0 + RW);
+            ROW_PIN(R0);
+            ROW_PIN(R1);
+            const bool robot = row_robot(R0);    // same endpoints for both
+            finish_row(R0, j0, m0, robot);
+            finish_row(R1, j1, m1, robot);
             const float fr = R0.h[1];
             const int s = f >> 6;           // f and f + 1 share the impulse register (f even)
             float fimp = s == 0 ? if0 : (s == 1 ? if1 : if2);
