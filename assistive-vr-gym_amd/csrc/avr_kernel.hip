@@ -32,6 +32,7 @@
 
 
 // --------------------------------------------------------------------------- LDS layout
+#define AVR_PROF_SLOTS 24   // diagnostic build: per-env cycle / event counters (tools/prof_phases.py)
 struct EnvLDS {
     float st[AVR_S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
@@ -45,7 +46,7 @@ struct EnvLDS {
     int nsp, nap, n_nc, n_c, flags, gender;
     int nla, nda;           // articulated links / DoFs of this env (the head chain counts under 'tremor')
 #ifdef AVR_PROF
-    unsigned long long prof[16];
+    unsigned long long prof[AVR_PROF_SLOTS];
 #endif
     union {
         struct {                           // collision detection
@@ -190,11 +191,19 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
 
 // y = M^-1 x (padding DoFs have identity rows)
 AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
+#ifdef AVR_MINV_LAUNDER
+    // keep the 196 M^-1 loads inside the caller's loops (hoisted, they pin ~200 VGPRs)
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const float *Mv = &L.Minv[0][0] + z;
+#else
+    const float *Mv = &L.Minv[0][0];
+#endif
 #pragma unroll
     for (int i = 0; i < MAXD; i++) {
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < MAXD; k++) s += L.Minv[i][k] * x[k];
+        for (int k = 0; k < MAXD; k++) s += Mv[i * MAXD + k] * x[k];
         y[i] = s;
     }
 }
@@ -982,6 +991,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
     const int lane = lane_id();
     const int gender = L.gender;
     (void)gender;
+    PROF_START(pb);
     int sa = 0, sb = 0, p = 0;
     if (lane < nq) { int k = L.u.c.qk[lane]; sa = k & 0xffff; sb = k >> 16; p = L.u.c.qp[lane]; }
     int rc = 0;
@@ -1002,6 +1012,19 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
     unsigned long long cm = __ballot(coop);
 #ifdef AVR_PROF
     if (lane == 0) L.prof[11] += __popcll(cm);
+    {   // coop pairs by body kinds: robot-robot, robot-free, robot-static/human, other
+        int kind = 3;
+        if (coop) {
+            const int ka = m.body_kind[m.shape_body[sa]], kb = m.body_kind[m.shape_body[sb]];
+            if (ka == AVR_BODY_ROBOT && kb == AVR_BODY_ROBOT) kind = 0;
+            else if (ka == AVR_BODY_ROBOT || kb == AVR_BODY_ROBOT) kind = (ka == AVR_BODY_FREE || kb == AVR_BODY_FREE) ? 1 : 2;
+        }
+        for (int q = 0; q < 4; q++) {
+            const unsigned long long bq = __ballot(coop && kind == q);
+            if (lane == 0) L.prof[19 + q] += __popcll(bq);
+        }
+    }
+    PROF_STOP(16, pb);
 #endif
     while (cm) {
         const int j = __ffsll((long long)cm) - 1;
@@ -1015,6 +1038,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2);
         if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
     }
+    PROF_STOP(17, pb);
 
     // manifold update (one lane per pair)
     unsigned pk = 0u;
@@ -1063,6 +1087,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         }
     }
     nnew += tot;
+    PROF_STOP(18, pb);
 }
 
 AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
@@ -1121,60 +1146,24 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     // child lists are culled against the other body first, which leaves the set of overlapping
     // child pairs and its i-major / j-minor order unchanged.
     int nq = 0, nsp = 0, nnew = 0;
-    for (int k = 0; k < nap; k++) {
-        const int p = L.u.c.apair[k];
-        const int ba = m.pair_a[p], bb = m.pair_b[p];
-        const int sa0 = m.body_shape_start[ba], na = m.body_shape_count[ba];
-        const int sb0 = m.body_shape_start[bb], nb = m.body_shape_count[bb];
-        const bool bare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
-        int ncA = na, ncB = nb;
-        const bool cull = !bare && na * nb > 1;
-        if (cull) {
-            const v3 bAmn = ld3(L.u.c.bmin[ba]), bAmx = ld3(L.u.c.bmax[ba]);
-            const v3 bBmn = ld3(L.u.c.bmin[bb]), bBmx = ld3(L.u.c.bmax[bb]);
-            ncA = 0;
-            for (int base = 0; base < na; base += 64) {
-                const int i = base + lane;
-                bool act = false;
-                if (i < na && shape_enabled(m, sa0 + i, gender)) {
-                    v3 a0, a1;
-                    child_aabb(m, L, sa0 + i, a0, a1);
-                    act = overlap(a0, a1, bBmn, bBmx);
-                }
-                int tot;
-                int pre = ballot_prefix(act, &tot);
-                if (act) L.u.c.candA[ncA + pre] = sa0 + i;
-                ncA += tot;
-            }
-            ncB = 0;
-            for (int base = 0; base < nb; base += 64) {
-                const int j = base + lane;
-                bool act = false;
-                if (j < nb && shape_enabled(m, sb0 + j, gender)) {
-                    v3 b0, b1;
-                    child_aabb(m, L, sb0 + j, b0, b1);
-                    act = overlap(b0, b1, bAmn, bAmx);
-                }
-                int tot;
-                int pre = ballot_prefix(act, &tot);
-                if (act) L.u.c.candB[ncB + pre] = sb0 + j;
-                ncB += tot;
-            }
-            SYNC();
-        }
-        const int nitems = ncA * ncB;
-#ifdef AVR_PROF
-        if (lane == 0) L.prof[4] += nitems;
-#endif
-        const float rcpB = 1.f / (float)(ncB > 0 ? ncB : 1);
-        for (int base = 0; base < nitems; base += 64) {
-            const int it = base + lane;
-            bool act = false;
-            int sa = 0, sb = 0;
-            if (it < nitems) {
-                const int i = (int)(((float)it + 0.5f) * rcpB);     // exact: it < 2^14, ncB <= 128
-                const int j = it - i * ncB;
-                if (cull) {
+    // Shape pairs are produced 64 at a time, in pair order (i-major, j-minor within a pair), from
+    // either a run of consecutive single-child pairs (1 x 1: food-food, robot link-link, ...; 80 %
+    // of the active pairs), one lane per pair, or one culled compound pair, one lane per item.
+    // Every round appends its pairs to the queue; a full queue (or the end) runs collide_batch.
+    // (One producer loop keeps a single inlined copy of collide_batch.)
+    int k = 0;                                      // next active pair
+    int gp = 0, gsa0 = 0, gsb0 = 0, gncB = 1, gn = 0, gbase = 0;
+    bool gcull = false, gbare = false;
+    float grcpB = 1.f;
+    for (;;) {
+        bool act = false, last = false;
+        int sa = 0, sb = 0, q = gp;
+        if (gbase < gn) {                           // the compound pair in progress
+            const int it = gbase + lane;
+            if (it < gn) {
+                const int i = (int)(((float)it + 0.5f) * grcpB);     // exact: it < 2^14, ncB <= 128
+                const int j = it - i * gncB;
+                if (gcull) {
                     sa = L.u.c.candA[i];
                     sb = L.u.c.candB[j];
                     v3 a0, a1, b0, b1;
@@ -1182,10 +1171,10 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                     child_aabb(m, L, sb, b0, b1);
                     act = overlap(a0, a1, b0, b1);
                 } else {
-                    sa = sa0 + i;
-                    sb = sb0 + j;
+                    sa = gsa0 + i;
+                    sb = gsb0 + j;
                     if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
-                        if (bare) act = true;
+                        if (gbare) act = true;
                         else {
                             v3 a0, a1, b0, b1;
                             child_aabb(m, L, sa, a0, a1);
@@ -1195,31 +1184,111 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                     }
                 }
             }
-            int tot;
-            int pre = ballot_prefix(act, &tot);
-            // the restated pipeline keeps at most MAXSP shape pairs per sub-step (flag 8)
-            if (act && nsp + pre < MAXSP) { L.u.c.qk[nq + pre] = sa | (sb << 16); L.u.c.qp[nq + pre] = p; }
-            const int add = nsp + tot <= MAXSP ? tot : (nsp < MAXSP ? MAXSP - nsp : 0);
-            nsp += tot;
-            nq += add;
-            if (nq >= 64) {
-                SYNC();
-                PROF_STOP(2, pt);
-                collide_batch(m, L, 64, gcp, nold, newcp, nnew, E);
-                PROF_STOP(3, pt);
-                SYNC();
-                if (lane < nq - 64) { L.u.c.qk[lane] = L.u.c.qk[64 + lane]; L.u.c.qp[lane] = L.u.c.qp[64 + lane]; }
-                nq -= 64;
-                SYNC();
+            gbase += 64;
+        } else if (k < nap) {
+            if (gcull) { SYNC(); gcull = false; }   // candA / candB are rewritten below
+            const int kk = k + lane;
+            bool one = false;
+            if (kk < nap) {
+                const int qq = L.u.c.apair[kk];
+                one = m.body_shape_count[m.pair_a[qq]] == 1 && m.body_shape_count[m.pair_b[qq]] == 1;
             }
+            const unsigned long long bm = __ballot(one);
+            const int run = bm == ~0ull ? 64 : __ffsll((long long)~bm) - 1;
+            if (run > 0) {                          // a run of 1 x 1 pairs
+                if (lane < run) {
+                    q = L.u.c.apair[k + lane];
+                    const int ba = m.pair_a[q], bb = m.pair_b[q];
+                    sa = m.body_shape_start[ba];
+                    sb = m.body_shape_start[bb];
+                    if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
+                        if ((m.body_flags[ba] & 1) && (m.body_flags[bb] & 1)) act = true;
+                        else {
+                            v3 a0, a1, b0, b1;
+                            child_aabb(m, L, sa, a0, a1);
+                            child_aabb(m, L, sb, b0, b1);
+                            act = overlap(a0, a1, b0, b1);
+                        }
+                    }
+                }
+#ifdef AVR_PROF
+                if (lane == 0) L.prof[4] += run;
+#endif
+                k += run;
+            } else {                                // set up compound pair k
+                gp = L.u.c.apair[k];
+                const int ba = m.pair_a[gp], bb = m.pair_b[gp];
+                const int na = m.body_shape_count[ba], nb = m.body_shape_count[bb];
+                gsa0 = m.body_shape_start[ba];
+                gsb0 = m.body_shape_start[bb];
+                gbare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
+                gcull = !gbare && na * nb > 1;
+                int ncA = na, ncB = nb;
+                if (gcull) {
+                    const v3 bAmn = ld3(L.u.c.bmin[ba]), bAmx = ld3(L.u.c.bmax[ba]);
+                    const v3 bBmn = ld3(L.u.c.bmin[bb]), bBmx = ld3(L.u.c.bmax[bb]);
+                    ncA = 0;
+                    for (int base = 0; base < na; base += 64) {
+                        const int i = base + lane;
+                        bool a = false;
+                        if (i < na && shape_enabled(m, gsa0 + i, gender)) {
+                            v3 a0, a1;
+                            child_aabb(m, L, gsa0 + i, a0, a1);
+                            a = overlap(a0, a1, bBmn, bBmx);
+                        }
+                        int tot;
+                        int pre = ballot_prefix(a, &tot);
+                        if (a) L.u.c.candA[ncA + pre] = gsa0 + i;
+                        ncA += tot;
+                    }
+                    ncB = 0;
+                    for (int base = 0; base < nb; base += 64) {
+                        const int j = base + lane;
+                        bool a = false;
+                        if (j < nb && shape_enabled(m, gsb0 + j, gender)) {
+                            v3 b0, b1;
+                            child_aabb(m, L, gsb0 + j, b0, b1);
+                            a = overlap(b0, b1, bAmn, bAmx);
+                        }
+                        int tot;
+                        int pre = ballot_prefix(a, &tot);
+                        if (a) L.u.c.candB[ncB + pre] = gsb0 + j;
+                        ncB += tot;
+                    }
+                    SYNC();
+                }
+                gn = ncA * ncB;
+                gncB = ncB > 0 ? ncB : 1;
+                grcpB = 1.f / (float)gncB;
+                gbase = 0;
+#ifdef AVR_PROF
+                if (lane == 0) L.prof[4] += gn;
+#endif
+                k++;
+                continue;
+            }
+        } else last = true;
+        // append in lane order; the restated pipeline keeps at most MAXSP shape pairs per
+        // sub-step (flag 8)
+        int tot;
+        int pre = ballot_prefix(act, &tot);
+        if (act && nsp + pre < MAXSP) { L.u.c.qk[nq + pre] = sa | (sb << 16); L.u.c.qp[nq + pre] = q; }
+        const int add = nsp + tot <= MAXSP ? tot : (nsp < MAXSP ? MAXSP - nsp : 0);
+        nsp += tot;
+        nq += add;
+        if (nq >= 64 || (last && nq > 0)) {
+            const int nb = nq >= 64 ? 64 : nq;
+            SYNC();
+            PROF_STOP(2, pt);
+            collide_batch(m, L, nb, gcp, nold, newcp, nnew, E);
+            PROF_STOP(3, pt);
+            SYNC();
+            if (lane < nq - nb) { L.u.c.qk[lane] = L.u.c.qk[nb + lane]; L.u.c.qp[lane] = L.u.c.qp[nb + lane]; }
+            nq -= nb;
+            SYNC();
+            if (last && nq > 0) continue;          // (cannot happen: at most 64 + 63 queued)
         }
-        if (cull) SYNC();
-    }
-    if (nq > 0) {
-        SYNC();
-        PROF_STOP(2, pt);
-        collide_batch(m, L, nq, gcp, nold, newcp, nnew, E);
-        PROF_STOP(3, pt);
+        if (last) break;
     }
     if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; }
 #ifdef AVR_PROF
@@ -1906,7 +1975,7 @@ AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
         L.nda = hd ? m.nd + m.hc_n : m.nd;
     }
 #ifdef AVR_PROF
-    if (lane < 16) L.prof[lane] = 0;
+    if (lane < AVR_PROF_SLOTS) L.prof[lane] = 0;
 #endif
     SYNC();
 }
@@ -1914,7 +1983,7 @@ AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
 AVR_DI void prof_flush(const KModel &m, EnvLDS &L, int env) {
 #ifdef AVR_PROF
     SYNC();
-    if (m.prof && lane_id() < 16) m.prof[(size_t)env * 16 + lane_id()] += L.prof[lane_id()];
+    if (m.prof && lane_id() < AVR_PROF_SLOTS) m.prof[(size_t)env * AVR_PROF_SLOTS + lane_id()] += L.prof[lane_id()];
 #else
     (void)m; (void)L; (void)env;
 #endif
@@ -2037,9 +2106,9 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
 #ifdef AVR_PROF
     unsigned long long t2 = __builtin_amdgcn_s_memtime();
     if (m.prof && lane == 0) {
-        m.prof[(size_t)env * 16 + 9] += t1 - t0;
-        m.prof[(size_t)env * 16 + 10] += t2 - t1;
-        m.prof[(size_t)env * 16 + 5] += __float_as_int(ws[WS_XCC]) != xcc_id() ? 1 : 0;   // A/B on different XCDs
+        m.prof[(size_t)env * AVR_PROF_SLOTS + 9] += t1 - t0;
+        m.prof[(size_t)env * AVR_PROF_SLOTS + 10] += t2 - t1;
+        m.prof[(size_t)env * AVR_PROF_SLOTS + 5] += __float_as_int(ws[WS_XCC]) != xcc_id() ? 1 : 0;   // A/B on different XCDs
     }
 #endif
 }

@@ -11,17 +11,18 @@ lib.avr_set_profile_buffer.argtypes = [C.c_void_p, C.c_void_p]
 import torch
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 A = ABI.load_scene(); md = ABI.ModelDesc(A)
-S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))))
+S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
 S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
 sim = _lib.Sim(md, N)
-prof = torch.zeros(N * 16, dtype=torch.int64, device='cuda')
+SLOTS = 24
+prof = torch.zeros(N * SLOTS, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
-names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs']
+names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
-    p = prof.cpu().numpy().reshape(N, 16).astype(np.float64)
+    p = prof.cpu().numpy().reshape(N, SLOTS).astype(np.float64)
     tot = p[:, [0, 13, 6, 7, 8, 9, 10, 12]].sum(1).mean()   # (coop part) is inside narrow+mf
     print('step %d wall %.1f ms, mean cycles/env %.3g' % (t, el * 1e3, tot))
     for k, nm in enumerate(names):
