@@ -18,6 +18,7 @@ EXPORTS = [
     'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
+    'avr_hull_support_table',
 ]
 
 
@@ -44,6 +45,9 @@ def load(path=LIB_PATH):
     lib = C.CDLL(path)
     vp = C.c_void_p
     lib.avr_create.argtypes = [C.POINTER(avr_config), vp, C.POINTER(vp)]
+    if hasattr(lib, 'avr_hull_support_table'):      # (absent in experiment builds of older trees)
+        lib.avr_hull_support_table.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, C.c_int32]
+        lib.avr_hull_support_table.restype = C.c_int32
     lib.avr_destroy.argtypes = [vp]
     lib.avr_set_state.argtypes = [vp, vp]
     lib.avr_get_state.argtypes = [vp, vp]
@@ -220,3 +224,16 @@ def random_actions(seed, env_ids, t, act_dim=ABI.ACT_DIM):
                 x = (r[k] >> np.uint64(8)).astype(np.float32)
                 out[:, j] = x * np.float32(1.0 / 16777216.0) * np.float32(2.0) - np.float32(1.0)
     return out
+
+
+def hull_support_table(verts, G=16):
+    """Host support table of one hull (avr_hull_support_table): (cell[6G^2, 2], idx[total])."""
+    lib = load()
+    v = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1, 3)
+    cell = np.zeros((6 * G * G, 2), dtype=np.int32)
+    tot = lib.avr_hull_support_table(v.ctypes.data, len(v), G, cell.ctypes.data, None, 0)
+    if tot < 0:
+        raise RuntimeError('avr_hull_support_table failed')
+    idx = np.zeros(max(tot, 1), dtype=np.int32)
+    lib.avr_hull_support_table(v.ctypes.data, len(v), G, cell.ctypes.data, idx.ctypes.data, tot)
+    return cell, idx[:tot]

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(HERE, 'libavr.so')
 ARCH = os.environ.get('AVR_OFFLOAD_ARCH', 'gfx950')
-SOURCES = ['avr_kernel.hip', 'avr_capi.hip']
+SOURCES = ['avr_kernel.hip', 'avr_capi.hip', 'avr_hulltab.cpp']
 HEADERS = ['avr_math.h', 'avr_kmodel.h']
 
 
@@ -36,7 +36,7 @@ def build_lib(force=False, extra=(), out=LIB):
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')]
     if not force and not _stale(out, deps):
         return out
-    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result',
+    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result', '-fno-slp-vectorize',
            '-o', out] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
     subprocess.check_call(cmd)
     return out
@@ -45,6 +45,11 @@ def build_lib(force=False, extra=(), out=LIB):
 def build_prof(force=False):
     """Diagnostic build with per-phase s_memtime counters (tools/prof_phases.py); never shipped."""
     return build_lib(force=force, extra=('-DAVR_PROF',), out=os.path.join(HERE, 'libavr_prof.so'))
+
+
+def build_wavetime(force=False):
+    """Diagnostic build with per-wave start/end stamps (tools/wavetime.py); never shipped."""
+    return build_lib(force=force, extra=('-DAVR_WAVETIME',), out=os.path.join(HERE, 'libavr_wt.so'))
 
 
 def build_oracle():
@@ -60,4 +65,6 @@ if __name__ == '__main__':
     build_all(force='--force' in sys.argv)
     if '--prof' in sys.argv:
         build_prof(force=True)
+    if '--wt' in sys.argv:
+        build_wavetime(force=True)
     print(LIB)

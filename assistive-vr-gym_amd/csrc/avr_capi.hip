@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <vector>
+#include <cstring>
 #include <cmath>
 
 #include "../../include/avr.h"
@@ -268,6 +269,35 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int i = 0; i < d->n_hull_verts; i++)
             hv[i] = make_float4((float)d->hull_verts[3 * i], (float)d->hull_verts[3 * i + 1], (float)d->hull_verts[3 * i + 2], 0.f);
         if ((r = upload(s, hv, &k.hull_verts))) return r;
+        // support tables for the large hulls (exact sub-linear support queries, avr_hulltab.cpp)
+        std::vector<int> stab(ns, -1);
+        std::vector<int2> cells;
+        std::vector<float4> cand;
+        const int G = AVR_TAB_G, nc = 6 * G * G;
+        for (int i = 0; i < ns; i++) {
+            const int vs = d->shape_hull[4 * i], nvh = d->shape_hull[4 * i + 1];
+            if (d->shape_kind[i] != AVR_HULL || nvh <= AVR_TAB_MIN_NV) continue;
+            std::vector<float> pv((size_t)nvh * 3);
+            for (int q = 0; q < nvh; q++) { pv[3 * q] = hv[vs + q].x; pv[3 * q + 1] = hv[vs + q].y; pv[3 * q + 2] = hv[vs + q].z; }
+            std::vector<int32_t> cl((size_t)2 * nc);
+            const int tot = avr_hull_support_table(pv.data(), nvh, G, cl.data(), nullptr, 0);
+            if (tot < 0) return fail(s, -2, "support table for shape %d failed", i);
+            std::vector<int32_t> ix((size_t)tot);
+            avr_hull_support_table(pv.data(), nvh, G, cl.data(), ix.data(), tot);
+            stab[i] = (int)cells.size();
+            const int base = (int)cand.size();
+            for (int c = 0; c < nc; c++) cells.push_back(make_int2(base + cl[2 * c], cl[2 * c + 1]));
+            for (int q = 0; q < tot; q++) {
+                const float4 v = hv[vs + ix[q]];
+                float w;
+                std::memcpy(&w, &ix[q], sizeof w);
+                cand.push_back(make_float4(v.x, v.y, v.z, w));
+            }
+        }
+        if (cells.empty()) { cells.push_back(make_int2(0, 0)); cand.push_back(make_float4(0.f, 0.f, 0.f, 0.f)); }
+        if ((r = upload(s, stab, &k.shape_tab))) return r;
+        if ((r = upload(s, cells, &k.tab_cell))) return r;
+        if ((r = upload(s, cand, &k.tab_vert))) return r;
     }
     {
         // child AABB cache slots for the non-static shapes; static shapes get host-computed AABBs

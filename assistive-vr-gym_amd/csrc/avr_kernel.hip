@@ -42,6 +42,7 @@ struct EnvLDS {
     float vq[MAXD];
     float fv[MAXF][4], fw[MAXF][4];
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
+    float gsc[MAXF][4];     // 1/sqrt(m), sqrt of the inverse principal inertias (mass-normalised rows)
     float h[MAXD], qdd[MAXD];
     int nsp, nap, n_nc, n_c, flags, gender;
     int nla, nda;           // articulated links / DoFs of this env (the head chain counts under 'tremor')
@@ -303,7 +304,7 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
 
 // --------------------------------------------------------------------------- shapes
 struct WShape {
-    int kind, nv, vs;
+    int kind, nv, vs, tab;
     tf t;
     float margin;
     v3 he;
@@ -320,6 +321,7 @@ AVR_DI WShape make_wshape(const KModel &m, int s, tf body) {
     else w.he = V(pa[0], 0.f, 0.f);
     w.vs = m.shape_hull[4 * s + 0];
     w.nv = w.kind == AVR_HULL ? m.shape_hull[4 * s + 1] : 0;
+    w.tab = w.kind == AVR_HULL ? m.shape_tab[s] : -1;
     return w;
 }
 
@@ -343,7 +345,46 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
     if (s.kind == AVR_SPHERE) r = V(0, 0, 0);
     else if (s.kind == AVR_CAPSULE) r = V(0, 0, l.z >= 0.f ? s.he.y : -s.he.y);
     else if (s.kind == AVR_BOX) r = V(l.x >= 0.f ? s.he.x : -s.he.x, l.y >= 0.f ? s.he.y : -s.he.y, l.z >= 0.f ? s.he.z : -s.he.z);
-    else {
+    else if (s.tab >= 0) {
+        // support table (avr_hulltab.cpp): the candidates of l's cube-map cell, ascending
+        // vertex order, hold the first strictly largest projection of the whole hull
+        const GlobalF4 tv{m.tab_vert};
+        const float ax = fabsf(l.x), ay = fabsf(l.y), az = fabsf(l.z);
+        const float mx = fmaxf(ax, fmaxf(ay, az));
+        if (!(mx > 0.f)) {               // zero / NaN direction: the scan keeps vertex 0
+            const float4 v = GlobalF4{m.hull_verts + s.vs}[0];
+            r = V(v.x, v.y, v.z);
+        } else {
+            int f;
+            float u, w;
+            if (ax >= ay && ax >= az) { f = l.x < 0.f; u = l.y; w = l.z; }
+            else if (ay >= az) { f = 2 + (l.y < 0.f); u = l.x; w = l.z; }
+            else { f = 4 + (l.z < 0.f); u = l.x; w = l.y; }
+            const float sc = 0.5f * (float)AVR_TAB_G / mx;
+            const int i = min(AVR_TAB_G - 1, max(0, (int)((u + mx) * sc)));
+            const int j = min(AVR_TAB_G - 1, max(0, (int)((w + mx) * sc)));
+            const int2 oc = m.tab_cell[s.tab + (f * AVR_TAB_G + i) * AVR_TAB_G + j];
+            float best = -BIGF;
+            float4 bv = tv[oc.x];
+            int k = 0;
+            for (; k + 4 <= oc.y; k += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) v[q] = tv[oc.x + k + q];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float dd = l.x * v[q].x + l.y * v[q].y + l.z * v[q].z;
+                    if (dd > best) { best = dd; bv = v[q]; }
+                }
+            }
+            for (; k < oc.y; k++) {
+                const float4 v = tv[oc.x + k];
+                const float dd = l.x * v.x + l.y * v.y + l.z * v.z;
+                if (dd > best) { best = dd; bv = v; }
+            }
+            r = V(bv.x, bv.y, bv.z);
+        }
+    } else {
         // vertices through the global address space, several loads in flight per pass; the
         // first vertex with the strictly largest projection wins (index order), as before
         const GlobalF4 hv{m.hull_verts + s.vs};
@@ -1002,7 +1043,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
         float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
         WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
-        if (A.nv > SMALL_NV || B.nv > SMALL_NV) coop = true;
+        if ((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0)) coop = true;
         else {
             rc = narrowphase<false>(m, E, A, B, thr, nB, pB, d);
             if (rc == 2) coop = true;
@@ -1331,45 +1372,55 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 }
 
 
-// Constraint rows live in a per-env buffer in global memory (L2-resident working set), one
-// 32-word record per row, in solve order [non-contact][normals][frictions]:
+// Constraint rows live in a per-env buffer in global memory, one 20-word record per row, in
+// solve order [non-contact][normals][frictions]:
 //   w0 info (iA | iB<<6 | robot<<12; 63 = endpoint is not a free body)   w1 friction coeff
-//   w2 inv   w3 rhs   w4 lo   w5 hi   w6 initial impulse   w7 -
-//   w8..13 free A Jacobian (lin, ang)   w14..19 free A  M^-1 J^T
-//   w20..25 free B Jacobian             w26..31 free B  M^-1 J^T
-// Rows with a robot endpoint also own a robot part at the same index in the second half of the
-// buffer: w0..11 J (A and B endpoints combined), w16..27 M^-1 J^T.  Everything a row resolve
-// needs is precomputed here, so the PGS chain (solve) is loads + register arithmetic only.
-#define RW 32
+//   w2 inv   w3 rhs   w4 lo   w5 hi   w6 initial impulse   w7 robot slot (int bits, -1: none)
+//   w8..13 free A Jacobian (lin, ang)   w14..19 free B Jacobian
+// Rows with an articulated endpoint own a robot part (slot): 16 (J[d], M^-1 J^T[d]) pairs, A and
+// B endpoints combined.  Non-contact rows take slots 0 .. n_nc-1, robot contacts 3 consecutive
+// slots each.  The free bodies' M^-1 J^T is not stored: part B forms it on the owner lane from
+// the body's inverse mass and world inverse inertia (the row set then fits in LDS there).
+#define RW 32       // allocation unit of the per-env row buffer (2 * rowcap * RW floats)
+#define RWC 20      // words per row record
+#define ROBW 32     // words per robot part
 // per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
 #define WS_WORDS 128
 #define WS_NNC 0     // int bits: non-contact rows
 #define WS_NC 1      // int bits: contact points (rows n_nc .. n_nc + 3 n_c)
 #define WS_ASQ 2     // sum of squared caller actions (take_step -> task glue)
 #define WS_XCC 3     // diagnostic builds: XCD that ran part A
+#define WS_NROB 4    // int bits: robot parts (slots) of the row set
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW 72     // [MAXF][4] angular
 #define RI_NONE 63
 #define RI_ROBOT (1 << 12)
 
-AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RW; }
-AVR_DI float *row_rob(const KModel &m, float *base, int r) { return base + (m.rowcap + r) * RW; }
+AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RWC; }
+AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.rowcap * RWC + slot * ROBW; }
 
-AVR_DI void put_free(float *w, v3 jl, v3 ja, v3 ml, v3 ma) {
-    w[0] = jl.x; w[1] = jl.y; w[2] = jl.z; w[3] = ja.x; w[4] = ja.y; w[5] = ja.z;
-    w[6] = ml.x; w[7] = ml.y; w[8] = ml.z; w[9] = ma.x; w[10] = ma.y; w[11] = ma.z;
+// A free endpoint's part is stored mass-normalised: g = (jl / sqrt(m), D^1/2 R^T ja) with
+// R D R^T the world inverse inertia.  Part B then keeps the body's velocity increment in the
+// same coordinates (dv = v~ / sqrt(m) ... ) so that J.dv = g.v~ and M^-1 J^T delta = g delta:
+// one 6-vector per endpoint serves both halves of a row resolve.
+AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
+    const float *g = L.gsc[f];
+    const qt q = ldq(L.st + AVR_S_FREE + AVR_FB_WORDS * f + 3);
+    const v3 b = qrot(qconj(q), ja);
+    w[0] = jl.x * g[0]; w[1] = jl.y * g[0]; w[2] = jl.z * g[0];
+    w[3] = b.x * g[1]; w[4] = b.y * g[2]; w[5] = b.z * g[3];
 }
 AVR_DI void put_free_zero(float *w) {
 #pragma unroll
-    for (int k = 0; k < 12; k++) w[k] = 0.f;
+    for (int k = 0; k < 6; k++) w[k] = 0.f;
 }
-AVR_DI void put_hdr(float *w, int info, float fric, float inv, float rhs, float lo, float hi, float imp0) {
-    w[0] = __int_as_float(info); w[1] = fric; w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = imp0; w[7] = 0.f;
+AVR_DI void put_hdr(float *w, int info, float fric, float inv, float rhs, float lo, float hi, float imp0, int slot) {
+    w[0] = __int_as_float(info); w[1] = fric; w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = imp0; w[7] = __int_as_float(slot);
 }
 AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 #pragma unroll
-    for (int d = 0; d < MAXD; d++) { w[d] = J[d]; w[16 + d] = MJ[d]; }
+    for (int d = 0; d < 16; d++) { w[2 * d] = d < MAXD ? J[d] : 0.f; w[2 * d + 1] = d < MAXD ? MJ[d] : 0.f; }
 }
 
 // Non-contact rows (limits, motors, fixed constraint), one lane per row.
@@ -1421,15 +1472,15 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         const float rel = sg * L.vq[dof];
         float *w = row_rec(m, rows, lane);
         if (kind < 2) {
-            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f);
+            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f, lane);
         } else {
             const float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
             const float kp = L.st[AVR_S_KP + dof], kd = 1.f;
             const float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
             const float mi = L.st[AVR_S_MAXIMP + dof];
-            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f);
+            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f, lane);
         }
-        put_free_zero(w + 8); put_free_zero(w + 20);
+        put_free_zero(w + 8); put_free_zero(w + 14);
         put_robot(row_rob(m, rows, lane), J, MJ);
     } else if (kind == 3) {
         v3 lin = V(0, 0, 0);
@@ -1476,9 +1527,9 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         rel += free_dot(L, fb, jbl, jba);
         const float mi = m.fixed_max_imp;
         float *w = row_rec(m, rows, lane);
-        put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f);
+        put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f, lane);
         put_free_zero(w + 8);
-        put_free(w + 20, jbl, jba, mbl, mba);
+        put_free(L, fb, w + 14, jbl, jba);
         put_robot(row_rob(m, rows, lane), JA, MA);
     }
     if (nrow > MAXNC) { if (lane == 0) L.flags |= 16; nrow = MAXNC; }
@@ -1511,17 +1562,26 @@ AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, in
 
 // Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal) and
 // n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions).
-AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
+AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
     const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
     const float erp = m.erp;
-    for (int i = lane; i < ncp; i += 64) {
+    int nrob = n_nc;                                 // robot parts: nc rows first, then 3 per robot contact
+    for (int base = 0; base < ncp; base += 64) {
+        const int i = base + lane;
+        const bool act = i < ncp;
         int kA = 0, iA = 0, kB = 0, iB = 0;
-        const float *c = gcp + AVR_CP_WORDS * i;
+        const float *c = gcp + AVR_CP_WORDS * (act ? i : 0);
         int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
         body_endpoint(m, L, ba, kA, iA);
         body_endpoint(m, L, bb, kB, iB);
+        const bool rob = kA == 1 || kB == 1;
+        int tot;
+        const int pre = ballot_prefix(act && rob, &tot);
+        const int slot0 = nrob + 3 * pre;
+        nrob += 3 * tot;
+        if (!act) continue;
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
         v3 n = ld3(c + AVR_CP_N);
@@ -1529,12 +1589,12 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
         plane_space(n, t1, t2);
         v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
         float fric = fminf(m.body_friction[ba] * m.body_friction[bb], 10.f);
-        bool rob = kA == 1 || kB == 1;
         int info = (kA == 2 ? iA : RI_NONE) | ((kB == 2 ? iB : RI_NONE) << 6) | (rob ? RI_ROBOT : 0);
         float imA = kA == 2 ? 1.f / m.fb_mass[iA] : 0.f, imB = kB == 2 ? 1.f / m.fb_mass[iB] : 0.f;
         for (int k = 0; k < 3; k++) {
             v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
             int row = k == 0 ? n_nc + i : n_nc + ncp + 2 * i + (k - 1);
+            const int slot = rob ? slot0 + k : -1;
             float *w = row_rec(m, rows, row);
             float den = 0.f, rel = 0.f;
             float J[MAXD], MJ[MAXD];
@@ -1551,7 +1611,7 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
                 v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
                 den += dot(dir, ml) + dot(ja, ma);
                 rel += free_dot(L, iA, dir, ja);
-                put_free(w + 8, dir, ja, ml, ma);
+                put_free(L, iA, w + 8, dir, ja);
             } else put_free_zero(w + 8);
             v3 nd = scl(dir, -1.f);
             if (kB == 1) {
@@ -1560,27 +1620,28 @@ AVR_DI void build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, flo
                 minv_mul(L, Jb, Mb);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; J[d] += Jb[d]; MJ[d] += Mb[d]; }
-                put_free_zero(w + 20);
+                put_free_zero(w + 14);
             } else if (kB == 2) {
                 v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
                 den += dot(nd, ml) + dot(jb, mb);
                 rel += free_dot(L, iB, nd, jb);
-                put_free(w + 20, nd, jb, ml, mb);
-            } else put_free_zero(w + 20);
-            if (rob) put_robot(row_rob(m, rows, row), J, MJ);
+                put_free(L, iB, w + 14, nd, jb);
+            } else put_free_zero(w + 14);
+            if (rob) put_robot(row_rob(m, rows, slot), J, MJ);
             float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
             if (k == 0) {
                 float pen = c[AVR_CP_DIST];
                 float velerr = -rel, poserr = 0.f;
                 if (pen > 0.f) velerr -= pen / dt;
                 else poserr = -pen * erp / dt;
-                put_hdr(w, info, fric, inv, (poserr + velerr) * inv, 0.f, 1e10f, c[AVR_CP_IMP] * m.warmstart);
+                put_hdr(w, info, fric, inv, (poserr + velerr) * inv, 0.f, 1e10f, c[AVR_CP_IMP] * m.warmstart, slot);
             } else {
-                put_hdr(w, info, fric, inv, -rel * inv, 0.f, 0.f, 0.f);
+                put_hdr(w, info, fric, inv, -rel * inv, 0.f, 0.f, 0.f, slot);
             }
         }
     }
     if (lane == 0) L.n_c = ncp;
+    return nrob;
 }
 
 // ---------------------------------------------------------------------------- PGS solve
@@ -1614,185 +1675,237 @@ AVR_DI float robot_reduce(float x) {
     return rdl(x, 15);
 }
 
-// scalar-cache view of the row buffer (the rows are written by this wave's vector stores
-// before each solve; solve() invalidates the scalar cache after the stores have completed)
-typedef float f8 __attribute__((ext_vector_type(8)));
-typedef float f16v __attribute__((ext_vector_type(16)));
-typedef const __attribute__((address_space(4))) f8 *cf8p;
-typedef const __attribute__((address_space(4))) f16v *cf16p;
+// Part B keeps the row set in LDS: the wave copies its records (and robot parts) in with
+// many loads in flight, then every row of the Gauss-Seidel chain resolves from LDS reads issued
+// one row (parts) / two rows (headers) ahead.  An env whose row set exceeds the LDS capacity
+// (> B_CAPR rows or > B_CAPS robot parts, rare) runs the same solver on the global buffer.
+#define B_CAPR 192
+#define B_CAPS 32
+#define B_LDS_WORDS (B_CAPR * RWC + B_CAPS * ROBW + 16)
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) float lds_f;
+typedef __attribute__((address_space(3))) f2v lds_f2;
+typedef __attribute__((address_space(3))) f4v lds_f4;
 typedef const __attribute__((address_space(1))) float *gfp;
+typedef const __attribute__((address_space(1))) f4v *gf4p;
+typedef const __attribute__((address_space(1))) f2v *gf2p;
 
-struct RowS { f8 h; f16v a; f8 b; float jr, mr; };   // header, free A + B(J) , B(MJ), robot parts
+// row sources: rec(r) = record base, own part = 3 x f2v at word 8 (endpoint A) / 14 (B),
+// robot part = f2v (J, M^-1 J^T) of DoF `lane` at slot.  The zero block stands in for "not mine".
+struct LdsRows {
+    const lds_f *rec, *rob, *zero;
+    AVR_DI void hdr(int r, f4v &h0, f4v &h1) const { const lds_f4 *p = (const lds_f4 *)(rec + r * RWC); h0 = p[0]; h1 = p[1]; }
+    AVR_DI void own(int r, int off, f2v &a, f2v &b, f2v &c) const {
+        const lds_f *p = off >= 0 ? rec + r * RWC + off : zero;
+        a = *(const lds_f2 *)p; b = *(const lds_f2 *)(p + 2); c = *(const lds_f2 *)(p + 4);
+    }
+    AVR_DI f2v robot(int slot, bool mine) const { return *(const lds_f2 *)(mine ? rob + slot * ROBW + 2 * lane_id() : zero); }
+    // the two friction rows r, r + 1 of one contact: same endpoints, consecutive robot slots
+    AVR_DI void own2(int r, int off, f2v *a, f2v *b) const {
+        const lds_f *p = off >= 0 ? rec + r * RWC + off : zero;
+        const lds_f *q = off >= 0 ? p + RWC : zero;
+        a[0] = *(const lds_f2 *)p; a[1] = *(const lds_f2 *)(p + 2); a[2] = *(const lds_f2 *)(p + 4);
+        b[0] = *(const lds_f2 *)q; b[1] = *(const lds_f2 *)(q + 2); b[2] = *(const lds_f2 *)(q + 4);
+    }
+    AVR_DI void robot2(int slot, bool mine, f2v &a, f2v &b) const {
+        const lds_f *p = mine ? rob + slot * ROBW + 2 * lane_id() : zero;
+        const lds_f *q = mine ? p + ROBW : zero;
+        a = *(const lds_f2 *)p; b = *(const lds_f2 *)q;
+    }
+};
+struct GlbRows {
+    const float *rec, *rob;
+    AVR_DI void hdr(int r, f4v &h0, f4v &h1) const { const gf4p p = (gf4p)(rec + r * RWC); h0 = p[0]; h1 = p[1]; }
+    AVR_DI void own(int r, int off, f2v &a, f2v &b, f2v &c) const {
+        const gf2p p = (gf2p)(rec + r * RWC + (off >= 0 ? off : 0));
+        const f2v z = {0.f, 0.f}, x = p[0], y = p[1], w = p[2];
+        a = off >= 0 ? x : z; b = off >= 0 ? y : z; c = off >= 0 ? w : z;
+    }
+    AVR_DI f2v robot(int slot, bool mine) const {
+        const f2v z = {0.f, 0.f}, x = ((gf2p)(rob + (slot > 0 ? slot : 0) * ROBW))[lane_id() & 15];
+        return mine ? x : z;
+    }
+    AVR_DI void own2(int r, int off, f2v *a, f2v *b) const { own(r, off, a[0], a[1], a[2]); own(r + 1, off, b[0], b[1], b[2]); }
+    AVR_DI void robot2(int slot, bool mine, f2v &a, f2v &b) const { a = robot(slot, mine); b = robot(slot + 1, mine); }
+};
 
-// A row's loads go out together: the record through the scalar cache and, speculatively, the
-// articulated part as two vector loads (lane & 15 keeps every lane in bounds).  Whether the row
-// has an articulated part is only known from its header, so the part is selected afterwards
-// (rows without one hold stale words there; a select, never arithmetic, discards them).
-#ifdef AVR_ROW_VLOAD
-// experiment: the record as wave-uniform vector loads (TA/L1 path) instead of the scalar cache
-typedef const __attribute__((address_space(1))) f8 *gf8p;
-typedef const __attribute__((address_space(1))) f16v *gf16p;
-#endif
-AVR_DI void issue_row(RowS &R, float &j, float &mj, const float *rec, const float *rob) {
-    const int l = lane_id() & 15;
-    j = ((gfp)rob)[l];
-    mj = ((gfp)rob)[16 + l];
-#ifdef AVR_ROW_VLOAD
-    R.h = *(gf8p)(rec);
-    R.a = *(gf16p)(rec + 8);
-    R.b = *(gf8p)(rec + 24);
-#else
-    R.h = *(cf8p)(rec);
-    R.a = *(cf16p)(rec + 8);
-    R.b = *(cf8p)(rec + 24);
-#endif
-}
-AVR_DI int row_info(const RowS &R) { return uni(__float_as_int(R.h[0])); }
-AVR_DI bool row_robot(const RowS &R) { return (row_info(R) & RI_ROBOT) != 0; }
-AVR_DI void finish_row(RowS &R, float j, float mj, bool robot) {
-    const bool own = robot && lane_id() < MAXD;
-    R.jr = own ? j : 0.f;
-    R.mr = own ? mj : 0.f;
-}
-// keep the scalar loads of a row pair ahead of the first row's arithmetic (the compiler would
-// otherwise sink the second row's loads below it: two round trips instead of one)
-#ifdef AVR_ROW_VLOAD
-#define ROW_PIN(R) (void)0
-#else
-#define ROW_PIN(R) asm volatile("" ::"s"(R.h), "s"(R.a), "s"(R.b))
-#endif
+// one row as this lane sees it: header (wave-uniform), its own free part (zero unless the lane
+// owns endpoint A or B), its own robot DoF's (J, M^-1 J^T)
+struct RowV { f4v h0, h1; f2v j0, j1, j2, r; };
 
-AVR_DI void load_row(RowS &R, const float *rec, const float *rob, bool robot) {
-    float j, mj;
-    issue_row(R, j, mj, rec, rob);
-    finish_row(R, j, mj, robot);
-}
-
-// one row: returns the clamped impulse increment and applies it
-AVR_DI float row_go(const RowS &R, DV &d, float imp, float lo, float hi, bool robot) {
+template <class SRC>
+AVR_DI void row_parts(const SRC &S, int r, RowV &R) {
     const int lane = lane_id();
-    const int info = row_info(R);
-    const int iA = info & 63, iB = (info >> 6) & 63;
-    // A: J = a[0..5], MJ = a[6..11]; B: J = a[12..15] b[0..1], MJ = b[2..7]
-    float pA = R.a[0] * d.vx + R.a[1] * d.vy + R.a[2] * d.vz + R.a[3] * d.wx + R.a[4] * d.wy + R.a[5] * d.wz;
-    float pB = R.a[12] * d.vx + R.a[13] * d.vy + R.a[14] * d.vz + R.a[15] * d.wx + R.b[0] * d.wy + R.b[1] * d.wz;
-    // (measured: reading the two owner lanes with v_readlane for rows without an articulated
-    // part is slower than this branch-free 16-lane DPP reduction)
-    float p = (lane == iA ? pA : 0.f) + (lane == iB ? pB : 0.f);
-    if (robot) p += R.jr * d.rq;
-    float dv = robot_reduce(p);
-    float inv = R.h[2], rhs = R.h[3];
-    float sum = imp + (rhs - dv * inv);
-    float ni = fminf(fmaxf(sum, lo), hi);
-    float delta = ni - imp;
-    float cA = lane == iA ? delta : 0.f, cB = lane == iB ? delta : 0.f;
-    d.vx += R.a[6] * cA + R.b[2] * cB;
-    d.vy += R.a[7] * cA + R.b[3] * cB;
-    d.vz += R.a[8] * cA + R.b[4] * cB;
-    d.wx += R.a[9] * cA + R.b[5] * cB;
-    d.wy += R.a[10] * cA + R.b[6] * cB;
-    d.wz += R.a[11] * cA + R.b[7] * cB;
-    if (robot) d.rq += R.mr * delta;
+    const int info = __builtin_amdgcn_readfirstlane(__float_as_int(R.h0.x));
+    const int slot = __builtin_amdgcn_readfirstlane(__float_as_int(R.h1.w));
+    const int off = lane == (info & 63) ? 8 : (lane == ((info >> 6) & 63) ? 14 : -1);
+    S.own(r, off, R.j0, R.j1, R.j2);
+    R.r = S.robot(slot, slot >= 0 && lane < 16);
+}
+
+// Free-body velocity increments are kept mass-normalised on the owner lane (see put_free):
+// J.dv = g.(v~, w~), and the update is (v~, w~) += g delta.
+
+// one row: returns the clamped impulse and applies the increment
+AVR_DI float row_go(const RowV &R, DV &d, float imp, float lo, float hi) {
+    float p = R.j0.x * d.vx + R.j0.y * d.vy + R.j1.x * d.vz;
+    float q = R.j1.y * d.wx + R.j2.x * d.wy + R.j2.y * d.wz;
+    p += q + R.r.x * d.rq;
+    const float dv = robot_reduce(p);
+    const float ni = __builtin_amdgcn_fmed3f(imp + (R.h0.w - dv * R.h0.z), lo, hi);
+    const float delta = ni - imp;
+    d.vx += R.j0.x * delta; d.vy += R.j0.y * delta; d.vz += R.j1.x * delta;
+    d.wx += R.j1.y * delta; d.wy += R.j2.x * delta; d.wz += R.j2.y * delta;
+    d.rq += R.r.y * delta;
     return ni;
+}
+
+template <class SRC>
+AVR_DI void row_fetch(const SRC &S, int r, RowV &R) { S.hdr(r, R.h0, R.h1); row_parts(S, r, R); }
+
+// the parts of a contact's two friction rows (headers in A.h*, B.h*), addressed once
+template <class SRC>
+AVR_DI void pair_parts(const SRC &S, int r, RowV &A, RowV &B) {
+    const int lane = lane_id();
+    const int info = __builtin_amdgcn_readfirstlane(__float_as_int(A.h0.x));
+    const int slot = __builtin_amdgcn_readfirstlane(__float_as_int(A.h1.w));
+    const int off = lane == (info & 63) ? 8 : (lane == ((info >> 6) & 63) ? 14 : -1);
+    f2v a[3], b[3];
+    S.own2(r, off, a, b);
+    A.j0 = a[0]; A.j1 = a[1]; A.j2 = a[2];
+    B.j0 = b[0]; B.j1 = b[1]; B.j2 = b[2];
+    S.robot2(slot, slot >= 0 && lane < 16, A.r, B.r);
+}
+
+// friction sweep over n active contacts, unit u = rows r(u), r(u) + 1: headers two units ahead,
+// parts one unit ahead (three rotating unit buffers)
+template <class SRC, class IDX, class GO>
+AVR_DI void sweep_pairs(const SRC &S, int n, const IDX &idx, const GO &go) {
+    if (n <= 0) return;
+    RowV A0, A1, B0, B1, C0, C1;
+#define AVR_PHDR(u, X0, X1) do { const int _r = idx(u); S.hdr(_r, X0.h0, X0.h1); S.hdr(_r + 1, X1.h0, X1.h1); } while (0)
+    AVR_PHDR(0, A0, A1);
+    if (n > 1) AVR_PHDR(1, B0, B1);
+    pair_parts(S, idx(0), A0, A1);
+    for (int u = 0;;) {
+        if (u + 2 < n) AVR_PHDR(u + 2, C0, C1);
+        if (u + 1 < n) pair_parts(S, idx(u + 1), B0, B1);
+        go(u, A0, A1);
+        if (++u >= n) break;
+        if (u + 2 < n) AVR_PHDR(u + 2, A0, A1);
+        if (u + 1 < n) pair_parts(S, idx(u + 1), C0, C1);
+        go(u, B0, B1);
+        if (++u >= n) break;
+        if (u + 2 < n) AVR_PHDR(u + 2, B0, B1);
+        if (u + 1 < n) pair_parts(S, idx(u + 1), A0, A1);
+        go(u, C0, C1);
+        if (++u >= n) break;
+    }
+#undef AVR_PHDR
+}
+
+// A sweep over n rows idx(0..n-1) resolved by go(j, row): headers are fetched two rows ahead,
+// the header-dependent parts one row ahead, through three rotating buffers (no register copies).
+template <class SRC, class IDX, class GO>
+AVR_DI void sweep(const SRC &S, int n, const IDX &idx, const GO &go) {
+    if (n <= 0) return;
+    RowV A, B, C;
+    S.hdr(idx(0), A.h0, A.h1);
+    if (n > 1) S.hdr(idx(1), B.h0, B.h1);
+    row_parts(S, idx(0), A);
+    for (int j = 0;;) {
+        if (j + 2 < n) S.hdr(idx(j + 2), C.h0, C.h1);
+        if (j + 1 < n) row_parts(S, idx(j + 1), B);
+        go(j, A);
+        if (++j >= n) break;
+        if (j + 2 < n) S.hdr(idx(j + 2), A.h0, A.h1);
+        if (j + 1 < n) row_parts(S, idx(j + 1), C);
+        go(j, B);
+        if (++j >= n) break;
+        if (j + 2 < n) S.hdr(idx(j + 2), B.h0, B.h1);
+        if (j + 1 < n) row_parts(S, idx(j + 1), A);
+        go(j, C);
+        if (++j >= n) break;
+    }
 }
 
 // Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order):
 // non-contact rows (sweep direction alternates per iteration), normal rows, friction rows.
 // Impulses are lane-distributed registers: nc row j -> lane j of inc; normal c -> lane c&63 of
-// in0/in1; friction row f -> lane f&63 of if0/if1/if2.  Returns the delta velocities in d and
-// the normal impulses in in0/in1 (contact c at lane c&63).
-AVR_DI void pgs_solve(const KModel &m, const float *rows, int n_nc, int n_c, DV &d, float &in0, float &in1) {
+// in0 (c < 64) / in1; friction row 2c+k -> lane c&63 of fk0 / fk1.  Returns the delta velocities
+// in d and the normal impulses in in0/in1.  `list` (LDS, 96 ints) holds the active contacts.
+template <class SRC>
+AVR_DI void pgs_solve(const KModel &m, const SRC &S, int *list, int n_nc, int n_c, DV &d, float &in0, float &in1) {
     const int lane = lane_id();
-    // Row records were written by the previous kernel (substep_a) with vector stores, and the
-    // scalar cache can still hold this env's rows from the previous sub-step: the launch-time
-    // acquire does NOT reliably clear it (measured: without this invalidate, 7 % of 4096 envs
-    // read stale rows).  Invalidate it and wait for the invalidation (an SMEM op itself)
-    // before the first row s_load.
-    asm volatile("s_dcache_inv\n\ts_waitcnt lgkmcnt(0)" : "+s"(rows) :: "memory");
-    const float *robs = rows + m.rowcap * RW;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
-    float inc = 0.f, if0 = 0.f, if1 = 0.f, if2 = 0.f;
-    in0 = 0.f; in1 = 0.f;
+    float inc = 0.f, f00 = 0.f, f01 = 0.f, f10 = 0.f, f11 = 0.f;
     // warm start (normal rows, contact order): impulse = cached * warmstart factor
-    for (int c = 0; c < n_c; c++) {
-        const float *rec = rows + (n_nc + c) * RW;
-        const f8 h = *(cf8p)rec;
-        const float imp0 = h[6];
-        if (lane == (c & 63)) { if (c < 64) in0 = imp0; else in1 = imp0; }
-        if (imp0 == 0.f) continue;
-        const bool robot = (__float_as_int(h[0]) & RI_ROBOT) != 0;
-        RowS R;
-        load_row(R, rec, robs + (n_nc + c) * RW, robot);
-        (void)row_go(R, d, 0.f, imp0, imp0, robot);     // delta = imp0
+    {
+        f4v h0, h1;
+        float w0 = 0.f, w1 = 0.f;
+        if (lane < n_c) { S.hdr(n_nc + lane, h0, h1); w0 = h1.z; }
+        if (lane + 64 < n_c) { S.hdr(n_nc + 64 + lane, h0, h1); w1 = h1.z; }
+        in0 = w0; in1 = w1;
+        unsigned long long m0 = __ballot(w0 != 0.f), m1 = __ballot(w1 != 0.f);
+        while (m0 | m1) {
+            const int c = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
+            if (c < 64) m0 &= m0 - 1; else m1 &= m1 - 1;
+            RowV R;
+            row_fetch(S, n_nc + c, R);
+            const float imp0 = R.h1.z;
+            (void)row_go(R, d, 0.f, imp0, imp0);     // delta = imp0
+        }
     }
+    const int nc0 = n_c < 64 ? n_c : 64;
     for (int it = 0; it < m.iters; it++) {
-        // two consecutive rows of the sweep per scalar round trip
-        for (int j = 0; j < n_nc; j += 2) {
-            const int k0 = (it & 1) ? j : n_nc - 1 - j;
-            const bool two = j + 1 < n_nc;
-            const int k1 = two ? ((it & 1) ? j + 1 : n_nc - 2 - j) : k0;
-            RowS R0, R1;
-            float j0, m0, j1, m1;
-            issue_row(R0, j0, m0, rows + k0 * RW, robs + k0 * RW);
-            issue_row(R1, j1, m1, rows + k1 * RW, robs + k1 * RW);
-            ROW_PIN(R0);
-            ROW_PIN(R1);
-            finish_row(R0, j0, m0, true);
-            float ni = row_go(R0, d, rdl(inc, k0), R0.h[4], R0.h[5], true);
-            if (lane == k0) inc = ni;
-            if (two) {
-                finish_row(R1, j1, m1, true);
-                ni = row_go(R1, d, rdl(inc, k1), R1.h[4], R1.h[5], true);
-                if (lane == k1) inc = ni;
-            }
+        const bool fwd = (it & 1) != 0;
+        sweep(S, n_nc, [&](int j) { return fwd ? j : n_nc - 1 - j; }, [&](int j, const RowV &R) {
+            const int k = fwd ? j : n_nc - 1 - j;
+            const float ni = row_go(R, d, rdl(inc, k), R.h1.x, R.h1.y);
+            inc = lane == k ? ni : inc;
+        });
+        sweep(S, nc0, [&](int j) { return n_nc + j; }, [&](int j, const RowV &R) {
+            const float ni = row_go(R, d, rdl(in0, j), 0.f, 1e10f);
+            in0 = lane == j ? ni : in0;
+        });
+        sweep(S, n_c - nc0, [&](int j) { return n_nc + 64 + j; }, [&](int j, const RowV &R) {
+            const float ni = row_go(R, d, rdl(in1, j), 0.f, 1e10f);
+            in1 = lane == j ? ni : in1;
+        });
+        // friction rows (two per contact) of the contacts with a positive normal impulse, in
+        // contact order: the active list goes through LDS (lane p reads the p-th active contact)
+        const bool a0 = lane < n_c && in0 > 0.f, a1 = lane + 64 < n_c && in1 > 0.f;
+        int t0, t1;
+        const int p0 = ballot_prefix(a0, &t0), p1 = ballot_prefix(a1, &t1);
+        if (t0 + t1 == 0) continue;
+        __builtin_amdgcn_s_barrier();
+        if (a0) list[p0] = lane;
+        if (a1) list[t0 + p1] = lane + 64;
+        __builtin_amdgcn_s_waitcnt(0xc07f);     // lgkmcnt(0): the list is written
+        const int lv0 = list[lane < t0 + t1 ? lane : 0], lv1 = list[lane + 64 < t0 + t1 ? lane + 64 : 0];
+        const int fr0 = n_nc + n_c;
+        // contacts < 64 (impulses in lane c of f00 / f10), then >= 64 (f01 / f11); ascending list
+        sweep_pairs(S, t0, [&](int u) { return fr0 + 2 * __builtin_amdgcn_readlane(lv0, u); }, [&](int u, const RowV &R0, const RowV &R1) {
+            const int c = __builtin_amdgcn_readlane(lv0, u);
+            const float lim = R0.h0.y * rdl(in0, c);
+            float ni = row_go(R0, d, rdl(f00, c), -lim, lim);
+            f00 = lane == c ? ni : f00;
+            ni = row_go(R1, d, rdl(f10, c), -lim, lim);
+            f10 = lane == c ? ni : f10;
+        });
+        if (t1 > 0) {
+            auto cidx = [&](int u) { const int p = u + t0; return p < 64 ? __builtin_amdgcn_readlane(lv0, p) : __builtin_amdgcn_readlane(lv1, p - 64); };
+            sweep_pairs(S, t1, [&](int u) { return fr0 + 2 * cidx(u); }, [&](int u, const RowV &R0, const RowV &R1) {
+                const int c = cidx(u) - 64;
+                const float lim = R0.h0.y * rdl(in1, c);
+                float ni = row_go(R0, d, rdl(f01, c), -lim, lim);
+                f01 = lane == c ? ni : f01;
+                ni = row_go(R1, d, rdl(f11, c), -lim, lim);
+                f11 = lane == c ? ni : f11;
+            });
         }
-        // rows are fetched two at a time (one scalar round trip for consecutive records)
-        for (int c = 0; c < n_c; c += 2) {
-            const float *rec = rows + (n_nc + c) * RW;
-            RowS R0, R1;
-            const bool two = c + 1 < n_c;
-            float j0, m0, j1, m1;
-            issue_row(R0, j0, m0, rec, robs + (n_nc + c) * RW);
-            issue_row(R1, j1, m1, rec + RW, robs + (n_nc + c + 1) * RW);
-            ROW_PIN(R0);
-            ROW_PIN(R1);
-            const bool rb0 = row_robot(R0);
-            finish_row(R0, j0, m0, rb0);
-            float ni = row_go(R0, d, rdl(c < 64 ? in0 : in1, c & 63), 0.f, 1e10f, rb0);
-            if (lane == (c & 63)) { if (c < 64) in0 = ni; else in1 = ni; }
-            if (two) {
-                const int c1 = c + 1;
-                const bool rb1 = row_robot(R1);
-                finish_row(R1, j1, m1, rb1);
-                ni = row_go(R1, d, rdl(c1 < 64 ? in0 : in1, c1 & 63), 0.f, 1e10f, rb1);
-                if (lane == (c1 & 63)) { if (c1 < 64) in0 = ni; else in1 = ni; }
-            }
-        }
-        for (int c = 0; c < n_c; c++) {
-            const float nimp = rdl(c < 64 ? in0 : in1, c & 63);
-            if (!(nimp > 0.f)) continue;
-            // the contact's two friction rows are adjacent records
-            const int f = 2 * c;
-            const float *rec = rows + (n_nc + n_c + f) * RW;
-            RowS R0, R1;
-            float j0, m0, j1, m1;
-            const float *q0 = robs + (n_nc + n_c + f) * RW;
-            issue_row(R0, j0, m0, rec, q0);
-            issue_row(R1, j1, m1, rec + RW, q0 + RW);
-            ROW_PIN(R0);
-            ROW_PIN(R1);
-            const bool robot = row_robot(R0);    // same endpoints for both
-            finish_row(R0, j0, m0, robot);
-            finish_row(R1, j1, m1, robot);
-            const float fr = R0.h[1];
-            const int s = f >> 6;           // f and f + 1 share the impulse register (f even)
-            float fimp = s == 0 ? if0 : (s == 1 ? if1 : if2);
-            float ni = row_go(R0, d, rdl(fimp, f & 63), -fr * nimp, fr * nimp, robot);
-            if (lane == (f & 63)) fimp = ni;
-            ni = row_go(R1, d, rdl(fimp, (f + 1) & 63), -fr * nimp, fr * nimp, robot);
-            if (lane == ((f + 1) & 63)) fimp = ni;
-            if (s == 0) if0 = fimp; else if (s == 1) if1 = fimp; else if2 = fimp;
-        }
+        __builtin_amdgcn_s_barrier();
     }
 }
 
@@ -1841,16 +1954,18 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
         float inv[3] = {I.x > 0.f ? 1.f / I.x : 0.f, I.y > 0.f ? 1.f / I.y : 0.f, I.z > 0.f ? 1.f / I.z : 0.f};
         for (int a = 0; a < 3; a++)
             for (int b = 0; b < 3; b++) L.Iinv[f][3 * a + b] = R.m[a][0] * inv[0] * R.m[b][0] + R.m[a][1] * inv[1] * R.m[b][1] + R.m[a][2] * inv[2] * R.m[b][2];
+        L.gsc[f][0] = 1.f / sqrtf(mass);
+        L.gsc[f][1] = sqrtf(inv[0]); L.gsc[f][2] = sqrtf(inv[1]); L.gsc[f][3] = sqrtf(inv[2]);
     }
     SYNC();
     PROF_STOP(6, ps);
     const int n_nc = build_noncontact_rows(m, L, rows, dt);
     PROF_STOP(7, ps);
-    build_contact_rows(m, L, gst + AVR_S_CP, rows, n_nc, dt);
+    const int n_rob = build_contact_rows(m, L, gst + AVR_S_CP, rows, n_nc, dt);
     SYNC();
     PROF_STOP(8, ps);
     // hand-over to part B
-    if (lane == 0) { ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); }
+    if (lane == 0) { ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); ws[WS_NROB] = __int_as_float(n_rob); }
     if (lane < MAXD) ws[WS_VQ + lane] = lane < L.nda ? L.vq[lane] : 0.f;
     if (lane < m.nf) {
         st3(ws + WS_FV + 4 * lane, ld3(L.fv[lane]));
@@ -2029,11 +2144,29 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     ws[WS_ASQ] = asq;
 }
 
+// Diagnostic wave timeline (-DAVR_WAVETIME builds only): global 100 MHz stamps at the start and
+// end of every wave of the last A / B launch, [2][n_envs][2] u64 in m.prof (tools/wavetime.py).
+#ifdef AVR_WAVETIME
+#define WT_START() const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime()
+#define WT_END(k)                                                                                   \
+    do {                                                                                            \
+        const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();                            \
+        if (m.prof && lane_id() == 0) {                                                             \
+            m.prof[((size_t)(k) * n_envs + env) * 2] = wt0;                                         \
+            m.prof[((size_t)(k) * n_envs + env) * 2 + 1] = wt1;                                     \
+        }                                                                                           \
+    } while (0)
+#else
+#define WT_START() (void)0
+#define WT_END(k) (void)0
+#endif
+
 // Sub-step part A: one 64-lane block per env, state staged in LDS.
 __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                                      const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
+    WT_START();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     load_state(m, L, gst);
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env));
@@ -2048,6 +2181,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     // written to global memory by collide)
     if (lane_id() < 16) gst[AVR_S_TASK + lane_id()] = L.st[AVR_S_TASK + lane_id()];
     prof_flush(m, L, env);
+    WT_END(0);
 }
 
 // Sub-step part B: PGS over the row buffer, then semi-implicit Euler (A.1) with the
@@ -2057,6 +2191,7 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
                                                            const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
                                                            int n_envs) {
     AVR_ENV_GUARD();
+    WT_START();
     const int lane = lane_id();
 #ifdef AVR_PROF
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -2064,9 +2199,69 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
     const float *ws = env_ws(m, env);
     float *st = state + (size_t)env * AVR_STATE_WORDS;
     const int n_nc = uni(__float_as_int(ws[WS_NNC])), n_c = uni(__float_as_int(ws[WS_NC]));
+    const int n_rob = uni(__float_as_int(ws[WS_NROB]));
+    // stage the row set in LDS (8 loads in flight per lane) unless it exceeds the capacity
+    __shared__ f4v bl4[B_LDS_WORDS / 4];
+    __shared__ int list[AVR_MAX_CONTACTS];
+    lds_f *bl = (lds_f *)(lds_f4 *)bl4;
+    const float *rows = env_rows(m, env);
+    const int n_rows = n_nc + 3 * n_c;
+    const bool in_lds = n_rows <= B_CAPR && n_rob <= B_CAPS;
     DV d;
     float in0, in1;
-    pgs_solve(m, env_rows(m, env), n_nc, n_c, d, in0, in1);
+    if (in_lds) {
+        const int n4r = n_rows * (RWC / 4), n4s = n_rob * (ROBW / 4);
+        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
+        lds_f4 *l0 = (lds_f4 *)bl, *l1 = (lds_f4 *)(bl + B_CAPR * RWC);
+        for (int base = 0; base < n4r; base += 8 * 64) {
+            f4v t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = base + 64 * q + lane;
+                t[q] = g0[i < n4r ? i : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = base + 64 * q + lane;
+                if (i < n4r) l0[i] = t[q];
+            }
+        }
+        for (int base = 0; base < n4s; base += 4 * 64) {
+            f4v t[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = base + 64 * q + lane;
+                t[q] = g1[i < n4s ? i : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = base + 64 * q + lane;
+                if (i < n4s) l1[i] = t[q];
+            }
+        }
+        if (lane < 16) bl[B_CAPR * RWC + B_CAPS * ROBW + lane] = 0.f;
+        __syncthreads();
+        LdsRows S;
+        S.rec = bl;
+        S.rob = bl + B_CAPR * RWC;
+        S.zero = bl + B_CAPR * RWC + B_CAPS * ROBW;
+        pgs_solve(m, S, list, n_nc, n_c, d, in0, in1);
+    } else {
+        GlbRows S;
+        S.rec = rows;
+        S.rob = rows + m.rowcap * RWC;
+        pgs_solve(m, S, list, n_nc, n_c, d, in0, in1);
+    }
+    // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
+    if (lane < m.nf) {
+        const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * lane + 3);
+        const v3 I = ld3(m.fb_inertia + 4 * lane);
+        const float rs = 1.f / sqrtf(m.fb_mass[lane]);
+        const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
+        const v3 w = qrot(q, V(d.wx * sd.x, d.wy * sd.y, d.wz * sd.z));
+        d.vx *= rs; d.vy *= rs; d.vz *= rs;
+        d.wx = w.x; d.wy = w.y; d.wz = w.z;
+    }
 #ifdef AVR_PROF
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2111,6 +2306,7 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
         m.prof[(size_t)env * AVR_PROF_SLOTS + 5] += __float_as_int(ws[WS_XCC]) != xcc_id() ? 1 : 0;   // A/B on different XCDs
     }
 #endif
+    WT_END(1);
 }
 
 // Task glue after the frames: update_targets (feeding.py:345-349), iteration count,

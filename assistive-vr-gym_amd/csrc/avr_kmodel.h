@@ -13,7 +13,7 @@
 #define MAXAP 256
 #define MAXNC 32
 #ifndef SMALL_NV
-#define SMALL_NV 64     // hulls with more vertices take the wave-cooperative narrowphase
+#define SMALL_NV 64     // hulls with more vertices and no support table take the wave-cooperative narrowphase
 #endif
 #define GJK_MAX_IT 64
 #define GJK_REL_EPS 1e-6f
@@ -49,6 +49,9 @@ struct KModel {
     const int *shape_kind, *shape_body, *shape_gender, *shape_hull;   // hull [ns][4]
     const float *shape_pose, *shape_param, *shape_margin, *shape_aabb; // [ns][8] [ns][4] [ns] [ns][8]
     const float4 *hull_verts;
+    const int *shape_tab;       // [ns] first support-table cell of a large hull, -1 without a table
+    const int2 *tab_cell;       // [cells] (offset, count) into tab_vert (avr_hulltab.cpp)
+    const float4 *tab_vert;     // candidate vertices (x, y, z, vertex index as int bits), ascending per cell
     const int *shape_cidx;      // [ns] index into the per-sub-step child AABB cache, -1 for static shapes
     const float *static_saabb;  // [ns][8] world AABB (min3, pad, max3, pad) of static shapes (host-computed)
     const int *pair_a, *pair_b;

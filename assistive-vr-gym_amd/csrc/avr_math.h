@@ -80,6 +80,7 @@ AVR_DI float wave_sum(float x) {
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
     return x;
 }
+AVR_DI float rdl_f(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
 // argmax with lowest-index tie break; returns winning index in all lanes
 AVR_DI int wave_argmax(float v, int idx) {
     for (int o = 32; o > 0; o >>= 1) {

@@ -103,6 +103,16 @@ int avr_kernel_times(avr_sim *sim, double *ms4, int64_t *count4);
  * [n_envs][16] uint64 cycle counters.  A no-op for the shipped kernel. */
 int avr_set_profile_buffer(avr_sim *sim, void *d_prof);
 
+/* Support-mapping table of one convex hull (host-only utility; avr_create builds one for every
+ * hull with more than AVR_TAB_MIN_NV vertices).  Cube map of 6*G*G direction cells; cell c lists,
+ * in ascending vertex order, every vertex that can be the support point (first strictly largest
+ * projection, as Bullet's btConvexHullShape scan) for some direction of the cell:
+ * cell[2c] = offset into idx, cell[2c+1] = count.  idx receives at most cap entries.  Returns the
+ * total entry count (allocate that many and call again), or -1 on bad arguments.  Replaces the
+ * per-query full vertex scan behind btConvexHullShape::localGetSupportingVertexWithoutMargin
+ * (reached from p.stepSimulation, env.py:342) with an exact sub-linear lookup. */
+int32_t avr_hull_support_table(const float *verts, int32_t nv, int32_t G, int32_t *cell, int32_t *idx, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

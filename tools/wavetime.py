@@ -1,0 +1,38 @@
+"""Diagnostic: wave timeline of the last sub-step kernels A and B (AVR_WAVETIME build,
+libavr_wt.so): per-wave durations (p50/p90/p99/max), kernel span, and how the span splits into
+'all waves busy' vs the tail.  python tools/wavetime.py [n_envs] [lib]"""
+import ctypes as C, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd')); sys.path.insert(0, ROOT)
+from avr import _abi as ABI, reset as RS, _lib
+so = os.path.join(ROOT, 'assistive-vr-gym_amd', 'avr', sys.argv[2] if len(sys.argv) > 2 else 'libavr_wt.so')
+_lib.LIB_PATH = so
+lib = _lib.load(so)
+lib.avr_set_profile_buffer.argtypes = [C.c_void_p, C.c_void_p]
+import torch
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+A = ABI.load_scene(); md = ABI.ModelDesc(A)
+S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
+S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
+sim = _lib.Sim(md, N)
+buf = torch.zeros(2 * N * 2, dtype=torch.int64, device='cuda')
+lib.avr_set_profile_buffer(sim.h, buf.data_ptr())
+sim.set_state(S.astype(np.float32)); sim.settle(20)
+for t in range(3):
+    sim.step(_lib.random_actions(1001, np.arange(N), t))
+    p = buf.cpu().numpy().reshape(2, N, 2).astype(np.float64) * 10.0   # 100 MHz ticks -> ns
+    for k, nm in enumerate(('A', 'B')):
+        s0, s1 = p[k, :, 0], p[k, :, 1]
+        d = (s1 - s0) / 1e3
+        span = (s1.max() - s0.min()) / 1e3
+        t0 = s0.min()
+        last_start = (s0.max() - t0) / 1e3
+        order = np.argsort(-d)
+        print('step %d kernel %s: span %.1f us, wave us p50 %.1f p90 %.1f p99 %.1f max %.1f mean %.1f, last wave starts at %.1f us; slowest envs %s'
+              % (t, nm, span, np.percentile(d, 50), np.percentile(d, 90), np.percentile(d, 99), d.max(), d.mean(), last_start,
+                 order[:6].tolist()))
+    St = sim.get_state()
+ncp = St[:, ABI.S_TASK + ABI.T_NCP]
+print('ncp of slowest A envs', ncp[order[:6]], 'mean ncp', ncp.mean())
+np.save(os.path.join(ROOT, 'gpurun_out', 'wavetime.npy'), p)
