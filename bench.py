@@ -101,6 +101,8 @@ def main():
     base_id, _ = D.shard(E, rank)
     S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)], impairment=args.impairment)
     n_tremor = sum(m['impairment'] == 'tremor' for m in meta)
+    import hashlib
+    pool_sha = hashlib.sha1(S_pool.astype(np.float32).tobytes()).hexdigest()[:12]
     S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
     sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
     sim.set_state(S.astype(np.float32))
@@ -197,6 +199,9 @@ def main():
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
                      'dominant_kernel': dominant, 'kernels': kernels},
         'nan_or_overflow_envs': int(np.count_nonzero(flags)),
+        'flagged_envs_by_bit': {name: int(np.count_nonzero(flags & (1 << b))) for b, name in enumerate(
+            ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full'))},
+        'reset_pool_sha1': pool_sha,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
