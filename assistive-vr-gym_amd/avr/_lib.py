@@ -22,6 +22,11 @@ EXPORTS = [
 ]
 
 
+# avr_config.flags bits (include/avr.h)
+CFG_B_FOUR_ENVS_PER_WAVE = 1  # part B as four envs per wavefront (default: one env per wavefront)
+CFG_B_GLOBAL_ROWS = 2         # diagnostic, four-env part B: rows read from global memory
+
+
 class avr_config(C.Structure):
     _fields_ = [('n_envs', C.c_int32), ('device', C.c_int32), ('env_offset', C.c_int32), ('flags', C.c_int32),
                 ('seed', C.c_uint64)]
@@ -82,11 +87,16 @@ def load(path=LIB_PATH):
 class Sim:
     """One libavr handle = one GPU, n_envs environments."""
 
-    def __init__(self, md, n_envs, device=0, seed=1001, env_offset=0):
+    def __init__(self, md, n_envs, device=0, seed=1001, env_offset=0, flags=0):
+        """flags: CFG_B_* bits (include/avr.h AVR_CFG_*); 0 = defaults (part B one env per wave)."""
         self.lib = load()
         self.md = md
         self.n = int(n_envs)
-        cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=0, seed=seed)
+        ev = os.environ.get('AVR_KERNEL_B', '')[:1]
+        b1 = ev == '1' or (ev != '4' and not flags & CFG_B_FOUR_ENVS_PER_WAVE)
+        self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel',
+                             'avr_substep_b_kernel' if b1 else 'avr_substep_b4_kernel', 'avr_task_kernel')
+        cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))
         self.h = h
@@ -170,7 +180,7 @@ class Sim:
     def stream(self):
         return self.lib.avr_stream(self.h)
 
-    KERNEL_KINDS = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b_kernel', 'avr_task_kernel')
+
 
     def profile_kernels(self, enable=True):
         self._chk(self.lib.avr_profile_kernels(self.h, int(bool(enable))))
@@ -180,7 +190,7 @@ class Sim:
         ms = np.zeros(4, np.float64)
         n = np.zeros(4, np.int64)
         self._chk(self.lib.avr_kernel_times(self.h, ms.ctypes.data, n.ctypes.data))
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_KINDS)}
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.kernel_kinds)}
 
     def kernel_info(self):
         out = np.zeros(8, np.int32)

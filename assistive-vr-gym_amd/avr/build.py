@@ -47,6 +47,13 @@ def build_prof(force=False):
     return build_lib(force=force, extra=('-DAVR_PROF',), out=os.path.join(HERE, 'libavr_prof.so'))
 
 
+def build_poison(force=False):
+    """Diagnostic build whose kernels NaN-fill their LDS blocks at entry (-DAVR_LDS_POISON): any
+    read of an LDS word the kernel did not write this launch changes its results
+    (tests/test_gpu_parity.py::test_lds_poison_build_is_bit_identical); never shipped."""
+    return build_lib(force=force, extra=('-DAVR_LDS_POISON',), out=os.path.join(HERE, 'libavr_poison.so'))
+
+
 def build_wavetime(force=False):
     """Diagnostic build with per-wave start/end stamps (tools/wavetime.py); never shipped."""
     return build_lib(force=force, extra=('-DAVR_WAVETIME',), out=os.path.join(HERE, 'libavr_wt.so'))
@@ -58,6 +65,7 @@ def build_oracle():
 
 def build_all(force=False):
     build_lib(force=force)
+    build_poison(force=force)
     build_oracle()
 
 

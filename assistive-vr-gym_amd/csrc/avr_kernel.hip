@@ -1687,6 +1687,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) float lds_f;
 typedef __attribute__((address_space(3))) f2v lds_f2;
 typedef __attribute__((address_space(3))) f4v lds_f4;
+typedef __attribute__((address_space(3))) int lds_i;
 typedef const __attribute__((address_space(1))) float *gfp;
 typedef const __attribute__((address_space(1))) f4v *gf4p;
 typedef const __attribute__((address_space(1))) f2v *gf2p;
@@ -1930,9 +1931,12 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     }
     SYNC();
     const float vmax = m.max_vel;
-    if (lane < L.nda) {
-        float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
-        L.vq[lane] = clampf(v, -vmax, vmax);
+    // every DoF slot is written: the row builders sum J[d] * vq[d] over all MAXD slots, and a
+    // slot left over from another kernel's LDS (NaN bit patterns included) would turn those
+    // zero-Jacobian terms into NaN (0 * NaN) -- inactive slots (d >= nda) hold 0
+    if (lane < MAXD) {
+        const float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
+        L.vq[lane] = lane < L.nda ? clampf(v, -vmax, vmax) : 0.f;
     }
     const float k1l = m.lin_damp, k1a = m.ang_damp;
     if (lane < m.nf) {
@@ -2081,6 +2085,11 @@ AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && g
 
 AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
     const int lane = lane_id();
+#ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the env's LDS block so that a read of a word this
+                        // kernel did not write shows up (tools/gpu_poison.sh)
+    for (int i = lane; i < (int)(sizeof(EnvLDS) / 4); i += 64) ((float *)&L)[i] = __int_as_float(-1);
+    SYNC();
+#endif
     for (int i = lane; i < AVR_S_CP; i += 64) L.st[i] = gst[i];
     if (lane == 0) {
         L.flags = 0;
@@ -2108,7 +2117,9 @@ AVR_DI void prof_flush(const KModel &m, EnvLDS &L, int env) {
 // One thread per env.
 __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
                                                            const unsigned char *__restrict__ mask, int mode, long long t, int env0, int n_envs) {
-    const int env = env0 + blockIdx.x * blockDim.x + threadIdx.x;
+    // XCD-consistent: lane l of block b takes env e - env0 = 512 (b / 8) + (b % 8) + 8 l, which
+    // part A runs on the same XCD (see avr_substep_b4_kernel)
+    const int env = env0 + 512 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
     float *st = state + (size_t)env * AVR_STATE_WORDS;
@@ -2309,6 +2320,330 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
     WT_END(1);
 }
 
+// ------------------------------------------------------------ part B, four envs per wavefront
+// The same PGS + integration as avr_substep_b_kernel, for four envs per wave: lanes 16g .. 16g+15
+// solve env 4*block + g, and lane sl = lane & 15 of a group holds robot DoF sl's and free body
+// sl's velocity increments (MAXD, MAXF <= 16).  A row's J.dv is one 16-lane DPP butterfly
+// (row_ror 8, 4, 2, 1: every lane of the row ends with the sum), so the four envs' Gauss-Seidel
+// chains advance in lockstep through one instruction stream and every VALU op does four envs'
+// work.  A group with fewer rows than the wave's longest sweep runs null rows (inv = lo = hi = 0:
+// delta = 0 exactly), which leaves its results identical to a solve on its own.  Row order and
+// per-row arithmetic are those of pgs_solve (btMultiBodyConstraintSolver::solveSingleIteration).
+// Impulses always live in LDS: in place in word 6 of the staged records, or (an env whose row
+// set exceeds the staging capacity: the wave reads its records from the global row buffer) in an
+// LDS array indexed by row, so every impulse read-after-write stays inside the wave's LDS.
+#define B4_CAPR 192
+#define B4_CAPS 30
+#define B4_NULLW (B4_CAPR * RWC + B4_CAPS * ROBW)   // two null records, then a zero block
+#define B4_ZEROW (B4_NULLW + 2 * RWC)
+#define B4_LISTW (B4_ZEROW + 32)                     // friction active list (ints)
+#define B4_WORDS (B4_LISTW + AVR_MAX_CONTACTS)
+#define B4_IMPNULL (MAXNC + 3 * AVR_MAX_CONTACTS)    // global path: null-row impulse slot
+static_assert(B4_WORDS % 4 == 0, "group regions must stay 16-byte aligned");
+static_assert(4 * B4_WORDS * 4 <= 81920, "two waves per CU");
+static_assert(B4_IMPNULL + 2 <= B4_LISTW, "global-path impulse array fits below the list");
+
+// null records + zero block for the global-memory path (info = no endpoint, slot = -1); read only
+__device__ int avr_b4_null[2 * RWC + 32] = {RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                            RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1};
+
+// One row as a lane sees it: record pointer, LDS impulse slot, header, current impulse, own free
+// part, robot part.
+template <class P>
+struct Row4 { P p; lds_f *ip; f4v h0, h1; float imp; f2v j0, j1, j2, r; };
+
+// LDS source: the wave's four group regions; pointers are per lane (group-uniform).
+struct B4Lds {
+    typedef lds_f *P;
+    lds_f *base;      // this lane's group region
+    AVR_DI lds_f *ipp(int r) const { return base + r * RWC + 6; }
+    // row r (< 0: null record; pair = 1 selects the second null record)
+    AVR_DI void at(Row4<P> &R, int r, int pair) const { R.p = r >= 0 ? base + r * RWC : base + B4_NULLW + pair * RWC; R.ip = R.p + 6; }
+    AVR_DI P zero() const { return base + B4_ZEROW; }
+    AVR_DI void hdr(Row4<P> &R) const { R.h0 = *(const lds_f4 *)R.p; R.h1 = *(const lds_f4 *)(R.p + 4); R.imp = R.h1.z; }
+    AVR_DI void own(P p, int off, f2v &a, f2v &b, f2v &c) const {
+        const P q = off >= 0 ? p + off : zero();
+        a = *(const lds_f2 *)q; b = *(const lds_f2 *)(q + 2); c = *(const lds_f2 *)(q + 4);
+    }
+    AVR_DI f2v robot(int slot) const {
+        return *(const lds_f2 *)(slot >= 0 ? base + B4_CAPR * RWC + slot * ROBW + 2 * (lane_id() & 15) : zero());
+    }
+};
+// Global source: records from the env's row buffer (read only), impulses in the group's LDS region.
+struct B4Glb {
+    typedef const float *P;
+    const float *rec, *robb;
+    lds_f *imp;
+    AVR_DI lds_f *ipp(int r) const { return imp + r; }
+    AVR_DI void at(Row4<P> &R, int r, int pair) const {
+        R.p = r >= 0 ? rec + r * RWC : (const float *)avr_b4_null + pair * RWC;
+        R.ip = imp + (r >= 0 ? r : B4_IMPNULL + pair);
+    }
+    AVR_DI P zero() const { return (const float *)avr_b4_null + 2 * RWC; }
+    AVR_DI void hdr(Row4<P> &R) const { R.h0 = *(const f4v *)R.p; R.h1 = *(const f4v *)(R.p + 4); R.imp = *R.ip; }
+    AVR_DI void own(P p, int off, f2v &a, f2v &b, f2v &c) const {
+        const P q = off >= 0 ? p + off : zero();
+        a = *(const f2v *)q; b = *(const f2v *)(q + 2); c = *(const f2v *)(q + 4);
+    }
+    AVR_DI f2v robot(int slot) const { return *(const f2v *)(slot >= 0 ? robb + slot * ROBW + 2 * (lane_id() & 15) : zero()); }
+};
+
+// sum over the 16 lanes of each DPP row, result in every lane of the row
+AVR_DI float row16_sum(float x) {
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x122, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x121, 0xf, 0xf, false));
+    return x;
+}
+
+template <class S>
+AVR_DI void parts4(const S &s, Row4<typename S::P> &R) {
+    const int sl = lane_id() & 15;
+    const int info = __float_as_int(R.h0.x), slot = __float_as_int(R.h1.w);
+    const int off = sl == (info & 63) ? 8 : (sl == ((info >> 6) & 63) ? 14 : -1);
+    s.own(R.p, off, R.j0, R.j1, R.j2);
+    R.r = s.robot(slot);
+}
+
+// resolve one row with its current impulse; the new impulse goes back to the row's LDS slot
+template <class P>
+AVR_DI float go4(const Row4<P> &R, DV &d, float imp, float lo, float hi) {
+    float p = R.j0.x * d.vx + R.j0.y * d.vy + R.j1.x * d.vz;
+    float q = R.j1.y * d.wx + R.j2.x * d.wy + R.j2.y * d.wz;
+    p += q + R.r.x * d.rq;
+    const float dv = row16_sum(p);
+    const float ni = __builtin_amdgcn_fmed3f(imp + (R.h0.w - dv * R.h0.z), lo, hi);
+    const float delta = ni - imp;
+    d.vx += R.j0.x * delta; d.vy += R.j0.y * delta; d.vz += R.j1.x * delta;
+    d.wx += R.j1.y * delta; d.wy += R.j2.x * delta; d.wz += R.j2.y * delta;
+    d.rq += R.r.y * delta;
+    return ni;
+}
+
+// sweep over n (wave-uniform) steps; rr(j) is this lane's row for step j (its group's row index,
+// or -1: a null row); headers two steps ahead, parts one step ahead, three rotating buffers
+template <class S, class RR, class GO>
+AVR_DI void sweep4(const S &s, int n, const RR &rr, const GO &go) {
+    if (n <= 0) return;
+    Row4<typename S::P> A, B, C;
+    s.at(A, rr(0), 0); s.hdr(A);
+    if (n > 1) { s.at(B, rr(1), 0); s.hdr(B); }
+    parts4(s, A);
+    for (int j = 0;;) {
+        if (j + 2 < n) { s.at(C, rr(j + 2), 0); s.hdr(C); }
+        if (j + 1 < n) parts4(s, B);
+        go(A);
+        if (++j >= n) break;
+        if (j + 2 < n) { s.at(A, rr(j + 2), 0); s.hdr(A); }
+        if (j + 1 < n) parts4(s, C);
+        go(B);
+        if (++j >= n) break;
+        if (j + 2 < n) { s.at(B, rr(j + 2), 0); s.hdr(B); }
+        if (j + 1 < n) parts4(s, A);
+        go(C);
+        if (++j >= n) break;
+    }
+}
+
+// friction unit: the two friction rows of one active contact and that contact's normal impulse
+template <class S>
+struct Pair4 { Row4<typename S::P> a, b; float in; };
+template <class S>
+AVR_DI void pair_hdr(const S &s, Pair4<S> &X, int r, int rn) {
+    s.at(X.a, r, 0);
+    s.at(X.b, r >= 0 ? r + 1 : -1, 1);
+    s.hdr(X.a); s.hdr(X.b);
+    X.in = rn >= 0 ? *s.ipp(rn) : 0.f;
+}
+template <class S>
+AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
+    const int sl = lane_id() & 15;
+    const int info = __float_as_int(X.a.h0.x), slot = __float_as_int(X.a.h1.w);
+    const int off = sl == (info & 63) ? 8 : (sl == ((info >> 6) & 63) ? 14 : -1);
+    s.own(X.a.p, off, X.a.j0, X.a.j1, X.a.j2);
+    s.own(X.b.p, off, X.b.j0, X.b.j1, X.b.j2);
+    X.a.r = s.robot(slot);
+    X.b.r = s.robot(slot >= 0 ? slot + 1 : -1);
+}
+
+template <class S>
+AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
+    typedef typename S::P P;
+    const int sl = lane_id() & 15;
+    d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
+    // warm start (normal rows, contact order): delta = cached impulse * warm-start factor, which
+    // is also the rows' starting impulse
+    sweep4(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+           [&](const Row4<P> &R) { (void)go4(R, d, 0.f, R.imp, R.imp); });
+    const int fr0 = n_nc + n_c;
+    for (int it = 0; it < m.iters; it++) {
+        const bool fwd = (it & 1) != 0;
+        sweep4(s, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
+               [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, R.h1.x, R.h1.y); });
+        sweep4(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+               [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, 0.f, 1e10f); });
+        // active contacts (positive normal impulse) of each group, in contact order
+        int t = 0;
+        for (int c0 = 0; c0 < nc_max; c0 += 16) {
+            const int c = c0 + sl;
+            const bool a = c < n_c && *s.ipp(n_nc + (c < n_c ? c : 0)) > 0.f;
+            const unsigned long long b = __ballot(a);
+            const unsigned gm = (unsigned)(b >> (lane_id() & 48)) & 0xffffu;
+            if (a) list[t + __popc(gm & ((1u << sl) - 1u))] = c;
+            t += __popc(gm);
+        }
+        int tmax = t;
+        tmax = max(tmax, __shfl_xor(tmax, 16));
+        tmax = max(tmax, __shfl_xor(tmax, 32));
+        tmax = uni(tmax);
+        if (tmax == 0) continue;
+        Pair4<S> X[3];
+        // list entries are read one step before the headers they address
+        auto lst = [&](int u) { return u < t ? list[u] : -1; };
+        auto hdr = [&](Pair4<S> &Y, int c) { pair_hdr(s, Y, c >= 0 ? fr0 + 2 * c : -1, c >= 0 ? n_nc + c : -1); };
+        auto go = [&](const Pair4<S> &Y) {
+            const float lim = Y.a.h0.y * Y.in;
+            *Y.a.ip = go4(Y.a, d, Y.a.imp, -lim, lim);
+            *Y.b.ip = go4(Y.b, d, Y.b.imp, -lim, lim);
+        };
+        int c2 = lst(0);
+        hdr(X[0], c2);
+        c2 = lst(1);
+        if (tmax > 1) hdr(X[1], c2);
+        c2 = lst(2);
+        pair_parts4(s, X[0]);
+        for (int u = 0;;) {
+            if (u + 2 < tmax) { hdr(X[2], c2); c2 = lst(u + 3); }
+            if (u + 1 < tmax) pair_parts4(s, X[1]);
+            go(X[0]);
+            if (++u >= tmax) break;
+            if (u + 2 < tmax) { hdr(X[0], c2); c2 = lst(u + 3); }
+            if (u + 1 < tmax) pair_parts4(s, X[2]);
+            go(X[1]);
+            if (++u >= tmax) break;
+            if (u + 2 < tmax) { hdr(X[1], c2); c2 = lst(u + 3); }
+            if (u + 1 < tmax) pair_parts4(s, X[0]);
+            go(X[2]);
+            if (++u >= tmax) break;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                            const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
+                                                            int n_envs) {
+    const KModel &m = *mp;
+    __shared__ f4v b4l[4 * B4_WORDS / 4];
+    const int lane = lane_id(), sl = lane & 15, g = lane >> 4;
+    // XCD-consistent mapping: blocks are dealt round-robin over the 8 XCDs, and part A runs env
+    // e as block e - env0, so block b takes the envs e - env0 = 32 (b / 8) + (b % 8) + 8 g, which
+    // part A ran on the same XCD: the rows, workspace and state it wrote are read through the
+    // same L2 (per-XCD L2s are not coherent with each other)
+    const int env = env0 + 32 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * g;
+    const bool live = env < n_envs && (!mask || mask[env]);
+    const int ev = live ? env : env0;
+    const float *ws = env_ws(m, ev);
+    float *st = state + (size_t)ev * AVR_STATE_WORDS;
+    const int n_nc = live ? __float_as_int(ws[WS_NNC]) : 0, n_c = live ? __float_as_int(ws[WS_NC]) : 0;
+    const int n_rob = live ? __float_as_int(ws[WS_NROB]) : 0;
+    const int n_rows = n_nc + 3 * n_c;
+    auto wmax = [&](int x) { x = max(x, __shfl_xor(x, 16)); x = max(x, __shfl_xor(x, 32)); return uni(x); };
+    const int nnc_max = wmax(n_nc), nc_max = wmax(n_c);
+    lds_f *gb = (lds_f *)(lds_f4 *)b4l + g * B4_WORDS;
+    lds_i *list = (lds_i *)(gb + B4_LISTW);
+    const float *rows = env_rows(m, ev);
+    const bool in_lds = !m.b_global && __ballot(n_rows > B4_CAPR || n_rob > B4_CAPS) == 0ull;
+#ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the block's LDS (see load_state)
+    for (int i = lane; i < 4 * B4_WORDS; i += 64) ((lds_f *)(lds_f4 *)b4l)[i] = __int_as_float(-1);
+    __syncthreads();
+#endif
+    DV d;
+    if (in_lds) {
+        // stage each group's records and robot parts (16 lanes per group, 8 loads in flight)
+        const int n4r = n_rows * (RWC / 4), n4s = n_rob * (ROBW / 4);
+        const int m4 = wmax(n4r + n4s);
+        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
+        lds_f4 *l0 = (lds_f4 *)gb, *l1 = (lds_f4 *)(gb + B4_CAPR * RWC);
+        for (int b = 0; b < m4; b += 8 * 16) {
+            f4v t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = b + 16 * q + sl;
+                t[q] = i < n4r ? g0[i] : (i < n4r + n4s ? g1[i - n4r] : g0[0]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = b + 16 * q + sl;
+                if (i < n4r) l0[i] = t[q];
+                else if (i < n4r + n4s) l1[i - n4r] = t[q];
+            }
+        }
+        // two null records (info: no endpoint, slot -1) and the zero block
+        for (int i = sl; i < 2 * RWC + 32; i += 16) {
+            const int k = i % RWC;
+            gb[B4_NULLW + i] = i < 2 * RWC && k == 0 ? __int_as_float(RI_NONE | (RI_NONE << 6)) : (i < 2 * RWC && k == 7 ? __int_as_float(-1) : 0.f);
+        }
+        __syncthreads();
+        B4Lds s;
+        s.base = gb;
+        pgs4(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
+        // normal impulses back to the manifold points (warm start + normalForce)
+        for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
+    } else {
+        // starting impulses (record word 6) into the LDS impulse array, null slots zero
+        for (int r = sl; r < n_rows; r += 16) gb[r] = rows[r * RWC + 6];
+        if (sl < 2) gb[B4_IMPNULL + sl] = 0.f;
+        __syncthreads();
+        B4Glb s;
+        s.rec = rows;
+        s.robb = rows + m.rowcap * RWC;
+        s.imp = gb;
+        pgs4(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
+        for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
+    }
+    if (!live) return;
+    // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
+    if (sl < m.nf) {
+        const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * sl + 3);
+        const v3 I = ld3(m.fb_inertia + 4 * sl);
+        const float rs = 1.f / sqrtf(m.fb_mass[sl]);
+        const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
+        const v3 w = qrot(q, V(d.wx * sd.x, d.wy * sd.y, d.wz * sd.z));
+        d.vx *= rs; d.vy *= rs; d.vz *= rs;
+        d.wx = w.x; d.wy = w.y; d.wz = w.z;
+    }
+    const float vmax = m.max_vel;
+    const int nda = env_hdyn(m, st) ? m.nd + m.hc_n : m.nd;
+    if (sl < nda) {
+        float v = clampf(ws[WS_VQ + sl] + d.rq, -vmax, vmax);
+        float q = st[AVR_S_Q + sl] + dt * v;
+        if (frame_end && sl >= m.nd) {
+            // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
+            const float lo = m.hc_lower[sl - m.nd], hi = m.hc_upper[sl - m.nd];
+            if (q < lo) { q = lo; v = 0.f; }
+            else if (q > hi) { q = hi; v = 0.f; }
+        }
+        st[AVR_S_QD + sl] = v;
+        st[AVR_S_Q + sl] = q;
+    }
+    if (sl < m.nf) {
+        float *fb = st + AVR_S_FREE + AVR_FB_WORDS * sl;
+        v3 v = clamp3(add(ld3(ws + WS_FV + 4 * sl), V(d.vx, d.vy, d.vz)), vmax);
+        v3 om = clamp3(add(ld3(ws + WS_FW + 4 * sl), V(d.wx, d.wy, d.wz)), vmax);
+        st3(fb + 7, v);
+        st3(fb + 10, om);
+        st3(fb, add(ld3(fb), scl(v, dt)));
+        float ang = len(om);
+        if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = (0.5f * 1.5707963267948966f) / dt;
+        v3 ax;
+        if (ang < 0.001f) ax = scl(om, 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang);
+        else ax = scl(om, sinf(0.5f * ang * dt) / ang);
+        qt dq = Q(ax.x, ax.y, ax.z, cosf(ang * dt * 0.5f));
+        stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
+    }
+}
+
 // Task glue after the frames: update_targets (feeding.py:345-349), iteration count,
 // get_total_force (83-90), get_food_rewards (92-121), _get_obs (123-142), reward (56-77),
 // TimeLimit; SETTLE mode: target + reset observation only.  NaN guard for every mode.
@@ -2435,6 +2770,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     if (n_envs <= 0) return hipSuccess;
     const int nsub = h_m->nsub > 0 ? h_m->nsub : 1;
     const float dt = h_m->time_step / (float)nsub;
+    const int b_variant = h_m->b_variant;
     auto mark = [&](int kind) {
         if (log && log->n < log->cap && hipEventRecord(log->ev[log->n], stream) == hipSuccess) log->kind[log->n++] = kind;
     };
@@ -2444,7 +2780,10 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
-        hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
+        if (b_variant == 1)
+            hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
+        else
+            hipLaunchKernelGGL(avr_substep_b4_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
     };
     if (mode == MODE_SUBSTEP) {
         float h;
@@ -2458,7 +2797,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
             for (int k = 0; k < nsub; k++) sub(dt, 0);
     } else {
         mark(AVR_K_TAKE);
-        hipLaunchKernelGGL(avr_take_step_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, stream, d_m, state, act, mask, mode, t, env0, env1);
+        hipLaunchKernelGGL(avr_take_step_kernel, dim3(8 * ((n_envs + 511) / 512)), dim3(64), 0, stream, d_m, state, act, mask, mode, t, env0, env1);
         for (int f = 0; f < h_m->frame_skip; f++)
             for (int k = 0; k < nsub; k++) sub(dt, k == nsub - 1);
     }

@@ -39,9 +39,13 @@ typedef struct avr_config {
     int32_t n_envs;        /* envs owned by this handle (one GPU)                          */
     int32_t device;        /* HIP device ordinal                                           */
     int32_t env_offset;    /* global id of local env 0 (keys per-env RNG; sharding-stable)  */
-    int32_t flags;         /* reserved, 0                                                  */
+    int32_t flags;         /* AVR_CFG_* bits, 0 = defaults                                  */
     uint64_t seed;         /* action RNG seed for avr_step_random (env.py:53 uses 1001)     */
 } avr_config;
+
+/* avr_config.flags: part B (PGS + integration) variant; default one env per wavefront */
+#define AVR_CFG_B_FOUR_ENVS_PER_WAVE 1 /* part B as four envs per wavefront (16 lanes each)    */
+#define AVR_CFG_B_GLOBAL_ROWS 2        /* diagnostic, four-env part B: rows from global memory */
 
 typedef struct avr_sim avr_sim;
 

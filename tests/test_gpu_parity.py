@@ -55,7 +55,8 @@ def test_kernel_resources(lib_and_scene):
     sim = make_sim(md, 4)
     ki = sim.kernel_info()
     assert ki['scratch_bytes'] == 0 and ki['b_scratch_bytes'] == 0     # no spills to scratch on gfx950
-    assert ki['lds_bytes'] <= 20 * 1024 and ki['b_lds_bytes'] <= 20 * 1024     # 8 env blocks per CU
+    assert ki['lds_bytes'] <= 20 * 1024              # part A: 8 env blocks per CU
+    assert ki['b_lds_bytes'] <= 20 * 1024            # part B: 8 env blocks per CU
     sim.close()
 
 
@@ -242,3 +243,80 @@ def test_tremor_targets_and_hard_limits_match_oracle(lib_and_scene):
         assert np.abs(G[:, dofs(md)] - C[:, dofs(md)]).max() < 1e-4
         assert np.abs(G[:, ABI.S_QD:ABI.S_QD + nd + 4] - C[:, ABI.S_QD:ABI.S_QD + nd + 4]).max() < 1e-3
     sim.close()
+
+
+def _b_variant_run(md, S, flags, steps=5, frames=30):
+    from avr import _lib
+    sim = make_sim(md, len(S), flags=flags)
+    sim.set_state(S)
+    sim.settle(frames)
+    outs = [sim.step(_lib.random_actions(1001, np.arange(len(S)), k)) for k in range(steps)]
+    G = sim.get_state()
+    sim.close()
+    return G, outs
+
+
+def test_part_b_row_sources_bit_identical(lib_and_scene):
+    """Four-env part B: rows staged in LDS and rows read from the global buffer (the fallback for
+    row sets beyond the staging capacity) run the same arithmetic -> bit-identical states."""
+    from avr import _lib
+    A, md = lib_and_scene
+    S = np.concatenate([reset_states(A, md, range(0, 20)), reset_states(A, md, range(20, 30), 'tremor')])
+    F = _lib.CFG_B_FOUR_ENVS_PER_WAVE
+    G_lds, o_lds = _b_variant_run(md, S, F)
+    G_glb, o_glb = _b_variant_run(md, S, F | _lib.CFG_B_GLOBAL_ROWS)
+    assert np.array_equal(G_lds, G_glb)
+    for a, b in zip(o_lds, o_glb):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_part_b_four_envs_per_wave_matches_one(lib_and_scene):
+    """Four envs per wave (16-lane DPP butterfly) vs one env per wave (scan reduction): the same
+    PGS up to fp32 summation order; held to the contact-rich chaos envelope on the arm joints,
+    and no env flagged (NaN guard, pool overflow)."""
+    from avr import _lib, _abi as ABI
+    A, md = lib_and_scene
+    S = np.concatenate([reset_states(A, md, range(0, 20)), reset_states(A, md, range(20, 30), 'tremor')])
+    G4, o4 = _b_variant_run(md, S, _lib.CFG_B_FOUR_ENVS_PER_WAVE)
+    G1, o1 = _b_variant_run(md, S, 0)
+    sl = dofs(md)
+    assert float(np.abs(G4[:, sl] - G1[:, sl]).max()) < 3e-3
+    assert not np.any(G4[:, ABI.S_TASK + ABI.T_FLAGS]) and not np.any(G1[:, ABI.S_TASK + ABI.T_FLAGS])
+    assert float(np.abs(o4[-1][1] - o1[-1][1]).max()) < 5e-2
+
+
+_POISON_RUN = r'''
+import os, sys, numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], 'assistive-vr-gym_amd'))
+from avr import _abi as ABI, reset as RS, _lib
+A = ABI.load_scene(); md = ABI.ModelDesc(A)
+S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(64)), impairment='random')
+sim = _lib.Sim(md, 64, flags=int(sys.argv[3]))
+sim.set_state(S.astype(np.float32)); sim.settle(20)
+for t in range(3):
+    sim.step(_lib.random_actions(1001, np.arange(64), t))
+np.save(sys.argv[2], sim.get_state())
+'''
+
+
+@pytest.mark.parametrize('flags', [0, 1])
+def test_lds_poison_build_is_bit_identical(lib_and_scene, tmp_path, flags):
+    """The diagnostic build NaN-fills every kernel's LDS block at entry (AVR_LDS_POISON).  Its
+    results equal the shipped build's bit for bit, so no kernel reads an LDS word it did not write
+    in the same launch (such a read once let another kernel's leftovers into the constraint rows:
+    0 * NaN in J.vq over inactive DoF slots)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    poison = os.path.join(root, 'assistive-vr-gym_amd', 'avr', 'libavr_poison.so')
+    assert os.path.exists(poison), 'build() makes libavr_poison.so'
+    outs = []
+    for lib in (None, poison):
+        env = dict(os.environ)
+        env.pop('AVR_LIB', None)
+        if lib:
+            env['AVR_LIB'] = lib
+        f = str(tmp_path / ('s%d.npy' % len(outs)))
+        subprocess.run([sys.executable, '-c', _POISON_RUN, root, f, str(flags)], env=env, check=True, timeout=150)
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0], outs[1])
