@@ -274,9 +274,12 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         std::vector<int2> cells;
         std::vector<float4> cand;
         const int G = AVR_TAB_G, nc = 6 * G * G;
+        // hulls with more than tab_min vertices get a table (AVR_TAB_MIN_NV overrides it for experiments)
+        int tab_min = AVR_TAB_MIN_NV;
+        if (const char *e = getenv("AVR_TAB_MIN_NV")) tab_min = atoi(e);
         for (int i = 0; i < ns; i++) {
             const int vs = d->shape_hull[4 * i], nvh = d->shape_hull[4 * i + 1];
-            if (d->shape_kind[i] != AVR_HULL || nvh <= AVR_TAB_MIN_NV) continue;
+            if (d->shape_kind[i] != AVR_HULL || nvh <= tab_min) continue;
             std::vector<float> pv((size_t)nvh * 3);
             for (int q = 0; q < nvh; q++) { pv[3 * q] = hv[vs + q].x; pv[3 * q + 1] = hv[vs + q].y; pv[3 * q + 2] = hv[vs + q].z; }
             std::vector<int32_t> cl((size_t)2 * nc);

@@ -364,23 +364,20 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
             const int i = min(AVR_TAB_G - 1, max(0, (int)((u + mx) * sc)));
             const int j = min(AVR_TAB_G - 1, max(0, (int)((w + mx) * sc)));
             const int2 oc = m.tab_cell[s.tab + (f * AVR_TAB_G + i) * AVR_TAB_G + j];
+            // batches of 4 candidates in flight; a short last batch re-reads the last candidate,
+            // which cannot displace an earlier winner under the strict ">" (exact)
             float best = -BIGF;
             float4 bv = tv[oc.x];
-            int k = 0;
-            for (; k + 4 <= oc.y; k += 4) {
+            const int last = oc.x + oc.y - 1;
+            for (int k = 0; k < oc.y; k += 4) {
                 float4 v[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) v[q] = tv[oc.x + k + q];
+                for (int q = 0; q < 4; q++) v[q] = tv[min(oc.x + k + q, last)];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const float dd = l.x * v[q].x + l.y * v[q].y + l.z * v[q].z;
                     if (dd > best) { best = dd; bv = v[q]; }
                 }
-            }
-            for (; k < oc.y; k++) {
-                const float4 v = tv[oc.x + k];
-                const float dd = l.x * v.x + l.y * v.y + l.z * v.z;
-                if (dd > best) { best = dd; bv = v; }
             }
             r = V(bv.x, bv.y, bv.z);
         }
@@ -410,23 +407,20 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
             const float4 v = hv[bi];
             r = V(v.x, v.y, v.z);
         } else {
+            // batches of 8 vertices in flight, ceil(nv / 8) round trips; a short last batch
+            // re-reads vertex nv - 1, which cannot displace an earlier winner under the strict ">"
             float best = -BIGF;
             float4 bv = hv[0];
-            int i = 0;
-            for (; i + 8 <= s.nv; i += 8) {
+            const int last = s.nv - 1;
+            for (int i = 0; i < s.nv; i += 8) {
                 float4 v[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) v[k] = hv[i + k];
+                for (int k = 0; k < 8; k++) v[k] = hv[min(i + k, last)];
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float dd = l.x * v[k].x + l.y * v[k].y + l.z * v[k].z;
                     if (dd > best) { best = dd; bv = v[k]; }
                 }
-            }
-            for (; i < s.nv; i++) {
-                const float4 v = hv[i];
-                const float dd = l.x * v.x + l.y * v.y + l.z * v.z;
-                if (dd > best) { best = dd; bv = v; }
             }
             r = V(bv.x, bv.y, bv.z);
         }
@@ -1679,8 +1673,12 @@ AVR_DI float robot_reduce(float x) {
 // many loads in flight, then every row of the Gauss-Seidel chain resolves from LDS reads issued
 // one row (parts) / two rows (headers) ahead.  An env whose row set exceeds the LDS capacity
 // (> B_CAPR rows or > B_CAPS robot parts, rare) runs the same solver on the global buffer.
+#ifndef B_CAPR
 #define B_CAPR 192
+#endif
+#ifndef B_CAPS
 #define B_CAPS 32
+#endif
 #define B_LDS_WORDS (B_CAPR * RWC + B_CAPS * ROBW + 16)
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));

@@ -24,7 +24,7 @@ extern "C" {
 #define AVR_MAX_FREE 10         /* free bodies (spoon, bowl, 8 food)                */
 #define AVR_MAX_HUMAN 20        /* per-env static human slots (19)                  */
 #define AVR_TAB_G 16            /* support tables: cube-map cells per face edge     */
-#define AVR_TAB_MIN_NV 64       /* hulls with more vertices get a support table     */
+#define AVR_TAB_MIN_NV 8        /* hulls with more vertices get a support table     */
 #define AVR_MAX_CONTACTS 96     /* persistent contact points per env                */
 #define AVR_MANIFOLD_POINTS 4   /* Bullet MANIFOLD_CACHE_SIZE                       */
 #define AVR_MAX_FOOD 8

@@ -99,3 +99,28 @@ def test_table_support_equals_full_scan(scene, which):
     got = table_scan(V, cell, idx, D)
     bad = np.nonzero(ref != got)[0]
     assert len(bad) == 0, (s, bad[:5], D[bad[:5]], ref[bad[:5]], got[bad[:5]])
+
+
+def small_hulls(A, lo=8, hi=64):
+    sh = A['shape_hull'].reshape(-1, 4)
+    for s in range(len(sh)):
+        if A['shape_kind'][s] == 3 and lo < sh[s, 1] <= hi:
+            yield s, A['hull_verts'][sh[s, 0]:sh[s, 0] + sh[s, 1]].astype(np.float32)
+
+
+def test_table_support_equals_full_scan_small_hulls(scene):
+    """Every hull above AVR_TAB_MIN_NV (8) vertices gets a table (spoon, bowl, wheelchair and head
+    VHACD pieces too): the lookup equals the full scan on each of them."""
+    A, _ = scene
+    from avr import _lib
+    hulls = list(small_hulls(A))
+    assert len(hulls) > 100
+    rng = np.random.default_rng(7)
+    for s, V in hulls:
+        cell, idx = _lib.hull_support_table(V, G)
+        assert cell[:, 1].min() >= 1
+        D = np.concatenate([directions(rng, 160), V[rng.choice(len(V), 20)] - V.mean(0)]).astype(np.float32)
+        ref = full_scan(V, D)
+        got = table_scan(V, cell, idx, D)
+        bad = np.nonzero(ref != got)[0]
+        assert len(bad) == 0, (s, bad[:5], D[bad[:5]], ref[bad[:5]], got[bad[:5]])
