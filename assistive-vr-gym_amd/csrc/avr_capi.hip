@@ -331,9 +331,8 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int i = 0; i < 3; i++) k.mouth[g][i] = (float)d->mouth_offset[g][i];
     k.time_step = (float)d->time_step;
     // part B variant (AVR_CFG_B_*); AVR_KERNEL_B=1 / =4 overrides it for experiments
-    k.b_variant = (cfg->flags & AVR_CFG_B_FOUR_ENVS_PER_WAVE) ? 4 : 1;
+    k.b_variant = (cfg->flags & AVR_CFG_B_ONE_ENV_PER_WAVE) ? 1 : 4;
     if (const char *e = getenv("AVR_KERNEL_B")) k.b_variant = e[0] == '1' ? 1 : 4;
-    k.b_global = (cfg->flags & AVR_CFG_B_GLOBAL_ROWS) ? 1 : 0;
     k.nsub = d->num_sub_steps; k.frame_skip = d->frame_skip; k.iters = d->solver_iterations; k.max_steps = d->max_episode_steps;
     k.erp = (float)d->erp; k.warmstart = (float)d->warmstart; k.lin_damp = (float)d->linear_damping; k.ang_damp = (float)d->angular_damping;
     k.max_vel = (float)d->max_coord_vel; k.robot_gain = (float)d->robot_gain; k.robot_force = (float)d->robot_force;

@@ -2320,26 +2320,25 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
 
 // ------------------------------------------------------------ part B, four envs per wavefront
 // The same PGS + integration as avr_substep_b_kernel, for four envs per wave: lanes 16g .. 16g+15
-// solve env 4*block + g, and lane sl = lane & 15 of a group holds robot DoF sl's and free body
+// solve env g of the block, and lane sl = lane & 15 of a group holds robot DoF sl's and free body
 // sl's velocity increments (MAXD, MAXF <= 16).  A row's J.dv is one 16-lane DPP butterfly
 // (row_ror 8, 4, 2, 1: every lane of the row ends with the sum), so the four envs' Gauss-Seidel
 // chains advance in lockstep through one instruction stream and every VALU op does four envs'
 // work.  A group with fewer rows than the wave's longest sweep runs null rows (inv = lo = hi = 0:
 // delta = 0 exactly), which leaves its results identical to a solve on its own.  Row order and
 // per-row arithmetic are those of pgs_solve (btMultiBodyConstraintSolver::solveSingleIteration).
-// Impulses always live in LDS: in place in word 6 of the staged records, or (an env whose row
-// set exceeds the staging capacity: the wave reads its records from the global row buffer) in an
-// LDS array indexed by row, so every impulse read-after-write stays inside the wave's LDS.
-#define B4_CAPR 192
-#define B4_CAPS 30
-#define B4_NULLW (B4_CAPR * RWC + B4_CAPS * ROBW)   // two null records, then a zero block
-#define B4_ZEROW (B4_NULLW + 2 * RWC)
-#define B4_LISTW (B4_ZEROW + 32)                     // friction active list (ints)
+// Rows are read from the global row buffer through a software pipeline (headers 2D rows ahead,
+// parts D ahead); impulses and the friction lists live in LDS (6.7 KB per block), so all 1024
+// blocks of a 4096-env launch are resident at once.  (Staging the rows in LDS instead, 79.5 KB per
+// block, measured slower: 2 blocks per CU.)
+#define B4_IMPNULL (MAXNC + 3 * AVR_MAX_CONTACTS)    // null-row impulse slots (2)
+#define B4_LISTW 324                                 // friction active list (ints) after the impulses
 #define B4_WORDS (B4_LISTW + AVR_MAX_CONTACTS)
-#define B4_IMPNULL (MAXNC + 3 * AVR_MAX_CONTACTS)    // global path: null-row impulse slot
+#ifndef B4_GD
+#define B4_GD 2          // software-pipeline depth (measured: 2 beats 3 and 5)
+#endif
 static_assert(B4_WORDS % 4 == 0, "group regions must stay 16-byte aligned");
-static_assert(4 * B4_WORDS * 4 <= 81920, "two waves per CU");
-static_assert(B4_IMPNULL + 2 <= B4_LISTW, "global-path impulse array fits below the list");
+static_assert(B4_IMPNULL + 2 <= B4_LISTW, "the impulse array fits below the list");
 
 // null records + zero block for the global-memory path (info = no endpoint, slot = -1); read only
 __device__ int avr_b4_null[2 * RWC + 32] = {RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -2350,24 +2349,7 @@ __device__ int avr_b4_null[2 * RWC + 32] = {RI_NONE | (RI_NONE << 6), 0, 0, 0, 0
 template <class P>
 struct Row4 { P p; lds_f *ip; f4v h0, h1; float imp; f2v j0, j1, j2, r; };
 
-// LDS source: the wave's four group regions; pointers are per lane (group-uniform).
-struct B4Lds {
-    typedef lds_f *P;
-    lds_f *base;      // this lane's group region
-    AVR_DI lds_f *ipp(int r) const { return base + r * RWC + 6; }
-    // row r (< 0: null record; pair = 1 selects the second null record)
-    AVR_DI void at(Row4<P> &R, int r, int pair) const { R.p = r >= 0 ? base + r * RWC : base + B4_NULLW + pair * RWC; R.ip = R.p + 6; }
-    AVR_DI P zero() const { return base + B4_ZEROW; }
-    AVR_DI void hdr(Row4<P> &R) const { R.h0 = *(const lds_f4 *)R.p; R.h1 = *(const lds_f4 *)(R.p + 4); R.imp = R.h1.z; }
-    AVR_DI void own(P p, int off, f2v &a, f2v &b, f2v &c) const {
-        const P q = off >= 0 ? p + off : zero();
-        a = *(const lds_f2 *)q; b = *(const lds_f2 *)(q + 2); c = *(const lds_f2 *)(q + 4);
-    }
-    AVR_DI f2v robot(int slot) const {
-        return *(const lds_f2 *)(slot >= 0 ? base + B4_CAPR * RWC + slot * ROBW + 2 * (lane_id() & 15) : zero());
-    }
-};
-// Global source: records from the env's row buffer (read only), impulses in the group's LDS region.
+// Row source: records from the env's row buffer (read only), impulses in the group's LDS region.
 struct B4Glb {
     typedef const float *P;
     const float *rec, *robb;
@@ -2420,27 +2402,29 @@ AVR_DI float go4(const Row4<P> &R, DV &d, float imp, float lo, float hi) {
 }
 
 // sweep over n (wave-uniform) steps; rr(j) is this lane's row for step j (its group's row index,
-// or -1: a null row); headers two steps ahead, parts one step ahead, three rotating buffers
-template <class S, class RR, class GO>
+// or -1: a null row).  Software pipeline of depth D: headers 2D steps ahead, the header-dependent
+// parts D steps ahead, in a ring of 2D + 1 buffers whose slots are compile-time after unrolling
+// (D = 1 for rows staged in LDS, deeper for rows read from global memory).
+template <int D, class S, class RR, class GO>
 AVR_DI void sweep4(const S &s, int n, const RR &rr, const GO &go) {
-    if (n <= 0) return;
-    Row4<typename S::P> A, B, C;
-    s.at(A, rr(0), 0); s.hdr(A);
-    if (n > 1) { s.at(B, rr(1), 0); s.hdr(B); }
-    parts4(s, A);
-    for (int j = 0;;) {
-        if (j + 2 < n) { s.at(C, rr(j + 2), 0); s.hdr(C); }
-        if (j + 1 < n) parts4(s, B);
-        go(A);
-        if (++j >= n) break;
-        if (j + 2 < n) { s.at(A, rr(j + 2), 0); s.hdr(A); }
-        if (j + 1 < n) parts4(s, C);
-        go(B);
-        if (++j >= n) break;
-        if (j + 2 < n) { s.at(B, rr(j + 2), 0); s.hdr(B); }
-        if (j + 1 < n) parts4(s, A);
-        go(C);
-        if (++j >= n) break;
+    constexpr int K = 2 * D + 1;
+    Row4<typename S::P> R[K];
+#pragma unroll
+    for (int q = 0; q < 2 * D; q++)
+        if (q < n) { s.at(R[q], rr(q), 0); s.hdr(R[q]); }
+#pragma unroll
+    for (int q = 0; q < D; q++)
+        if (q < n) parts4(s, R[q]);
+    for (int j = 0; j < n; j += K) {
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const int jj = j + q;
+            if (jj < n) {
+                if (jj + 2 * D < n) { s.at(R[(q + 2 * D) % K], rr(jj + 2 * D), 0); s.hdr(R[(q + 2 * D) % K]); }
+                if (jj + D < n) parts4(s, R[(q + D) % K]);
+                go(R[q]);
+            }
+        }
     }
 }
 
@@ -2465,21 +2449,21 @@ AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
     X.b.r = s.robot(slot >= 0 ? slot + 1 : -1);
 }
 
-template <class S>
+template <int D, class S>
 AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename S::P P;
     const int sl = lane_id() & 15;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
     // warm start (normal rows, contact order): delta = cached impulse * warm-start factor, which
     // is also the rows' starting impulse
-    sweep4(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+    sweep4<D>(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
            [&](const Row4<P> &R) { (void)go4(R, d, 0.f, R.imp, R.imp); });
     const int fr0 = n_nc + n_c;
     for (int it = 0; it < m.iters; it++) {
         const bool fwd = (it & 1) != 0;
-        sweep4(s, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
+        sweep4<D>(s, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
                [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, R.h1.x, R.h1.y); });
-        sweep4(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+        sweep4<D>(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
                [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, 0.f, 1e10f); });
         // active contacts (positive normal impulse) of each group, in contact order
         int t = 0;
@@ -2496,8 +2480,10 @@ AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, in
         tmax = max(tmax, __shfl_xor(tmax, 32));
         tmax = uni(tmax);
         if (tmax == 0) continue;
-        Pair4<S> X[3];
-        // list entries are read one step before the headers they address
+        // the same depth-D pipeline over friction units; list entries are read one step before
+        // the headers they address
+        constexpr int K = 2 * D + 1;
+        Pair4<S> X[K];
         auto lst = [&](int u) { return u < t ? list[u] : -1; };
         auto hdr = [&](Pair4<S> &Y, int c) { pair_hdr(s, Y, c >= 0 ? fr0 + 2 * c : -1, c >= 0 ? n_nc + c : -1); };
         auto go = [&](const Pair4<S> &Y) {
@@ -2505,25 +2491,25 @@ AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, in
             *Y.a.ip = go4(Y.a, d, Y.a.imp, -lim, lim);
             *Y.b.ip = go4(Y.b, d, Y.b.imp, -lim, lim);
         };
-        int c2 = lst(0);
-        hdr(X[0], c2);
-        c2 = lst(1);
-        if (tmax > 1) hdr(X[1], c2);
-        c2 = lst(2);
-        pair_parts4(s, X[0]);
-        for (int u = 0;;) {
-            if (u + 2 < tmax) { hdr(X[2], c2); c2 = lst(u + 3); }
-            if (u + 1 < tmax) pair_parts4(s, X[1]);
-            go(X[0]);
-            if (++u >= tmax) break;
-            if (u + 2 < tmax) { hdr(X[0], c2); c2 = lst(u + 3); }
-            if (u + 1 < tmax) pair_parts4(s, X[2]);
-            go(X[1]);
-            if (++u >= tmax) break;
-            if (u + 2 < tmax) { hdr(X[1], c2); c2 = lst(u + 3); }
-            if (u + 1 < tmax) pair_parts4(s, X[0]);
-            go(X[2]);
-            if (++u >= tmax) break;
+        int cn = lst(0);
+#pragma unroll
+        for (int q = 0; q < 2 * D; q++) {
+            if (q < tmax) hdr(X[q], cn);
+            cn = lst(q + 1);
+        }
+#pragma unroll
+        for (int q = 0; q < D; q++)
+            if (q < tmax) pair_parts4(s, X[q]);
+        for (int u0 = 0; u0 < tmax; u0 += K) {
+#pragma unroll
+            for (int q = 0; q < K; q++) {
+                const int u = u0 + q;
+                if (u < tmax) {
+                    if (u + 2 * D < tmax) { hdr(X[(q + 2 * D) % K], cn); cn = lst(u + 2 * D + 1); }
+                    if (u + D < tmax) pair_parts4(s, X[(q + D) % K]);
+                    go(X[q]);
+                }
+            }
         }
     }
 }
@@ -2544,62 +2530,28 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     const float *ws = env_ws(m, ev);
     float *st = state + (size_t)ev * AVR_STATE_WORDS;
     const int n_nc = live ? __float_as_int(ws[WS_NNC]) : 0, n_c = live ? __float_as_int(ws[WS_NC]) : 0;
-    const int n_rob = live ? __float_as_int(ws[WS_NROB]) : 0;
     const int n_rows = n_nc + 3 * n_c;
     auto wmax = [&](int x) { x = max(x, __shfl_xor(x, 16)); x = max(x, __shfl_xor(x, 32)); return uni(x); };
     const int nnc_max = wmax(n_nc), nc_max = wmax(n_c);
     lds_f *gb = (lds_f *)(lds_f4 *)b4l + g * B4_WORDS;
     lds_i *list = (lds_i *)(gb + B4_LISTW);
     const float *rows = env_rows(m, ev);
-    const bool in_lds = !m.b_global && __ballot(n_rows > B4_CAPR || n_rob > B4_CAPS) == 0ull;
 #ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the block's LDS (see load_state)
     for (int i = lane; i < 4 * B4_WORDS; i += 64) ((lds_f *)(lds_f4 *)b4l)[i] = __int_as_float(-1);
     __syncthreads();
 #endif
     DV d;
-    if (in_lds) {
-        // stage each group's records and robot parts (16 lanes per group, 8 loads in flight)
-        const int n4r = n_rows * (RWC / 4), n4s = n_rob * (ROBW / 4);
-        const int m4 = wmax(n4r + n4s);
-        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
-        lds_f4 *l0 = (lds_f4 *)gb, *l1 = (lds_f4 *)(gb + B4_CAPR * RWC);
-        for (int b = 0; b < m4; b += 8 * 16) {
-            f4v t[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int i = b + 16 * q + sl;
-                t[q] = i < n4r ? g0[i] : (i < n4r + n4s ? g1[i - n4r] : g0[0]);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int i = b + 16 * q + sl;
-                if (i < n4r) l0[i] = t[q];
-                else if (i < n4r + n4s) l1[i - n4r] = t[q];
-            }
-        }
-        // two null records (info: no endpoint, slot -1) and the zero block
-        for (int i = sl; i < 2 * RWC + 32; i += 16) {
-            const int k = i % RWC;
-            gb[B4_NULLW + i] = i < 2 * RWC && k == 0 ? __int_as_float(RI_NONE | (RI_NONE << 6)) : (i < 2 * RWC && k == 7 ? __int_as_float(-1) : 0.f);
-        }
-        __syncthreads();
-        B4Lds s;
-        s.base = gb;
-        pgs4(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
-        // normal impulses back to the manifold points (warm start + normalForce)
-        for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
-    } else {
-        // starting impulses (record word 6) into the LDS impulse array, null slots zero
-        for (int r = sl; r < n_rows; r += 16) gb[r] = rows[r * RWC + 6];
-        if (sl < 2) gb[B4_IMPNULL + sl] = 0.f;
-        __syncthreads();
-        B4Glb s;
-        s.rec = rows;
-        s.robb = rows + m.rowcap * RWC;
-        s.imp = gb;
-        pgs4(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
-        for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
-    }
+    // starting impulses (record word 6) into the LDS impulse array, null slots zero
+    for (int r = sl; r < n_rows; r += 16) gb[r] = rows[r * RWC + 6];
+    if (sl < 2) gb[B4_IMPNULL + sl] = 0.f;
+    __syncthreads();
+    B4Glb s;
+    s.rec = rows;
+    s.robb = rows + m.rowcap * RWC;
+    s.imp = gb;
+    pgs4<B4_GD>(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
+    // normal impulses back to the manifold points (warm start + normalForce)
+    for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
     if (!live) return;
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
     if (sl < m.nf) {

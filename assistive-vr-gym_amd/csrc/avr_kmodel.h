@@ -75,7 +75,6 @@ struct KModel {
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
     int b_variant;             // part B kernel: 4 = four envs per wave, 1 = one env per wave
-    int b_global;              // diagnostic: part B (four-env) reads its rows from global memory
 };
 
 // Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):

@@ -43,9 +43,8 @@ typedef struct avr_config {
     uint64_t seed;         /* action RNG seed for avr_step_random (env.py:53 uses 1001)     */
 } avr_config;
 
-/* avr_config.flags: part B (PGS + integration) variant; default one env per wavefront */
-#define AVR_CFG_B_FOUR_ENVS_PER_WAVE 1 /* part B as four envs per wavefront (16 lanes each)    */
-#define AVR_CFG_B_GLOBAL_ROWS 2        /* diagnostic, four-env part B: rows from global memory */
+/* avr_config.flags: part B (PGS + integration) runs four envs per wavefront by default */
+#define AVR_CFG_B_ONE_ENV_PER_WAVE 1   /* part B as one env per wavefront (rows staged in LDS)  */
 
 typedef struct avr_sim avr_sim;
 

@@ -5,7 +5,7 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 170 --timeou
 rc=$?
 grep -E "passed|failed|FAILED|Error" gpurun_out/b4/pytest_gpu.log | tail -12
 if [ $rc -ne 0 ]; then echo rc=$rc; exit $rc; fi
-for v in 4 1 4; do
+for v in 4 1; do
   timeout -k 10 300 env AVR_KERNEL_B=$v python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/b4/bench$v.json 2> gpurun_out/b4/bench$v.err || { rc=$?; echo bench rc=$rc; exit $rc; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/b4/bench$v.json').read().strip().splitlines()[-1]); k=d['roofline']['kernels']

@@ -17,7 +17,7 @@ import sys
 
 import numpy as np
 
-STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_a_kernel': 10, 'avr_substep_b_kernel': 10, 'avr_task_kernel': 1}
+STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_a_kernel': 10, 'avr_substep_b_kernel': 10, 'avr_substep_b4_kernel': 10, 'avr_task_kernel': 1}
 
 
 def db(d):
