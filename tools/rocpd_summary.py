@@ -51,9 +51,11 @@ def counters(c, names):
 
 def per_step(cnt, name):
     """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS)."""
-    if not cnt or any(name not in cnt.get(k, {}) for k in STEP_KERNELS):
+    # part B runs as one of two kernels (avr_substep_b4_kernel by default): sum what ran
+    ran = [k for k in STEP_KERNELS if name in cnt.get(k, {})] if cnt else []
+    if 'avr_substep_a_kernel' not in ran or not any(k.startswith('avr_substep_b') for k in ran):
         return None
-    return sum(cnt[k][name] * m for k, m in STEP_KERNELS.items())
+    return sum(cnt[k][name] * STEP_KERNELS[k] for k in ran)
 
 
 def main(pdir, tag, envs=4096):
