@@ -56,7 +56,9 @@ struct EnvLDS {
             int okey[AVR_MAX_CONTACTS];    // (sa | sb << 16) of the previous contact pool
             int qk[128], qp[128];          // shape-pair queue: (sa | sb << 16), body pair
             int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
+#ifndef AVR_CAABB_ONDEMAND
             float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
+#endif
         } c;
         struct {
             float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
@@ -1017,7 +1019,11 @@ AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, 
 
 AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, v3 &mn, v3 &mx) {
     const int c = m.shape_cidx[s];
+#ifdef AVR_CAABB_ONDEMAND   // experiment: world AABB of a non-static child computed where it is used
+    if (c >= 0) shape_aabb(m, s, ldtf(L.btf[m.shape_body[s]]), mn, mx);
+#else
     if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
+#endif
     else { const float *a = m.static_saabb + 8 * s; mn = ld3(a); mx = ld3(a + 4); }
 }
 
@@ -1148,6 +1154,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     for (int i = lane; i < nold; i += 64)
         L.u.c.okey[i] = (int)gcp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gcp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     SYNC();
+#ifndef AVR_CAABB_ONDEMAND
     // world AABBs of the non-static child shapes
     for (int s = lane; s < m.ns; s += 64) {
         const int c = m.shape_cidx[s];
@@ -1158,6 +1165,7 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
             st3(L.u.c.caabb[c] + 3, mx);
         }
     }
+#endif
     // broadphase over the candidate pair list, order-preserving compaction
     int nap = 0;
     const int npe = L.nla > m.nl ? m.np : m.np_base;   // chain-vs-static pairs: 'tremor' envs only
@@ -2331,14 +2339,26 @@ __global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restr
 // parts D ahead); impulses and the friction lists live in LDS (6.7 KB per block), so all 1024
 // blocks of a 4096-env launch are resident at once.  (Staging the rows in LDS instead, 79.5 KB per
 // block, measured slower: 2 blocks per CU.)
+// LDS per group: impulses [rowcap + 2 null slots], friction list [96 ints], then the first B4_SR
+// records and B4_SP robot parts of the env's row set (staged copies; the rest stays in global
+// memory).  4 groups x 2540 words = 39.7 KB per block: 4 blocks per CU, all blocks resident.
 #define B4_IMPNULL (MAXNC + 3 * AVR_MAX_CONTACTS)    // null-row impulse slots (2)
-#define B4_LISTW 324                                 // friction active list (ints) after the impulses
-#define B4_WORDS (B4_LISTW + AVR_MAX_CONTACTS)
+#define B4_LISTW 324
+#define B4_RECW (B4_LISTW + AVR_MAX_CONTACTS)
+#ifndef B4_SR
+#define B4_SR 68
+#endif
+#ifndef B4_SP
+#define B4_SP 24
+#endif
+#define B4_ROBW (B4_RECW + B4_SR * RWC)
+#define B4_WORDS (B4_ROBW + B4_SP * ROBW)
 #ifndef B4_GD
 #define B4_GD 2          // software-pipeline depth (measured: 2 beats 3 and 5)
 #endif
 static_assert(B4_WORDS % 4 == 0, "group regions must stay 16-byte aligned");
 static_assert(B4_IMPNULL + 2 <= B4_LISTW, "the impulse array fits below the list");
+static_assert(4 * B4_WORDS * 4 <= 40960, "four blocks per CU");
 
 // null records + zero block for the global-memory path (info = no endpoint, slot = -1); read only
 __device__ int avr_b4_null[2 * RWC + 32] = {RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -2351,12 +2371,13 @@ struct Row4 { P p; lds_f *ip; f4v h0, h1; float imp; f2v j0, j1, j2, r; };
 
 // Row source: records from the env's row buffer (read only), impulses in the group's LDS region.
 struct B4Glb {
-    typedef const float *P;
-    const float *rec, *robb;
+    typedef const float *P;           // generic: staged rows resolve to LDS, the rest to global
+    const float *rec, *robb;          // global row buffer: records, robot parts
+    const float *lrec, *lrob;         // staged copies (generic pointers into this group's LDS)
     lds_f *imp;
     AVR_DI lds_f *ipp(int r) const { return imp + r; }
     AVR_DI void at(Row4<P> &R, int r, int pair) const {
-        R.p = r >= 0 ? rec + r * RWC : (const float *)avr_b4_null + pair * RWC;
+        R.p = r < 0 ? (const float *)avr_b4_null + pair * RWC : (r < B4_SR ? lrec : rec) + r * RWC;
         R.ip = imp + (r >= 0 ? r : B4_IMPNULL + pair);
     }
     AVR_DI P zero() const { return (const float *)avr_b4_null + 2 * RWC; }
@@ -2365,7 +2386,9 @@ struct B4Glb {
         const P q = off >= 0 ? p + off : zero();
         a = *(const f2v *)q; b = *(const f2v *)(q + 2); c = *(const f2v *)(q + 4);
     }
-    AVR_DI f2v robot(int slot) const { return *(const f2v *)(slot >= 0 ? robb + slot * ROBW + 2 * (lane_id() & 15) : zero()); }
+    AVR_DI f2v robot(int slot) const {
+        return *(const f2v *)(slot < 0 ? zero() : (slot < B4_SP ? lrob : robb) + slot * ROBW + 2 * (lane_id() & 15));
+    }
 };
 
 // sum over the 16 lanes of each DPP row, result in every lane of the row
@@ -2541,13 +2564,37 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     __syncthreads();
 #endif
     DV d;
-    // starting impulses (record word 6) into the LDS impulse array, null slots zero
+    // starting impulses (record word 6) into the LDS impulse array, null slots zero; the first
+    // B4_SR records and B4_SP robot parts staged (8 loads in flight per lane)
     for (int r = sl; r < n_rows; r += 16) gb[r] = rows[r * RWC + 6];
     if (sl < 2) gb[B4_IMPNULL + sl] = 0.f;
+    {
+        const int n_rob = live ? __float_as_int(ws[WS_NROB]) : 0;
+        const int n4r = min(n_rows, B4_SR) * (RWC / 4), n4s = min(n_rob, B4_SP) * (ROBW / 4);
+        const int m4 = wmax(n4r + n4s);
+        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
+        lds_f4 *l0 = (lds_f4 *)(gb + B4_RECW), *l1 = (lds_f4 *)(gb + B4_ROBW);
+        for (int b = 0; b < m4; b += 8 * 16) {
+            f4v t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = b + 16 * q + sl;
+                t[q] = i < n4r ? g0[i] : (i < n4r + n4s ? g1[i - n4r] : g0[0]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int i = b + 16 * q + sl;
+                if (i < n4r) l0[i] = t[q];
+                else if (i < n4r + n4s) l1[i - n4r] = t[q];
+            }
+        }
+    }
     __syncthreads();
     B4Glb s;
     s.rec = rows;
     s.robb = rows + m.rowcap * RWC;
+    s.lrec = (const float *)(gb + B4_RECW);
+    s.lrob = (const float *)(gb + B4_ROBW);
     s.imp = gb;
     pgs4<B4_GD>(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
     // normal impulses back to the manifold points (warm start + normalForce)
