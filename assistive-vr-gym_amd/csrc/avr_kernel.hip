@@ -56,9 +56,7 @@ struct EnvLDS {
             int okey[AVR_MAX_CONTACTS];    // (sa | sb << 16) of the previous contact pool
             int qk[128], qp[128];          // shape-pair queue: (sa | sb << 16), body pair
             int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
-#ifndef AVR_CAABB_ONDEMAND
             float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
-#endif
         } c;
         struct {
             float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
@@ -1019,11 +1017,7 @@ AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, 
 
 AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, v3 &mn, v3 &mx) {
     const int c = m.shape_cidx[s];
-#ifdef AVR_CAABB_ONDEMAND   // experiment: world AABB of a non-static child computed where it is used
-    if (c >= 0) shape_aabb(m, s, ldtf(L.btf[m.shape_body[s]]), mn, mx);
-#else
     if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
-#endif
     else { const float *a = m.static_saabb + 8 * s; mn = ld3(a); mx = ld3(a + 4); }
 }
 
@@ -1154,7 +1148,6 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     for (int i = lane; i < nold; i += 64)
         L.u.c.okey[i] = (int)gcp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gcp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     SYNC();
-#ifndef AVR_CAABB_ONDEMAND
     // world AABBs of the non-static child shapes
     for (int s = lane; s < m.ns; s += 64) {
         const int c = m.shape_cidx[s];
@@ -1165,7 +1158,6 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
             st3(L.u.c.caabb[c] + 3, mx);
         }
     }
-#endif
     // broadphase over the candidate pair list, order-preserving compaction
     int nap = 0;
     const int npe = L.nla > m.nl ? m.np : m.np_base;   // chain-vs-static pairs: 'tremor' envs only
