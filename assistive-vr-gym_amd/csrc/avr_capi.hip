@@ -354,12 +354,19 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     size_t E = (size_t)cfg->n_envs;
     // per-env constraint-row scratch (written and read inside each sub-step)
     k.rowcap = MAXNC + 3 * AVR_MAX_CONTACTS;
+    // records [rowcap][20] then robot parts [rowcap][32]; AVR_ROW_STRIDE (floats) overrides the
+    // per-env stride for experiments (it must cover 52 * rowcap floats, 16-byte aligned)
+    k.rowstride = 2 * k.rowcap * 32;
+    if (const char *e = getenv("AVR_ROW_STRIDE")) {
+        const int v = atoi(e);
+        if (v >= 52 * k.rowcap && v % 4 == 0) k.rowstride = v;
+    }
     {
         float *rows = nullptr;
-        HIPCHK(s, hipMalloc(&rows, E * 2 * (size_t)k.rowcap * 32 * sizeof(float)));
+        HIPCHK(s, hipMalloc(&rows, E * (size_t)k.rowstride * sizeof(float)));
         s->allocs.push_back(rows);
         // diagnostic: NaN-fill the row scratch so that a read of a word no kernel wrote shows
-        if (getenv("AVR_DEBUG_NANFILL")) HIPCHK(s, hipMemset(rows, 0xFF, E * 2 * (size_t)k.rowcap * 32 * sizeof(float)));
+        if (getenv("AVR_DEBUG_NANFILL")) HIPCHK(s, hipMemset(rows, 0xFF, E * (size_t)k.rowstride * sizeof(float)));
         k.rows = rows;
         float *ws = nullptr;
         HIPCHK(s, hipMalloc(&ws, E * 128 * sizeof(float)));

@@ -2077,7 +2077,7 @@ AVR_DI int xcc_id() {   // XCD of the executing CU (HW_REG_XCC_ID, id 20, bits 3
 #endif
 
 AVR_DI float *env_ws(const KModel &m, int env) { return m.ws + (size_t)env * WS_WORDS; }
-AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)(2 * m.rowcap * RW); }
+AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)m.rowstride; }
 
 AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[AVR_S_TASK + AVR_T_HDYN] != 0.f; }
 

@@ -72,6 +72,7 @@ struct KModel {
     float hc_lower[AVR_HC_N], hc_upper[AVR_HC_N], human_gain, human_force;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
     int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
+    int rowstride;             // floats between consecutive envs' row buffers
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
     int b_variant;             // part B kernel: 4 = four envs per wave, 1 = one env per wave
