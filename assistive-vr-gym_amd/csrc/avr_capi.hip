@@ -162,8 +162,9 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     HIPCHK(s, hipSetDevice(cfg->device));
     HIPCHK(s, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     {
-        // default 1: concurrent env groups gained ~4 %, and every wrong-result run observed so
-        // far ran them; opt in with AVR_ENV_GROUPS=2..8
+        // default 1: with the four-env part B, 2 / 4 concurrent groups measure 347k / 239k vs 355k
+        // env-steps/s (their earlier wrong results were the uninitialized-LDS read fixed in part A,
+        // DESIGN.md); opt in with AVR_ENV_GROUPS=2..8
         const char *g = getenv("AVR_ENV_GROUPS");
         int ng = g ? atoi(g) : 1;
         if (ng < 1) ng = 1;
