@@ -22,8 +22,7 @@ EXPORTS = [
 ]
 
 
-# avr_config.flags bits (include/avr.h)
-CFG_B_ONE_ENV_PER_WAVE = 1    # part B as one env per wavefront (default: four envs per wavefront)
+# avr_config.flags: no bit is defined (include/avr.h); avr_create rejects any set bit
 
 
 class avr_config(C.Structure):
@@ -87,14 +86,11 @@ class Sim:
     """One libavr handle = one GPU, n_envs environments."""
 
     def __init__(self, md, n_envs, device=0, seed=1001, env_offset=0, flags=0):
-        """flags: CFG_B_* bits (include/avr.h AVR_CFG_*); 0 = defaults (part B four envs per wave)."""
+        """flags: avr_config.flags, must be 0 (include/avr.h)."""
         self.lib = load()
         self.md = md
         self.n = int(n_envs)
-        ev = os.environ.get('AVR_KERNEL_B', '')[:1]
-        b1 = ev == '1' or (ev != '4' and bool(flags & CFG_B_ONE_ENV_PER_WAVE))
-        self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel',
-                             'avr_substep_b_kernel' if b1 else 'avr_substep_b4_kernel', 'avr_task_kernel')
+        self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel')
         cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))

@@ -25,23 +25,57 @@ def _hipcc():
     raise RuntimeError('hipcc not found')
 
 
-def _stale(target, deps):
+def _stale(target, deps, cmd):
+    """Rebuild when the target is missing, older than a dependency, or was built by a different
+    command line (recorded in <target>.cmd: flags and sources, so a flag change rebuilds)."""
     if not os.path.exists(target):
+        return True
+    side = target + '.cmd'
+    if not os.path.exists(side) or open(side).read() != ' '.join(cmd):
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+_PROBED = {}
+
+
+def _supported(flags):
+    """True if hipcc accepts `flags` (probed once per flag set on an empty gfx950 kernel)."""
+    key = tuple(flags)
+    if key not in _PROBED:
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            src = os.path.join(d, 'p.hip')
+            open(src, 'w').write('__global__ void k() {}\n')
+            r = subprocess.run([_hipcc(), '--offload-arch=%s' % ARCH, '--cuda-device-only', '-c', '-o', os.path.join(d, 'p.o'), src] + list(flags),
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            _PROBED[key] = r.returncode == 0
+    return _PROBED[key]
+
+
+# AMDGPU register-pressure trackers in the scheduler: part B 0.590 -> 0.564 ms, A 0.552 -> 0.560 ms,
+# 356k -> 361k env-steps/s (round 1, tools/gpu_flags.sh VARIANTS=trackers).  An internal LLVM
+# option: dropped (with a warning) when this hipcc does not know it.
+TRACKERS = ('-mllvm', '-amdgpu-use-amdgpu-trackers=1')
+
+
+def lib_cmd(extra=(), out=LIB):
+    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result', '-fno-slp-vectorize']
+    if _supported(TRACKERS):
+        cmd += list(TRACKERS)
+    else:
+        sys.stderr.write('avr.build: hipcc does not accept %s; building without it\n' % ' '.join(TRACKERS))
+    return cmd + ['-o', out] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
+
+
 def build_lib(force=False, extra=(), out=LIB):
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')]
-    if not force and not _stale(out, deps):
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')] + [os.path.abspath(__file__)]
+    cmd = lib_cmd(extra, out)
+    if not force and not _stale(out, deps, cmd):
         return out
-    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result', '-fno-slp-vectorize',
-           # AMDGPU register-pressure trackers in the scheduler: part B 0.590 -> 0.564 ms, A 0.552 -> 0.560 ms,
-           # 356k -> 361k env-steps/s (tools/gpu_flags.sh, VARIANTS=trackers)
-           '-mllvm', '-amdgpu-use-amdgpu-trackers=1',
-           '-o', out] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
     subprocess.check_call(cmd)
+    open(out + '.cmd', 'w').write(' '.join(cmd))
     return out
 
 

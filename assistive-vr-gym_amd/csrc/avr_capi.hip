@@ -147,6 +147,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     memset(s->err, 0, sizeof(s->err));
     s->cfg = *cfg;
     if (cfg->n_envs <= 0) { int r = fail(s, -1, "n_envs must be > 0"); *out = s; return r; }
+    if (cfg->flags & AVR_CFG_RESERVED_MASK) { int r = fail(s, -1, "avr_config.flags 0x%x: no flag is defined", (unsigned)cfg->flags); *out = s; return r; }
     const int hc = d->hc_n > 0 ? d->hc_n : 0;
     if (d->n_links + hc > AVR_MAX_LINKS || d->n_dof + hc > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
         d->n_bodies > MAXB || d->n_arm > AVR_ACT_DIM || hc > AVR_HC_N) {
@@ -331,9 +332,6 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     for (int g = 0; g < 2; g++)
         for (int i = 0; i < 3; i++) k.mouth[g][i] = (float)d->mouth_offset[g][i];
     k.time_step = (float)d->time_step;
-    // part B variant (AVR_CFG_B_*); AVR_KERNEL_B=1 / =4 overrides it for experiments
-    k.b_variant = (cfg->flags & AVR_CFG_B_ONE_ENV_PER_WAVE) ? 1 : 4;
-    if (const char *e = getenv("AVR_KERNEL_B")) k.b_variant = e[0] == '1' ? 1 : 4;
     k.nsub = d->num_sub_steps; k.frame_skip = d->frame_skip; k.iters = d->solver_iterations; k.max_steps = d->max_episode_steps;
     k.erp = (float)d->erp; k.warmstart = (float)d->warmstart; k.lin_damp = (float)d->linear_damping; k.ang_damp = (float)d->angular_damping;
     k.max_vel = (float)d->max_coord_vel; k.robot_gain = (float)d->robot_gain; k.robot_force = (float)d->robot_force;
@@ -355,12 +353,14 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     size_t E = (size_t)cfg->n_envs;
     // per-env constraint-row scratch (written and read inside each sub-step)
     k.rowcap = MAXNC + 3 * AVR_MAX_CONTACTS;
-    // records [rowcap][20] then robot parts [rowcap][32]; AVR_ROW_STRIDE (floats) overrides the
-    // per-env stride for experiments (it must cover 52 * rowcap floats, 16-byte aligned)
-    k.rowstride = 2 * k.rowcap * 32;
-    if (const char *e = getenv("AVR_ROW_STRIDE")) {
-        const int v = atoi(e);
-        if (v >= 52 * k.rowcap && v % 4 == 0) k.rowstride = v;
+    // records [rowcap][20] then robot parts [rowcap][32]; part B reads the whole row buffer
+    // through one buffer resource with 32-bit byte offsets below B4_OOB (avr_kernel.hip)
+    k.rowstride = 52 * k.rowcap;
+    k.rows_envs = (int)E;
+    k.b4_global = getenv("AVR_B4_GLOBAL") && getenv("AVR_B4_GLOBAL")[0] == '1';
+    if (E * (size_t)k.rowstride * sizeof(float) >= 0x7fff0000ull) {
+        int r = fail(s, -2, "n_envs %d exceeds the row-buffer addressing limit (%d per handle)", cfg->n_envs, (int)(0x7fff0000ull / (k.rowstride * sizeof(float))));
+        return r;
     }
     {
         float *rows = nullptr;

@@ -1366,17 +1366,28 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 }
 
 
-// Constraint rows live in a per-env buffer in global memory, one 20-word record per row, in
-// solve order [non-contact][normals][frictions]:
-//   w0 info (iA | iB<<6 | robot<<12; 63 = endpoint is not a free body)   w1 friction coeff
-//   w2 inv   w3 rhs   w4 lo   w5 hi   w6 initial impulse   w7 robot slot (int bits, -1: none)
+// Constraint rows live in a per-env buffer in global memory, in solve order [non-contact]
+// [normals][frictions].  A row's `info` names its free-body endpoints as 1-based body indices
+// (bits 0-5: endpoint A, bits 6-11: endpoint B, 0 = not a free body) and bit 12 marks an
+// articulated endpoint; an all-zero header is a null row (no endpoint, inv = rhs = lo = hi = 0).
+// Non-contact rows have 20-word records at word 20 r:
+//   w0 info   w1 robot slot + 1 (int bits, 0: none)   w2 inv   w3 rhs   w4 lo   w5 hi
 //   w8..13 free A Jacobian (lin, ang)   w14..19 free B Jacobian
-// Rows with an articulated endpoint own a robot part (slot): 16 (J[d], M^-1 J^T[d]) pairs, A and
-// B endpoints combined.  Non-contact rows take slots 0 .. n_nc-1, robot contacts 3 consecutive
-// slots each.  The free bodies' M^-1 J^T is not stored: part B forms it on the owner lane from
-// the body's inverse mass and world inverse inertia (the row set then fits in LDS there).
+// Contact rows (row n_nc + k, k = c for contact c's normal, n_c + 2c + {0,1} for its frictions)
+// have 16-word records at word CR_BASE + 16 k:
+//   w0 info | (robot slot + 1) << 13   w1 inv   w2 rhs   w3 friction coefficient
+//   w4..9 free A Jacobian   w10..15 free B Jacobian
+// (normal rows clamp to [0, 1e10], frictions to +-friction * normal impulse; the normal row's
+// starting impulse is the manifold point's cached impulse x warm-start factor, read by part B
+// from the contact pool).  Rows with an articulated endpoint own a robot part (slot): 16 (J[d],
+// M^-1 J^T[d]) pairs, A and B endpoints combined.  Non-contact rows take slots 0 .. n_nc-1,
+// robot contacts 3 consecutive slots each.  The free bodies' M^-1 J^T is not stored: part B
+// forms it on the owner lane from the mass-normalised part (see put_free).
 #define RW 32       // allocation unit of the per-env row buffer (2 * rowcap * RW floats)
-#define RWC 20      // words per row record
+#define RWC 20      // words per non-contact record
+#define CRW 16      // words per contact record
+#define CR_BASE (MAXNC * RWC)
+#define CI_SLOT 13  // contact info: robot slot + 1 from this bit
 #define ROBW 32     // words per robot part
 // per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
 #define WS_WORDS 128
@@ -1388,10 +1399,12 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW 72     // [MAXF][4] angular
-#define RI_NONE 63
+#define RI_FREE(f) ((f) + 1)    // info: free body f as an endpoint (0 = none)
 #define RI_ROBOT (1 << 12)
+static_assert(CR_BASE + 3 * AVR_MAX_CONTACTS * CRW <= (MAXNC + 3 * AVR_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
 
 AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RWC; }
+AVR_DI float *row_crec(float *base, int k) { return base + CR_BASE + k * CRW; }
 AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.rowcap * RWC + slot * ROBW; }
 
 // A free endpoint's part is stored mass-normalised: g = (jl / sqrt(m), D^1/2 R^T ja) with
@@ -1409,8 +1422,8 @@ AVR_DI void put_free_zero(float *w) {
 #pragma unroll
     for (int k = 0; k < 6; k++) w[k] = 0.f;
 }
-AVR_DI void put_hdr(float *w, int info, float fric, float inv, float rhs, float lo, float hi, float imp0, int slot) {
-    w[0] = __int_as_float(info); w[1] = fric; w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = imp0; w[7] = __int_as_float(slot);
+AVR_DI void put_hdr(float *w, int info, float inv, float rhs, float lo, float hi, int slot) {
+    w[0] = __int_as_float(info); w[1] = __int_as_float(slot + 1); w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = 0.f; w[7] = 0.f;
 }
 AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 #pragma unroll
@@ -1466,13 +1479,13 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         const float rel = sg * L.vq[dof];
         float *w = row_rec(m, rows, lane);
         if (kind < 2) {
-            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, 0.f, lane);
+            put_hdr(w, RI_ROBOT, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, lane);
         } else {
             const float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
             const float kp = L.st[AVR_S_KP + dof], kd = 1.f;
             const float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
             const float mi = L.st[AVR_S_MAXIMP + dof];
-            put_hdr(w, RI_NONE | (RI_NONE << 6) | RI_ROBOT, 0.f, inv, (desired - rel) * inv, -mi, mi, 0.f, lane);
+            put_hdr(w, RI_ROBOT, inv, (desired - rel) * inv, -mi, mi, lane);
         }
         put_free_zero(w + 8); put_free_zero(w + 14);
         put_robot(row_rob(m, rows, lane), J, MJ);
@@ -1521,7 +1534,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         rel += free_dot(L, fb, jbl, jba);
         const float mi = m.fixed_max_imp;
         float *w = row_rec(m, rows, lane);
-        put_hdr(w, RI_NONE | (fb << 6) | RI_ROBOT, 0.f, inv, (-pos * erp / dt - rel) * inv, -mi, mi, 0.f, lane);
+        put_hdr(w, (RI_FREE(fb) << 6) | RI_ROBOT, inv, (-pos * erp / dt - rel) * inv, -mi, mi, lane);
         put_free_zero(w + 8);
         put_free(L, fb, w + 14, jbl, jba);
         put_robot(row_rob(m, rows, lane), JA, MA);
@@ -1583,13 +1596,12 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         plane_space(n, t1, t2);
         v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
         float fric = fminf(m.body_friction[ba] * m.body_friction[bb], 10.f);
-        int info = (kA == 2 ? iA : RI_NONE) | ((kB == 2 ? iB : RI_NONE) << 6) | (rob ? RI_ROBOT : 0);
+        int info = (kA == 2 ? RI_FREE(iA) : 0) | ((kB == 2 ? RI_FREE(iB) : 0) << 6) | (rob ? RI_ROBOT : 0);
         float imA = kA == 2 ? 1.f / m.fb_mass[iA] : 0.f, imB = kB == 2 ? 1.f / m.fb_mass[iB] : 0.f;
         for (int k = 0; k < 3; k++) {
             v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
-            int row = k == 0 ? n_nc + i : n_nc + ncp + 2 * i + (k - 1);
             const int slot = rob ? slot0 + k : -1;
-            float *w = row_rec(m, rows, row);
+            float *w = row_crec(rows, k == 0 ? i : ncp + 2 * i + (k - 1));
             float den = 0.f, rel = 0.f;
             float J[MAXD], MJ[MAXD];
 #pragma unroll
@@ -1600,13 +1612,13 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 minv_mul(L, Ja, Ma);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; J[d] += Ja[d]; MJ[d] += Ma[d]; }
-                put_free_zero(w + 8);
+                put_free_zero(w + 4);
             } else if (kA == 2) {
                 v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
                 den += dot(dir, ml) + dot(ja, ma);
                 rel += free_dot(L, iA, dir, ja);
-                put_free(L, iA, w + 8, dir, ja);
-            } else put_free_zero(w + 8);
+                put_free(L, iA, w + 4, dir, ja);
+            } else put_free_zero(w + 4);
             v3 nd = scl(dir, -1.f);
             if (kB == 1) {
                 float Jb[MAXD], Mb[MAXD];
@@ -1614,298 +1626,28 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 minv_mul(L, Jb, Mb);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; J[d] += Jb[d]; MJ[d] += Mb[d]; }
-                put_free_zero(w + 14);
+                put_free_zero(w + 10);
             } else if (kB == 2) {
                 v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
                 den += dot(nd, ml) + dot(jb, mb);
                 rel += free_dot(L, iB, nd, jb);
-                put_free(L, iB, w + 14, nd, jb);
-            } else put_free_zero(w + 14);
+                put_free(L, iB, w + 10, nd, jb);
+            } else put_free_zero(w + 10);
             if (rob) put_robot(row_rob(m, rows, slot), J, MJ);
             float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
+            float rhs = -rel * inv;
             if (k == 0) {
                 float pen = c[AVR_CP_DIST];
                 float velerr = -rel, poserr = 0.f;
                 if (pen > 0.f) velerr -= pen / dt;
                 else poserr = -pen * erp / dt;
-                put_hdr(w, info, fric, inv, (poserr + velerr) * inv, 0.f, 1e10f, c[AVR_CP_IMP] * m.warmstart, slot);
-            } else {
-                put_hdr(w, info, fric, inv, -rel * inv, 0.f, 0.f, 0.f, slot);
+                rhs = (poserr + velerr) * inv;
             }
+            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs; w[3] = fric;
         }
     }
     if (lane == 0) L.n_c = ncp;
     return nrob;
-}
-
-// ---------------------------------------------------------------------------- PGS solve
-// Delta velocities live in registers, distributed over lanes: lane d < nd holds the robot's
-// dq[d]; lane f < nf holds free body f's (dv, dw).  A row's uniform data (header, free-body
-// Jacobians) arrives through the scalar cache (s_load into SGPRs); each endpoint's owner lane
-// forms its partial J.dv against its own registers, one 16-lane DPP reduction sums them, and
-// the owner lanes apply M^-1 J^T delta.  No LDS access and no barrier on the row-to-row chain.
-struct DV { float rq, vx, vy, vz, wx, wy, wz; };
-
-AVR_DI float rdl(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
-AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-AVR_DI float unif(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-AVR_DI float dpp_shr(float x, int n) {
-    int v = __float_as_int(x);
-    int r;
-    switch (n) {
-    case 1: r = __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true); break;
-    case 2: r = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true); break;
-    case 4: r = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true); break;
-    default: r = __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true); break;
-    }
-    return __int_as_float(r);
-}
-// sum over lanes 0..15 (lanes >= 16 must pass 0), broadcast as a uniform value
-AVR_DI float robot_reduce(float x) {
-    x += dpp_shr(x, 1);
-    x += dpp_shr(x, 2);
-    x += dpp_shr(x, 4);
-    x += dpp_shr(x, 8);
-    return rdl(x, 15);
-}
-
-// Part B keeps the row set in LDS: the wave copies its records (and robot parts) in with
-// many loads in flight, then every row of the Gauss-Seidel chain resolves from LDS reads issued
-// one row (parts) / two rows (headers) ahead.  An env whose row set exceeds the LDS capacity
-// (> B_CAPR rows or > B_CAPS robot parts, rare) runs the same solver on the global buffer.
-#ifndef B_CAPR
-#define B_CAPR 192
-#endif
-#ifndef B_CAPS
-#define B_CAPS 32
-#endif
-#define B_LDS_WORDS (B_CAPR * RWC + B_CAPS * ROBW + 16)
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) float lds_f;
-typedef __attribute__((address_space(3))) f2v lds_f2;
-typedef __attribute__((address_space(3))) f4v lds_f4;
-typedef __attribute__((address_space(3))) int lds_i;
-typedef const __attribute__((address_space(1))) float *gfp;
-typedef const __attribute__((address_space(1))) f4v *gf4p;
-typedef const __attribute__((address_space(1))) f2v *gf2p;
-
-// row sources: rec(r) = record base, own part = 3 x f2v at word 8 (endpoint A) / 14 (B),
-// robot part = f2v (J, M^-1 J^T) of DoF `lane` at slot.  The zero block stands in for "not mine".
-struct LdsRows {
-    const lds_f *rec, *rob, *zero;
-    AVR_DI void hdr(int r, f4v &h0, f4v &h1) const { const lds_f4 *p = (const lds_f4 *)(rec + r * RWC); h0 = p[0]; h1 = p[1]; }
-    AVR_DI void own(int r, int off, f2v &a, f2v &b, f2v &c) const {
-        const lds_f *p = off >= 0 ? rec + r * RWC + off : zero;
-        a = *(const lds_f2 *)p; b = *(const lds_f2 *)(p + 2); c = *(const lds_f2 *)(p + 4);
-    }
-    AVR_DI f2v robot(int slot, bool mine) const { return *(const lds_f2 *)(mine ? rob + slot * ROBW + 2 * lane_id() : zero); }
-    // the two friction rows r, r + 1 of one contact: same endpoints, consecutive robot slots
-    AVR_DI void own2(int r, int off, f2v *a, f2v *b) const {
-        const lds_f *p = off >= 0 ? rec + r * RWC + off : zero;
-        const lds_f *q = off >= 0 ? p + RWC : zero;
-        a[0] = *(const lds_f2 *)p; a[1] = *(const lds_f2 *)(p + 2); a[2] = *(const lds_f2 *)(p + 4);
-        b[0] = *(const lds_f2 *)q; b[1] = *(const lds_f2 *)(q + 2); b[2] = *(const lds_f2 *)(q + 4);
-    }
-    AVR_DI void robot2(int slot, bool mine, f2v &a, f2v &b) const {
-        const lds_f *p = mine ? rob + slot * ROBW + 2 * lane_id() : zero;
-        const lds_f *q = mine ? p + ROBW : zero;
-        a = *(const lds_f2 *)p; b = *(const lds_f2 *)q;
-    }
-};
-struct GlbRows {
-    const float *rec, *rob;
-    AVR_DI void hdr(int r, f4v &h0, f4v &h1) const { const gf4p p = (gf4p)(rec + r * RWC); h0 = p[0]; h1 = p[1]; }
-    AVR_DI void own(int r, int off, f2v &a, f2v &b, f2v &c) const {
-        const gf2p p = (gf2p)(rec + r * RWC + (off >= 0 ? off : 0));
-        const f2v z = {0.f, 0.f}, x = p[0], y = p[1], w = p[2];
-        a = off >= 0 ? x : z; b = off >= 0 ? y : z; c = off >= 0 ? w : z;
-    }
-    AVR_DI f2v robot(int slot, bool mine) const {
-        const f2v z = {0.f, 0.f}, x = ((gf2p)(rob + (slot > 0 ? slot : 0) * ROBW))[lane_id() & 15];
-        return mine ? x : z;
-    }
-    AVR_DI void own2(int r, int off, f2v *a, f2v *b) const { own(r, off, a[0], a[1], a[2]); own(r + 1, off, b[0], b[1], b[2]); }
-    AVR_DI void robot2(int slot, bool mine, f2v &a, f2v &b) const { a = robot(slot, mine); b = robot(slot + 1, mine); }
-};
-
-// one row as this lane sees it: header (wave-uniform), its own free part (zero unless the lane
-// owns endpoint A or B), its own robot DoF's (J, M^-1 J^T)
-struct RowV { f4v h0, h1; f2v j0, j1, j2, r; };
-
-template <class SRC>
-AVR_DI void row_parts(const SRC &S, int r, RowV &R) {
-    const int lane = lane_id();
-    const int info = __builtin_amdgcn_readfirstlane(__float_as_int(R.h0.x));
-    const int slot = __builtin_amdgcn_readfirstlane(__float_as_int(R.h1.w));
-    const int off = lane == (info & 63) ? 8 : (lane == ((info >> 6) & 63) ? 14 : -1);
-    S.own(r, off, R.j0, R.j1, R.j2);
-    R.r = S.robot(slot, slot >= 0 && lane < 16);
-}
-
-// Free-body velocity increments are kept mass-normalised on the owner lane (see put_free):
-// J.dv = g.(v~, w~), and the update is (v~, w~) += g delta.
-
-// one row: returns the clamped impulse and applies the increment
-AVR_DI float row_go(const RowV &R, DV &d, float imp, float lo, float hi) {
-    float p = R.j0.x * d.vx + R.j0.y * d.vy + R.j1.x * d.vz;
-    float q = R.j1.y * d.wx + R.j2.x * d.wy + R.j2.y * d.wz;
-    p += q + R.r.x * d.rq;
-    const float dv = robot_reduce(p);
-    const float ni = __builtin_amdgcn_fmed3f(imp + (R.h0.w - dv * R.h0.z), lo, hi);
-    const float delta = ni - imp;
-    d.vx += R.j0.x * delta; d.vy += R.j0.y * delta; d.vz += R.j1.x * delta;
-    d.wx += R.j1.y * delta; d.wy += R.j2.x * delta; d.wz += R.j2.y * delta;
-    d.rq += R.r.y * delta;
-    return ni;
-}
-
-template <class SRC>
-AVR_DI void row_fetch(const SRC &S, int r, RowV &R) { S.hdr(r, R.h0, R.h1); row_parts(S, r, R); }
-
-// the parts of a contact's two friction rows (headers in A.h*, B.h*), addressed once
-template <class SRC>
-AVR_DI void pair_parts(const SRC &S, int r, RowV &A, RowV &B) {
-    const int lane = lane_id();
-    const int info = __builtin_amdgcn_readfirstlane(__float_as_int(A.h0.x));
-    const int slot = __builtin_amdgcn_readfirstlane(__float_as_int(A.h1.w));
-    const int off = lane == (info & 63) ? 8 : (lane == ((info >> 6) & 63) ? 14 : -1);
-    f2v a[3], b[3];
-    S.own2(r, off, a, b);
-    A.j0 = a[0]; A.j1 = a[1]; A.j2 = a[2];
-    B.j0 = b[0]; B.j1 = b[1]; B.j2 = b[2];
-    S.robot2(slot, slot >= 0 && lane < 16, A.r, B.r);
-}
-
-// friction sweep over n active contacts, unit u = rows r(u), r(u) + 1: headers two units ahead,
-// parts one unit ahead (three rotating unit buffers)
-template <class SRC, class IDX, class GO>
-AVR_DI void sweep_pairs(const SRC &S, int n, const IDX &idx, const GO &go) {
-    if (n <= 0) return;
-    RowV A0, A1, B0, B1, C0, C1;
-#define AVR_PHDR(u, X0, X1) do { const int _r = idx(u); S.hdr(_r, X0.h0, X0.h1); S.hdr(_r + 1, X1.h0, X1.h1); } while (0)
-    AVR_PHDR(0, A0, A1);
-    if (n > 1) AVR_PHDR(1, B0, B1);
-    pair_parts(S, idx(0), A0, A1);
-    for (int u = 0;;) {
-        if (u + 2 < n) AVR_PHDR(u + 2, C0, C1);
-        if (u + 1 < n) pair_parts(S, idx(u + 1), B0, B1);
-        go(u, A0, A1);
-        if (++u >= n) break;
-        if (u + 2 < n) AVR_PHDR(u + 2, A0, A1);
-        if (u + 1 < n) pair_parts(S, idx(u + 1), C0, C1);
-        go(u, B0, B1);
-        if (++u >= n) break;
-        if (u + 2 < n) AVR_PHDR(u + 2, B0, B1);
-        if (u + 1 < n) pair_parts(S, idx(u + 1), A0, A1);
-        go(u, C0, C1);
-        if (++u >= n) break;
-    }
-#undef AVR_PHDR
-}
-
-// A sweep over n rows idx(0..n-1) resolved by go(j, row): headers are fetched two rows ahead,
-// the header-dependent parts one row ahead, through three rotating buffers (no register copies).
-template <class SRC, class IDX, class GO>
-AVR_DI void sweep(const SRC &S, int n, const IDX &idx, const GO &go) {
-    if (n <= 0) return;
-    RowV A, B, C;
-    S.hdr(idx(0), A.h0, A.h1);
-    if (n > 1) S.hdr(idx(1), B.h0, B.h1);
-    row_parts(S, idx(0), A);
-    for (int j = 0;;) {
-        if (j + 2 < n) S.hdr(idx(j + 2), C.h0, C.h1);
-        if (j + 1 < n) row_parts(S, idx(j + 1), B);
-        go(j, A);
-        if (++j >= n) break;
-        if (j + 2 < n) S.hdr(idx(j + 2), A.h0, A.h1);
-        if (j + 1 < n) row_parts(S, idx(j + 1), C);
-        go(j, B);
-        if (++j >= n) break;
-        if (j + 2 < n) S.hdr(idx(j + 2), B.h0, B.h1);
-        if (j + 1 < n) row_parts(S, idx(j + 1), A);
-        go(j, C);
-        if (++j >= n) break;
-    }
-}
-
-// Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order):
-// non-contact rows (sweep direction alternates per iteration), normal rows, friction rows.
-// Impulses are lane-distributed registers: nc row j -> lane j of inc; normal c -> lane c&63 of
-// in0 (c < 64) / in1; friction row 2c+k -> lane c&63 of fk0 / fk1.  Returns the delta velocities
-// in d and the normal impulses in in0/in1.  `list` (LDS, 96 ints) holds the active contacts.
-template <class SRC>
-AVR_DI void pgs_solve(const KModel &m, const SRC &S, int *list, int n_nc, int n_c, DV &d, float &in0, float &in1) {
-    const int lane = lane_id();
-    d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
-    float inc = 0.f, f00 = 0.f, f01 = 0.f, f10 = 0.f, f11 = 0.f;
-    // warm start (normal rows, contact order): impulse = cached * warmstart factor
-    {
-        f4v h0, h1;
-        float w0 = 0.f, w1 = 0.f;
-        if (lane < n_c) { S.hdr(n_nc + lane, h0, h1); w0 = h1.z; }
-        if (lane + 64 < n_c) { S.hdr(n_nc + 64 + lane, h0, h1); w1 = h1.z; }
-        in0 = w0; in1 = w1;
-        unsigned long long m0 = __ballot(w0 != 0.f), m1 = __ballot(w1 != 0.f);
-        while (m0 | m1) {
-            const int c = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
-            if (c < 64) m0 &= m0 - 1; else m1 &= m1 - 1;
-            RowV R;
-            row_fetch(S, n_nc + c, R);
-            const float imp0 = R.h1.z;
-            (void)row_go(R, d, 0.f, imp0, imp0);     // delta = imp0
-        }
-    }
-    const int nc0 = n_c < 64 ? n_c : 64;
-    for (int it = 0; it < m.iters; it++) {
-        const bool fwd = (it & 1) != 0;
-        sweep(S, n_nc, [&](int j) { return fwd ? j : n_nc - 1 - j; }, [&](int j, const RowV &R) {
-            const int k = fwd ? j : n_nc - 1 - j;
-            const float ni = row_go(R, d, rdl(inc, k), R.h1.x, R.h1.y);
-            inc = lane == k ? ni : inc;
-        });
-        sweep(S, nc0, [&](int j) { return n_nc + j; }, [&](int j, const RowV &R) {
-            const float ni = row_go(R, d, rdl(in0, j), 0.f, 1e10f);
-            in0 = lane == j ? ni : in0;
-        });
-        sweep(S, n_c - nc0, [&](int j) { return n_nc + 64 + j; }, [&](int j, const RowV &R) {
-            const float ni = row_go(R, d, rdl(in1, j), 0.f, 1e10f);
-            in1 = lane == j ? ni : in1;
-        });
-        // friction rows (two per contact) of the contacts with a positive normal impulse, in
-        // contact order: the active list goes through LDS (lane p reads the p-th active contact)
-        const bool a0 = lane < n_c && in0 > 0.f, a1 = lane + 64 < n_c && in1 > 0.f;
-        int t0, t1;
-        const int p0 = ballot_prefix(a0, &t0), p1 = ballot_prefix(a1, &t1);
-        if (t0 + t1 == 0) continue;
-        __builtin_amdgcn_s_barrier();
-        if (a0) list[p0] = lane;
-        if (a1) list[t0 + p1] = lane + 64;
-        __builtin_amdgcn_s_waitcnt(0xc07f);     // lgkmcnt(0): the list is written
-        const int lv0 = list[lane < t0 + t1 ? lane : 0], lv1 = list[lane + 64 < t0 + t1 ? lane + 64 : 0];
-        const int fr0 = n_nc + n_c;
-        // contacts < 64 (impulses in lane c of f00 / f10), then >= 64 (f01 / f11); ascending list
-        sweep_pairs(S, t0, [&](int u) { return fr0 + 2 * __builtin_amdgcn_readlane(lv0, u); }, [&](int u, const RowV &R0, const RowV &R1) {
-            const int c = __builtin_amdgcn_readlane(lv0, u);
-            const float lim = R0.h0.y * rdl(in0, c);
-            float ni = row_go(R0, d, rdl(f00, c), -lim, lim);
-            f00 = lane == c ? ni : f00;
-            ni = row_go(R1, d, rdl(f10, c), -lim, lim);
-            f10 = lane == c ? ni : f10;
-        });
-        if (t1 > 0) {
-            auto cidx = [&](int u) { const int p = u + t0; return p < 64 ? __builtin_amdgcn_readlane(lv0, p) : __builtin_amdgcn_readlane(lv1, p - 64); };
-            sweep_pairs(S, t1, [&](int u) { return fr0 + 2 * cidx(u); }, [&](int u, const RowV &R0, const RowV &R1) {
-                const int c = cidx(u) - 64;
-                const float lim = R0.h0.y * rdl(in1, c);
-                float ni = row_go(R0, d, rdl(f01, c), -lim, lim);
-                f01 = lane == c ? ni : f01;
-                ni = row_go(R1, d, rdl(f11, c), -lim, lim);
-                f11 = lane == c ? ni : f11;
-            });
-        }
-        __builtin_amdgcn_s_barrier();
-    }
 }
 
 // --------------------------------------------------------------------------- one sub-step
@@ -2193,298 +1935,260 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     WT_END(0);
 }
 
-// Sub-step part B: PGS over the row buffer, then semi-implicit Euler (A.1) with the
-// quaternion exp-map update of btTransformUtil::integrateTransform for the free bodies.
-// No LDS: velocities and impulses stay in registers.
-__global__ __launch_bounds__(64) void avr_substep_b_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                           const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
-                                                           int n_envs) {
-    AVR_ENV_GUARD();
-    WT_START();
-    const int lane = lane_id();
-#ifdef AVR_PROF
-    unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-    const float *ws = env_ws(m, env);
-    float *st = state + (size_t)env * AVR_STATE_WORDS;
-    const int n_nc = uni(__float_as_int(ws[WS_NNC])), n_c = uni(__float_as_int(ws[WS_NC]));
-    const int n_rob = uni(__float_as_int(ws[WS_NROB]));
-    // stage the row set in LDS (8 loads in flight per lane) unless it exceeds the capacity
-    __shared__ f4v bl4[B_LDS_WORDS / 4];
-    __shared__ int list[AVR_MAX_CONTACTS];
-    lds_f *bl = (lds_f *)(lds_f4 *)bl4;
-    const float *rows = env_rows(m, env);
-    const int n_rows = n_nc + 3 * n_c;
-    const bool in_lds = n_rows <= B_CAPR && n_rob <= B_CAPS;
-    DV d;
-    float in0, in1;
-    if (in_lds) {
-        const int n4r = n_rows * (RWC / 4), n4s = n_rob * (ROBW / 4);
-        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
-        lds_f4 *l0 = (lds_f4 *)bl, *l1 = (lds_f4 *)(bl + B_CAPR * RWC);
-        for (int base = 0; base < n4r; base += 8 * 64) {
-            f4v t[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int i = base + 64 * q + lane;
-                t[q] = g0[i < n4r ? i : 0];
-            }
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int i = base + 64 * q + lane;
-                if (i < n4r) l0[i] = t[q];
-            }
-        }
-        for (int base = 0; base < n4s; base += 4 * 64) {
-            f4v t[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int i = base + 64 * q + lane;
-                t[q] = g1[i < n4s ? i : 0];
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int i = base + 64 * q + lane;
-                if (i < n4s) l1[i] = t[q];
-            }
-        }
-        if (lane < 16) bl[B_CAPR * RWC + B_CAPS * ROBW + lane] = 0.f;
-        __syncthreads();
-        LdsRows S;
-        S.rec = bl;
-        S.rob = bl + B_CAPR * RWC;
-        S.zero = bl + B_CAPR * RWC + B_CAPS * ROBW;
-        pgs_solve(m, S, list, n_nc, n_c, d, in0, in1);
-    } else {
-        GlbRows S;
-        S.rec = rows;
-        S.rob = rows + m.rowcap * RWC;
-        pgs_solve(m, S, list, n_nc, n_c, d, in0, in1);
-    }
-    // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
-    if (lane < m.nf) {
-        const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * lane + 3);
-        const v3 I = ld3(m.fb_inertia + 4 * lane);
-        const float rs = 1.f / sqrtf(m.fb_mass[lane]);
-        const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
-        const v3 w = qrot(q, V(d.wx * sd.x, d.wy * sd.y, d.wz * sd.z));
-        d.vx *= rs; d.vy *= rs; d.vz *= rs;
-        d.wx = w.x; d.wy = w.y; d.wz = w.z;
-    }
-#ifdef AVR_PROF
-    unsigned long long t1 = __builtin_amdgcn_s_memtime();
-#endif
-    const float vmax = m.max_vel;
-    const int nda = env_hdyn(m, st) ? m.nd + m.hc_n : m.nd;
-    if (lane < nda) {
-        float v = clampf(ws[WS_VQ + lane] + d.rq, -vmax, vmax);
-        float q = st[AVR_S_Q + lane] + dt * v;
-        if (frame_end && lane >= m.nd) {
-            // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
-            const float lo = m.hc_lower[lane - m.nd], hi = m.hc_upper[lane - m.nd];
-            if (q < lo) { q = lo; v = 0.f; }
-            else if (q > hi) { q = hi; v = 0.f; }
-        }
-        st[AVR_S_QD + lane] = v;
-        st[AVR_S_Q + lane] = q;
-    }
-    if (lane < m.nf) {
-        float *fb = st + AVR_S_FREE + AVR_FB_WORDS * lane;
-        v3 v = clamp3(add(ld3(ws + WS_FV + 4 * lane), V(d.vx, d.vy, d.vz)), vmax);
-        v3 om = clamp3(add(ld3(ws + WS_FW + 4 * lane), V(d.wx, d.wy, d.wz)), vmax);
-        st3(fb + 7, v);
-        st3(fb + 10, om);
-        st3(fb, add(ld3(fb), scl(v, dt)));
-        float ang = len(om);
-        if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = (0.5f * 1.5707963267948966f) / dt;
-        v3 ax;
-        if (ang < 0.001f) ax = scl(om, 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang);
-        else ax = scl(om, sinf(0.5f * ang * dt) / ang);
-        qt dq = Q(ax.x, ax.y, ax.z, cosf(ang * dt * 0.5f));
-        stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
-    }
-    // normal impulses back to the manifold points (warm start + normalForce); rows are in
-    // contact order, so contact c is manifold point c
-    if (lane < n_c) st[AVR_S_CP + AVR_CP_WORDS * lane + AVR_CP_IMP] = in0;
-    if (lane + 64 < n_c) st[AVR_S_CP + AVR_CP_WORDS * (lane + 64) + AVR_CP_IMP] = in1;
-#ifdef AVR_PROF
-    unsigned long long t2 = __builtin_amdgcn_s_memtime();
-    if (m.prof && lane == 0) {
-        m.prof[(size_t)env * AVR_PROF_SLOTS + 9] += t1 - t0;
-        m.prof[(size_t)env * AVR_PROF_SLOTS + 10] += t2 - t1;
-        m.prof[(size_t)env * AVR_PROF_SLOTS + 5] += __float_as_int(ws[WS_XCC]) != xcc_id() ? 1 : 0;   // A/B on different XCDs
-    }
-#endif
-    WT_END(1);
+// ---------------------------------------------------------------------------- part B: PGS solve
+// Projected Gauss-Seidel (btMultiBodyConstraintSolver::solveSingleIteration order: non-contact
+// rows with the sweep direction alternating per iteration, normal rows, then the two friction
+// rows of every contact with a positive normal impulse) and semi-implicit Euler, four envs per
+// wavefront.  Lanes 16g .. 16g+15 solve env g of the block; lane sl = lane & 15 of a group holds
+// robot DoF sl's and free body sl's velocity increments (MAXD, MAXF <= 16).  A row's J.dv is one
+// 16-lane DPP butterfly (row_ror 8, 4, 2, 1: every lane of the row ends with the sum), so the
+// four envs' Gauss-Seidel chains advance in lockstep through one instruction stream.  A group
+// with fewer rows than the wave's longest sweep runs null rows (inv = rhs = lo = hi = 0, so
+// delta = 0 exactly), which leaves its results identical to a solve on its own.
+//
+// Where the rows come from: the non-contact rows (~20 per env: motors, violated limits, the
+// spoon weld) are read from the env's row buffer in global memory (they stay L2-resident); the
+// contact rows -- the bulk -- are copied into LDS at kernel entry whenever the block's four
+// envs fit (40 KB per block, 4 blocks per CU), otherwise the whole wave reads them from global
+// memory too.  Every load is typed by address space (ds_read / global_load, never flat) and a
+// lane's choice between real data and the zero block is an address select, never a value
+// select: the waits the compiler places for a row then count only that row's loads, and the
+// software pipeline's read-ahead (headers 2D rows ahead, the header-dependent parts D ahead)
+// stays in flight.
+struct DV { float rq, vx, vy, vz, wx, wy, wz; };
+
+AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) float lds_f;
+typedef __attribute__((address_space(3))) f2v lds_f2;
+typedef __attribute__((address_space(3))) f4v lds_f4;
+typedef __attribute__((address_space(3))) int lds_i;
+typedef const __attribute__((address_space(1))) float *gfp;
+typedef const __attribute__((address_space(1))) f4v *gf4p;
+typedef const __attribute__((address_space(1))) f2v *gf2p;
+
+// Global row data is read with buffer loads through one resource over the whole row buffer
+// (uniform base in SGPRs, 32-bit per-lane byte offsets): a null row or a lane with no part to
+// read addresses B4_OOB, past the end of the buffer, and the range check returns zeros -- an
+// all-zero header is a null row (no endpoint, inv = rhs = lo = hi = 0), a zero part contributes
+// nothing.
+#define B4_OOB 0x7fff0000
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef unsigned u3v __attribute__((ext_vector_type(3)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+AVR_DI f4v bld4(rsrc_t r, int o) { u4v x = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0); return *(f4v *)&x; }
+AVR_DI f2v bld2(rsrc_t r, int o) { u2v x = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0); return *(f2v *)&x; }
+AVR_DI f4v bld3(rsrc_t r, int o) {
+    u3v x = __builtin_amdgcn_raw_buffer_load_b96(r, o, 0, 0);
+    f4v y = {__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), 0.f};
+    return y;
 }
 
-// ------------------------------------------------------------ part B, four envs per wavefront
-// The same PGS + integration as avr_substep_b_kernel, for four envs per wave: lanes 16g .. 16g+15
-// solve env g of the block, and lane sl = lane & 15 of a group holds robot DoF sl's and free body
-// sl's velocity increments (MAXD, MAXF <= 16).  A row's J.dv is one 16-lane DPP butterfly
-// (row_ror 8, 4, 2, 1: every lane of the row ends with the sum), so the four envs' Gauss-Seidel
-// chains advance in lockstep through one instruction stream and every VALU op does four envs'
-// work.  A group with fewer rows than the wave's longest sweep runs null rows (inv = lo = hi = 0:
-// delta = 0 exactly), which leaves its results identical to a solve on its own.  Row order and
-// per-row arithmetic are those of pgs_solve (btMultiBodyConstraintSolver::solveSingleIteration).
-// Rows are read from the global row buffer through a software pipeline (headers 2D rows ahead,
-// parts D ahead); impulses and the friction lists live in LDS (6.7 KB per block), so all 1024
-// blocks of a 4096-env launch are resident at once.  (Staging the rows in LDS instead, 79.5 KB per
-// block, measured slower: 2 blocks per CU.)
-// LDS per group: impulses [rowcap + 2 null slots], friction list [96 ints], then the first B4_SR
-// records and B4_SP robot parts of the env's row set (staged copies; the rest stays in global
-// memory).  4 groups x 2540 words = 39.7 KB per block: 4 blocks per CU, all blocks resident.
-#define B4_IMPNULL (MAXNC + 3 * AVR_MAX_CONTACTS)    // null-row impulse slots (2)
-#define B4_LISTW 324
-#define B4_RECW (B4_LISTW + AVR_MAX_CONTACTS)
-#ifndef B4_SR
-#define B4_SR 68
-#endif
-#ifndef B4_SP
-#define B4_SP 24
-#endif
-#define B4_ROBW (B4_RECW + B4_SR * RWC)
-#define B4_WORDS (B4_ROBW + B4_SP * ROBW)
-#ifndef B4_GD
-#define B4_GD 2          // software-pipeline depth (measured: 2 beats 3 and 5)
-#endif
-static_assert(B4_WORDS % 4 == 0, "group regions must stay 16-byte aligned");
-static_assert(B4_IMPNULL + 2 <= B4_LISTW, "the impulse array fits below the list");
-static_assert(4 * B4_WORDS * 4 <= 40960, "four blocks per CU");
+// LDS of a block (40 KB: 4 blocks per CU, all blocks of a 4096-env launch resident): a null
+// contact header and a zero block, then the four groups' regions, packed:
+//   impulses [n_rows + 2 null slots] | active-contact list [n_c] | contact records [3 n_c][16]
+//   | robot parts of robot-contact rows [n_rob - n_nc][32]
+// (the last two only when the block's four envs fit).
+#define B4_LDSW 10240
+#define LN_C 0
+#define LN_ZERO 4
+#define LN_GROUPS 16
+AVR_DI int al4(int x) { return (x + 3) & ~3; }
 
-// null records + zero block for the global-memory path (info = no endpoint, slot = -1); read only
-__device__ int avr_b4_null[2 * RWC + 32] = {RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                            RI_NONE | (RI_NONE << 6), 0, 0, 0, 0, 0, 0, -1};
+// the two endpoints of a row, 0-based (-1: not a free body), and this lane's part: 0 endpoint
+// A, 1 endpoint B, -1 none
+AVR_DI int own_of(int info) {
+    const int sl = lane_id() & 15;
+    return sl == (info & 63) - 1 ? 0 : (sl == ((info >> 6) & 63) - 1 ? 1 : -1);
+}
 
-// One row as a lane sees it: record pointer, LDS impulse slot, header, current impulse, own free
-// part, robot part.
-template <class P>
-struct Row4 { P p; lds_f *ip; f4v h0, h1; float imp; f2v j0, j1, j2, r; };
-
-// Row source: records from the env's row buffer (read only), impulses in the group's LDS region.
-struct B4Glb {
-    typedef const float *P;           // generic: staged rows resolve to LDS, the rest to global
-    const float *rec, *robb;          // global row buffer: records, robot parts
-    const float *lrec, *lrob;         // staged copies (generic pointers into this group's LDS)
+// non-contact rows: buffer loads (they stay L2-resident)
+struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2, r; };
+struct NcSrc {
+    typedef NcRow Row;
+    rsrc_t rs;
+    int eo, ro;                // this env's records / robot parts (byte offsets)
     lds_f *imp;
-    AVR_DI lds_f *ipp(int r) const { return imp + r; }
-    AVR_DI void at(Row4<P> &R, int r, int pair) const {
-        R.p = r < 0 ? (const float *)avr_b4_null + pair * RWC : (r < B4_SR ? lrec : rec) + r * RWC;
-        R.ip = imp + (r >= 0 ? r : B4_IMPNULL + pair);
+    int nullslot;
+    AVR_DI void at(Row &R, int r, int pair) const {
+        R.o = r < 0 ? B4_OOB : eo + r * (RWC * 4);
+        R.ip = imp + (r >= 0 ? r : nullslot + pair);
     }
-    AVR_DI P zero() const { return (const float *)avr_b4_null + 2 * RWC; }
-    AVR_DI void hdr(Row4<P> &R) const { R.h0 = *(const f4v *)R.p; R.h1 = *(const f4v *)(R.p + 4); R.imp = *R.ip; }
-    AVR_DI void own(P p, int off, f2v &a, f2v &b, f2v &c) const {
-        const P q = off >= 0 ? p + off : zero();
-        a = *(const f2v *)q; b = *(const f2v *)(q + 2); c = *(const f2v *)(q + 4);
+    AVR_DI void hdr(Row &R) const { R.h0 = bld4(rs, R.o); R.h1 = bld2(rs, R.o + 16); R.imp = *R.ip; }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h0.x); }
+    AVR_DI int slot(const Row &R) const { return __float_as_int(R.h0.y) - 1; }
+    AVR_DI void own(Row &R, int off) const {
+        const int o = off >= 0 ? R.o + 32 + 24 * off : B4_OOB;
+        R.j0 = bld2(rs, o); R.j1 = bld2(rs, o + 8); R.j2 = bld2(rs, o + 16);
+    }
+    AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
+};
+
+// contact rows staged in LDS
+struct CRowL { int w; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+struct CLds {
+    typedef CRowL Row;
+    lds_f *blk;
+    int cw, rw, n_nc;          // contact records / robot parts of this group (LDS word index)
+    lds_f *imp;
+    int nullslot;
+    AVR_DI void at(Row &R, int r, int pair) const {
+        R.w = r < 0 ? LN_C : cw + (r - n_nc) * CRW;
+        R.ip = imp + (r >= 0 ? r : nullslot + pair);
+    }
+    AVR_DI void hdr(Row &R) const { R.h = *(const lds_f4 *)(blk + R.w); R.imp = *R.ip; }
+    AVR_DI void hdr3(Row &R) const {   // normal rows: the friction coefficient is not read
+        const lds_f *q = blk + R.w;
+        const f2v a = *(const lds_f2 *)q;
+        R.h.x = a.x; R.h.y = a.y; R.h.z = q[2];
+        R.imp = *R.ip;
+    }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }
+    AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
+    AVR_DI void own(Row &R, int off) const {
+        const lds_f2 *q = (const lds_f2 *)(blk + (off >= 0 ? R.w + 4 + 6 * off : LN_ZERO));
+        R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2];
     }
     AVR_DI f2v robot(int slot) const {
-        return *(const f2v *)(slot < 0 ? zero() : (slot < B4_SP ? lrob : robb) + slot * ROBW + 2 * (lane_id() & 15));
+        return *(const lds_f2 *)(blk + (slot >= 0 ? rw + (slot - n_nc) * ROBW + 2 * (lane_id() & 15) : LN_ZERO));
     }
 };
 
-// sum over the 16 lanes of each DPP row, result in every lane of the row
+// contact rows, buffer loads (blocks whose four envs do not fit the LDS)
+struct CRowG { int o; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+struct CGlb {
+    typedef CRowG Row;
+    rsrc_t rs;
+    int co, ro, n_nc;          // this env's contact records / robot parts (byte offsets)
+    lds_f *imp;
+    int nullslot;
+    AVR_DI void at(Row &R, int r, int pair) const {
+        R.o = r < 0 ? B4_OOB : co + (r - n_nc) * (CRW * 4);
+        R.ip = imp + (r >= 0 ? r : nullslot + pair);
+    }
+    AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
+    AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }
+    AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
+    AVR_DI void own(Row &R, int off) const {
+        const int o = off >= 0 ? R.o + 16 + 24 * off : B4_OOB;
+        R.j0 = bld2(rs, o); R.j1 = bld2(rs, o + 8); R.j2 = bld2(rs, o + 16);
+    }
+    AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
+};
+
+// sum over the 16 lanes of each DPP row, result in every lane of the row (each rotate folds
+// into the add as a DPP source operand)
 AVR_DI float row16_sum(float x) {
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xf, 0xf, false));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xf, 0xf, false));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x122, 0xf, 0xf, false));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x121, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xf, 0xf, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xf, 0xf, true));
     return x;
 }
 
+// the header-dependent parts of a row: this lane's free part (if it owns an endpoint) and its
+// robot DoF's (J, M^-1 J^T)
 template <class S>
-AVR_DI void parts4(const S &s, Row4<typename S::P> &R) {
-    const int sl = lane_id() & 15;
-    const int info = __float_as_int(R.h0.x), slot = __float_as_int(R.h1.w);
-    const int off = sl == (info & 63) ? 8 : (sl == ((info >> 6) & 63) ? 14 : -1);
-    s.own(R.p, off, R.j0, R.j1, R.j2);
-    R.r = s.robot(slot);
+AVR_DI void parts4(const S &s, typename S::Row &R) {
+    s.own(R, own_of(s.info(R)));
+    R.r = s.robot(s.slot(R));
 }
 
-// resolve one row with its current impulse; the new impulse goes back to the row's LDS slot
-template <class P>
-AVR_DI float go4(const Row4<P> &R, DV &d, float imp, float lo, float hi) {
-    float p = R.j0.x * d.vx + R.j0.y * d.vy + R.j1.x * d.vz;
-    float q = R.j1.y * d.wx + R.j2.x * d.wy + R.j2.y * d.wz;
-    p += q + R.r.x * d.rq;
-    const float dv = row16_sum(p);
-    const float ni = __builtin_amdgcn_fmed3f(imp + (R.h0.w - dv * R.h0.z), lo, hi);
+// resolve one row with its current impulse; returns the new impulse.  The fused multiply-adds
+// are spelled out and nothing else may contract: every unrolled copy of a row resolve (and every
+// pipeline depth) then rounds the same way, so an env's results do not depend on which copy
+// resolves its rows or on the row counts of the other envs in its wavefront.
+template <class R>
+AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi) {
+#pragma clang fp contract(off)
+    const float p = fmaf(X.j1.x, d.vz, fmaf(X.j0.y, d.vy, X.j0.x * d.vx));
+    const float q = fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.x, d.rq, X.j1.y * d.wx)));
+    const float dv = row16_sum(p + q);
+    const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
     const float delta = ni - imp;
-    d.vx += R.j0.x * delta; d.vy += R.j0.y * delta; d.vz += R.j1.x * delta;
-    d.wx += R.j1.y * delta; d.wy += R.j2.x * delta; d.wz += R.j2.y * delta;
-    d.rq += R.r.y * delta;
+    d.vx = fmaf(X.j0.x, delta, d.vx); d.vy = fmaf(X.j0.y, delta, d.vy); d.vz = fmaf(X.j1.x, delta, d.vz);
+    d.wx = fmaf(X.j1.y, delta, d.wx); d.wy = fmaf(X.j2.x, delta, d.wy); d.wz = fmaf(X.j2.y, delta, d.wz);
+    d.rq = fmaf(X.r.y, delta, d.rq);
     return ni;
 }
 
 // sweep over n (wave-uniform) steps; rr(j) is this lane's row for step j (its group's row index,
-// or -1: a null row).  Software pipeline of depth D: headers 2D steps ahead, the header-dependent
-// parts D steps ahead, in a ring of 2D + 1 buffers whose slots are compile-time after unrolling
-// (D = 1 for rows staged in LDS, deeper for rows read from global memory).
-template <int D, class S, class RR, class GO>
+// or -1: a null row, also for every j >= n).  Software pipeline of depth D: headers 2D steps
+// ahead, the header-dependent parts D steps ahead, in a ring of K = 2D + 1 buffers whose slots
+// are compile-time after unrolling.  The sweep runs whole rounds of K steps (the last round pads
+// with null rows, delta = 0) and issues its read-ahead unconditionally: with no conditional
+// load in the loop the compiler's wait counts are exact (a load that may or may not have been
+// issued on some path makes it wait for everything).
+template <int D, bool H3, class S>
+AVR_DI void hdr_of(const S &s, typename S::Row &R) {
+    if constexpr (H3) s.hdr3(R);
+    else s.hdr(R);
+}
+template <int D, bool H3, class S, class RR, class GO>
 AVR_DI void sweep4(const S &s, int n, const RR &rr, const GO &go) {
+    if (n <= 0) return;
     constexpr int K = 2 * D + 1;
-    Row4<typename S::P> R[K];
+    typename S::Row R[K];
 #pragma unroll
-    for (int q = 0; q < 2 * D; q++)
-        if (q < n) { s.at(R[q], rr(q), 0); s.hdr(R[q]); }
+    for (int q = 0; q < 2 * D; q++) { s.at(R[q], rr(q), 0); hdr_of<D, H3>(s, R[q]); }
 #pragma unroll
-    for (int q = 0; q < D; q++)
-        if (q < n) parts4(s, R[q]);
+    for (int q = 0; q < D; q++) parts4(s, R[q]);
     for (int j = 0; j < n; j += K) {
 #pragma unroll
         for (int q = 0; q < K; q++) {
-            const int jj = j + q;
-            if (jj < n) {
-                if (jj + 2 * D < n) { s.at(R[(q + 2 * D) % K], rr(jj + 2 * D), 0); s.hdr(R[(q + 2 * D) % K]); }
-                if (jj + D < n) parts4(s, R[(q + D) % K]);
-                go(R[q]);
-            }
+            s.at(R[(q + 2 * D) % K], rr(j + q + 2 * D), 0);
+            hdr_of<D, H3>(s, R[(q + 2 * D) % K]);
+            parts4(s, R[(q + D) % K]);
+            go(R[q]);
         }
     }
 }
 
 // friction unit: the two friction rows of one active contact and that contact's normal impulse
 template <class S>
-struct Pair4 { Row4<typename S::P> a, b; float in; };
+struct Pair4 { typename S::Row a, b; float in; };
 template <class S>
-AVR_DI void pair_hdr(const S &s, Pair4<S> &X, int r, int rn) {
+AVR_DI void pair_hdr(const S &s, Pair4<S> &X, int r, lds_f *in) {
     s.at(X.a, r, 0);
     s.at(X.b, r >= 0 ? r + 1 : -1, 1);
     s.hdr(X.a); s.hdr(X.b);
-    X.in = rn >= 0 ? *s.ipp(rn) : 0.f;
+    X.in = r >= 0 ? *in : 0.f;
 }
 template <class S>
 AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
-    const int sl = lane_id() & 15;
-    const int info = __float_as_int(X.a.h0.x), slot = __float_as_int(X.a.h1.w);
-    const int off = sl == (info & 63) ? 8 : (sl == ((info >> 6) & 63) ? 14 : -1);
-    s.own(X.a.p, off, X.a.j0, X.a.j1, X.a.j2);
-    s.own(X.b.p, off, X.b.j0, X.b.j1, X.b.j2);
+    const int slot = s.slot(X.a);
+    const int off = own_of(s.info(X.a));
+    s.own(X.a, off);
+    s.own(X.b, off);
     X.a.r = s.robot(slot);
     X.b.r = s.robot(slot >= 0 ? slot + 1 : -1);
 }
 
-template <int D, class S>
-AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
-    typedef typename S::P P;
+template <int DN, int DC, class NS, class CS>
+AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
+    typedef typename NS::Row NR;
+    typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
-    // warm start (normal rows, contact order): delta = cached impulse * warm-start factor, which
+    // warm start (normal rows, contact order): delta = cached impulse x warm-start factor, which
     // is also the rows' starting impulse
-    sweep4<D>(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-           [&](const Row4<P> &R) { (void)go4(R, d, 0.f, R.imp, R.imp); });
+    sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+                     [&](const CR &R) { (void)go4(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
     const int fr0 = n_nc + n_c;
     for (int it = 0; it < m.iters; it++) {
         const bool fwd = (it & 1) != 0;
-        sweep4<D>(s, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
-               [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, R.h1.x, R.h1.y); });
-        sweep4<D>(s, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-               [&](const Row4<P> &R) { *R.ip = go4(R, d, R.imp, 0.f, 1e10f); });
+        sweep4<DN, false>(ns, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
+                          [&](const NR &R) { *R.ip = go4(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y); });
+        sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
+                         [&](const CR &R) { *R.ip = go4(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
         // active contacts (positive normal impulse) of each group, in contact order
         int t = 0;
         for (int c0 = 0; c0 < nc_max; c0 += 16) {
             const int c = c0 + sl;
-            const bool a = c < n_c && *s.ipp(n_nc + (c < n_c ? c : 0)) > 0.f;
+            const bool a = c < n_c && imp[n_nc + (c < n_c ? c : 0)] > 0.f;
             const unsigned long long b = __ballot(a);
             const unsigned gm = (unsigned)(b >> (lane_id() & 48)) & 0xffffu;
             if (a) list[t + __popc(gm & ((1u << sl) - 1u))] = c;
@@ -2495,45 +2199,51 @@ AVR_DI void pgs4(const KModel &m, const S &s, lds_i *list, int n_nc, int n_c, in
         tmax = max(tmax, __shfl_xor(tmax, 32));
         tmax = uni(tmax);
         if (tmax == 0) continue;
-        // the same depth-D pipeline over friction units; list entries are read one step before
+        // the same depth-DC pipeline over friction units; list entries are read one step before
         // the headers they address
-        constexpr int K = 2 * D + 1;
-        Pair4<S> X[K];
+        constexpr int K = 2 * DC + 1;
+        Pair4<CS> X[K];
         auto lst = [&](int u) { return u < t ? list[u] : -1; };
-        auto hdr = [&](Pair4<S> &Y, int c) { pair_hdr(s, Y, c >= 0 ? fr0 + 2 * c : -1, c >= 0 ? n_nc + c : -1); };
-        auto go = [&](const Pair4<S> &Y) {
-            const float lim = Y.a.h0.y * Y.in;
-            *Y.a.ip = go4(Y.a, d, Y.a.imp, -lim, lim);
-            *Y.b.ip = go4(Y.b, d, Y.b.imp, -lim, lim);
+        auto hdr = [&](Pair4<CS> &Y, int c) { pair_hdr(cs, Y, c >= 0 ? fr0 + 2 * c : -1, imp + n_nc + (c >= 0 ? c : 0)); };
+        auto go = [&](const Pair4<CS> &Y) {
+            const float lim = Y.a.h.w * Y.in;
+            *Y.a.ip = go4(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
+            *Y.b.ip = go4(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
         };
+        // (whole rounds of K units, null units past the end, unconditional read-ahead: sweep4)
         int cn = lst(0);
 #pragma unroll
-        for (int q = 0; q < 2 * D; q++) {
-            if (q < tmax) hdr(X[q], cn);
-            cn = lst(q + 1);
-        }
+        for (int q = 0; q < 2 * DC; q++) { hdr(X[q], cn); cn = lst(q + 1); }
 #pragma unroll
-        for (int q = 0; q < D; q++)
-            if (q < tmax) pair_parts4(s, X[q]);
+        for (int q = 0; q < DC; q++) pair_parts4(cs, X[q]);
         for (int u0 = 0; u0 < tmax; u0 += K) {
 #pragma unroll
             for (int q = 0; q < K; q++) {
-                const int u = u0 + q;
-                if (u < tmax) {
-                    if (u + 2 * D < tmax) { hdr(X[(q + 2 * D) % K], cn); cn = lst(u + 2 * D + 1); }
-                    if (u + D < tmax) pair_parts4(s, X[(q + D) % K]);
-                    go(X[q]);
-                }
+                hdr(X[(q + 2 * DC) % K], cn);
+                cn = lst(u0 + q + 2 * DC + 1);
+                pair_parts4(cs, X[(q + DC) % K]);
+                go(X[q]);
             }
         }
     }
 }
 
+#ifndef B4_DN
+#define B4_DN 3          // pipeline depth, non-contact rows (global memory, L2-resident)
+#endif
+#ifndef B4_DC
+#define B4_DC 2          // pipeline depth, contact rows staged in LDS
+#endif
+#ifndef B4_DG
+#define B4_DG 3          // pipeline depth, contact rows from global memory (blocks that do not fit)
+#endif
+
 __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                             const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
                                                             int n_envs) {
     const KModel &m = *mp;
-    __shared__ f4v b4l[4 * B4_WORDS / 4];
+    __shared__ f4v b4l[B4_LDSW / 4];
+    lds_f *blk = (lds_f *)(lds_f4 *)b4l;
     const int lane = lane_id(), sl = lane & 15, g = lane >> 4;
     // XCD-consistent mapping: blocks are dealt round-robin over the 8 XCDs, and part A runs env
     // e as block e - env0, so block b takes the envs e - env0 = 32 (b / 8) + (b % 8) + 8 g, which
@@ -2542,56 +2252,74 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     const int env = env0 + 32 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * g;
     const bool live = env < n_envs && (!mask || mask[env]);
     const int ev = live ? env : env0;
-    const float *ws = env_ws(m, ev);
+    const gfp wsg = (gfp)env_ws(m, ev);
     float *st = state + (size_t)ev * AVR_STATE_WORDS;
-    const int n_nc = live ? __float_as_int(ws[WS_NNC]) : 0, n_c = live ? __float_as_int(ws[WS_NC]) : 0;
-    const int n_rows = n_nc + 3 * n_c;
+    const int n_nc = live ? __float_as_int(wsg[WS_NNC]) : 0, n_c = live ? __float_as_int(wsg[WS_NC]) : 0;
+    const int n_rob = live ? __float_as_int(wsg[WS_NROB]) : 0;
+    const int n_rows = n_nc + 3 * n_c, n_rc = max(n_rob - n_nc, 0);
     auto wmax = [&](int x) { x = max(x, __shfl_xor(x, 16)); x = max(x, __shfl_xor(x, 32)); return uni(x); };
     const int nnc_max = wmax(n_nc), nc_max = wmax(n_c);
-    lds_f *gb = (lds_f *)(lds_f4 *)b4l + g * B4_WORDS;
-    lds_i *list = (lds_i *)(gb + B4_LISTW);
-    const float *rows = env_rows(m, ev);
+    // the row buffer of every env as one buffer resource; this env's records at byte eo
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.rows, 0, m.rows_envs * m.rowstride * 4, 0x00020000);
+    const int eo = ev * m.rowstride * 4, ro = eo + m.rowcap * RWC * 4;
 #ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the block's LDS (see load_state)
-    for (int i = lane; i < 4 * B4_WORDS; i += 64) ((lds_f *)(lds_f4 *)b4l)[i] = __int_as_float(-1);
+    for (int i = lane; i < B4_LDSW; i += 64) blk[i] = __int_as_float(-1);
     __syncthreads();
 #endif
-    DV d;
-    // starting impulses (record word 6) into the LDS impulse array, null slots zero; the first
-    // B4_SR records and B4_SP robot parts staged (8 loads in flight per lane)
-    for (int r = sl; r < n_rows; r += 16) gb[r] = rows[r * RWC + 6];
-    if (sl < 2) gb[B4_IMPNULL + sl] = 0.f;
-    {
-        const int n_rob = live ? __float_as_int(ws[WS_NROB]) : 0;
-        const int n4r = min(n_rows, B4_SR) * (RWC / 4), n4s = min(n_rob, B4_SP) * (ROBW / 4);
+    // pack the groups' regions; stage the contact rows when all four fit
+    const int szA = al4(n_rows + 2) + al4(n_c), szB = 3 * n_c * CRW + n_rc * ROBW;
+    const int t0 = __shfl(szA + szB, 0), t1 = __shfl(szA + szB, 16), t2 = __shfl(szA + szB, 32), t3 = __shfl(szA + szB, 48);
+    const bool in_lds = uni(t0 + t1 + t2 + t3) <= B4_LDSW - LN_GROUPS && !m.b4_global;
+    int base;
+    if (in_lds) base = g == 0 ? 0 : g == 1 ? t0 : g == 2 ? t0 + t1 : t0 + t1 + t2;
+    else {
+        const int a0 = __shfl(szA, 0), a1 = __shfl(szA, 16), a2 = __shfl(szA, 32);
+        base = g == 0 ? 0 : g == 1 ? a0 : g == 2 ? a0 + a1 : a0 + a1 + a2;
+    }
+    base += LN_GROUPS;
+    lds_f *imp = blk + base;
+    lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
+    const int cw = base + szA, rw = cw + 3 * n_c * CRW;
+    // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
+    // warm-start factor; null slots 0
+    const gfp cpool = (gfp)(st + AVR_S_CP);
+    for (int r = sl; r < n_rows + 2; r += 16) {
+        const int c = r - n_nc;
+        imp[r] = c >= 0 && c < n_c ? cpool[AVR_CP_WORDS * c + AVR_CP_IMP] * m.warmstart : 0.f;
+    }
+    if (lane < LN_GROUPS) blk[lane] = 0.f;      // null contact header, zero block
+    if (in_lds) {   // contact records and robot-contact parts, 8 loads in flight per lane
+        const int n4r = 3 * n_c * (CRW / 4), n4s = n_rc * (ROBW / 4);
         const int m4 = wmax(n4r + n4s);
-        const gf4p g0 = (gf4p)rows, g1 = (gf4p)(rows + m.rowcap * RWC);
-        lds_f4 *l0 = (lds_f4 *)(gb + B4_RECW), *l1 = (lds_f4 *)(gb + B4_ROBW);
+        lds_f4 *l0 = (lds_f4 *)(blk + cw);
         for (int b = 0; b < m4; b += 8 * 16) {
             f4v t[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int i = b + 16 * q + sl;
-                t[q] = i < n4r ? g0[i] : (i < n4r + n4s ? g1[i - n4r] : g0[0]);
+                t[q] = bld4(rs, i < n4r ? eo + CR_BASE * 4 + 16 * i : (i < n4r + n4s ? ro + n_nc * ROBW * 4 + 16 * (i - n4r) : B4_OOB));
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int i = b + 16 * q + sl;
-                if (i < n4r) l0[i] = t[q];
-                else if (i < n4r + n4s) l1[i - n4r] = t[q];
+                if (i < n4r + n4s) l0[i] = t[q];
             }
         }
     }
     __syncthreads();
-    B4Glb s;
-    s.rec = rows;
-    s.robb = rows + m.rowcap * RWC;
-    s.lrec = (const float *)(gb + B4_RECW);
-    s.lrob = (const float *)(gb + B4_ROBW);
-    s.imp = gb;
-    pgs4<B4_GD>(m, s, list, n_nc, n_c, nnc_max, nc_max, d);
+    NcSrc ns{rs, eo, ro, imp, n_rows};
+    DV d;
+    if (in_lds) {
+        CLds cs{blk, cw, rw, n_nc, imp, n_rows};
+        pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+    } else {
+        CGlb cs{rs, eo + CR_BASE * 4, ro, n_nc, imp, n_rows};
+        pgs4<B4_DN, B4_DG>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+    }
     // normal impulses back to the manifold points (warm start + normalForce)
-    for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = *s.ipp(n_nc + c);
+    for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = imp[n_nc + c];
     if (!live) return;
+    const float *ws = env_ws(m, ev);
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
     if (sl < m.nf) {
         const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * sl + 3);
@@ -2759,7 +2487,6 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     if (n_envs <= 0) return hipSuccess;
     const int nsub = h_m->nsub > 0 ? h_m->nsub : 1;
     const float dt = h_m->time_step / (float)nsub;
-    const int b_variant = h_m->b_variant;
     auto mark = [&](int kind) {
         if (log && log->n < log->cap && hipEventRecord(log->ev[log->n], stream) == hipSuccess) log->kind[log->n++] = kind;
     };
@@ -2769,10 +2496,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
-        if (b_variant == 1)
-            hipLaunchKernelGGL(avr_substep_b_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
-        else
-            hipLaunchKernelGGL(avr_substep_b4_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
+        hipLaunchKernelGGL(avr_substep_b4_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
     };
     if (mode == MODE_SUBSTEP) {
         float h;
@@ -2805,7 +2529,7 @@ extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env
 
 // [vgprs, 0, lds bytes, scratch bytes] of substep_a, then of substep_b
 extern "C" hipError_t avr_kernel_attrs(int *out8) {
-    const void *k[2] = {(const void *)avr_substep_a_kernel, (const void *)avr_substep_b_kernel};
+    const void *k[2] = {(const void *)avr_substep_a_kernel, (const void *)avr_substep_b4_kernel};
     for (int i = 0; i < 2; i++) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, k[i]);

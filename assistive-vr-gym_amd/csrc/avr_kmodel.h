@@ -73,9 +73,10 @@ struct KModel {
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
     int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
     int rowstride;             // floats between consecutive envs' row buffers
+    int rows_envs;             // envs covered by the row buffer (the handle's n_envs)
+    int b4_global;             // diagnostic (AVR_B4_GLOBAL=1): part B reads every row from global memory
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
-    int b_variant;             // part B kernel: 4 = four envs per wave, 1 = one env per wave
 };
 
 // Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):

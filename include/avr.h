@@ -43,8 +43,9 @@ typedef struct avr_config {
     uint64_t seed;         /* action RNG seed for avr_step_random (env.py:53 uses 1001)     */
 } avr_config;
 
-/* avr_config.flags: part B (PGS + integration) runs four envs per wavefront by default */
-#define AVR_CFG_B_ONE_ENV_PER_WAVE 1   /* part B as one env per wavefront (rows staged in LDS)  */
+/* avr_config.flags: no flag is defined; avr_create rejects any set bit (bit 0 selected the
+ * one-env-per-wavefront part-B kernel, removed in round 2: part B runs four envs per wavefront) */
+#define AVR_CFG_RESERVED_MASK 0xffffffff
 
 typedef struct avr_sim avr_sim;
 

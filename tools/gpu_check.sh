@@ -1,9 +1,9 @@
-# GPU test suite + kernel-trace stats of a short bench (per-kernel split)
+# One GPU call: parity suite, then a short bench line (each step time-limited, chained with &&).
 set -o pipefail
-cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/chk
-timeout -k 10 600 python3 -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/chk/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/chk/kt -o kt -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/chk/kt_bench.log 2>&1
+cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/c
+timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/c/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/c/bench.json 2> gpurun_out/c/bench.err
 rc=$?
-tail -3 gpurun_out/chk/pytest_gpu.log
-grep -v amdgpu.ids gpurun_out/chk/kt_bench.log | grep '"value"' | cut -c1-200
+grep -E "PASS|FAIL|passed|failed|Error|assert" gpurun_out/c/pytest_gpu.log | tail -30
+python3 -c "import json;d=json.loads(open('gpurun_out/c/bench.json').read().strip().splitlines()[-1]);k=d['roofline']['kernels'];print(round(d['value']), d['nan_or_overflow_envs'], {n[4:16]:round(x['avg_ms'],4) for n,x in k.items()})" 2>/dev/null
 echo rc=$rc
