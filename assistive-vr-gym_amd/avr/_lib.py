@@ -90,7 +90,8 @@ class Sim:
         self.lib = load()
         self.md = md
         self.n = int(n_envs)
-        self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel')
+        self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel',
+                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel')
         cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))
@@ -182,16 +183,17 @@ class Sim:
 
     def kernel_times(self):
         """{kernel: (total_ms, launches)} accumulated since profile_kernels(True)."""
-        ms = np.zeros(4, np.float64)
-        n = np.zeros(4, np.int64)
+        ms = np.zeros(8, np.float64)
+        n = np.zeros(8, np.int64)
         self._chk(self.lib.avr_kernel_times(self.h, ms.ctypes.data, n.ctypes.data))
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.kernel_kinds)}
 
     def kernel_info(self):
-        out = np.zeros(8, np.int32)
+        """{kernel: dict(vgprs, lds_bytes, scratch_bytes)} of the four sub-step kernels."""
+        out = np.zeros(16, np.int32)
         self._chk(self.lib.avr_kernel_info(self.h, out.ctypes.data))
-        return dict(vgprs=int(out[0]), lds_bytes=int(out[2]), scratch_bytes=int(out[3]),
-                    b_vgprs=int(out[4]), b_lds_bytes=int(out[6]), b_scratch_bytes=int(out[7]))
+        names = ('pairs', 'narrowphase', 'a', 'b')
+        return {n: dict(vgprs=int(out[4 * i]), lds_bytes=int(out[4 * i + 2]), scratch_bytes=int(out[4 * i + 3])) for i, n in enumerate(names)}
 
 
 # ---------------------------------------------------------------- Philox4x32-10 (host mirror)

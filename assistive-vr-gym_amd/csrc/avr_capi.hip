@@ -22,7 +22,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
 extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
 extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream);
-extern "C" hipError_t avr_kernel_attrs(int *out8);
+extern "C" hipError_t avr_kernel_attrs(int *out16);
 
 #define AVR_MAX_GROUPS 8
 
@@ -316,6 +316,19 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         if (nc > MAXCC) return fail(s, -2, "model has %d non-static shapes > MAXCC %d", nc, MAXCC);
         if ((r = upload(s, cidx, &k.shape_cidx))) return r;
         if ((r = upload(s, saabb, &k.static_saabb))) return r;
+        // packed per-shape and per-candidate-pair records: one load each in the pair kernel
+        std::vector<int> sinfo(ns);
+        for (int i = 0; i < ns; i++) sinfo[i] = (cidx[i] + 1) | ((d->shape_gender[i] + 1) << 9);
+        if ((r = upload(s, sinfo, &k.shape_info))) return r;
+        std::vector<int4> prec(d->n_pairs > 0 ? d->n_pairs : 1);
+        for (int p = 0; p < d->n_pairs; p++) {
+            const int ba = d->pair_a[p], bb = d->pair_b[p];
+            const int na = d->body_shape_count[ba], nbs = d->body_shape_count[bb];
+            const int bare = (d->body_flags[ba] & 1) && (d->body_flags[bb] & 1);
+            prec[p] = make_int4(ba | (bb << 16), d->body_shape_start[ba] | (na << 16), d->body_shape_start[bb] | (nbs << 16),
+                                bare | ((na == 1 && nbs == 1) ? 2 : 0));
+        }
+        if ((r = upload(s, prec, &k.pair_rec))) return r;
     }
     if ((r = upload(s, ivec(d->pair_a, d->n_pairs), &k.pair_a))) return r;
     if ((r = upload(s, ivec(d->pair_b, d->n_pairs), &k.pair_b))) return r;
@@ -350,6 +363,12 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         for (int q = l; q >= 0; q = par[q]) mask |= 1u << q;
         k.anc_mask[l] = mask;
     }
+    // tree levels (parents precede children in DFS order): the kinematics passes run level by level
+    k.nlev = 0;
+    for (int l = 0; l < nla; l++) {
+        k.rl_level[l] = par[l] < 0 ? 0 : k.rl_level[par[l]] + 1;
+        if (k.rl_level[l] + 1 > k.nlev) k.nlev = k.rl_level[l] + 1;
+    }
     size_t E = (size_t)cfg->n_envs;
     // per-env constraint-row scratch (written and read inside each sub-step)
     k.rowcap = MAXNC + 3 * AVR_MAX_CONTACTS;
@@ -374,6 +393,11 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         HIPCHK(s, hipMemset(ws, 0, E * 128 * sizeof(float)));
         s->allocs.push_back(ws);
         k.ws = ws;
+        float *cscr = nullptr;
+        HIPCHK(s, hipMalloc(&cscr, E * (size_t)CS_WORDS * sizeof(float)));
+        HIPCHK(s, hipMemset(cscr, 0, E * (size_t)CS_WORDS * sizeof(float)));
+        s->allocs.push_back(cscr);
+        k.cscr = cscr;
     }
     HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
@@ -558,9 +582,9 @@ extern "C" int avr_set_profile_buffer(avr_sim *s, void *d_prof) {
     return 0;
 }
 
-extern "C" int avr_kernel_info(avr_sim *s, int32_t *out8) {
+extern "C" int avr_kernel_info(avr_sim *s, int32_t *out16) {
     (void)s;
-    hipError_t e = avr_kernel_attrs(out8);
+    hipError_t e = avr_kernel_attrs(out16);
     return e == hipSuccess ? 0 : -3;
 }
 
@@ -597,9 +621,9 @@ extern "C" int avr_profile_kernels(avr_sim *s, int32_t enable) {
     return 0;
 }
 
-extern "C" int avr_kernel_times(avr_sim *s, double *ms4, int64_t *count4) {
+extern "C" int avr_kernel_times(avr_sim *s, double *ms8, int64_t *count8) {
     CHECK_SIM(s);
     if (drain_evlog(s)) return -3;
-    for (int k = 0; k < AVR_K_KINDS; k++) { ms4[k] = s->kt_ms[k]; count4[k] = s->kt_n[k]; }
+    for (int k = 0; k < AVR_K_KINDS; k++) { ms8[k] = s->kt_ms[k]; count8[k] = s->kt_n[k]; }
     return 0;
 }

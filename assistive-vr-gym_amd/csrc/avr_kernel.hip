@@ -28,11 +28,23 @@
 
 #include "avr_kmodel.h"
 
+// explicitly addressed memory: LDS (ds_read / ds_write) and global (global_load) pointers, so that
+// no hot loop goes through flat instructions (a flat load makes every wait cover both counters)
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) float lds_f;
+typedef __attribute__((address_space(3))) f2v lds_f2;
+typedef __attribute__((address_space(3))) f4v lds_f4;
+typedef __attribute__((address_space(3))) int lds_i;
+typedef const __attribute__((address_space(1))) float *gfp;
+typedef const __attribute__((address_space(1))) f4v *gf4p;
+typedef const __attribute__((address_space(1))) f2v *gf2p;
+
 // --------------------------------------------------------------------------- device model
 
 
 // --------------------------------------------------------------------------- LDS layout
-#define AVR_PROF_SLOTS 24   // diagnostic build: per-env cycle / event counters (tools/prof_phases.py)
+#define AVR_PROF_SLOTS 48   // diagnostic build: per-env cycle / event counters (tools/prof_phases.py)
 struct EnvLDS {
     float st[AVR_S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
@@ -49,7 +61,7 @@ struct EnvLDS {
 #ifdef AVR_PROF
     unsigned long long prof[AVR_PROF_SLOTS];
 #endif
-    union {
+    union __attribute__((aligned(16))) {
         struct {                           // collision detection
             float bmin[MAXB][4], bmax[MAXB][4];
             int apair[MAXAP];              // active body pairs (broadphase output, in pair order)
@@ -58,8 +70,13 @@ struct EnvLDS {
             int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
             float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
         } c;
+        struct {                           // contact update (part A3)
+            float ocp[AVR_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
+            int okey[AVR_MAX_CONTACTS];                   // its (sa | sb << 16) keys
+        } k;
         struct {
             float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
+            float iw[MAXL][8];             // world inertia (xx yy zz xy xz yz), mass
         } d;
     } u;
 };
@@ -77,37 +94,55 @@ struct EnvLDS {
 #endif
 
 // --------------------------------------------------------------------------- kinematics
-// robot_fk: serial recursion over the (DFS-ordered) links on lane 0, frames published in LDS.
-// Under 'tremor' the head chain follows the robot's links: its root hangs off the static chest
-// slot (parent -2) and its link frames (== COM frames) are published into the human slot poses,
-// where collision and the task glue (getLinkState(human, 27), feeding.py:134,254) read them.
+// robot_fk: link frames published in LDS, level by level (lane i = link i; the joint rotations
+// and the per-link model data are formed in parallel, then each level composes onto its parents'
+// frames).  Under 'tremor' the head chain follows the robot's links: its root hangs off the
+// static chest slot (parent -2) and its link frames (== COM frames) are published into the human
+// slot poses, where collision and the task glue (getLinkState(human, 27), feeding.py:134,254)
+// read them.
 AVR_DI int lgo(const EnvLDS &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
 
 AVR_DI void robot_fk(const KModel &m, EnvLDS &L) {
-    if (lane_id() == 0) {
-        tf base = ldtf(m.base);
+    const int i = lane_id();
+    const bool mine = i < L.nla;
+    int p = -3, jt = AVR_J_FIXED, lev = -1;
+    tf jo, com;
+    v3 axl = V(0, 0, 0);
+    qt qj = Q(0, 0, 0, 1);
+    float qv = 0.f;
+    if (mine) {
         const int go = lgo(L, m);
-        for (int i = 0; i < L.nla; i++) {
-            int p = m.rl_parent[i];
-            tf par = p == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : p < 0 ? base : ldtf(L.lk[p]);
-            tf t = tfmul(par, ldtf(m.rl_jorig + 8 * (go + i)));
-            v3 axl = ld3(m.rl_axis + 4 * i);
-            v3 axw = qrot(t.q, axl);
-            int dof = m.rl_dof[i];
-            int jt = m.rl_jtype[i];
+        p = m.rl_parent[i];
+        jt = m.rl_jtype[i];
+        lev = m.rl_level[i];
+        jo = ldtf(m.rl_jorig + 8 * (go + i));
+        com = ldtf(m.rl_com + 8 * (go + i));
+        axl = ld3(m.rl_axis + 4 * i);
+        const int dof = m.rl_dof[i];
+        qv = dof >= 0 ? L.st[AVR_S_Q + dof] : 0.f;
+        if (jt == AVR_J_REVOLUTE) qj = qaxis(axl, qv);
+    }
+    for (int d = 0; d < m.nlev; d++) {
+        if (lev == d) {
+            const tf par = p == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : p < 0 ? ldtf(m.base) : ldtf(L.lk[p]);
+            tf t = tfmul(par, jo);
+            const v3 axw = qrot(t.q, axl);
             st3(L.org[i], t.p);
             st3(L.ax[i], axw);
-            if (jt == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(axl, L.st[AVR_S_Q + dof]));
-            else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(axw, L.st[AVR_S_Q + dof]));
+            if (jt == AVR_J_REVOLUTE) t.q = qmul(t.q, qj);
+            else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(axw, qv));
             sttf(L.lk[i], t);
-            sttf(L.cm[i], tfmul(t, ldtf(m.rl_com + 8 * (go + i))));
+            sttf(L.cm[i], tfmul(t, com));
         }
-        for (int c = 0; c < L.nla - m.nl; c++) {
-            const int slot = m.hc_slot[c];
-            if (slot < 0) continue;
+        SYNC();
+    }
+    const int c = i - m.nl;
+    if (mine && c >= 0) {
+        const int slot = m.hc_slot[c];
+        if (slot >= 0) {
             float *h = L.st + AVR_S_HUMAN + 7 * slot;
-            st3(h, ld3(L.cm[m.nl + c]));
-            stq(h + 3, ldq(L.cm[m.nl + c] + 3));
+            st3(h, ld3(L.cm[i]));
+            stq(h + 3, ldq(L.cm[i] + 3));
         }
     }
     SYNC();
@@ -131,9 +166,21 @@ AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &
 AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x);
 
 AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
+    PROF_START(pm);
     const int nd = L.nda;
     const int go = lgo(L, m);
     const int lane = lane_id();
+    if (lane < L.nla) {   // world inertia R diag(I) R^T and mass of link `lane`
+        const m3 R = qmat(ldq(L.cm[lane] + 3));
+        const v3 I = ld3(m.rl_inertia + 4 * (go + lane));
+        float *w = L.u.d.iw[lane];
+#define AVR_IW(a, b) (R.m[a][0] * R.m[b][0] * I.x + R.m[a][1] * R.m[b][1] * I.y + R.m[a][2] * R.m[b][2] * I.z)
+        w[0] = AVR_IW(0, 0); w[1] = AVR_IW(1, 1); w[2] = AVR_IW(2, 2);
+        w[3] = AVR_IW(0, 1); w[4] = AVR_IW(0, 2); w[5] = AVR_IW(1, 2);
+#undef AVR_IW
+        w[6] = m.rl_mass[go + lane];
+    }
+    SYNC();
     const int ne = MAXD * (MAXD + 1) / 2;
     for (int e = lane; e < ne; e += 64) {
         int a = 0, rem = e;
@@ -141,17 +188,19 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         int b = rem;
         float s = 0.f;
         if (a < nd && b < nd) {
-            int la = m.dof_link[a], lb = m.dof_link[b];
+            const int la = m.dof_link[a], lb = m.dof_link[b];
+            const v3 axa = ld3(L.ax[la]), oa = ld3(L.org[la]), axb = ld3(L.ax[lb]), ob = ld3(L.org[lb]);
+            const bool ra = m.rl_jtype[la] == AVR_J_REVOLUTE, rb = m.rl_jtype[lb] == AVR_J_REVOLUTE;
             for (int i = 0; i < L.nla; i++) {
-                float mi = m.rl_mass[go + i];
-                if (mi <= 0.f) continue;
                 if (!is_ancestor(m, i, la) || !is_ancestor(m, i, lb)) continue;
-                v3 c = ld3(L.cm[i]);
-                qt q = ldq(L.cm[i] + 3);
-                v3 lina, anga, linb, angb;
-                dof_col(m, L, la, c, lina, anga);
-                dof_col(m, L, lb, c, linb, angb);
-                v3 Ia = inertia_mul(q, ld3(m.rl_inertia + 4 * (go + i)), anga);
+                const float *w = L.u.d.iw[i];
+                const float mi = w[6];
+                if (mi <= 0.f) continue;
+                const v3 c = ld3(L.cm[i]);
+                const v3 lina = ra ? crs(axa, sub(c, oa)) : axa, linb = rb ? crs(axb, sub(c, ob)) : axb;
+                const v3 anga = ra ? axa : V(0, 0, 0), angb = rb ? axb : V(0, 0, 0);
+                const v3 Ia = V(w[0] * anga.x + w[3] * anga.y + w[4] * anga.z, w[3] * anga.x + w[1] * anga.y + w[5] * anga.z,
+                                w[4] * anga.x + w[5] * anga.y + w[2] * anga.z);
                 s += mi * dot(lina, linb) + dot(Ia, angb);
             }
         } else if (a == b) s = 1.f;
@@ -159,6 +208,7 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         if (a != b) L.Mi[b][a] = 0.f;
     }
     SYNC();
+    PROF_STOP(24, pm);
     // column Cholesky, rows of each column in parallel (one lane per row)
     int ok = 1;
     for (int j = 0; j < MAXD; j++) {
@@ -177,6 +227,7 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         if (i == j) L.Mi[j][j] = d;
         SYNC();
     }
+    PROF_STOP(25, pm);
     // columns of M^-1 (one lane per DoF): every robot row gets M^-1 J^T from these
     if (lane < MAXD) {
         float e[MAXD], x[MAXD];
@@ -187,6 +238,7 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         for (int k = 0; k < MAXD; k++) L.Minv[k][lane] = x[k];
     }
     SYNC();
+    PROF_STOP(26, pm);
     return ok != 0;
 }
 
@@ -229,29 +281,44 @@ AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *
     }
 }
 
-// Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping) on lane 0,
-// temporaries in LDS; result in L.h.
+// Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping), result in L.h.
+// Forward pass level by level (lane i = link i, temporaries in LDS); the backward force
+// accumulation is summed per DoF instead: the DoF of link j sees the moment about its joint
+// origin of every force in its subtree, h_j = ax_j . sum_k (N_k + (c_k - o_j) x F_k) (revolute;
+// ax_j . sum_k F_k prismatic), which is what the recursion (F_p += F_k, N_p += N_k + (c_k - c_p)
+// x F_k) evaluates.
 AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
-    if (lane_id() == 0) {
-        float (*OM)[4] = L.u.d.rn[0], (*VC)[4] = L.u.d.rn[1], (*AL)[4] = L.u.d.rn[2], (*AC)[4] = L.u.d.rn[3], (*FF)[4] = L.u.d.rn[4], (*NN)[4] = L.u.d.rn[5];
-        const float k1l = m.lin_damp, k1a = m.ang_damp;
+    float (*OM)[4] = L.u.d.rn[0], (*VC)[4] = L.u.d.rn[1], (*AL)[4] = L.u.d.rn[2], (*AC)[4] = L.u.d.rn[3], (*FF)[4] = L.u.d.rn[4], (*NN)[4] = L.u.d.rn[5];
+    const float k1l = m.lin_damp, k1a = m.ang_damp;
+    const int i = lane_id();
+    const bool mine = i < L.nla;
+    int p = -3, jt = AVR_J_FIXED, lev = -1;
+    float mi = 0.f, qd = 0.f;
+    v3 I = V(0, 0, 0), o = V(0, 0, 0), c = V(0, 0, 0), axw = V(0, 0, 0);
+    qt q = Q(0, 0, 0, 1);
+    if (mine) {
         const int go = lgo(L, m);
-        tf base = ldtf(m.base);
-        for (int i = 0; i < L.nla; i++) {
-            int p = m.rl_parent[i];          // < 0: fixed robot base or (-2) the static chest slot
+        p = m.rl_parent[i];          // < 0: fixed robot base or (-2) the static chest slot
+        jt = m.rl_jtype[i];
+        lev = m.rl_level[i];
+        const int dof = m.rl_dof[i];
+        qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
+        o = ld3(L.org[i]); c = ld3(L.cm[i]); axw = ld3(L.ax[i]);
+        q = ldq(L.cm[i] + 3);
+        mi = m.rl_mass[go + i];
+        I = ld3(m.rl_inertia + 4 * (go + i));
+    }
+    const v3 bp = ld3(m.base);
+    for (int d = 0; d < m.nlev; d++) {
+        if (lev == d) {
             v3 omp = p < 0 ? V(0, 0, 0) : ld3(OM[p]);
             v3 vp = p < 0 ? V(0, 0, 0) : ld3(VC[p]);
             v3 alp = p < 0 ? V(0, 0, 0) : ld3(AL[p]);
             v3 acp = p < 0 ? V(0, 0, 0) : ld3(AC[p]);
-            v3 cp = p < 0 ? base.p : ld3(L.cm[p]);
-            int dof = m.rl_dof[i];
-            float qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
-            v3 o = ld3(L.org[i]), c = ld3(L.cm[i]);
-            v3 axw = ld3(L.ax[i]);
+            v3 cp = p < 0 ? bp : ld3(L.cm[p]);
             v3 rpo = sub(o, cp), roc = sub(c, o);
             v3 vo = add(vp, crs(omp, rpo));
             v3 ao = add(acp, add(crs(alp, rpo), crs(omp, crs(omp, rpo))));
-            int jt = m.rl_jtype[i];
             v3 om, vc, al, ac;
             if (jt == AVR_J_REVOLUTE) {
                 v3 wj = scl(axw, qd);
@@ -271,9 +338,6 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
                 vc = add(vo, crs(om, roc));
                 ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
             }
-            float mi = m.rl_mass[go + i];
-            qt q = ldq(L.cm[i] + 3);
-            v3 I = ld3(m.rl_inertia + 4 * (go + i));
             v3 Iw = inertia_mul(q, I, om);
             float vn = len(vc), wn = len(om);
             v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
@@ -282,22 +346,23 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
             st3(FF[i], sub(scl(ac, mi), fdamp));
             st3(NN[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
         }
-        for (int d = 0; d < MAXD; d++) L.h[d] = 0.f;
-        for (int i = L.nla - 1; i >= 0; i--) {
-            int dof = m.rl_dof[i];
-            v3 o = ld3(L.org[i]), c = ld3(L.cm[i]);
-            v3 axw = ld3(L.ax[i]);
-            v3 F = ld3(FF[i]), N = ld3(NN[i]);
-            if (dof >= 0) {
-                if (m.rl_jtype[i] == AVR_J_REVOLUTE) L.h[dof] = dot(axw, add(N, crs(sub(c, o), F)));
-                else L.h[dof] = dot(axw, F);
+        SYNC();
+    }
+    if (i < MAXD) {
+        float h = 0.f;
+        if (i < L.nda) {
+            const int j = m.dof_link[i];
+            const v3 aj = ld3(L.ax[j]), oj = ld3(L.org[j]);
+            const bool rev = m.rl_jtype[j] == AVR_J_REVOLUTE;
+            v3 acc = V(0, 0, 0);
+            for (int k = 0; k < L.nla; k++) {
+                if (!is_ancestor(m, k, j)) continue;
+                const v3 F = ld3(FF[k]);
+                acc = add(acc, rev ? add(ld3(NN[k]), crs(sub(ld3(L.cm[k]), oj), F)) : F);
             }
-            int p = m.rl_parent[i];
-            if (p >= 0) {
-                st3(FF[p], add(ld3(FF[p]), F));
-                st3(NN[p], add(ld3(NN[p]), add(N, crs(sub(c, ld3(L.cm[p])), F))));
-            }
+            h = dot(aj, acc);
         }
+        L.h[i] = h;
     }
     SYNC();
 }
@@ -558,7 +623,7 @@ AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
 #endif
 
 template <bool COOP>
-AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S) {
+AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
     v3 v = sub(A.t.p, B.t.p);
     if (len2(v) < 1e-20f) v = V(1, 0, 0);
     S.n = 0;
@@ -568,6 +633,7 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     const int max_it = COOP ? GJK_MAX_IT : GJK_LANE_IT;
     bool converged = false;
     for (int it = 0; it < max_it; it++) {
+        nit = it + 1;
         v3 sa = support<COOP>(m, A, scl(v, -1.f)), sb = support<COOP>(m, B, v);
         v3 wv = sub(sa, sb);
         float vv = len2(v), vw = dot(v, wv);
@@ -754,10 +820,15 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
 
 // --------------------------------------------------------------------------- narrowphase
 // returns: 0 no contact, 1 contact (nB, pB, dist), 2 needs the cooperative path
+// (nit, kind: diagnostic out-parameters -- GJK iterations, and 0 sphere-sphere, 1 sphere-box,
+// 2 sphere-capsule, 3 GJK; unused outside the AVR_PROF build)
 template <bool COOP>
-AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist) {
+AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist, int &nit, int &kind) {
     int ka = A.kind, kb = B.kind;
+    nit = 0;
+    kind = 3;
     if (ka == AVR_SPHERE && kb == AVR_SPHERE) {
+        kind = 0;
         v3 diff = sub(A.t.p, B.t.p);
         float l = len(diff), ra = A.he.x, rb = B.he.x;
         if (l > ra + rb) return 0;
@@ -769,6 +840,7 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
     }
     if ((ka == AVR_SPHERE && kb == AVR_BOX) || (ka == AVR_BOX && kb == AVR_SPHERE)) {
         bool swapped = ka == AVR_BOX;
+        kind = 1;
         const WShape Sp = swapped ? B : A;
         const WShape X = swapped ? A : B;
         v3 rel = tfinvpt(X.t, Sp.t.p);
@@ -801,6 +873,7 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
     }
     if ((ka == AVR_SPHERE || ka == AVR_CAPSULE) && (kb == AVR_SPHERE || kb == AVR_CAPSULE) && !(ka == AVR_CAPSULE && kb == AVR_CAPSULE)) {
         bool swapped = ka == AVR_CAPSULE;
+        kind = 2;
         const WShape Sp = swapped ? B : A;
         const WShape Cp = swapped ? A : B;
         v3 az = qrot(Cp.t.q, V(0, 0, 1));
@@ -823,7 +896,7 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
     v3 pa, pb;
     float cd;
     Simplex S;
-    int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S);
+    int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S, nit);
     if (st == GJK_FAR) return 0;
     if (st == GJK_UNFINISHED) return 2;
     v3 n;
@@ -889,13 +962,13 @@ struct MfNew { float p[AVR_CP_WORDS]; };
 
 AVR_DI int mf_idx(unsigned pk, int j) { return (int)((pk >> (8 * j)) & 255u); }
 AVR_DI unsigned mf_set(unsigned pk, int j, int v) { return (pk & ~(255u << (8 * j))) | ((unsigned)v << (8 * j)); }
-AVR_DI float mf_rd(const float *cp, const MfNew &nw, int idx, int w) {
+AVR_DI float mf_rd(const lds_f *cp, const MfNew &nw, int idx, int w) {
     return idx == MF_NEW ? nw.p[w] : cp[AVR_CP_WORDS * idx + w];
 }
-AVR_DI v3 mf_rd3(const float *cp, const MfNew &nw, int idx, int w) {
+AVR_DI v3 mf_rd3(const lds_f *cp, const MfNew &nw, int idx, int w) {
     return V(mf_rd(cp, nw, idx, w), mf_rd(cp, nw, idx, w + 1), mf_rd(cp, nw, idx, w + 2));
 }
-AVR_DI void mf_wr(float *cp, MfNew &nw, int idx, int w, float x) {
+AVR_DI void mf_wr(lds_f *cp, MfNew &nw, int idx, int w, float x) {
     if (idx == MF_NEW) {
 #pragma unroll
         for (int k = 0; k < AVR_CP_WORDS; k++)
@@ -904,7 +977,7 @@ AVR_DI void mf_wr(float *cp, MfNew &nw, int idx, int w, float x) {
 }
 
 // btPersistentManifold::sortCachedPoints
-AVR_DI int sort_cached(const float *cp, const MfNew &nw, unsigned pk, v3 la_new, float d_new) {
+AVR_DI int sort_cached(const lds_f *cp, const MfNew &nw, unsigned pk, v3 la_new, float d_new) {
     int maxi = -1;
     float maxpen = d_new;
     v3 p[4];
@@ -929,7 +1002,7 @@ AVR_DI int sort_cached(const float *cp, const MfNew &nw, unsigned pk, v3 la_new,
 }
 
 // btManifoldResult::addContactPoint (getCacheEntry / replaceContactPoint / addManifoldPoint)
-AVR_DI void manifold_add(float *cp, MfNew &nw, unsigned &pk, int &n, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB,
+AVR_DI void manifold_add(lds_f *cp, MfNew &nw, unsigned &pk, int &n, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB,
                          float dist, float thr) {
     if (dist > thr) return;
     v3 pA = add(pB, scl(nB, dist));
@@ -967,7 +1040,7 @@ AVR_DI void manifold_add(float *cp, MfNew &nw, unsigned &pk, int &n, int sa, int
 }
 
 // btPersistentManifold::refreshContactPoints
-AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, tf tb, float thr) {
+AVR_DI void manifold_refresh(lds_f *cp, MfNew &nw, unsigned &pk, int &n, tf ta, tf tb, float thr) {
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
         if (k < n) {
@@ -1015,33 +1088,36 @@ AVR_DI void manifold_refresh(float *cp, MfNew &nw, unsigned &pk, int &n, tf ta, 
 #define SCR_EPA 0                                   // EpaBuf
 #define SCR_NEWCP 2560                              // new contact pool [AVR_MAX_CONTACTS][16]
 
-AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, v3 &mn, v3 &mx) {
-    const int c = m.shape_cidx[s];
-    if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
-    else { const float *a = m.static_saabb + 8 * s; mn = ld3(a); mx = ld3(a + 4); }
-}
+AVR_DI float *env_cs(const KModel &m, int env) { return m.cscr + (size_t)env * CS_WORDS; }
 
-// narrowphase + manifold update for the nq (<= 64) queued pairs, lane q <-> queue entry q
-AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int nold, float *newcp, int &nnew, EpaBuf &E) {
+// world AABB of child shape s from its packed info (m.shape_info): the per-sub-step cache for a
+// non-static shape, the host-precomputed box for a static one
+AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, int info, v3 &mn, v3 &mx) {
+    const int c = (info & 511) - 1;
+    if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
+    else { const gf4p a = (gf4p)(m.static_saabb + 8 * s); const f4v x = a[0], y = a[1]; mn = V(x.x, x.y, x.z); mx = V(y.x, y.y, y.z); }
+}
+AVR_DI bool info_enabled(int info, int gender) { const int g = (info >> 9) - 1; return g < 0 || g == gender; }
+
+// manifold update for the nq (<= 64) shape pairs k0 .. k0 + nq - 1 of the list, lane q <-> pair
+// k0 + q: the narrowphase result comes from avr_narrowphase_kernel; pairs it left to the
+// cooperative path (big hulls without a support table, EPA) are finished here, in pair order
+AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew, EpaBuf &E) {
     const int lane = lane_id();
-    const int gender = L.gender;
-    (void)gender;
     PROF_START(pb);
     int sa = 0, sb = 0, p = 0;
-    if (lane < nq) { int k = L.u.c.qk[lane]; sa = k & 0xffff; sb = k >> 16; p = L.u.c.qp[lane]; }
     int rc = 0;
     v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
     float d = 0.f;
     bool coop = false;
     if (lane < nq) {
-        int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-        WShape A = make_wshape(m, sa, ldtf(L.btf[ba])), B = make_wshape(m, sb, ldtf(L.btf[bb]));
-        if ((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0)) coop = true;
-        else {
-            rc = narrowphase<false>(m, E, A, B, thr, nB, pB, d);
-            if (rc == 2) coop = true;
-        }
+        const int k = __float_as_int(cs[CS_PAIRS + 2 * (k0 + lane)]);
+        sa = k & 0xffff; sb = k >> 16;
+        p = __float_as_int(cs[CS_PAIRS + 2 * (k0 + lane) + 1]);
+        const float4 r0 = ((const float4 *)(cs + CS_RES))[2 * (k0 + lane)], r1 = ((const float4 *)(cs + CS_RES))[2 * (k0 + lane) + 1];
+        rc = __float_as_int(r0.x);
+        nB = V(r0.y, r0.z, r0.w); pB = V(r1.x, r1.y, r1.z); d = r1.w;
+        coop = rc == 2;
     }
     // wave-cooperative narrowphase, in pair order
     unsigned long long cm = __ballot(coop);
@@ -1070,7 +1146,8 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         WShape A = make_wshape(m, sj, ldtf(L.btf[ba])), B = make_wshape(m, tj, ldtf(L.btf[bb]));
         v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
         float d2 = 0.f;
-        int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2);
+        int nit2, nk2;
+        int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit2, nk2);
         if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
     }
     PROF_STOP(17, pb);
@@ -1085,8 +1162,9 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
         int ba = m.shape_body[sa], bb = m.shape_body[sb];
         float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
         const int key = sa | (sb << 16);
-        for (int i = 0; i < nold && n < AVR_MANIFOLD_POINTS; i++)
-            if (L.u.c.okey[i] == key) { pk = mf_set(pk, n, i); n++; }
+        const lds_i *ok = (const lds_i *)L.u.k.okey;
+        for (int i = 0; i < nold; i++)      // (no early exit: the key reads stay independent)
+            if (ok[i] == key && n < AVR_MANIFOLD_POINTS) { pk = mf_set(pk, n, i); n++; }
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         if (rc == 1) manifold_add(oldcp, nw, pk, n, sa, sb, p, ta, tb, nB, pB, d, thr);
         manifold_refresh(oldcp, nw, pk, n, ta, tb, thr);
@@ -1112,11 +1190,12 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
                     o[2] = make_float4(nw.p[8], nw.p[9], nw.p[10], nw.p[11]);
                     o[3] = make_float4(nw.p[12], nw.p[13], nw.p[14], nw.p[15]);
                 } else {
-                    const float *q = oldcp + AVR_CP_WORDS * id;     // state rows are only 4-byte aligned
-                    o[0] = make_float4(q[0], q[1], q[2], q[3]);
-                    o[1] = make_float4(q[4], q[5], q[6], q[7]);
-                    o[2] = make_float4(q[8], q[9], q[10], q[11]);
-                    o[3] = make_float4(q[12], q[13], q[14], q[15]);
+                    const lds_f4 *q = (const lds_f4 *)(oldcp + AVR_CP_WORDS * id);
+                    const f4v q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+                    o[0] = make_float4(q0.x, q0.y, q0.z, q0.w);
+                    o[1] = make_float4(q1.x, q1.y, q1.z, q1.w);
+                    o[2] = make_float4(q2.x, q2.y, q2.z, q2.w);
+                    o[3] = make_float4(q3.x, q3.y, q3.z, q3.w);
                 }
             }
         }
@@ -1125,11 +1204,11 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, int nq, float *oldcp, int 
     PROF_STOP(18, pb);
 }
 
-AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
+// Part A1 (avr_substep_pairs_kernel): body frames, fattened AABBs, broadphase and the ordered
+// shape-pair list, written to the env's collision scratch.
+AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
     const int lane = lane_id();
     const int gender = L.gender;
-    EpaBuf &E = *(EpaBuf *)(scratch + SCR_EPA);
-    float *newcp = scratch + SCR_NEWCP;
     PROF_START(pt);
     // body transforms + fattened AABBs
     for (int b = lane; b < m.nb; b += 64) {
@@ -1140,13 +1219,10 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
         aabb_of(t, ld3(a), ld3(a + 3), mn, mx);
         v3 e = V(BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND);
         sttf(L.btf[b], t);
+        sttf(cs + CS_BTF + 8 * b, t);
         st3(L.u.c.bmin[b], sub(mn, e));
         st3(L.u.c.bmax[b], add(mx, e));
     }
-    // keys of the previous contact pool (matching in the manifold update)
-    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
-    for (int i = lane; i < nold; i += 64)
-        L.u.c.okey[i] = (int)gcp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gcp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     SYNC();
     // world AABBs of the non-static child shapes
     for (int s = lane; s < m.ns; s += 64) {
@@ -1176,16 +1252,14 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
     PROF_STOP(1, pt);
-    // child shape pairs -> queue -> batches of 64.  A child's world AABB lies inside its body's
-    // fattened AABB, so children of A that miss B's body AABB cannot meet any child of B: the
-    // child lists are culled against the other body first, which leaves the set of overlapping
-    // child pairs and its i-major / j-minor order unchanged.
-    int nq = 0, nsp = 0, nnew = 0;
-    // Shape pairs are produced 64 at a time, in pair order (i-major, j-minor within a pair), from
-    // either a run of consecutive single-child pairs (1 x 1: food-food, robot link-link, ...; 80 %
-    // of the active pairs), one lane per pair, or one culled compound pair, one lane per item.
-    // Every round appends its pairs to the queue; a full queue (or the end) runs collide_batch.
-    // (One producer loop keeps a single inlined copy of collide_batch.)
+    // Child shape pairs, in pair order (i-major, j-minor within a body pair), appended to the
+    // list.  A child's world AABB lies inside its body's fattened AABB, so children of A that
+    // miss B's body AABB cannot meet any child of B: the child lists are culled against the other
+    // body first, which leaves the set of overlapping child pairs and its order unchanged.
+    // Pairs are produced 64 at a time from either a run of consecutive single-child pairs (1 x 1:
+    // food-food, robot link-link, ...; 80 % of the active pairs), one lane per pair, or one culled
+    // compound pair, one lane per item.
+    int nsp = 0;
     int k = 0;                                      // next active pair
     int gp = 0, gsa0 = 0, gsb0 = 0, gncB = 1, gn = 0, gbase = 0;
     bool gcull = false, gbare = false;
@@ -1202,18 +1276,19 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                     sa = L.u.c.candA[i];
                     sb = L.u.c.candB[j];
                     v3 a0, a1, b0, b1;
-                    child_aabb(m, L, sa, a0, a1);
-                    child_aabb(m, L, sb, b0, b1);
+                    child_aabb(m, L, sa, m.shape_info[sa], a0, a1);
+                    child_aabb(m, L, sb, m.shape_info[sb], b0, b1);
                     act = overlap(a0, a1, b0, b1);
                 } else {
                     sa = gsa0 + i;
                     sb = gsb0 + j;
-                    if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
+                    const int ia = m.shape_info[sa], ib = m.shape_info[sb];
+                    if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (gbare) act = true;
                         else {
                             v3 a0, a1, b0, b1;
-                            child_aabb(m, L, sa, a0, a1);
-                            child_aabb(m, L, sb, b0, b1);
+                            child_aabb(m, L, sa, ia, a0, a1);
+                            child_aabb(m, L, sb, ib, b0, b1);
                             act = overlap(a0, a1, b0, b1);
                         }
                     }
@@ -1223,25 +1298,22 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
         } else if (k < nap) {
             if (gcull) { SYNC(); gcull = false; }   // candA / candB are rewritten below
             const int kk = k + lane;
-            bool one = false;
-            if (kk < nap) {
-                const int qq = L.u.c.apair[kk];
-                one = m.body_shape_count[m.pair_a[qq]] == 1 && m.body_shape_count[m.pair_b[qq]] == 1;
-            }
-            const unsigned long long bm = __ballot(one);
+            int4 rec = make_int4(0, 0, 0, 0);
+            if (kk < nap) rec = m.pair_rec[L.u.c.apair[kk]];
+            const unsigned long long bm = __ballot(kk < nap && (rec.w & 2));
             const int run = bm == ~0ull ? 64 : __ffsll((long long)~bm) - 1;
             if (run > 0) {                          // a run of 1 x 1 pairs
                 if (lane < run) {
-                    q = L.u.c.apair[k + lane];
-                    const int ba = m.pair_a[q], bb = m.pair_b[q];
-                    sa = m.body_shape_start[ba];
-                    sb = m.body_shape_start[bb];
-                    if (shape_enabled(m, sa, gender) && shape_enabled(m, sb, gender)) {
-                        if ((m.body_flags[ba] & 1) && (m.body_flags[bb] & 1)) act = true;
+                    q = L.u.c.apair[kk];
+                    sa = rec.y & 0xffff;
+                    sb = rec.z & 0xffff;
+                    const int ia = m.shape_info[sa], ib = m.shape_info[sb];
+                    if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
+                        if (rec.w & 1) act = true;
                         else {
                             v3 a0, a1, b0, b1;
-                            child_aabb(m, L, sa, a0, a1);
-                            child_aabb(m, L, sb, b0, b1);
+                            child_aabb(m, L, sa, ia, a0, a1);
+                            child_aabb(m, L, sb, ib, b0, b1);
                             act = overlap(a0, a1, b0, b1);
                         }
                     }
@@ -1250,13 +1322,14 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                 if (lane == 0) L.prof[4] += run;
 #endif
                 k += run;
-            } else {                                // set up compound pair k
+            } else {                                // set up compound pair k (lane 0's record)
                 gp = L.u.c.apair[k];
-                const int ba = m.pair_a[gp], bb = m.pair_b[gp];
-                const int na = m.body_shape_count[ba], nb = m.body_shape_count[bb];
-                gsa0 = m.body_shape_start[ba];
-                gsb0 = m.body_shape_start[bb];
-                gbare = (m.body_flags[ba] & 1) && (m.body_flags[bb] & 1);
+                const int4 r0 = m.pair_rec[gp];
+                const int ba = r0.x & 0xffff, bb = r0.x >> 16;
+                const int na = r0.y >> 16, nb = r0.z >> 16;
+                gsa0 = r0.y & 0xffff;
+                gsb0 = r0.z & 0xffff;
+                gbare = r0.w & 1;
                 gcull = !gbare && na * nb > 1;
                 int ncA = na, ncB = nb;
                 if (gcull) {
@@ -1266,10 +1339,13 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                     for (int base = 0; base < na; base += 64) {
                         const int i = base + lane;
                         bool a = false;
-                        if (i < na && shape_enabled(m, gsa0 + i, gender)) {
-                            v3 a0, a1;
-                            child_aabb(m, L, gsa0 + i, a0, a1);
-                            a = overlap(a0, a1, bBmn, bBmx);
+                        if (i < na) {
+                            const int ia = m.shape_info[gsa0 + i];
+                            if (info_enabled(ia, gender)) {
+                                v3 a0, a1;
+                                child_aabb(m, L, gsa0 + i, ia, a0, a1);
+                                a = overlap(a0, a1, bBmn, bBmx);
+                            }
                         }
                         int tot;
                         int pre = ballot_prefix(a, &tot);
@@ -1280,10 +1356,13 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
                     for (int base = 0; base < nb; base += 64) {
                         const int j = base + lane;
                         bool a = false;
-                        if (j < nb && shape_enabled(m, gsb0 + j, gender)) {
-                            v3 b0, b1;
-                            child_aabb(m, L, gsb0 + j, b0, b1);
-                            a = overlap(b0, b1, bAmn, bAmx);
+                        if (j < nb) {
+                            const int ib = m.shape_info[gsb0 + j];
+                            if (info_enabled(ib, gender)) {
+                                v3 b0, b1;
+                                child_aabb(m, L, gsb0 + j, ib, b0, b1);
+                                a = overlap(b0, b1, bAmn, bAmx);
+                            }
                         }
                         int tot;
                         int pre = ballot_prefix(a, &tot);
@@ -1307,35 +1386,53 @@ AVR_DI void collide(const KModel &m, EnvLDS &L, float *gcp, float *scratch) {
         // sub-step (flag 8)
         int tot;
         int pre = ballot_prefix(act, &tot);
-        if (act && nsp + pre < MAXSP) { L.u.c.qk[nq + pre] = sa | (sb << 16); L.u.c.qp[nq + pre] = q; }
-        const int add = nsp + tot <= MAXSP ? tot : (nsp < MAXSP ? MAXSP - nsp : 0);
-        nsp += tot;
-        nq += add;
-        if (nq >= 64 || (last && nq > 0)) {
-            const int nb = nq >= 64 ? 64 : nq;
-            SYNC();
-            PROF_STOP(2, pt);
-            collide_batch(m, L, nb, gcp, nold, newcp, nnew, E);
-            PROF_STOP(3, pt);
-            SYNC();
-            if (lane < nq - nb) { L.u.c.qk[lane] = L.u.c.qk[nb + lane]; L.u.c.qp[lane] = L.u.c.qp[nb + lane]; }
-            nq -= nb;
-            SYNC();
-            if (last && nq > 0) continue;          // (cannot happen: at most 64 + 63 queued)
+        if (act && nsp + pre < MAXSP) {
+            cs[CS_PAIRS + 2 * (nsp + pre)] = __int_as_float(sa | (sb << 16));
+            cs[CS_PAIRS + 2 * (nsp + pre) + 1] = __int_as_float(q);
         }
+        nsp += tot;
         if (last) break;
     }
-    if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; }
+    if (nsp > MAXSP) { if (lane == 0) L.flags |= 8; nsp = MAXSP; }
 #ifdef AVR_PROF
-    if (lane == 0) { L.prof[14] += nsp < MAXSP ? nsp : MAXSP; L.prof[15] += nap; }
+    if (lane == 0) { L.prof[14] += nsp; L.prof[15] += nap; }
 #endif
+    if (lane == 0) { cs[CS_NSP] = __int_as_float(nsp); cs[CS_FLAGS] = __int_as_float(L.flags); }
+    PROF_STOP(2, pt);
+}
+
+// Part A3 (avr_substep_a_kernel): manifold update of every listed shape pair from its
+// narrowphase result, 64 pairs at a time, and the new contact pool.  The previous contact pool
+// stays in the env's global state (read, and updated in place by the single lane that owns each
+// point); the new pool is appended to global scratch and copied over the old one at the end.
+AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float *gcp, float *scratch) {
+    const int lane = lane_id();
+    EpaBuf &E = *(EpaBuf *)(scratch + SCR_EPA);
+    float *newcp = scratch + SCR_NEWCP;
+    PROF_START(pt);
+    // the previous contact pool in LDS (the manifold update reads and updates it in place) and
+    // its keys (matching in the manifold update)
+    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    lds_f *ocp = (lds_f *)L.u.k.ocp;
+    const gfp gp = (gfp)gcp;
+    for (int i = lane; i < nold * AVR_CP_WORDS; i += 64) ocp[i] = gp[i];
+    for (int i = lane; i < nold; i += 64)
+        L.u.k.okey[i] = (int)gp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
+    if (lane == 0) L.flags |= __float_as_int(cs[CS_FLAGS]);
+    SYNC();
+    const int nsp = __float_as_int(cs[CS_NSP]);
+    int nnew = 0;
+    for (int k0 = 0; k0 < nsp; k0 += 64) {
+        collide_batch(m, L, cs, k0, min(64, nsp - k0), ocp, nold, newcp, nnew, E);
+        SYNC();
+    }
     if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
     SYNC();
     // the new pool replaces the old one
     for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) gcp[i] = newcp[i];
     if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
     SYNC();
-    PROF_STOP(2, pt);
+    PROF_STOP(3, pt);
 }
 
 // --------------------------------------------------------------------------- constraint rows
@@ -1651,19 +1748,28 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
 }
 
 // --------------------------------------------------------------------------- one sub-step
-// Sub-step part A (kernel avr_substep_a): forward kinematics, collision, unconstrained
-// velocities, constraint rows.  Part B (avr_substep_b): PGS + integration.  What crosses the
-// kernel boundary goes through the per-env workspace (m.ws) and the row buffer (m.rows).
-AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows) {
+// A sub-step is four kernels: avr_substep_pairs_kernel (forward kinematics, body frames,
+// broadphase, shape-pair list), avr_narrowphase_kernel (one lane per listed shape pair, across
+// all envs), avr_substep_a_kernel (manifold update, unconstrained velocities, constraint rows)
+// and avr_substep_b4_kernel (PGS + integration).  What crosses the kernel boundaries goes
+// through the per-env collision scratch (m.cscr), the workspace (m.ws) and the row buffer
+// (m.rows).
+AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows, const float *cs) {
     const int lane = lane_id();
     PROF_START(ps);
-    robot_fk(m, L);
+    // body and link frames from the pair kernel
+    for (int i = lane; i < m.nb * 8; i += 64) (&L.btf[0][0])[i] = cs[CS_BTF + i];
+    for (int i = lane; i < L.nla * 8; i += 64) (&L.cm[0][0])[i] = cs[CS_CM + i];
+    for (int i = lane; i < L.nla * 4; i += 64) { (&L.ax[0][0])[i] = cs[CS_AX + i]; (&L.org[0][0])[i] = cs[CS_ORG + i]; }
+    SYNC();
     PROF_STOP(0, ps);
-    collide(m, L, gst + AVR_S_CP, rows);
+    collide_contacts(m, L, cs, gst + AVR_S_CP, rows);
     PROF_STOP(13, ps);
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
+    PROF_START(pbias);
     robot_bias(m, L);
+    PROF_STOP(27, pbias);
     if (lane < MAXD) {                      // qdd = -M^-1 h, one lane per DoF
         float s = 0.f;
         for (int k = 0; k < L.nda; k++) s -= L.Minv[lane][k] * L.h[k];
@@ -1912,7 +2018,74 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
 #define WT_END(k) (void)0
 #endif
 
-// Sub-step part A: one 64-lane block per env, state staged in LDS.
+// Sub-step part A1: one 64-lane block per env -- forward kinematics, body frames, broadphase,
+// shape-pair list (collide_pairs) into the env's collision scratch.
+__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                                         const unsigned char *__restrict__ mask, int env0, int n_envs) {
+    __shared__ EnvLDS L;
+    AVR_ENV_GUARD();
+    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    load_state(m, L, gst);
+    PROF_START(ps);
+    robot_fk(m, L);
+    PROF_STOP(0, ps);
+    float *cs = env_cs(m, env);
+    for (int i = lane_id(); i < L.nla * 8; i += 64) cs[CS_CM + i] = (&L.cm[0][0])[i];
+    for (int i = lane_id(); i < L.nla * 4; i += 64) { cs[CS_AX + i] = (&L.ax[0][0])[i]; cs[CS_ORG + i] = (&L.org[0][0])[i]; }
+    collide_pairs(m, L, cs);
+    prof_flush(m, L, env);
+}
+
+// Sub-step part A2: the narrowphase of every listed shape pair, one lane per pair, across all
+// envs (64 pairs per block, 4 blocks per env cover MAXSP; blocks past an env's list exit).  Pairs
+// with a big hull that has no support table, and penetrating pairs that need EPA, are marked
+// rc = 2 and finished by the wave-cooperative path in part A3.  Block b takes env
+// 8 (b / 32) + b % 8, chunk (b / 8) % 4: the same XCD as parts A1 and A3 for that env.
+__global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
+                                                             int n_envs) {
+    const int env = env0 + 8 * (blockIdx.x >> 5) + (blockIdx.x & 7);
+    const int k = ((blockIdx.x >> 3) & 3) * 64 + lane_id();
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const KModel &m = *mp;
+    float *cs = env_cs(m, env);
+    if (k >= __float_as_int(cs[CS_NSP])) return;
+    const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
+    const int sa = key & 0xffff, sb = key >> 16;
+    const int ba = m.shape_body[sa], bb = m.shape_body[sb];
+    const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+    const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+    int rc = 2;
+    v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+    float d = 0.f;
+    if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
+        int nit, nkind;
+        rc = narrowphase<false>(m, *(EpaBuf *)cs, A, B, thr, nB, pB, d, nit, nkind);   // (the lane path never touches the EPA buffer)
+#ifdef AVR_PROF
+        if (m.prof) {   // pairs and GJK iterations per pair category (atomics: diagnostic build only)
+            // 0 sphere-sphere, 1 other closed form, 2 sphere-small hull, 3 sphere-table hull,
+            // 4 box-hull, 5 small hull-small hull, 6 hull-hull with a table, 7 other GJK
+            const bool sA = A.kind == AVR_SPHERE, sB = B.kind == AVR_SPHERE;
+            const bool hA = A.kind == AVR_HULL, hB = B.kind == AVR_HULL;
+            const bool tA = A.tab >= 0, tB = B.tab >= 0;
+            int cat = 7;
+            if (nkind == 0) cat = 0;
+            else if (nkind == 1 || nkind == 2) cat = 1;
+            else if ((sA && hB) || (sB && hA)) cat = (tA || tB) ? 3 : 2;
+            else if ((A.kind == AVR_BOX && hB) || (B.kind == AVR_BOX && hA)) cat = 4;
+            else if (hA && hB) cat = (tA || tB) ? 6 : 5;
+            unsigned long long *pr = m.prof + (size_t)env * AVR_PROF_SLOTS;
+            atomicAdd(pr + 32 + cat, 1ull);
+            atomicAdd(pr + 40 + cat, (unsigned long long)nit);
+        }
+#endif
+    }
+    float4 *o = (float4 *)(cs + CS_RES) + 2 * k;
+    o[0] = make_float4(__int_as_float(rc), nB.x, nB.y, nB.z);
+    o[1] = make_float4(pB.x, pB.y, pB.z, d);
+}
+
+// Sub-step part A3: one 64-lane block per env, state staged in LDS -- manifold update,
+// unconstrained velocities, constraint rows.
 __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                                      const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
     __shared__ EnvLDS L;
@@ -1920,7 +2093,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     WT_START();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     load_state(m, L, gst);
-    bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env));
+    bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
 #ifdef AVR_PROF
     if (lane_id() == 0) env_ws(m, env)[WS_XCC] = __int_as_float(xcc_id());
 #endif
@@ -1929,7 +2102,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     if (lane_id() == 0) L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)((int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags);
     SYNC();
     // write back what part A changes in LDS: contact count and flags (the pool itself was
-    // written to global memory by collide)
+    // written to global memory by collide_contacts)
     if (lane_id() < 16) gst[AVR_S_TASK + lane_id()] = L.st[AVR_S_TASK + lane_id()];
     prof_flush(m, L, env);
     WT_END(0);
@@ -1958,15 +2131,6 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 struct DV { float rq, vx, vy, vz, wx, wy, wz; };
 
 AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) float lds_f;
-typedef __attribute__((address_space(3))) f2v lds_f2;
-typedef __attribute__((address_space(3))) f4v lds_f4;
-typedef __attribute__((address_space(3))) int lds_i;
-typedef const __attribute__((address_space(1))) float *gfp;
-typedef const __attribute__((address_space(1))) f4v *gf4p;
-typedef const __attribute__((address_space(1))) f2v *gf2p;
 
 // Global row data is read with buffer loads through one resource over the whole row buffer
 // (uniform base in SGPRs, 32-bit per-lane byte offsets): a null row or a lane with no part to
@@ -2493,6 +2657,10 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     // frame_end: the sub-step closes a gym frame (stepSimulation) and B applies
     // enforce_hard_human_joint_limits (env.py:342-343); the reset's settle frames do not
     auto sub = [&](float h, int frame_end) {
+        mark(AVR_K_PAIRS);
+        hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
+        mark(AVR_K_NARROW);
+        hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(32 * ((n_envs + 7) / 8)), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
@@ -2527,17 +2695,18 @@ extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env
     return hipGetLastError();
 }
 
-// [vgprs, 0, lds bytes, scratch bytes] of substep_a, then of substep_b
-extern "C" hipError_t avr_kernel_attrs(int *out8) {
-    const void *k[2] = {(const void *)avr_substep_a_kernel, (const void *)avr_substep_b4_kernel};
-    for (int i = 0; i < 2; i++) {
+// [vgprs, 0, lds bytes, scratch bytes] of each sub-step kernel: pairs, narrowphase, a, b4
+extern "C" hipError_t avr_kernel_attrs(int *out16) {
+    const void *k[4] = {(const void *)avr_substep_pairs_kernel, (const void *)avr_narrowphase_kernel, (const void *)avr_substep_a_kernel,
+                        (const void *)avr_substep_b4_kernel};
+    for (int i = 0; i < 4; i++) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, k[i]);
         if (e != hipSuccess) return e;
-        out8[4 * i + 0] = a.numRegs;
-        out8[4 * i + 1] = 0;
-        out8[4 * i + 2] = (int)a.sharedSizeBytes;
-        out8[4 * i + 3] = (int)a.localSizeBytes;
+        out16[4 * i + 0] = a.numRegs;
+        out16[4 * i + 1] = 0;
+        out16[4 * i + 2] = (int)a.sharedSizeBytes;
+        out16[4 * i + 3] = (int)a.localSizeBytes;
     }
     return hipSuccess;
 }

@@ -27,6 +27,20 @@
 #define BIGF 1e30f
 
 
+// Per-env collision scratch (m.cscr, CS_WORDS floats per env), the hand-over between the three
+// kernels of a sub-step's part A: avr_substep_pairs_kernel writes the shape-pair list, the body
+// COM frames and the link frames; avr_narrowphase_kernel writes one result per pair;
+// avr_substep_a_kernel consumes them.
+#define CS_NSP 0                                    // int bits: shape pairs
+#define CS_FLAGS 1                                  // int bits: flags raised by the pair kernel
+#define CS_PAIRS 4                                  // [MAXSP] (sa | sb << 16, body pair) int bits
+#define CS_RES (CS_PAIRS + 2 * MAXSP)               // [MAXSP][8] rc, nB, pB, dist (rc 2: cooperative path)
+#define CS_BTF (CS_RES + 8 * MAXSP)                 // [MAXB][8] body COM frames
+#define CS_CM (CS_BTF + 8 * MAXB)                   // [MAXL][8] link COM frames
+#define CS_AX (CS_CM + 8 * MAXL)                    // [MAXL][4] joint axes (world)
+#define CS_ORG (CS_AX + 4 * MAXL)                   // [MAXL][4] joint origins (world)
+#define CS_WORDS (CS_ORG + 4 * MAXL)
+
 // Articulated links: the robot's nl links, then (impairment 'tremor') the head/neck chain's
 // hc_n links with DoFs nd .. nd + hc_n - 1; nla = nl + hc_n.  The chain root's parent is -2:
 // the static human slot hc_parent_slot.  Per-link tables are [nla]; the tables that differ by
@@ -55,6 +69,8 @@ struct KModel {
     const int *shape_cidx;      // [ns] index into the per-sub-step child AABB cache, -1 for static shapes
     const float *static_saabb;  // [ns][8] world AABB (min3, pad, max3, pad) of static shapes (host-computed)
     const int *pair_a, *pair_b;
+    const int *shape_info;      // [ns] (child AABB cache index + 1, 0 static) | (shape_gender + 1) << 9
+    const int4 *pair_rec;       // [np] (ba | bb << 16, sa0 | na << 16, sb0 | nb << 16, bare | one-by-one << 1)
     int n_arm, arm_dofs[8], n_finger, finger_dofs[4];
     int tool_link, torso_link, head_slot, spoon_free, bowl_free, food_free0, n_food;
     int table_body, bowl_body, spoon_body, food_body0, tool_body;
@@ -68,6 +84,8 @@ struct KModel {
     int env_offset;
     int dof_link[MAXD];        // link owning each DoF
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+    int rl_level[MAXL];        // depth of each link in the tree (roots 0)
+    int nlev;                  // number of levels
     int hc_parent_slot, hc_slot[AVR_HC_N], hc_body[AVR_HC_N];
     float hc_lower[AVR_HC_N], hc_upper[AVR_HC_N], human_gain, human_force;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
@@ -76,12 +94,13 @@ struct KModel {
     int rows_envs;             // envs covered by the row buffer (the handle's n_envs)
     int b4_global;             // diagnostic (AVR_B4_GLOBAL=1): part B reads every row from global memory
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
+    float *cscr;               // per-env collision scratch between the part-A kernels: [n_envs][CS_WORDS]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
 };
 
 // Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):
 // an event is recorded before every launch (kind = AVR_K_*) and after the last one (kind -1).
-enum { AVR_K_TAKE = 0, AVR_K_A = 1, AVR_K_B = 2, AVR_K_TASK = 3, AVR_K_KINDS = 4 };
+enum { AVR_K_TAKE = 0, AVR_K_A = 1, AVR_K_B = 2, AVR_K_TASK = 3, AVR_K_PAIRS = 4, AVR_K_NARROW = 5, AVR_K_KINDS = 8 };
 struct avr_evlog {
     hipEvent_t *ev;
     int *kind;

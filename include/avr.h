@@ -91,17 +91,19 @@ void *avr_state_device_ptr(avr_sim *sim);
 int32_t avr_n_envs(avr_sim *sim);
 int32_t avr_state_words(void);
 int32_t avr_abi_version(void);
-/* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of the sub-step kernel A
- * (kinematics, collision, rows), then the same four for kernel B (PGS + integration). */
-int avr_kernel_info(avr_sim *sim, int32_t *out8);
+/* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of each sub-step kernel, in
+ * launch order: pairs (kinematics, broadphase, shape-pair list), narrowphase, a (manifolds,
+ * dynamics, constraint rows), b (PGS + integration). */
+int avr_kernel_info(avr_sim *sim, int32_t *out16);
 const char *avr_last_error(avr_sim *sim);
 
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
  * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times
  * returns the accumulated milliseconds and launch counts per kernel kind
- * [take_step, substep_a, substep_b, task] since enabling (synchronises the stream). */
+ * [take_step, substep_a, substep_b, task, substep_pairs, narrowphase, -, -] since enabling
+ * (synchronises the stream). */
 int avr_profile_kernels(avr_sim *sim, int32_t enable);
-int avr_kernel_times(avr_sim *sim, double *ms4, int64_t *count4);
+int avr_kernel_times(avr_sim *sim, double *ms8, int64_t *count8);
 
 /* Diagnostics (phase-timer builds only, -DAVR_PROF): attach a device buffer of
  * [n_envs][16] uint64 cycle counters.  A no-op for the shipped kernel. */

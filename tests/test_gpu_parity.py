@@ -54,9 +54,10 @@ def test_kernel_resources(lib_and_scene):
     A, md = lib_and_scene
     sim = make_sim(md, 4)
     ki = sim.kernel_info()
-    assert ki['scratch_bytes'] == 0 and ki['b_scratch_bytes'] == 0     # no spills to scratch on gfx950
-    assert ki['lds_bytes'] <= 20 * 1024              # part A: 8 env blocks per CU
-    assert ki['b_lds_bytes'] <= 40 * 1024            # part B (four envs per wave): 4 blocks per CU, all resident
+    assert all(k['scratch_bytes'] == 0 for k in ki.values())     # no spills to scratch on gfx950
+    assert ki['narrowphase']['lds_bytes'] == 0
+    assert ki['a']['lds_bytes'] <= 20 * 1024 and ki['pairs']['lds_bytes'] <= 20 * 1024    # 8 env blocks per CU
+    assert ki['b']['lds_bytes'] <= 40 * 1024            # part B (four envs per wave): 4 blocks per CU, all resident
     sim.close()
 
 

@@ -1,0 +1,35 @@
+"""Experiment builds of libavr.so: exp/libavr_<name>.so with the extra hipcc flags of VARIANTS
+(tools/gpu_variants.sh benches them against the shipped build).
+
+    python tools/build_variants.py name [name ...]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd'))
+from avr import build as B  # noqa: E402
+
+VARIANTS = {
+    # round 1 flag experiments
+    'ftz': ('-fgpu-flush-denormals-to-zero',),
+    'ftzapx': ('-fgpu-flush-denormals-to-zero', '-fgpu-approx-transcendentals'),
+    'slp': ('-fslp-vectorize',),
+    'unclustered': ('-mllvm', '-amdgpu-disable-unclustered-high-rp-reschedule'),
+    # round 2
+    'fdiv': ('-fno-hip-fp32-correctly-rounded-divide-sqrt',),
+    'dc1': ('-DB4_DC=1',), 'dc3': ('-DB4_DC=3',), 'dc4': ('-DB4_DC=4',),
+    'dn2': ('-DB4_DN=2',), 'dn4': ('-DB4_DN=4',),
+}
+
+
+def main(names):
+    os.makedirs(os.path.join(ROOT, 'exp'), exist_ok=True)
+    for n in names:
+        out = os.path.join(ROOT, 'exp', 'libavr_%s.so' % n)
+        B.build_lib(extra=VARIANTS[n], out=out)
+        print(out)
+
+
+if __name__ == '__main__':
+    main(sys.argv[1:] or sorted(VARIANTS))

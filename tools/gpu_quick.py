@@ -39,4 +39,9 @@ for k in range(K):
     if k % 5 == 0 or k == K - 1:
         print('step', k, 'max|dq_arm|', dq, 'obs', np.abs(og - oc).max(), 'rew', np.abs(rg - rc).max(), 'info', np.abs(ig - ic).max(), flush=True)
 print('worst arm dq', worst)
+# contact-rich chaos envelope of tests/test_gpu_parity.py (settle + steps): a build past it fails
+TOL = 3e-3
+if not worst < TOL:
+    print('FAIL: worst arm dq %.3g >= %.3g' % (worst, TOL))
+    sys.exit(1)
 print('flags', G[:, ABI.S_TASK+ABI.T_FLAGS], C[:, ABI.S_TASK+ABI.T_FLAGS])

@@ -14,11 +14,14 @@ A = ABI.load_scene(); md = ABI.ModelDesc(A)
 S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
 S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
 sim = _lib.Sim(md, N)
-SLOTS = 24
+SLOTS = 48
 prof = torch.zeros(N * SLOTS, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
-names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-']
+names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-',
+         ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '-', '-', '-', '-',
+         '#sph-sph', '#closed form', '#sph-small hull', '#sph-table hull', '#box-hull', '#small-small hull', '#hull-table hull', '#other GJK',
+         '#it sph-sph', '#it closed', '#it sph-small', '#it sph-table', '#it box-hull', '#it small-small', '#it hull-table', '#it other']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0

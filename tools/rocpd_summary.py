@@ -17,7 +17,9 @@ import sys
 
 import numpy as np
 
-STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_a_kernel': 10, 'avr_substep_b_kernel': 10, 'avr_substep_b4_kernel': 10, 'avr_task_kernel': 1}
+# launches per env-step (FeedingJaco: 10 sub-steps of four kernels, one take_step, one task launch)
+STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': 10, 'avr_narrowphase_kernel': 10, 'avr_substep_a_kernel': 10,
+                'avr_substep_b4_kernel': 10, 'avr_task_kernel': 1}
 
 
 def db(d):
@@ -50,12 +52,11 @@ def counters(c, names):
 
 
 def per_step(cnt, name):
-    """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS)."""
-    # part B runs as one of two kernels (avr_substep_b4_kernel by default): sum what ran
-    ran = [k for k in STEP_KERNELS if name in cnt.get(k, {})] if cnt else []
-    if 'avr_substep_a_kernel' not in ran or not any(k.startswith('avr_substep_b') for k in ran):
+    """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS); None unless
+    every step kernel has the counter."""
+    if not cnt or any(name not in cnt.get(k, {}) for k in STEP_KERNELS):
         return None
-    return sum(cnt[k][name] * STEP_KERNELS[k] for k in ran)
+    return sum(cnt[k][name] * STEP_KERNELS[k] for k in STEP_KERNELS)
 
 
 def main(pdir, tag, envs=4096):
@@ -71,7 +72,7 @@ def main(pdir, tag, envs=4096):
                 f.write('%s,%d,%.0f,%.1f,%.1f,%.0f,%.0f,%.2f\n' % r)
         for r in st:
             print('%-28s calls %4d avg %10.3f ms  median %10.3f ms  %5.1f%%' % (r[0], r[1], r[3] / 1e6, r[4] / 1e6, r[7]))
-    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs}
+    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs}   # (only kernels that run in a step)
     cf, cw, cs = db(os.path.join(pdir, 'fetch')), db(os.path.join(pdir, 'write')), db(os.path.join(pdir, 'sq'))
     fetch = counters(cf, ['FETCH_SIZE']) if cf else {}
     write = counters(cw, ['WRITE_SIZE']) if cw else {}
