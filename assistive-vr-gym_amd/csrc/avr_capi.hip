@@ -318,7 +318,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         if ((r = upload(s, saabb, &k.static_saabb))) return r;
         // packed per-shape and per-candidate-pair records: one load each in the pair kernel
         std::vector<int> sinfo(ns);
-        for (int i = 0; i < ns; i++) sinfo[i] = (cidx[i] + 1) | ((d->shape_gender[i] + 1) << 9);
+        for (int i = 0; i < ns; i++) sinfo[i] = (cidx[i] + 1) | ((d->shape_gender[i] + 1) << 9) | (d->shape_kind[i] << 11);
         if ((r = upload(s, sinfo, &k.shape_info))) return r;
         std::vector<int4> prec(d->n_pairs > 0 ? d->n_pairs : 1);
         for (int p = 0; p < d->n_pairs; p++) {

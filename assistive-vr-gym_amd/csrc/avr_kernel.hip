@@ -494,9 +494,17 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
 }
 
 // --------------------------------------------------------------------------- GJK
+// GJK simplex: Minkowski vertices w = a - b with their support points on A and B
 struct Simplex { v3 w[4], a[4], b[4]; int n; };
+// GJK simplex of a point core (sphere) against a hull: only w and the hull's support points h
+// are kept (the point's side is the constant core)
+struct SimplexP { v3 w[4], h[4]; int n; };
 
 AVR_DI void sx_copy(Simplex &S, int dst, int src) { S.w[dst] = S.w[src]; S.a[dst] = S.a[src]; S.b[dst] = S.b[src]; }
+AVR_DI void sx_copy(SimplexP &S, int dst, int src) { S.w[dst] = S.w[src]; S.h[dst] = S.h[src]; }
+// vertices (1, 2, 3) -> (3, 1, .): the tetrahedron face 1 moved to slots 0, 1, 2
+AVR_DI void sx_face1(Simplex &S) { const v3 w1 = S.w[1], a1 = S.a[1], b1 = S.b[1]; sx_copy(S, 1, 3); S.w[2] = w1; S.a[2] = a1; S.b[2] = b1; }
+AVR_DI void sx_face1(SimplexP &S) { const v3 w1 = S.w[1], h1 = S.h[1]; sx_copy(S, 1, 3); S.w[2] = w1; S.h[2] = h1; }
 
 // Closest point of triangle ABC to the origin (Ericson 5.1.5).  used: bit mask of the vertices
 // spanning the closest feature (1=A 2=B 4=C); l*: barycentric weights.
@@ -533,7 +541,8 @@ AVR_DI v3 tri_cp(v3 A, v3 B, v3 C, int &used, float &la, float &lb, float &lc) {
 }
 
 // keep the vertices of slots 0..2 selected by `used`, compacted in order; lam in slot order
-AVR_DI void tri_compact(Simplex &S, int used, float la, float lb, float lc, float lam[4]) {
+template <class SX>
+AVR_DI void tri_compact(SX &S, int used, float la, float lb, float lc, float lam[4]) {
     switch (used) {
     case 1: S.n = 1; lam[0] = la; break;
     case 2: sx_copy(S, 0, 1); S.n = 1; lam[0] = lb; break;
@@ -545,7 +554,8 @@ AVR_DI void tri_compact(Simplex &S, int used, float la, float lb, float lc, floa
     }
 }
 
-AVR_DI int tri_closest(Simplex &S, v3 &vout, float lam[4]) {
+template <class SX>
+AVR_DI int tri_closest(SX &S, v3 &vout, float lam[4]) {
     int used;
     float la, lb, lc;
     vout = tri_cp(S.w[0], S.w[1], S.w[2], used, la, lb, lc);
@@ -554,7 +564,8 @@ AVR_DI int tri_closest(Simplex &S, v3 &vout, float lam[4]) {
 }
 
 // one face (i0,i1,i2) of the tetrahedron, opposite vertex i3 (literal indices at every call)
-AVR_DI void tetra_face(const Simplex &S, int f, int i0, int i1, int i2, int i3, bool &outside_any, float &best, int &bf, int &bused,
+template <class SX>
+AVR_DI void tetra_face(const SX &S, int f, int i0, int i1, int i2, int i3, bool &outside_any, float &best, int &bf, int &bused,
                        float &bla, float &blb, float &blc, v3 &bestv) {
     v3 A = S.w[i0], B = S.w[i1], C = S.w[i2], D = S.w[i3];
     v3 n = crs(sub(B, A), sub(C, A));
@@ -570,7 +581,8 @@ AVR_DI void tetra_face(const Simplex &S, int f, int i0, int i1, int i2, int i3, 
     }
 }
 
-AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
+template <class SX>
+AVR_DI int simplex_closest(SX &S, v3 &vout, float lam[4]) {
     if (S.n == 1) { lam[0] = 1.f; vout = S.w[0]; return 0; }
     if (S.n == 2) {
         v3 A = S.w[0], B = S.w[1], ab = sub(B, A);
@@ -596,12 +608,7 @@ AVR_DI int simplex_closest(Simplex &S, v3 &vout, float lam[4]) {
     // move the winning face's vertices to slots 0,1,2 (in face order), then compact
     switch (bf) {
     case 0: break;
-    case 1: {
-        v3 w1 = S.w[1], a1 = S.a[1], b1 = S.b[1];
-        sx_copy(S, 1, 3);
-        S.w[2] = w1; S.a[2] = a1; S.b[2] = b1;
-        break;
-    }
+    case 1: sx_face1(S); break;
     case 2: sx_copy(S, 1, 2); sx_copy(S, 2, 3); break;
     default: sx_copy(S, 0, 1); sx_copy(S, 1, 3); break;
     }
@@ -1097,7 +1104,13 @@ AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, int info, v3 &mn
     if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
     else { const gf4p a = (gf4p)(m.static_saabb + 8 * s); const f4v x = a[0], y = a[1]; mn = V(x.x, x.y, x.z); mx = V(y.x, y.y, y.z); }
 }
-AVR_DI bool info_enabled(int info, int gender) { const int g = (info >> 9) - 1; return g < 0 || g == gender; }
+AVR_DI bool info_enabled(int info, int gender) { const int g = (info >> 9 & 3) - 1; return g < 0 || g == gender; }
+AVR_DI int info_kind(int info) { return (info >> 11) & 3; }
+// a sphere against a convex hull: the narrowphase kernel runs these on the point-core GJK
+AVR_DI bool sphere_hull(int ia, int ib) {
+    const int ka = info_kind(ia), kb = info_kind(ib);
+    return (ka == AVR_SPHERE && kb == AVR_HULL) || (ka == AVR_HULL && kb == AVR_SPHERE);
+}
 
 // manifold update for the nq (<= 64) shape pairs k0 .. k0 + nq - 1 of the list, lane q <-> pair
 // k0 + q: the narrowphase result comes from avr_narrowphase_kernel; pairs it left to the
@@ -1264,9 +1277,10 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
     int gp = 0, gsa0 = 0, gsb0 = 0, gncB = 1, gn = 0, gbase = 0;
     bool gcull = false, gbare = false;
     float grcpB = 1.f;
+    int n0 = 0, n1 = 0;                             // sphere-hull / other pairs
     for (;;) {
         bool act = false, last = false;
-        int sa = 0, sb = 0, q = gp;
+        int sa = 0, sb = 0, q = gp, ia = 0, ib = 0;
         if (gbase < gn) {                           // the compound pair in progress
             const int it = gbase + lane;
             if (it < gn) {
@@ -1275,14 +1289,15 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
                 if (gcull) {
                     sa = L.u.c.candA[i];
                     sb = L.u.c.candB[j];
+                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
                     v3 a0, a1, b0, b1;
-                    child_aabb(m, L, sa, m.shape_info[sa], a0, a1);
-                    child_aabb(m, L, sb, m.shape_info[sb], b0, b1);
+                    child_aabb(m, L, sa, ia, a0, a1);
+                    child_aabb(m, L, sb, ib, b0, b1);
                     act = overlap(a0, a1, b0, b1);
                 } else {
                     sa = gsa0 + i;
                     sb = gsb0 + j;
-                    const int ia = m.shape_info[sa], ib = m.shape_info[sb];
+                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
                     if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (gbare) act = true;
                         else {
@@ -1307,7 +1322,7 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
                     q = L.u.c.apair[kk];
                     sa = rec.y & 0xffff;
                     sb = rec.z & 0xffff;
-                    const int ia = m.shape_info[sa], ib = m.shape_info[sb];
+                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
                     if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (rec.w & 1) act = true;
                         else {
@@ -1386,10 +1401,20 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
         // sub-step (flag 8)
         int tot;
         int pre = ballot_prefix(act, &tot);
-        if (act && nsp + pre < MAXSP) {
-            cs[CS_PAIRS + 2 * (nsp + pre)] = __int_as_float(sa | (sb << 16));
-            cs[CS_PAIRS + 2 * (nsp + pre) + 1] = __int_as_float(q);
+        const int kq = nsp + pre;
+        const bool ok = act && kq < MAXSP;
+        if (ok) {
+            cs[CS_PAIRS + 2 * kq] = __int_as_float(sa | (sb << 16));
+            cs[CS_PAIRS + 2 * kq + 1] = __int_as_float(q);
         }
+        // the narrowphase kernel's two work lists (pair indices, ascending)
+        const bool sh = ok && sphere_hull(ia, ib);
+        int t0, t1;
+        const int p0 = ballot_prefix(sh, &t0), p1 = ballot_prefix(ok && !sh, &t1);
+        if (sh) cs[CS_L0 + n0 + p0] = __int_as_float(kq);
+        else if (ok) cs[CS_L1 + n1 + p1] = __int_as_float(kq);
+        n0 += t0;
+        n1 += t1;
         nsp += tot;
         if (last) break;
     }
@@ -1397,7 +1422,10 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
 #ifdef AVR_PROF
     if (lane == 0) { L.prof[14] += nsp; L.prof[15] += nap; }
 #endif
-    if (lane == 0) { cs[CS_NSP] = __int_as_float(nsp); cs[CS_FLAGS] = __int_as_float(L.flags); }
+    if (lane == 0) {
+        cs[CS_NSP] = __int_as_float(nsp); cs[CS_FLAGS] = __int_as_float(L.flags);
+        cs[CS_N0] = __int_as_float(n0); cs[CS_N1] = __int_as_float(n1);
+    }
     PROF_STOP(2, pt);
 }
 
@@ -2036,52 +2064,173 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const K
     prof_flush(m, L, env);
 }
 
-// Sub-step part A2: the narrowphase of every listed shape pair, one lane per pair, across all
-// envs (64 pairs per block, 4 blocks per env cover MAXSP; blocks past an env's list exit).  Pairs
-// with a big hull that has no support table, and penetrating pairs that need EPA, are marked
-// rc = 2 and finished by the wave-cooperative path in part A3.  Block b takes env
-// 8 (b / 32) + b % 8, chunk (b / 8) % 4: the same XCD as parts A1 and A3 for that env.
-__global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
-                                                             int n_envs) {
-    const int env = env0 + 8 * (blockIdx.x >> 5) + (blockIdx.x & 7);
-    const int k = ((blockIdx.x >> 3) & 3) * 64 + lane_id();
-    if (env >= n_envs || (mask && !mask[env])) return;
-    const KModel &m = *mp;
-    float *cs = env_cs(m, env);
-    if (k >= __float_as_int(cs[CS_NSP])) return;
+// Sphere against convex hull (most of the scene's shape pairs: food against the spoon's and the
+// bowl's VHACD pieces): the GJK of narrowphase() restated for a point core -- the sphere's
+// support point is its centre, so the simplex keeps only the Minkowski vertices and the hull's
+// support points -- with the same iteration, tests and closest-point sums.  A lane works one
+// pair at a time; a lane whose pair finishes takes the next pair of the list, so a wave runs
+// the list's total iteration count rather than 64-lane maxima.
+struct PH {
+    int k;                  // pair index
+    bool sw;                // the sphere is shape B of the pair
+    v3 c;                   // sphere centre (its core)
+    WShape H;               // the hull
+    float ma, mb, thr, maxd2, prev;
+    int it;
+    v3 v;
+    float lam[4];
+    SimplexP S;
+};
+
+// (selects of values, never of lvalues: a select between two addresses keeps the simplex in
+// scratch memory)
+AVR_DI v3 sel3(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+AVR_DI WShape selw(bool c, const WShape &a, const WShape &b) {
+    WShape r;
+    r.kind = c ? a.kind : b.kind; r.nv = c ? a.nv : b.nv; r.vs = c ? a.vs : b.vs; r.tab = c ? a.tab : b.tab;
+    r.t.p = sel3(c, a.t.p, b.t.p);
+    r.t.q = Q(c ? a.t.q.x : b.t.q.x, c ? a.t.q.y : b.t.q.y, c ? a.t.q.z : b.t.q.z, c ? a.t.q.w : b.t.q.w);
+    r.margin = c ? a.margin : b.margin;
+    r.he = sel3(c, a.he, b.he);
+    return r;
+}
+
+AVR_DI void ph_init(const KModel &m, const float *cs, int k, PH &P) {
     const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
     const int sa = key & 0xffff, sb = key >> 16;
     const int ba = m.shape_body[sa], bb = m.shape_body[sb];
-    const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+    P.k = k;
+    P.thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
     const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
-    int rc = 2;
-    v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
-    float d = 0.f;
-    if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
-        int nit, nkind;
-        rc = narrowphase<false>(m, *(EpaBuf *)cs, A, B, thr, nB, pB, d, nit, nkind);   // (the lane path never touches the EPA buffer)
-#ifdef AVR_PROF
-        if (m.prof) {   // pairs and GJK iterations per pair category (atomics: diagnostic build only)
-            // 0 sphere-sphere, 1 other closed form, 2 sphere-small hull, 3 sphere-table hull,
-            // 4 box-hull, 5 small hull-small hull, 6 hull-hull with a table, 7 other GJK
-            const bool sA = A.kind == AVR_SPHERE, sB = B.kind == AVR_SPHERE;
-            const bool hA = A.kind == AVR_HULL, hB = B.kind == AVR_HULL;
-            const bool tA = A.tab >= 0, tB = B.tab >= 0;
-            int cat = 7;
-            if (nkind == 0) cat = 0;
-            else if (nkind == 1 || nkind == 2) cat = 1;
-            else if ((sA && hB) || (sB && hA)) cat = (tA || tB) ? 3 : 2;
-            else if ((A.kind == AVR_BOX && hB) || (B.kind == AVR_BOX && hA)) cat = 4;
-            else if (hA && hB) cat = (tA || tB) ? 6 : 5;
-            unsigned long long *pr = m.prof + (size_t)env * AVR_PROF_SLOTS;
-            atomicAdd(pr + 32 + cat, 1ull);
-            atomicAdd(pr + 40 + cat, (unsigned long long)nit);
+    P.sw = A.kind != AVR_SPHERE;
+    P.c = sel3(P.sw, B.t.p, A.t.p);
+    P.H = selw(P.sw, A, B);
+    P.ma = A.margin;
+    P.mb = B.margin;
+    const float maxd = P.ma + P.mb + P.thr;
+    P.maxd2 = maxd * maxd;
+    P.v = sub(A.t.p, B.t.p);
+    if (len2(P.v) < 1e-20f) P.v = V(1, 0, 0);
+    P.S.n = 0;
+    P.prev = BIGF;
+    P.it = 0;
+    P.lam[0] = 1.f; P.lam[1] = P.lam[2] = P.lam[3] = 0.f;
+}
+
+// one GJK iteration; true when the pair is finished, with its narrowphase result (rc 0 no
+// contact, 1 contact, 2 cooperative path: penetrating cores need EPA, or the iteration cap)
+AVR_DI bool ph_step(const KModel &m, PH &P, int &rc, v3 &nB, v3 &pB, float &dist) {
+    const v3 h = support<false>(m, P.H, sel3(P.sw, scl(P.v, -1.f), P.v));
+    const v3 sa = sel3(P.sw, h, P.c), sb = sel3(P.sw, P.c, h);
+    const v3 wv = sub(sa, sb);
+    const float vv = len2(P.v), vw = dot(P.v, wv);
+    if (vw > 0.f && vw * vw > vv * P.maxd2) { rc = 0; return true; }       // GJK_FAR
+    bool dup = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < P.S.n && P.S.w[k].x == wv.x && P.S.w[k].y == wv.y && P.S.w[k].z == wv.z) dup = true;
+    bool conv = (dup && P.S.n > 0) || (P.S.n > 0 && vv - vw <= GJK_REL_EPS * vv);
+    if (!conv) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {       // (value selects: a store at a computed slot would keep the simplex in scratch)
+            P.S.w[k] = sel3(k == P.S.n, wv, P.S.w[k]);
+            P.S.h[k] = sel3(k == P.S.n, h, P.S.h[k]);
         }
-#endif
+        P.S.n++;
+        v3 nv;
+        if (simplex_closest(P.S, nv, P.lam)) { rc = 2; return true; }      // penetrating
+        const float nvv = len2(nv);
+        if (nvv < 1e-14f * (1.f + len2(wv))) { rc = 2; return true; }     // penetrating
+        if (nvv >= P.prev) { P.v = nv; conv = true; }
+        else {
+            P.prev = nvv;
+            P.v = nv;
+            if (++P.it >= GJK_MAX_IT) { rc = 2; return true; }            // unfinished
+            return false;
+        }
     }
+    // separated: closest points from the simplex weights (as gjk())
+    v3 a = V(0, 0, 0), b = V(0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < P.S.n) {
+            a = add(a, scl(sel3(P.sw, P.S.h[k], P.c), P.lam[k]));
+            b = add(b, scl(sel3(P.sw, P.c, P.S.h[k]), P.lam[k]));
+        }
+    const float cd = len(sub(a, b));
+    if (!(cd > 1e-9f)) { rc = 2; return true; }
+    const v3 n = scl(sub(a, b), 1.f / cd);
+    const float d = cd - P.ma - P.mb;
+    if (d > P.thr) { rc = 0; return true; }
+    nB = n;
+    pB = add(b, scl(n, P.mb));
+    dist = d;
+    rc = 1;
+    return true;
+}
+
+AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
     float4 *o = (float4 *)(cs + CS_RES) + 2 * k;
     o[0] = make_float4(__int_as_float(rc), nB.x, nB.y, nB.z);
     o[1] = make_float4(pB.x, pB.y, pB.z, d);
+}
+
+// Sub-step part A2: the narrowphase of every listed shape pair across all envs, in two blocks
+// per env: the sphere-hull list (point-core GJK with refill) and the other pairs (one lane per
+// pair, narrowphase()).  Pairs with a big hull that has no support table, and penetrating pairs
+// that need EPA, are marked rc = 2 and finished by the wave-cooperative path in part A3.  Block b
+// takes env 8 (b / 16) + b % 8 (the XCD of parts A1 and A3 for that env), list (b / 8) % 2.
+__global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
+                                                             int n_envs) {
+    const int env = env0 + 8 * (blockIdx.x >> 4) + (blockIdx.x & 7);
+    const int list = (blockIdx.x >> 3) & 1;
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const KModel &m = *mp;
+    const int lane = lane_id();
+    float *cs = env_cs(m, env);
+    if (list == 0) {
+        const int n0 = __float_as_int(cs[CS_N0]);
+        PH P;
+        bool act = lane < n0;
+        if (act) ph_init(m, cs, __float_as_int(cs[CS_L0 + lane]), P);
+        int next = 64;
+        while (__ballot(act)) {
+            bool done = false;
+            int rc = 0;
+            v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+            float d = 0.f;
+            if (act) {
+                done = ph_step(m, P, rc, nB, pB, d);
+                if (done) np_store(cs, P.k, rc, nB, pB, d);
+            }
+            const unsigned long long dm = __ballot(done);
+            if (done) {
+                const int j = next + __popcll(dm & ((1ull << lane) - 1ull));
+                act = j < n0;
+                if (act) ph_init(m, cs, __float_as_int(cs[CS_L0 + j]), P);
+            }
+            next += __popcll(dm);
+        }
+        return;
+    }
+    const int n1 = __float_as_int(cs[CS_N1]);
+    for (int c0 = 0; c0 < n1; c0 += 64) {
+        if (c0 + lane >= n1) break;
+        const int k = __float_as_int(cs[CS_L1 + c0 + lane]);
+        const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
+        const int sa = key & 0xffff, sb = key >> 16;
+        const int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+        int rc = 2;
+        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+        float d = 0.f;
+        if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
+            int nit, nkind;
+            rc = narrowphase<false>(m, *(EpaBuf *)cs, A, B, thr, nB, pB, d, nit, nkind);   // (the lane path never touches the EPA buffer)
+        }
+        np_store(cs, k, rc, nB, pB, d);
+    }
 }
 
 // Sub-step part A3: one 64-lane block per env, state staged in LDS -- manifold update,
@@ -2164,14 +2313,15 @@ AVR_DI int al4(int x) { return (x + 3) & ~3; }
 // the two endpoints of a row, 0-based (-1: not a free body), and this lane's part: 0 endpoint
 // A, 1 endpoint B, -1 none
 AVR_DI int own_of(int info) {
-    const int sl = lane_id() & 15;
-    return sl == (info & 63) - 1 ? 0 : (sl == ((info >> 6) & 63) - 1 ? 1 : -1);
+    const int sl1 = (lane_id() & 15) + 1;
+    return (info & 63) == sl1 ? 0 : (((info >> 6) & 63) == sl1 ? 1 : -1);
 }
 
 // non-contact rows: buffer loads (they stay L2-resident)
 struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2, r; };
 struct NcSrc {
     typedef NcRow Row;
+    static constexpr bool robot_parts = true;
     rsrc_t rs;
     int eo, ro;                // this env's records / robot parts (byte offsets)
     lds_f *imp;
@@ -2190,10 +2340,13 @@ struct NcSrc {
     AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
 };
 
-// contact rows staged in LDS
+// contact rows staged in LDS; RC: the block has robot contacts (otherwise no contact row has a
+// robot part and the resolves skip it)
 struct CRowL { int w; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+template <bool RC>
 struct CLds {
     typedef CRowL Row;
+    static constexpr bool robot_parts = RC;
     lds_f *blk;
     int cw, rw, n_nc;          // contact records / robot parts of this group (LDS word index)
     lds_f *imp;
@@ -2216,6 +2369,7 @@ struct CLds {
         R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2];
     }
     AVR_DI f2v robot(int slot) const {
+        if constexpr (!RC) { (void)slot; return f2v{0.f, 0.f}; }
         return *(const lds_f2 *)(blk + (slot >= 0 ? rw + (slot - n_nc) * ROBW + 2 * (lane_id() & 15) : LN_ZERO));
     }
 };
@@ -2224,6 +2378,7 @@ struct CLds {
 struct CRowG { int o; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
 struct CGlb {
     typedef CRowG Row;
+    static constexpr bool robot_parts = true;
     rsrc_t rs;
     int co, ro, n_nc;          // this env's contact records / robot parts (byte offsets)
     lds_f *imp;
@@ -2265,17 +2420,18 @@ AVR_DI void parts4(const S &s, typename S::Row &R) {
 // are spelled out and nothing else may contract: every unrolled copy of a row resolve (and every
 // pipeline depth) then rounds the same way, so an env's results do not depend on which copy
 // resolves its rows or on the row counts of the other envs in its wavefront.
-template <class R>
+template <bool RP, class R>
 AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi) {
 #pragma clang fp contract(off)
     const float p = fmaf(X.j1.x, d.vz, fmaf(X.j0.y, d.vy, X.j0.x * d.vx));
-    const float q = fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.x, d.rq, X.j1.y * d.wx)));
+    const float q = RP ? fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.x, d.rq, X.j1.y * d.wx)))
+                       : fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, X.j1.y * d.wx));
     const float dv = row16_sum(p + q);
     const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
     const float delta = ni - imp;
     d.vx = fmaf(X.j0.x, delta, d.vx); d.vy = fmaf(X.j0.y, delta, d.vy); d.vz = fmaf(X.j1.x, delta, d.vz);
     d.wx = fmaf(X.j1.y, delta, d.wx); d.wy = fmaf(X.j2.x, delta, d.wy); d.wz = fmaf(X.j2.y, delta, d.wz);
-    d.rq = fmaf(X.r.y, delta, d.rq);
+    if (RP) d.rq = fmaf(X.r.y, delta, d.rq);
     return ni;
 }
 
@@ -2340,14 +2496,14 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
     // warm start (normal rows, contact order): delta = cached impulse x warm-start factor, which
     // is also the rows' starting impulse
     sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-                     [&](const CR &R) { (void)go4(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
+                     [&](const CR &R) { (void)go4<CS::robot_parts>(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
     const int fr0 = n_nc + n_c;
     for (int it = 0; it < m.iters; it++) {
         const bool fwd = (it & 1) != 0;
         sweep4<DN, false>(ns, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
-                          [&](const NR &R) { *R.ip = go4(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y); });
+                          [&](const NR &R) { *R.ip = go4<true>(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y); });
         sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-                         [&](const CR &R) { *R.ip = go4(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
+                         [&](const CR &R) { *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
         // active contacts (positive normal impulse) of each group, in contact order
         int t = 0;
         for (int c0 = 0; c0 < nc_max; c0 += 16) {
@@ -2371,8 +2527,8 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
         auto hdr = [&](Pair4<CS> &Y, int c) { pair_hdr(cs, Y, c >= 0 ? fr0 + 2 * c : -1, imp + n_nc + (c >= 0 ? c : 0)); };
         auto go = [&](const Pair4<CS> &Y) {
             const float lim = Y.a.h.w * Y.in;
-            *Y.a.ip = go4(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
-            *Y.b.ip = go4(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
+            *Y.a.ip = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
+            *Y.b.ip = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
         };
         // (whole rounds of K units, null units past the end, unconditional read-ahead: sweep4)
         int cn = lst(0);
@@ -2393,10 +2549,10 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
 }
 
 #ifndef B4_DN
-#define B4_DN 3          // pipeline depth, non-contact rows (global memory, L2-resident)
+#define B4_DN 2          // pipeline depth, non-contact rows (global memory, L2-resident)
 #endif
 #ifndef B4_DC
-#define B4_DC 2          // pipeline depth, contact rows staged in LDS
+#define B4_DC 1          // pipeline depth, contact rows staged in LDS
 #endif
 #ifndef B4_DG
 #define B4_DG 3          // pipeline depth, contact rows from global memory (blocks that do not fit)
@@ -2474,8 +2630,13 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     NcSrc ns{rs, eo, ro, imp, n_rows};
     DV d;
     if (in_lds) {
-        CLds cs{blk, cw, rw, n_nc, imp, n_rows};
-        pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+        if (wmax(n_rc) > 0) {
+            CLds<true> cs{blk, cw, rw, n_nc, imp, n_rows};
+            pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+        } else {
+            CLds<false> cs{blk, cw, rw, n_nc, imp, n_rows};
+            pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+        }
     } else {
         CGlb cs{rs, eo + CR_BASE * 4, ro, n_nc, imp, n_rows};
         pgs4<B4_DN, B4_DG>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
@@ -2660,7 +2821,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
         mark(AVR_K_PAIRS);
         hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
         mark(AVR_K_NARROW);
-        hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(32 * ((n_envs + 7) / 8)), dim3(64), 0, stream, d_m, mask, env0, env1);
+        hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 7) / 8)), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);

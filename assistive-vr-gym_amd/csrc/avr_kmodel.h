@@ -33,13 +33,17 @@
 // avr_substep_a_kernel consumes them.
 #define CS_NSP 0                                    // int bits: shape pairs
 #define CS_FLAGS 1                                  // int bits: flags raised by the pair kernel
+#define CS_N0 2                                     // int bits: sphere-hull pairs (list CS_L0)
+#define CS_N1 3                                     // int bits: the other pairs (list CS_L1)
 #define CS_PAIRS 4                                  // [MAXSP] (sa | sb << 16, body pair) int bits
 #define CS_RES (CS_PAIRS + 2 * MAXSP)               // [MAXSP][8] rc, nB, pB, dist (rc 2: cooperative path)
 #define CS_BTF (CS_RES + 8 * MAXSP)                 // [MAXB][8] body COM frames
 #define CS_CM (CS_BTF + 8 * MAXB)                   // [MAXL][8] link COM frames
 #define CS_AX (CS_CM + 8 * MAXL)                    // [MAXL][4] joint axes (world)
 #define CS_ORG (CS_AX + 4 * MAXL)                   // [MAXL][4] joint origins (world)
-#define CS_WORDS (CS_ORG + 4 * MAXL)
+#define CS_L0 (CS_ORG + 4 * MAXL)                   // [MAXSP] indices of the sphere-hull pairs, ascending
+#define CS_L1 (CS_L0 + MAXSP)                       // [MAXSP] indices of the other pairs, ascending
+#define CS_WORDS (CS_L1 + MAXSP)
 
 // Articulated links: the robot's nl links, then (impairment 'tremor') the head/neck chain's
 // hc_n links with DoFs nd .. nd + hc_n - 1; nla = nl + hc_n.  The chain root's parent is -2:
@@ -69,7 +73,7 @@ struct KModel {
     const int *shape_cidx;      // [ns] index into the per-sub-step child AABB cache, -1 for static shapes
     const float *static_saabb;  // [ns][8] world AABB (min3, pad, max3, pad) of static shapes (host-computed)
     const int *pair_a, *pair_b;
-    const int *shape_info;      // [ns] (child AABB cache index + 1, 0 static) | (shape_gender + 1) << 9
+    const int *shape_info;      // [ns] (child AABB cache index + 1, 0 static) | (shape_gender + 1) << 9 | shape_kind << 11
     const int4 *pair_rec;       // [np] (ba | bb << 16, sa0 | na << 16, sb0 | nb << 16, bare | one-by-one << 1)
     int n_arm, arm_dofs[8], n_finger, finger_dofs[4];
     int tool_link, torso_link, head_slot, spoon_free, bowl_free, food_free0, n_food;
