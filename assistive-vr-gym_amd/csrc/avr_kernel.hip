@@ -1492,15 +1492,15 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 
 
 // Constraint rows live in a per-env buffer in global memory, in solve order [non-contact]
-// [normals][frictions].  A row's `info` names its free-body endpoints as 1-based body indices
-// (bits 0-5: endpoint A, bits 6-11: endpoint B, 0 = not a free body) and bit 12 marks an
-// articulated endpoint; an all-zero header is a null row (no endpoint, inv = rhs = lo = hi = 0).
+// [normals][frictions].  A row's ownership mask (own_mask) names its free-body endpoints: 2 bits
+// per free body f, 1 = endpoint A, 2 = endpoint B (part B's lane f holds body f); an all-zero
+// header is a null row (no endpoint, inv = rhs = lo = hi = 0).
 // Non-contact rows have 20-word records at word 20 r:
-//   w0 info   w1 robot slot + 1 (int bits, 0: none)   w2 inv   w3 rhs   w4 lo   w5 hi
+//   w0 ownership mask   w1 robot slot + 1 (int bits, 0: none)   w2 inv   w3 rhs   w4 lo   w5 hi
 //   w8..13 free A Jacobian (lin, ang)   w14..19 free B Jacobian
 // Contact rows (row n_nc + k, k = c for contact c's normal, n_c + 2c + {0,1} for its frictions)
 // have 16-word records at word CR_BASE + 16 k:
-//   w0 info | (robot slot + 1) << 13   w1 inv   w2 rhs   w3 friction coefficient
+//   w0 ownership mask | (robot slot + 1) << 20   w1 inv   w2 rhs   w3 friction coefficient
 //   w4..9 free A Jacobian   w10..15 free B Jacobian
 // (normal rows clamp to [0, 1e10], frictions to +-friction * normal impulse; the normal row's
 // starting impulse is the manifold point's cached impulse x warm-start factor, read by part B
@@ -1512,7 +1512,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define RWC 20      // words per non-contact record
 #define CRW 16      // words per contact record
 #define CR_BASE (MAXNC * RWC)
-#define CI_SLOT 13  // contact info: robot slot + 1 from this bit
+#define CI_SLOT 20  // contact header word 0: robot slot + 1 from this bit
 #define ROBW 32     // words per robot part
 // per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
 #define WS_WORDS 128
@@ -1524,8 +1524,8 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW 72     // [MAXF][4] angular
-#define RI_FREE(f) ((f) + 1)    // info: free body f as an endpoint (0 = none)
-#define RI_ROBOT (1 << 12)
+// A row's ownership mask: 2 bits per free body f (= part-B lane f): 1 endpoint A, 2 endpoint B
+AVR_DI int own_mask(int fa, int fb) { return (fa >= 0 ? 1 << (2 * fa) : 0) | (fb >= 0 ? 2 << (2 * fb) : 0); }
 static_assert(CR_BASE + 3 * AVR_MAX_CONTACTS * CRW <= (MAXNC + 3 * AVR_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
 
 AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RWC; }
@@ -1604,13 +1604,13 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         const float rel = sg * L.vq[dof];
         float *w = row_rec(m, rows, lane);
         if (kind < 2) {
-            put_hdr(w, RI_ROBOT, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, lane);
+            put_hdr(w, 0, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, lane);
         } else {
             const float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
             const float kp = L.st[AVR_S_KP + dof], kd = 1.f;
             const float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
             const float mi = L.st[AVR_S_MAXIMP + dof];
-            put_hdr(w, RI_ROBOT, inv, (desired - rel) * inv, -mi, mi, lane);
+            put_hdr(w, 0, inv, (desired - rel) * inv, -mi, mi, lane);
         }
         put_free_zero(w + 8); put_free_zero(w + 14);
         put_robot(row_rob(m, rows, lane), J, MJ);
@@ -1659,7 +1659,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         rel += free_dot(L, fb, jbl, jba);
         const float mi = m.fixed_max_imp;
         float *w = row_rec(m, rows, lane);
-        put_hdr(w, (RI_FREE(fb) << 6) | RI_ROBOT, inv, (-pos * erp / dt - rel) * inv, -mi, mi, lane);
+        put_hdr(w, own_mask(-1, fb), inv, (-pos * erp / dt - rel) * inv, -mi, mi, lane);
         put_free_zero(w + 8);
         put_free(L, fb, w + 14, jbl, jba);
         put_robot(row_rob(m, rows, lane), JA, MA);
@@ -1721,7 +1721,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         plane_space(n, t1, t2);
         v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
         float fric = fminf(m.body_friction[ba] * m.body_friction[bb], 10.f);
-        int info = (kA == 2 ? RI_FREE(iA) : 0) | ((kB == 2 ? RI_FREE(iB) : 0) << 6) | (rob ? RI_ROBOT : 0);
+        const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / m.fb_mass[iA] : 0.f, imB = kB == 2 ? 1.f / m.fb_mass[iB] : 0.f;
         for (int k = 0; k < 3; k++) {
             v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
@@ -2310,12 +2310,8 @@ AVR_DI f4v bld3(rsrc_t r, int o) {
 #define LN_GROUPS 16
 AVR_DI int al4(int x) { return (x + 3) & ~3; }
 
-// the two endpoints of a row, 0-based (-1: not a free body), and this lane's part: 0 endpoint
-// A, 1 endpoint B, -1 none
-AVR_DI int own_of(int info) {
-    const int sl1 = (lane_id() & 15) + 1;
-    return (info & 63) == sl1 ? 0 : (((info >> 6) & 63) == sl1 ? 1 : -1);
-}
+// this lane's part of a row from the row's ownership mask: 1 endpoint A, 2 endpoint B, 0 none
+AVR_DI int own_of(int mask) { return (int)__builtin_amdgcn_ubfe((unsigned)mask, 2 * (lane_id() & 15), 2); }
 
 // non-contact rows: buffer loads (they stay L2-resident)
 struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2, r; };
@@ -2331,11 +2327,11 @@ struct NcSrc {
         R.ip = imp + (r >= 0 ? r : nullslot + pair);
     }
     AVR_DI void hdr(Row &R) const { R.h0 = bld4(rs, R.o); R.h1 = bld2(rs, R.o + 16); R.imp = *R.ip; }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h0.x); }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h0.x); }   // ownership mask
     AVR_DI int slot(const Row &R) const { return __float_as_int(R.h0.y) - 1; }
-    AVR_DI void own(Row &R, int off) const {
-        const int o = off >= 0 ? R.o + 32 + 24 * off : B4_OOB;
-        R.j0 = bld2(rs, o); R.j1 = bld2(rs, o + 8); R.j2 = bld2(rs, o + 16);
+    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 8), 2 endpoint B (word 14), 0 none
+        const int b = o ? R.o + 8 + 24 * o : B4_OOB;
+        R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16);
     }
     AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
 };
@@ -2362,10 +2358,15 @@ struct CLds {
         R.h.x = a.x; R.h.y = a.y; R.h.z = q[2];
         R.imp = *R.ip;
     }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }
+    AVR_DI void hdr2(Row &R) const {   // second friction row of a pair: inv, rhs (the rest is the first row's)
+        const lds_f *q = blk + R.w;
+        R.h.y = q[1]; R.h.z = q[2];
+        R.imp = *R.ip;
+    }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }   // ownership mask
     AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
-    AVR_DI void own(Row &R, int off) const {
-        const lds_f2 *q = (const lds_f2 *)(blk + (off >= 0 ? R.w + 4 + 6 * off : LN_ZERO));
+    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 4), 2 endpoint B (word 10), 0 none
+        const lds_f2 *q = (const lds_f2 *)(blk + (o ? R.w - 2 + 6 * o : LN_ZERO));
         R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2];
     }
     AVR_DI f2v robot(int slot) const {
@@ -2389,11 +2390,12 @@ struct CGlb {
     }
     AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }
+    AVR_DI void hdr2(Row &R) const { const f2v a = bld2(rs, R.o + 4); R.h.y = a.x; R.h.z = a.y; R.imp = *R.ip; }
+    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }   // ownership mask
     AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
-    AVR_DI void own(Row &R, int off) const {
-        const int o = off >= 0 ? R.o + 16 + 24 * off : B4_OOB;
-        R.j0 = bld2(rs, o); R.j1 = bld2(rs, o + 8); R.j2 = bld2(rs, o + 16);
+    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 4), 2 endpoint B (word 10), 0 none
+        const int b = o ? R.o - 8 + 24 * o : B4_OOB;
+        R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16);
     }
     AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
 };
@@ -2474,8 +2476,9 @@ template <class S>
 AVR_DI void pair_hdr(const S &s, Pair4<S> &X, int r, lds_f *in) {
     s.at(X.a, r, 0);
     s.at(X.b, r >= 0 ? r + 1 : -1, 1);
-    s.hdr(X.a); s.hdr(X.b);
-    X.in = r >= 0 ? *in : 0.f;
+    s.hdr(X.a); s.hdr2(X.b);
+    const float x = *in;                // (read unconditionally: no branch in the pipeline)
+    X.in = r >= 0 ? x : 0.f;
 }
 template <class S>
 AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
@@ -2523,7 +2526,7 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
         // the headers they address
         constexpr int K = 2 * DC + 1;
         Pair4<CS> X[K];
-        auto lst = [&](int u) { return u < t ? list[u] : -1; };
+        auto lst = [&](int u) { const int c = list[u < t ? u : 0]; return u < t ? c : -1; };   // (unconditional read)
         auto hdr = [&](Pair4<CS> &Y, int c) { pair_hdr(cs, Y, c >= 0 ? fr0 + 2 * c : -1, imp + n_nc + (c >= 0 ? c : 0)); };
         auto go = [&](const Pair4<CS> &Y) {
             const float lim = Y.a.h.w * Y.in;
