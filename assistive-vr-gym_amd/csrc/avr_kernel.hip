@@ -65,8 +65,6 @@ struct EnvLDS {
         struct {                           // collision detection
             float bmin[MAXB][4], bmax[MAXB][4];
             int apair[MAXAP];              // active body pairs (broadphase output, in pair order)
-            int okey[AVR_MAX_CONTACTS];    // (sa | sb << 16) of the previous contact pool
-            int qk[128], qp[128];          // shape-pair queue: (sa | sb << 16), body pair
             int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
             float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
         } c;
@@ -78,6 +76,26 @@ struct EnvLDS {
             float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
             float iw[MAXL][8];             // world inertia (xx yy zz xy xz yz), mass
         } d;
+    } u;
+};
+
+// LDS of the pair kernel (avr_substep_pairs_kernel): the state words, link and body frames and
+// the collision scratch only, so that more of its waves are resident than of EnvLDS's kernels
+struct PairsLDS {
+    float st[AVR_S_CP];
+    float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
+    float btf[MAXB][8];
+    int flags, gender, nla, nda;
+#ifdef AVR_PROF
+    unsigned long long prof[AVR_PROF_SLOTS];
+#endif
+    union __attribute__((aligned(16))) {
+        struct {
+            float bmin[MAXB][4], bmax[MAXB][4];
+            int apair[MAXAP];
+            int candA[128], candB[128];
+            float caabb[MAXCC][6];
+        } c;
     } u;
 };
 
@@ -100,9 +118,11 @@ struct EnvLDS {
 // static chest slot (parent -2) and its link frames (== COM frames) are published into the human
 // slot poses, where collision and the task glue (getLinkState(human, 27), feeding.py:134,254)
 // read them.
-AVR_DI int lgo(const EnvLDS &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
+template <class LT>
+AVR_DI int lgo(const LT &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
 
-AVR_DI void robot_fk(const KModel &m, EnvLDS &L) {
+template <class LT>
+AVR_DI void robot_fk(const KModel &m, LT &L) {
     const int i = lane_id();
     const bool mine = i < L.nla;
     int p = -3, jt = AVR_J_FIXED, lev = -1;
@@ -927,7 +947,8 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
 }
 
 // --------------------------------------------------------------------------- bodies
-AVR_DI tf body_tf(const KModel &m, const EnvLDS &L, int b) {
+template <class LT>
+AVR_DI tf body_tf(const KModel &m, const LT &L, int b) {
     int kind = m.body_kind[b], idx = m.body_index[b];
     if (kind == AVR_BODY_ROBOT) return ldtf(L.cm[idx]);
     if (kind == AVR_BODY_FREE) return ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * idx);
@@ -1099,7 +1120,8 @@ AVR_DI float *env_cs(const KModel &m, int env) { return m.cscr + (size_t)env * C
 
 // world AABB of child shape s from its packed info (m.shape_info): the per-sub-step cache for a
 // non-static shape, the host-precomputed box for a static one
-AVR_DI void child_aabb(const KModel &m, const EnvLDS &L, int s, int info, v3 &mn, v3 &mx) {
+template <class LT>
+AVR_DI void child_aabb(const KModel &m, const LT &L, int s, int info, v3 &mn, v3 &mx) {
     const int c = (info & 511) - 1;
     if (c >= 0) { mn = ld3(L.u.c.caabb[c]); mx = ld3(L.u.c.caabb[c] + 3); }
     else { const gf4p a = (gf4p)(m.static_saabb + 8 * s); const f4v x = a[0], y = a[1]; mn = V(x.x, x.y, x.z); mx = V(y.x, y.y, y.z); }
@@ -1113,9 +1135,8 @@ AVR_DI bool sphere_hull(int ia, int ib) {
 }
 
 // manifold update for the nq (<= 64) shape pairs k0 .. k0 + nq - 1 of the list, lane q <-> pair
-// k0 + q: the narrowphase result comes from avr_narrowphase_kernel; pairs it left to the
-// cooperative path (big hulls without a support table, EPA) are finished here, in pair order
-AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew, EpaBuf &E) {
+// k0 + q, from the narrowphase results of avr_narrowphase_kernel
+AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew) {
     const int lane = lane_id();
     PROF_START(pb);
     int sa = 0, sb = 0, p = 0;
@@ -1132,37 +1153,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, i
         nB = V(r0.y, r0.z, r0.w); pB = V(r1.x, r1.y, r1.z); d = r1.w;
         coop = rc == 2;
     }
-    // wave-cooperative narrowphase, in pair order
-    unsigned long long cm = __ballot(coop);
-#ifdef AVR_PROF
-    if (lane == 0) L.prof[11] += __popcll(cm);
-    {   // coop pairs by body kinds: robot-robot, robot-free, robot-static/human, other
-        int kind = 3;
-        if (coop) {
-            const int ka = m.body_kind[m.shape_body[sa]], kb = m.body_kind[m.shape_body[sb]];
-            if (ka == AVR_BODY_ROBOT && kb == AVR_BODY_ROBOT) kind = 0;
-            else if (ka == AVR_BODY_ROBOT || kb == AVR_BODY_ROBOT) kind = (ka == AVR_BODY_FREE || kb == AVR_BODY_FREE) ? 1 : 2;
-        }
-        for (int q = 0; q < 4; q++) {
-            const unsigned long long bq = __ballot(coop && kind == q);
-            if (lane == 0) L.prof[19 + q] += __popcll(bq);
-        }
-    }
-    PROF_STOP(16, pb);
-#endif
-    while (cm) {
-        const int j = __ffsll((long long)cm) - 1;
-        cm &= cm - 1;
-        const int sj = __shfl(sa, j, 64), tj = __shfl(sb, j, 64);
-        int ba = m.shape_body[sj], bb = m.shape_body[tj];
-        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-        WShape A = make_wshape(m, sj, ldtf(L.btf[ba])), B = make_wshape(m, tj, ldtf(L.btf[bb]));
-        v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
-        float d2 = 0.f;
-        int nit2, nk2;
-        int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit2, nk2);
-        if (lane == j) { rc = r2; nB = n2; pB = p2; d = d2; }
-    }
+    (void)coop;     // (the narrowphase kernel finished every pair: rc is 0 or 1)
     PROF_STOP(17, pb);
 
     // manifold update (one lane per pair)
@@ -1219,7 +1210,8 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, i
 
 // Part A1 (avr_substep_pairs_kernel): body frames, fattened AABBs, broadphase and the ordered
 // shape-pair list, written to the env's collision scratch.
-AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
+template <class LT>
+AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     const int lane = lane_id();
     const int gender = L.gender;
     PROF_START(pt);
@@ -1435,7 +1427,6 @@ AVR_DI void collide_pairs(const KModel &m, EnvLDS &L, float *cs) {
 // point); the new pool is appended to global scratch and copied over the old one at the end.
 AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float *gcp, float *scratch) {
     const int lane = lane_id();
-    EpaBuf &E = *(EpaBuf *)(scratch + SCR_EPA);
     float *newcp = scratch + SCR_NEWCP;
     PROF_START(pt);
     // the previous contact pool in LDS (the manifold update reads and updates it in place) and
@@ -1451,7 +1442,7 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     const int nsp = __float_as_int(cs[CS_NSP]);
     int nnew = 0;
     for (int k0 = 0; k0 < nsp; k0 += 64) {
-        collide_batch(m, L, cs, k0, min(64, nsp - k0), ocp, nold, newcp, nnew, E);
+        collide_batch(m, L, cs, k0, min(64, nsp - k0), ocp, nold, newcp, nnew);
         SYNC();
     }
     if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
@@ -1776,10 +1767,11 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
 }
 
 // --------------------------------------------------------------------------- one sub-step
-// A sub-step is four kernels: avr_substep_pairs_kernel (forward kinematics, body frames,
+// A sub-step is five kernels: avr_substep_pairs_kernel (forward kinematics, body frames,
 // broadphase, shape-pair list), avr_narrowphase_kernel (one lane per listed shape pair, across
-// all envs), avr_substep_a_kernel (manifold update, unconstrained velocities, constraint rows)
-// and avr_substep_b4_kernel (PGS + integration).  What crosses the kernel boundaries goes
+// all envs), avr_coop_kernel (the rare pairs that need the wave-cooperative narrowphase),
+// avr_substep_a_kernel (manifold update, unconstrained velocities, constraint rows) and
+// avr_substep_b4_kernel (PGS + integration).  What crosses the kernel boundaries goes
 // through the per-env collision scratch (m.cscr), the workspace (m.ws) and the row buffer
 // (m.rows).
 AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows, const float *cs) {
@@ -1957,11 +1949,12 @@ AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env *
 
 AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[AVR_S_TASK + AVR_T_HDYN] != 0.f; }
 
-AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
+template <class LT>
+AVR_DI void load_state(const KModel &m, LT &L, const float *gst) {
     const int lane = lane_id();
 #ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the env's LDS block so that a read of a word this
                         // kernel did not write shows up (tools/gpu_poison.sh)
-    for (int i = lane; i < (int)(sizeof(EnvLDS) / 4); i += 64) ((float *)&L)[i] = __int_as_float(-1);
+    for (int i = lane; i < (int)(sizeof(LT) / 4); i += 64) ((float *)&L)[i] = __int_as_float(-1);
     SYNC();
 #endif
     for (int i = lane; i < AVR_S_CP; i += 64) L.st[i] = gst[i];
@@ -1978,7 +1971,8 @@ AVR_DI void load_state(const KModel &m, EnvLDS &L, const float *gst) {
     SYNC();
 }
 
-AVR_DI void prof_flush(const KModel &m, EnvLDS &L, int env) {
+template <class LT>
+AVR_DI void prof_flush(const KModel &m, LT &L, int env) {
 #ifdef AVR_PROF
     SYNC();
     if (m.prof && lane_id() < AVR_PROF_SLOTS) m.prof[(size_t)env * AVR_PROF_SLOTS + lane_id()] += L.prof[lane_id()];
@@ -2050,7 +2044,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
 // shape-pair list (collide_pairs) into the env's collision scratch.
 __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                                          const unsigned char *__restrict__ mask, int env0, int n_envs) {
-    __shared__ EnvLDS L;
+    __shared__ PairsLDS L;
     AVR_ENV_GUARD();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
     load_state(m, L, gst);
@@ -2175,6 +2169,34 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
     o[1] = make_float4(pB.x, pB.y, pB.z, d);
 }
 
+// the listed pairs (n of them) that the lane path left to the wave-cooperative narrowphase (rc 2:
+// a big hull without a support table, penetrating cores that need EPA, the lane iteration cap):
+// the whole wave runs narrowphase<true> on each, E = the env's EPA buffer
+AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
+    const int lane = lane_id();
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int k = c0 + lane < n ? c0 + lane : -1;
+        unsigned long long cm = __ballot(k >= 0 && __float_as_int(cs[CS_RES + 8 * (k >= 0 ? k : 0)]) == 2);
+        while (cm) {
+            const int j = __ffsll((long long)cm) - 1;
+            cm &= cm - 1;
+            const int kj = __shfl(k, j, 64);
+            const int key = __float_as_int(cs[CS_PAIRS + 2 * kj]);
+            const int sa = key & 0xffff, sb = key >> 16;
+            const int ba = m.shape_body[sa], bb = m.shape_body[sb];
+            const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+            const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+            v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
+            float d2 = 0.f;
+            int nit, nk;
+            const int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk);
+            SYNC();
+            if (lane == 0) np_store(cs, kj, r2, n2, p2, d2);
+            SYNC();
+        }
+    }
+}
+
 // Sub-step part A2: the narrowphase of every listed shape pair across all envs, in two blocks
 // per env: the sphere-hull list (point-core GJK with refill) and the other pairs (one lane per
 // pair, narrowphase()).  Pairs with a big hull that has no support table, and penetrating pairs
@@ -2215,7 +2237,7 @@ __global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__res
     }
     const int n1 = __float_as_int(cs[CS_N1]);
     for (int c0 = 0; c0 < n1; c0 += 64) {
-        if (c0 + lane >= n1) break;
+        if (c0 + lane >= n1) continue;
         const int k = __float_as_int(cs[CS_L1 + c0 + lane]);
         const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
         const int sa = key & 0xffff, sb = key >> 16;
@@ -2231,6 +2253,18 @@ __global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__res
         }
         np_store(cs, k, rc, nB, pB, d);
     }
+}
+
+// Sub-step part A2b: the pairs the narrowphase kernel left to the wave-cooperative path (rc 2),
+// one block per env (nearly all exit after a scan of their results; its own kernel, so that the
+// cooperative GJK/EPA does not inflate the register budget of the lane kernels).
+__global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0, int n_envs) {
+    const int env = env0 + blockIdx.x;
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const KModel &m = *mp;
+    __shared__ EpaBuf E;        // the EPA polytope in LDS (9.5 KB; this kernel has no other LDS)
+    float *cs = env_cs(m, env);
+    np_coop(m, cs, __float_as_int(cs[CS_NSP]), E);
 }
 
 // Sub-step part A3: one 64-lane block per env, state staged in LDS -- manifold update,
@@ -2825,6 +2859,8 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
         hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
         mark(AVR_K_NARROW);
         hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 7) / 8)), dim3(64), 0, stream, d_m, mask, env0, env1);
+        mark(AVR_K_COOP);
+        hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);

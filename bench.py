@@ -198,7 +198,7 @@ def main():
                      # it and are limited by VALU issue and memory latency
                      'limiter': 'valu-issue/latency' if achieved / HBM_PEAK_GBS < 0.05 else 'hbm',
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': 'one env-step = 1 take_step + 10 x (substep_pairs, narrowphase, substep_a, substep_b4) + 1 task launch; '
+                     'scope': 'one env-step = 1 take_step + 10 x (substep_pairs, narrowphase, coop, substep_a, substep_b4) + 1 task launch; '
                               'achieved = algorithmic bytes of the step / summed launch durations; '
                               'traffic = PMC HBM bytes of the step (profiles/pmc_traffic.json), traffic_GBs = traffic / summed launch durations',
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(ABI),

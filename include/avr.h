@@ -100,7 +100,7 @@ const char *avr_last_error(avr_sim *sim);
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
  * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times
  * returns the accumulated milliseconds and launch counts per kernel kind
- * [take_step, substep_a, substep_b, task, substep_pairs, narrowphase, -, -] since enabling
+ * [take_step, substep_a, substep_b, task, substep_pairs, narrowphase, coop, -] since enabling
  * (synchronises the stream). */
 int avr_profile_kernels(avr_sim *sim, int32_t enable);
 int avr_kernel_times(avr_sim *sim, double *ms8, int64_t *count8);

@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 # launches per env-step (FeedingJaco: 10 sub-steps of four kernels, one take_step, one task launch)
-STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': 10, 'avr_narrowphase_kernel': 10, 'avr_substep_a_kernel': 10,
+STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': 10, 'avr_narrowphase_kernel': 10, 'avr_coop_kernel': 10, 'avr_substep_a_kernel': 10,
                 'avr_substep_b4_kernel': 10, 'avr_task_kernel': 1}
 
 
