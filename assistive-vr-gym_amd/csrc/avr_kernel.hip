@@ -769,11 +769,19 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
     int nf = 0;
     if (epa_add_face(L, nf, 0, 1, 2) || epa_add_face(L, nf, 0, 3, 1) || epa_add_face(L, nf, 0, 2, 3) || epa_add_face(L, nf, 1, 3, 2)) return -1;
     int best = -1;
+    const int lane = lane_id();
     for (int it = 0; it < EPA_MAX_IT; it++) {
-        best = -1;
+        // closest alive face: the first strictly smallest d (wave argmin, lowest index on ties)
         float bd = BIGF;
-        for (int f = 0; f < nf; f++)
-            if (L.eFi[f][3] && L.eFn[f][3] < bd) { bd = L.eFn[f][3]; best = f; }
+        int bf = 0x7fffffff;
+        for (int f = lane; f < nf; f += 64)
+            if (L.eFi[f][3] && L.eFn[f][3] < bd) { bd = L.eFn[f][3]; bf = f; }
+        for (int o = 32; o > 0; o >>= 1) {
+            const float od = __shfl_xor(bd, o, 64);
+            const int of = __shfl_xor(bf, o, 64);
+            if (od < bd || (od == bd && of < bf)) { bd = od; bf = of; }
+        }
+        best = bf == 0x7fffffff ? -1 : bf;
         if (best < 0) return -1;
         v3 n = ld3(L.eFn[best]);
         v3 sa = support<true>(m, A, n), sb = support<true>(m, B, scl(n, -1.f));
@@ -782,49 +790,79 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
         if (dist - L.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
         int vi = nv++;
         epa_set_vert(L, vi, wv, sa, sb);
+        // visible faces die and leave the horizon edge list: one lane, serial (the order of the
+        // list, with its swap-with-last removals, is that of the CPU restatement)
         int ne = 0;
-        for (int f = 0; f < nf; f++) {
-            if (!L.eFi[f][3]) continue;
-            if (dot(ld3(L.eFn[f]), sub(wv, ld3(L.eW[L.eFi[f][0]]))) > 0.f) {
-                int fi = L.eFi[f][0], fj = L.eFi[f][1], fk = L.eFi[f][2];
-                SYNC();
-                if (lane_id() == 0) L.eFi[f][3] = 0;
-                SYNC();
-                int e3[3][2] = {{fi, fj}, {fj, fk}, {fk, fi}};
-                for (int e = 0; e < 3; e++) {
-                    int found = -1;
-                    for (int q = 0; q < ne; q++)
-                        if (L.eEdge[q][0] == e3[e][1] && L.eEdge[q][1] == e3[e][0]) { found = q; break; }
-                    int n0 = L.eEdge[ne - 1 < 0 ? 0 : ne - 1][0], n1 = L.eEdge[ne - 1 < 0 ? 0 : ne - 1][1];
-                    SYNC();
-                    if (lane_id() == 0) {
-                        if (found >= 0) { L.eEdge[found][0] = n0; L.eEdge[found][1] = n1; }
-                        else { L.eEdge[ne][0] = e3[e][0]; L.eEdge[ne][1] = e3[e][1]; }
+        if (lane == 0) {
+            for (int f = 0; f < nf; f++) {
+                if (!L.eFi[f][3]) continue;
+                if (dot(ld3(L.eFn[f]), sub(wv, ld3(L.eW[L.eFi[f][0]]))) > 0.f) {
+                    const int fi = L.eFi[f][0], fj = L.eFi[f][1], fk = L.eFi[f][2];
+                    L.eFi[f][3] = 0;
+                    const int e3[3][2] = {{fi, fj}, {fj, fk}, {fk, fi}};
+                    for (int e = 0; e < 3; e++) {
+                        int found = -1;
+                        for (int q = 0; q < ne; q++)
+                            if (L.eEdge[q][0] == e3[e][1] && L.eEdge[q][1] == e3[e][0]) { found = q; break; }
+                        if (found >= 0) { L.eEdge[found][0] = L.eEdge[ne - 1][0]; L.eEdge[found][1] = L.eEdge[ne - 1][1]; ne--; }
+                        else { L.eEdge[ne][0] = e3[e][0]; L.eEdge[ne][1] = e3[e][1]; ne++; }
                     }
-                    SYNC();
-                    if (found >= 0) ne--; else ne++;
                 }
             }
         }
-        // compact dead faces (uniform read, lane 0 writes in order)
+        ne = __shfl(ne, 0, 64);
+        SYNC();
+        // compact the dead faces away, in order (lane-parallel: reads of a chunk precede its writes,
+        // which land at or below the chunk)
         int k = 0;
-        for (int f = 0; f < nf; f++) {
-            int alive = L.eFi[f][3];
+        for (int base = 0; base < nf; base += 64) {
+            const int f = base + lane;
+            const bool alive = f < nf && L.eFi[f][3];
+            int fi0 = 0, fi1 = 0, fi2 = 0;
+            float fn0 = 0.f, fn1 = 0.f, fn2 = 0.f, fn3 = 0.f;
+            if (alive) { fi0 = L.eFi[f][0]; fi1 = L.eFi[f][1]; fi2 = L.eFi[f][2]; fn0 = L.eFn[f][0]; fn1 = L.eFn[f][1]; fn2 = L.eFn[f][2]; fn3 = L.eFn[f][3]; }
+            int tot;
+            const int pre = ballot_prefix(alive, &tot);
+            SYNC();
             if (alive) {
-                int a0 = L.eFi[f][0], a1 = L.eFi[f][1], a2 = L.eFi[f][2];
-                float n0 = L.eFn[f][0], n1 = L.eFn[f][1], n2 = L.eFn[f][2], n3 = L.eFn[f][3];
-                SYNC();
-                if (lane_id() == 0) {
-                    L.eFi[k][0] = a0; L.eFi[k][1] = a1; L.eFi[k][2] = a2; L.eFi[k][3] = 1;
-                    L.eFn[k][0] = n0; L.eFn[k][1] = n1; L.eFn[k][2] = n2; L.eFn[k][3] = n3;
-                }
-                SYNC();
-                k++;
+                L.eFi[k + pre][0] = fi0; L.eFi[k + pre][1] = fi1; L.eFi[k + pre][2] = fi2; L.eFi[k + pre][3] = 1;
+                L.eFn[k + pre][0] = fn0; L.eFn[k + pre][1] = fn1; L.eFn[k + pre][2] = fn2; L.eFn[k + pre][3] = fn3;
             }
+            k += tot;
+            SYNC();
         }
         nf = k;
-        for (int e = 0; e < ne; e++)
-            if (epa_add_face(L, nf, L.eEdge[e][0], L.eEdge[e][1], vi) == -1) return -1;
+        // the new faces (horizon edge, new vertex), in edge order; a degenerate one is skipped, a
+        // full face array ends EPA (epa_add_face semantics, lane-parallel)
+        const v3 Wv = ld3(L.eW[vi]);
+        for (int e0 = 0; e0 < ne; e0 += 64) {
+            const int e = e0 + lane;
+            int ei = 0, ej = 0;
+            v3 fn = V(0, 0, 0);
+            bool ok = false;
+            if (e < ne) {
+                ei = L.eEdge[e][0]; ej = L.eEdge[e][1];
+                const v3 Wi = ld3(L.eW[ei]), Wj = ld3(L.eW[ej]);
+                fn = crs(sub(Wj, Wi), sub(Wv, Wi));
+                const float l = len(fn);
+                ok = !(l < 1e-18f);
+                if (ok) fn = scl(fn, 1.f / l);
+            }
+            int tot;
+            const int pre = ballot_prefix(ok, &tot);
+            const int last = min(ne - e0, 64) - 1;          // the chunk's last edge: the fullest array it meets
+            const int before_last = __shfl(pre, last, 64);
+            if (nf + before_last >= EPA_MAX_F) return -1;
+            SYNC();
+            if (ok) {
+                const int f = nf + pre;
+                L.eFi[f][0] = ei; L.eFi[f][1] = ej; L.eFi[f][2] = vi; L.eFi[f][3] = 1;
+                st3(L.eFn[f], fn);
+                L.eFn[f][3] = dot(fn, ld3(L.eW[ei]));
+            }
+            nf += tot;
+            SYNC();
+        }
     }
     if (best < 0) return -1;
     v3 n = ld3(L.eFn[best]);
@@ -2190,6 +2228,13 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
             float d2 = 0.f;
             int nit, nk;
             const int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk);
+#ifdef AVR_PROF
+            if (m.prof && lane == 0) {     // cooperative pairs, their GJK iterations, the time they took
+                unsigned long long *pr = m.prof + (size_t)(cs - m.cscr) / CS_WORDS * AVR_PROF_SLOTS;
+                atomicAdd(pr + 11, 1ull);
+                atomicAdd(pr + 28, (unsigned long long)nit);
+            }
+#endif
             SYNC();
             if (lane == 0) np_store(cs, kj, r2, n2, p2, d2);
             SYNC();

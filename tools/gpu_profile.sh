@@ -1,5 +1,6 @@
 # Round profile: rocprofv3 kernel-trace stats of the default bench workload, then separate PMC
-# passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix), then the full bench line.
+# passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix), then the full bench line (with the CPU
+# baseline).  Summaries: python tools/rocpd_summary.py gpurun_out/prof <tag>.
 set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/prof
 B="bench.py --steps 20 --warmup 3 --no-cpu-baseline"
@@ -11,6 +12,5 @@ timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_
 timeout -k 10 600 python3 bench.py > gpurun_out/prof/bench_full.log 2>&1
 rc=$?
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_after.txt
-find gpurun_out/prof -name "*.csv" | head -20
-tail -1 gpurun_out/prof/bench_full.log
+tail -1 gpurun_out/prof/bench_full.log | cut -c1-600
 echo rc=$rc

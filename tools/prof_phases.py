@@ -19,7 +19,7 @@ prof = torch.zeros(N * SLOTS, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
 names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-',
-         ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '-', '-', '-', '-',
+         ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '-', '-', '-',
          '#sph-sph', '#closed form', '#sph-small hull', '#sph-table hull', '#box-hull', '#small-small hull', '#hull-table hull', '#other GJK',
          '#it sph-sph', '#it closed', '#it sph-small', '#it sph-table', '#it box-hull', '#it small-small', '#it hull-table', '#it other']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
