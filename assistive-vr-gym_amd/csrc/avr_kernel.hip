@@ -62,12 +62,6 @@ struct EnvLDS {
     unsigned long long prof[AVR_PROF_SLOTS];
 #endif
     union __attribute__((aligned(16))) {
-        struct {                           // collision detection
-            float bmin[MAXB][4], bmax[MAXB][4];
-            int apair[MAXAP];              // active body pairs (broadphase output, in pair order)
-            int candA[128], candB[128];    // children of A (B) whose AABB meets B's (A's) body AABB
-            float caabb[MAXCC][6];         // world AABBs of the non-static shapes (min3, max3)
-        } c;
         struct {                           // contact update (part A3)
             float ocp[AVR_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
             int okey[AVR_MAX_CONTACTS];                   // its (sa | sb << 16) keys
@@ -79,25 +73,33 @@ struct EnvLDS {
     } u;
 };
 
-// LDS of the pair kernel (avr_substep_pairs_kernel): the state words, link and body frames and
-// the collision scratch only, so that more of its waves are resident than of EnvLDS's kernels
+// LDS of the pair kernel (avr_substep_pairs_kernel), <= 10 KB so that 16 blocks (a 4096-env
+// launch) are resident at once.  The state words and link frames are dead once the body frames
+// exist, so the collision scratch overlays them.
 struct PairsLDS {
-    float st[AVR_S_CP];
-    float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
     float btf[MAXB][8];
     int flags, gender, nla, nda;
 #ifdef AVR_PROF
     unsigned long long prof[AVR_PROF_SLOTS];
 #endif
     union __attribute__((aligned(16))) {
+        struct {                           // forward kinematics and body frames
+            float st[AVR_S_CP];
+            float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
+        };
         struct {
-            float bmin[MAXB][4], bmax[MAXB][4];
-            int apair[MAXAP];
-            int candA[128], candB[128];
-            float caabb[MAXCC][6];
-        } c;
-    } u;
+            struct {                       // collision detection
+                float bmin[MAXB][4], bmax[MAXB][4];
+                unsigned short apair[MAXAP];        // active body pairs (broadphase output, in pair order)
+                unsigned short candA[128], candB[128];   // children of A (B) whose AABB meets B's (A's) body AABB
+                float caabb[MAXCC][6];     // world AABBs of the non-static shapes (min3, max3)
+            } c;
+        } u;
+    };
 };
+#ifndef AVR_PROF
+static_assert(sizeof(PairsLDS) <= 10240, "pair kernel: 16 blocks per CU");
+#endif
 
 #define SYNC() __syncthreads()
 
@@ -423,7 +425,7 @@ struct GlobalF4 {
     }
 };
 
-template <bool COOP>
+template <bool COOP, int NB = 8>
 AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
     v3 l = qrot(qconj(s.t.q), d);
     v3 r;
@@ -492,17 +494,17 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
             const float4 v = hv[bi];
             r = V(v.x, v.y, v.z);
         } else {
-            // batches of 8 vertices in flight, ceil(nv / 8) round trips; a short last batch
+            // batches of NB vertices in flight, ceil(nv / NB) round trips; a short last batch
             // re-reads vertex nv - 1, which cannot displace an earlier winner under the strict ">"
             float best = -BIGF;
             float4 bv = hv[0];
             const int last = s.nv - 1;
-            for (int i = 0; i < s.nv; i += 8) {
-                float4 v[8];
+            for (int i = 0; i < s.nv; i += NB) {
+                float4 v[NB];
 #pragma unroll
-                for (int k = 0; k < 8; k++) v[k] = hv[min(i + k, last)];
+                for (int k = 0; k < NB; k++) v[k] = hv[min(i + k, last)];
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
+                for (int k = 0; k < NB; k++) {
                     const float dd = l.x * v[k].x + l.y * v[k].y + l.z * v[k].z;
                     if (dd > best) { best = dd; bv = v[k]; }
                 }
@@ -649,6 +651,11 @@ AVR_DI int simplex_closest(SX &S, v3 &vout, float lam[4]) {
 #define GJK_LANE_IT GJK_MAX_IT     // measured: a cap of 4..16 does not pay on this scene
 #endif
 
+// hull vertices in flight per support scan of the lane GJK (hull-hull pairs: two scans per
+// iteration; 4 keeps the narrowphase kernel within 128 VGPRs)
+#ifndef GJK_NB
+#define GJK_NB 4
+#endif
 template <bool COOP>
 AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
     v3 v = sub(A.t.p, B.t.p);
@@ -661,7 +668,7 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     bool converged = false;
     for (int it = 0; it < max_it; it++) {
         nit = it + 1;
-        v3 sa = support<COOP>(m, A, scl(v, -1.f)), sb = support<COOP>(m, B, v);
+        v3 sa = support<COOP, GJK_NB>(m, A, scl(v, -1.f)), sb = support<COOP, GJK_NB>(m, B, v);
         v3 wv = sub(sa, sb);
         float vv = len2(v), vw = dot(v, wv);
         if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
@@ -1253,8 +1260,10 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     const int lane = lane_id();
     const int gender = L.gender;
     PROF_START(pt);
-    // body transforms + fattened AABBs
-    for (int b = lane; b < m.nb; b += 64) {
+    // body transforms + fattened AABBs (one lane per body: nb <= MAXB < 64)
+    v3 bmn = V(0, 0, 0), bmx = V(0, 0, 0);
+    if (lane < m.nb) {
+        const int b = lane;
         tf t = body_tf(m, L, b);
         int g = m.body_kind[b] == AVR_BODY_HUMAN ? gender : 0;
         const float *a = m.body_aabb + 12 * b + 6 * g;
@@ -1263,8 +1272,13 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
         v3 e = V(BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND);
         sttf(L.btf[b], t);
         sttf(cs + CS_BTF + 8 * b, t);
-        st3(L.u.c.bmin[b], sub(mn, e));
-        st3(L.u.c.bmax[b], add(mx, e));
+        bmn = sub(mn, e);
+        bmx = add(mx, e);
+    }
+    SYNC();     // the state words and link frames are dead: the collision scratch overlays them
+    if (lane < m.nb) {
+        st3(L.u.c.bmin[lane], bmn);
+        st3(L.u.c.bmax[lane], bmx);
     }
     SYNC();
     // world AABBs of the non-static child shapes
@@ -2247,7 +2261,10 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
 // pair, narrowphase()).  Pairs with a big hull that has no support table, and penetrating pairs
 // that need EPA, are marked rc = 2 and finished by the wave-cooperative path in part A3.  Block b
 // takes env 8 (b / 16) + b % 8 (the XCD of parts A1 and A3 for that env), list (b / 8) % 2.
-__global__ __launch_bounds__(64) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
+#ifndef NP_WAVES
+#define NP_WAVES 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
                                                              int n_envs) {
     const int env = env0 + 8 * (blockIdx.x >> 4) + (blockIdx.x & 7);
     const int list = (blockIdx.x >> 3) & 1;

@@ -20,6 +20,7 @@ VARIANTS = {
     'fdiv': ('-fno-hip-fp32-correctly-rounded-divide-sqrt',),
     'dc1': ('-DB4_DC=1',), 'dc3': ('-DB4_DC=3',), 'dc4': ('-DB4_DC=4',),
     'dn2': ('-DB4_DN=2',), 'dn4': ('-DB4_DN=4',),
+    'np4': ('-DNP_WAVES=4',), 'np4nb4': ('-DNP_WAVES=4', '-DGJK_NB=4'),
 }
 
 
