@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 #include <cstring>
 #include <cmath>
@@ -163,17 +164,18 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     HIPCHK(s, hipSetDevice(cfg->device));
     HIPCHK(s, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     {
-        // default 1: with the four-env part B, 2 / 4 concurrent groups measure 347k / 239k vs 355k
-        // env-steps/s (their earlier wrong results were the uninitialized-LDS read fixed in part A,
-        // DESIGN.md); opt in with AVR_ENV_GROUPS=2..8
+        // default: one group per 1024 envs, at most 4 (4096 envs: 600k -> 680k env-steps/s, the
+        // groups' kernels fill each other's launch tails; 4 streams stay within the runtime's
+        // default of 4 hardware queues, past which streams share queues and serialise).
+        // AVR_ENV_GROUPS=1..8 overrides.
         const char *g = getenv("AVR_ENV_GROUPS");
-        int ng = g ? atoi(g) : 1;
+        int ng = g ? atoi(g) : std::min(4, std::max(1, cfg->n_envs / 1024));
         if (ng < 1) ng = 1;
         if (ng > AVR_MAX_GROUPS) ng = AVR_MAX_GROUPS;
         if (ng > cfg->n_envs) ng = cfg->n_envs;
         s->ngroups = ng;
         HIPCHK(s, hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
-        for (int i = 0; i < ng; i++) {
+        for (int i = 1; i < ng; i++) {      // (group 0 runs on the handle's stream)
             HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));
             HIPCHK(s, hipEventCreateWithFlags(&s->join_ev[i], hipEventDisableTiming));
         }
@@ -415,23 +417,29 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
 
 
 // one launch sequence over all envs: on the handle's stream (1 group, or while per-kernel
-// timing is on), else forked over the group streams and joined back
+// timing is on), else split into env groups (boundaries on multiples of 32 envs, one part-B
+// block's share) whose sequences run concurrently: group 0 on the handle's stream itself, the
+// others forked from it and joined back (ngroups streams in all, within the device's hardware
+// queues)
 static hipError_t run_step(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
                            const unsigned char *mask, int mode, long long t) {
     const int E = s->cfg.n_envs;
     if (s->ngroups <= 1 || s->evlog.cap)
         return avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, 0, E, s->stream,
                                s->evlog.cap ? &s->evlog : nullptr);
+    auto bound = [&](int g) { return g >= s->ngroups ? E : std::min(E, (int)(((long long)E * g / s->ngroups + 16) / 32 * 32)); };
     hipError_t e = hipEventRecord(s->fork_ev, s->stream);
     if (e != hipSuccess) return e;
-    for (int g = 0; g < s->ngroups; g++) {
-        const int e0 = (int)((long long)E * g / s->ngroups), e1 = (int)((long long)E * (g + 1) / s->ngroups);
+    for (int g = 1; g < s->ngroups; g++) {
         if ((e = hipStreamWaitEvent(s->gstream[g], s->fork_ev, 0)) != hipSuccess) return e;
-        if ((e = avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, e0, e1, s->gstream[g], nullptr)) != hipSuccess)
+        if ((e = avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, bound(g), bound(g + 1), s->gstream[g], nullptr)) !=
+            hipSuccess)
             return e;
         if ((e = hipEventRecord(s->join_ev[g], s->gstream[g])) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s->stream, s->join_ev[g], 0)) != hipSuccess) return e;
     }
+    if ((e = avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, 0, bound(1), s->stream, nullptr)) != hipSuccess) return e;
+    for (int g = 1; g < s->ngroups; g++)
+        if ((e = hipStreamWaitEvent(s->stream, s->join_ev[g], 0)) != hipSuccess) return e;
     return hipSuccess;
 }
 

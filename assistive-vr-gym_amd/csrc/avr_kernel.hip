@@ -1990,7 +1990,7 @@ enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
     const KModel &m = *mp;                   \
     (void)m
 
-#ifdef AVR_PROF
+#if defined(AVR_PROF) || defined(AVR_WAVETIME)
 AVR_DI int xcc_id() {   // XCD of the executing CU (HW_REG_XCC_ID, id 20, bits 3:0)
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xf);
 }
@@ -2587,7 +2587,7 @@ AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
 }
 
 template <int DN, int DC, class NS, class CS>
-AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
+AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename NS::Row NR;
     typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
@@ -2597,6 +2597,7 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
     sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
                      [&](const CR &R) { (void)go4<CS::robot_parts>(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
     const int fr0 = n_nc + n_c;
+    int units = 0;      // friction units swept (diagnostics)
     for (int it = 0; it < m.iters; it++) {
         const bool fwd = (it & 1) != 0;
         sweep4<DN, false>(ns, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
@@ -2617,6 +2618,7 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
         tmax = max(tmax, __shfl_xor(tmax, 16));
         tmax = max(tmax, __shfl_xor(tmax, 32));
         tmax = uni(tmax);
+        units += tmax;
         if (tmax == 0) continue;
         // the same depth-DC pipeline over friction units; list entries are read one step before
         // the headers they address
@@ -2645,6 +2647,7 @@ AVR_DI void pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i 
             }
         }
     }
+    return units;
 }
 
 #ifndef B4_DN
@@ -2661,6 +2664,9 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
                                                             const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
                                                             int n_envs) {
     const KModel &m = *mp;
+#ifdef AVR_WAVETIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     __shared__ f4v b4l[B4_LDSW / 4];
     lds_f *blk = (lds_f *)(lds_f4 *)b4l;
     const int lane = lane_id(), sl = lane & 15, g = lane >> 4;
@@ -2728,20 +2734,35 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     __syncthreads();
     NcSrc ns{rs, eo, ro, imp, n_rows};
     DV d;
+    int units, rcb = 0;
     if (in_lds) {
         if (wmax(n_rc) > 0) {
             CLds<true> cs{blk, cw, rw, n_nc, imp, n_rows};
-            pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+            rcb = 1;
         } else {
             CLds<false> cs{blk, cw, rw, n_nc, imp, n_rows};
-            pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else {
         CGlb cs{rs, eo + CR_BASE * 4, ro, n_nc, imp, n_rows};
-        pgs4<B4_DN, B4_DG>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+        units = pgs4<B4_DN, B4_DG>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
     }
+    (void)units; (void)rcb;
     // normal impulses back to the manifold points (warm start + normalForce)
     for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = imp[n_nc + c];
+#ifdef AVR_WAVETIME   // block timeline at its group-0 env: [1][env] (start, end); [2][env] (sweep lengths, LDS path, friction units)
+    {
+        const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
+        const int e0 = env0 + 32 * (blockIdx.x >> 3) + (blockIdx.x & 7);
+        if (m.prof && lane == 0 && e0 < n_envs) {
+            m.prof[((size_t)1 * n_envs + e0) * 2] = wt0;
+            m.prof[((size_t)1 * n_envs + e0) * 2 + 1] = wt1;
+            m.prof[((size_t)2 * n_envs + e0) * 2] = (unsigned long long)nnc_max | (unsigned long long)nc_max << 16 | (unsigned long long)in_lds << 32;
+            m.prof[((size_t)2 * n_envs + e0) * 2 + 1] = (unsigned long long)wmax(n_rows) | (unsigned long long)units << 16 | (unsigned long long)rcb << 40 | (unsigned long long)xcc_id() << 44;
+        }
+    }
+#endif
     if (!live) return;
     const float *ws = env_ws(m, ev);
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)

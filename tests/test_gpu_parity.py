@@ -246,17 +246,21 @@ def test_tremor_targets_and_hard_limits_match_oracle(lib_and_scene):
     sim.close()
 
 
-def _b_path_run(md, S, force_global, steps=5, frames=30):
+def _b_path_run(md, S, force_global, steps=5, frames=30, env=None):
     from avr import _lib
-    old = os.environ.pop('AVR_B4_GLOBAL', None)
+    env = dict(env or {})
     if force_global:
-        os.environ['AVR_B4_GLOBAL'] = '1'
+        env['AVR_B4_GLOBAL'] = '1'
+    keys = ('AVR_B4_GLOBAL', 'AVR_ENV_GROUPS')
+    old = {k: os.environ.pop(k, None) for k in keys}
+    os.environ.update(env)
     try:
         sim = make_sim(md, len(S))
     finally:
-        os.environ.pop('AVR_B4_GLOBAL', None)
-        if old is not None:
-            os.environ['AVR_B4_GLOBAL'] = old
+        for k in keys:
+            os.environ.pop(k, None)
+            if old[k] is not None:
+                os.environ[k] = old[k]
     sim.set_state(S)
     sim.settle(frames)
     outs = [sim.step(_lib.random_actions(1001, np.arange(len(S)), k)) for k in range(steps)]
@@ -279,6 +283,21 @@ def test_part_b_lds_and_global_row_paths_bit_identical(lib_and_scene):
     for a, b in zip(o_l, o_g):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+
+
+def test_env_groups_bit_identical(lib_and_scene):
+    """A handle splits its envs into groups whose launch sequences run concurrently on separate
+    streams (AVR_ENV_GROUPS, default one per 1024 envs): envs are independent, so any grouping --
+    including group bounds that leave part-B blocks partly filled -- gives the same bits."""
+    A, md = lib_and_scene
+    S = np.concatenate([reset_states(A, md, range(0, 150), 'random'), reset_states(A, md, range(150, 200), 'tremor')])
+    G1, o1 = _b_path_run(md, S, False, steps=3, frames=10, env={'AVR_ENV_GROUPS': '1'})
+    for g in ('3', '4'):
+        Gg, og = _b_path_run(md, S, False, steps=3, frames=10, env={'AVR_ENV_GROUPS': g})
+        assert np.array_equal(G1, Gg)
+        for a, b in zip(o1, og):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
 
 
 _POISON_RUN = r'''

@@ -16,14 +16,16 @@ A = ABI.load_scene(); md = ABI.ModelDesc(A)
 S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
 S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
 sim = _lib.Sim(md, N)
-buf = torch.zeros(2 * N * 2, dtype=torch.int64, device='cuda')
+buf = torch.zeros(3 * N * 2, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, buf.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(20)
 for t in range(3):
     sim.step(_lib.random_actions(1001, np.arange(N), t))
-    p = buf.cpu().numpy().reshape(2, N, 2).astype(np.float64) * 10.0   # 100 MHz ticks -> ns
+    raw = buf.cpu().numpy().reshape(3, N, 2)
+    p = raw[:2].astype(np.float64) * 10.0   # 100 MHz ticks -> ns
     for k, nm in enumerate(('A', 'B')):
-        s0, s1 = p[k, :, 0], p[k, :, 1]
+        sel = p[k, :, 0] > 0        # B: one record per block (its group-0 env)
+        s0, s1 = p[k, sel, 0], p[k, sel, 1]
         d = (s1 - s0) / 1e3
         span = (s1.max() - s0.min()) / 1e3
         t0 = s0.min()
@@ -32,7 +34,17 @@ for t in range(3):
         print('step %d kernel %s: span %.1f us, wave us p50 %.1f p90 %.1f p99 %.1f max %.1f mean %.1f, last wave starts at %.1f us; slowest envs %s'
               % (t, nm, span, np.percentile(d, 50), np.percentile(d, 90), np.percentile(d, 99), d.max(), d.mean(), last_start,
                  order[:6].tolist()))
+        if nm == 'B':
+            w = raw[2, sel]
+            nnc, nc, lds, nrows = w[:, 0] & 0xffff, (w[:, 0] >> 16) & 0xffff, (w[:, 0] >> 32) & 1, w[:, 1] & 0xffff
+            print('   B blocks %d: in LDS %.3f; nnc_max mean %.1f max %d; nc_max mean %.1f max %d; rows_max mean %.1f max %d'
+                  % (len(d), lds.mean(), nnc.mean(), nnc.max(), nc.mean(), nc.max(), nrows.mean(), nrows.max()))
+            c = np.polyfit(nrows.astype(np.float64), d, 1)
+            print('   B us ~ %.3f * rows_max + %.1f (corr %.3f); slowest blocks: us %s rows %s lds %s'
+                  % (c[0], c[1], np.corrcoef(nrows, d)[0, 1], np.round(d[order[:6]], 1).tolist(), nrows[order[:6]].tolist(), lds[order[:6]].tolist()))
+            hist = np.histogram(d, bins=10)
+            print('   B duration histogram', hist[0].tolist(), np.round(hist[1], 1).tolist())
     St = sim.get_state()
 ncp = St[:, ABI.S_TASK + ABI.T_NCP]
 print('ncp of slowest A envs', ncp[order[:6]], 'mean ncp', ncp.mean())
-np.save(os.path.join(ROOT, 'gpurun_out', 'wavetime.npy'), p)
+np.save(os.path.join(ROOT, 'gpurun_out', 'wavetime_%d.npy' % N), raw)
