@@ -2400,14 +2400,26 @@ AVR_DI f4v bld3(rsrc_t r, int o) {
 //   impulses [n_rows + 2 null slots] | active-contact list [n_c] | contact records [3 n_c][16]
 //   | robot parts of robot-contact rows [n_rob - n_nc][32]
 // (the last two only when the block's four envs fit).
-#define B4_LDSW 10240
-#define LN_C 0
-#define LN_ZERO 4
-#define LN_GROUPS 16
+#ifndef B4_LDSW
+#define B4_LDSW 10240    // LDS words per block
+#endif
 AVR_DI int al4(int x) { return (x + 3) & ~3; }
 
-// this lane's part of a row from the row's ownership mask: 1 endpoint A, 2 endpoint B, 0 none
-AVR_DI int own_of(int mask) { return (int)__builtin_amdgcn_ubfe((unsigned)mask, 2 * (lane_id() & 15), 2); }
+// this lane's part of a row from the row's ownership mask (2 bits per free body: 1 endpoint A,
+// 2 endpoint B, 0 none).  Lanes sl >= MAXF own no free body and read bits 30-31, which every
+// header keeps 0 (a contact header's robot slot + 1 sits in bits CI_SLOT..29), so no lane masks
+// the slot bits off.
+AVR_DI int own_of(int mask) {
+    const int sl = lane_id() & 15;
+    return (int)__builtin_amdgcn_ubfe((unsigned)mask, sl < MAXF ? 2 * sl : 30, 2);
+}
+static_assert(2 * MAXF <= CI_SLOT && MAXNC + 3 * AVR_MAX_CONTACTS < (1 << (30 - CI_SLOT)), "own mask and slot bit fields");
+
+// Row sources.  A sweep step sets a row's addresses with set(R, valid, address, impulse slot)
+// from per-lane bases plus a wave-uniform step offset (an invalid step is a null row), reads its
+// header D steps early (hdr / hdr3) and its header-dependent parts (parts) after that.  The two
+// friction rows of a unit are consecutive records (the second 64 bytes on) with consecutive
+// impulse slots: the second row's loads are the first's plus immediate offsets.
 
 // non-contact rows: buffer loads (they stay L2-resident)
 struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2, r; };
@@ -2416,84 +2428,88 @@ struct NcSrc {
     static constexpr bool robot_parts = true;
     rsrc_t rs;
     int eo, ro;                // this env's records / robot parts (byte offsets)
-    lds_f *imp;
-    int nullslot;
-    AVR_DI void at(Row &R, int r, int pair) const {
-        R.o = r < 0 ? B4_OOB : eo + r * (RWC * 4);
-        R.ip = imp + (r >= 0 ? r : nullslot + pair);
-    }
+    lds_f *ip0, *nullip;       // impulse slots: row 0, null rows
+    AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h0 = bld4(rs, R.o); R.h1 = bld2(rs, R.o + 16); R.imp = *R.ip; }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h0.x); }   // ownership mask
-    AVR_DI int slot(const Row &R) const { return __float_as_int(R.h0.y) - 1; }
-    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 8), 2 endpoint B (word 14), 0 none
+    AVR_DI void parts(Row &R) const {
+        const int o = own_of(__float_as_int(R.h0.x));     // endpoint A at word 8, B at word 14
         const int b = o ? R.o + 8 + 24 * o : B4_OOB;
         R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16);
+        const int slot = __float_as_int(R.h0.y) - 1;
+        R.r = bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB);
     }
-    AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
 };
 
-// contact rows staged in LDS; RC: the block has robot contacts (otherwise no contact row has a
-// robot part and the resolves skip it)
-struct CRowL { int w; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
-template <bool RC>
+// contact rows staged in LDS, by byte address: a row's wb is its record's address - 8, so its
+// header is read at wb + 8 and its endpoint part o (1 A, 2 B) at wb + 24 o.  Null rows and zero
+// parts come from the block's zero-filled head (LN_HEAD words): the null record's headers at
+// words 8-11 and 24-27 (a null friction unit), zero parts at words 12-17 and 28-33, zero robot
+// parts at words 12-13 and 44-45.
+#define LN_HEAD 48
+#define LNB_NULL 24                // null record - 8 (bytes)
+#define LNB_ZERO 48                // zero block (bytes)
+typedef __attribute__((address_space(3))) char lds_c;
+struct CRowL { unsigned wb; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+template <bool RC>             // RC: the block has robot contacts (otherwise no contact row has a robot part)
 struct CLds {
     typedef CRowL Row;
     static constexpr bool robot_parts = RC;
-    lds_f *blk;
-    int cw, rw, n_nc;          // contact records / robot parts of this group (LDS word index)
-    lds_f *imp;
-    int nullslot;
-    AVR_DI void at(Row &R, int r, int pair) const {
-        R.w = r < 0 ? LN_C : cw + (r - n_nc) * CRW;
-        R.ip = imp + (r >= 0 ? r : nullslot + pair);
-    }
-    AVR_DI void hdr(Row &R) const { R.h = *(const lds_f4 *)(blk + R.w); R.imp = *R.ip; }
+    lds_c *blk;
+    unsigned cn, cf;           // normal record 0 / friction unit 0 of this group, - 8 (bytes)
+    unsigned rob;              // robot part of the row with slot + 1 = s: rob + 128 s (bytes, this lane's DoF)
+    lds_f *ipn, *ipf, *nullip; // impulse slots: normal row 0, friction unit 0, null rows
+    AVR_DI void set(Row &R, bool v, unsigned wb, lds_f *ip) const { R.wb = v ? wb : LNB_NULL; R.ip = v ? ip : nullip; }
+    AVR_DI void hdr(Row &R) const { R.h = *(const lds_f4 *)(blk + R.wb + 8); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const {   // normal rows: the friction coefficient is not read
-        const lds_f *q = blk + R.w;
+        const lds_f *q = (const lds_f *)(blk + R.wb + 8);
         const f2v a = *(const lds_f2 *)q;
         R.h.x = a.x; R.h.y = a.y; R.h.z = q[2];
         R.imp = *R.ip;
     }
-    AVR_DI void hdr2(Row &R) const {   // second friction row of a pair: inv, rhs (the rest is the first row's)
-        const lds_f *q = blk + R.w;
-        R.h.y = q[1]; R.h.z = q[2];
-        R.imp = *R.ip;
+    AVR_DI void hdr2(Row &B, const Row &A) const {   // a unit's second row: inv, rhs (the rest is the first row's)
+        const lds_f *q = (const lds_f *)(blk + A.wb + 8 + CRW * 4);
+        B.h.y = q[1]; B.h.z = q[2];
+        B.imp = A.ip[1];
     }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }   // ownership mask
-    AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
-    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 4), 2 endpoint B (word 10), 0 none
-        const lds_f2 *q = (const lds_f2 *)(blk + (o ? R.w - 2 + 6 * o : LN_ZERO));
-        R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2];
+    AVR_DI unsigned own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.wb + 24 * o : LNB_ZERO; }
+    AVR_DI void own_at(Row &R, unsigned b) const { const lds_f2 *q = (const lds_f2 *)(blk + b); R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2]; }
+    AVR_DI unsigned rob_b(const Row &R) const { const unsigned s = (unsigned)__float_as_int(R.h.x) >> CI_SLOT; return s ? rob + 128 * s : LNB_ZERO; }
+    AVR_DI f2v rob_at(unsigned b) const {
+        if constexpr (!RC) { (void)b; return f2v{0.f, 0.f}; }
+        return *(const lds_f2 *)(blk + b);
     }
-    AVR_DI f2v robot(int slot) const {
-        if constexpr (!RC) { (void)slot; return f2v{0.f, 0.f}; }
-        return *(const lds_f2 *)(blk + (slot >= 0 ? rw + (slot - n_nc) * ROBW + 2 * (lane_id() & 15) : LN_ZERO));
+    AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
+    AVR_DI void unit_parts(Row &A, Row &B) const {
+        const unsigned b = own_b(A), r = rob_b(A);
+        own_at(A, b); own_at(B, b + CRW * 4);
+        A.r = rob_at(r); B.r = rob_at(r + ROBW * 4);
     }
 };
 
-// contact rows, buffer loads (blocks whose four envs do not fit the LDS)
+// contact rows, buffer loads (blocks whose four envs do not fit the LDS); a null row or part
+// reads at B4_OOB (+ immediate offsets), past the buffer: zeros
 struct CRowG { int o; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
 struct CGlb {
     typedef CRowG Row;
     static constexpr bool robot_parts = true;
     rsrc_t rs;
-    int co, ro, n_nc;          // this env's contact records / robot parts (byte offsets)
-    lds_f *imp;
-    int nullslot;
-    AVR_DI void at(Row &R, int r, int pair) const {
-        R.o = r < 0 ? B4_OOB : co + (r - n_nc) * (CRW * 4);
-        R.ip = imp + (r >= 0 ? r : nullslot + pair);
-    }
+    int cn, cf;                // normal record 0 / friction unit 0 of this env (byte offsets)
+    int rob;                   // robot part of the row with slot + 1 = s: rob + 128 s (this lane's DoF)
+    lds_f *ipn, *ipf, *nullip;
+    AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
-    AVR_DI void hdr2(Row &R) const { const f2v a = bld2(rs, R.o + 4); R.h.y = a.x; R.h.z = a.y; R.imp = *R.ip; }
-    AVR_DI int info(const Row &R) const { return __float_as_int(R.h.x) & ((1 << CI_SLOT) - 1); }   // ownership mask
-    AVR_DI int slot(const Row &R) const { return (__float_as_int(R.h.x) >> CI_SLOT) - 1; }
-    AVR_DI void own(Row &R, int o) const {     // o: 1 endpoint A (word 4), 2 endpoint B (word 10), 0 none
-        const int b = o ? R.o - 8 + 24 * o : B4_OOB;
-        R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16);
+    AVR_DI void hdr2(Row &B, const Row &A) const { const f2v a = bld2(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.imp = A.ip[1]; }
+    AVR_DI int own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.o - 8 + 24 * o : B4_OOB; }
+    AVR_DI void own_at(Row &R, int b) const { R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16); }
+    AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + 128 * s : B4_OOB; }
+    AVR_DI f2v rob_at(int b) const { return bld2(rs, b); }
+    AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
+    AVR_DI void unit_parts(Row &A, Row &B) const {
+        const int b = own_b(A), r = rob_b(A);
+        own_at(A, b); own_at(B, b + CRW * 4);
+        A.r = rob_at(r); B.r = rob_at(r + ROBW * 4);
     }
-    AVR_DI f2v robot(int slot) const { return bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB); }
 };
 
 // sum over the 16 lanes of each DPP row, result in every lane of the row (each rotate folds
@@ -2504,14 +2520,6 @@ AVR_DI float row16_sum(float x) {
     x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xf, 0xf, true));
     x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xf, 0xf, true));
     return x;
-}
-
-// the header-dependent parts of a row: this lane's free part (if it owns an endpoint) and its
-// robot DoF's (J, M^-1 J^T)
-template <class S>
-AVR_DI void parts4(const S &s, typename S::Row &R) {
-    s.own(R, own_of(s.info(R)));
-    R.r = s.robot(s.slot(R));
 }
 
 // resolve one row with its current impulse; returns the new impulse.  The fused multiply-adds
@@ -2533,10 +2541,10 @@ AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, f
     return ni;
 }
 
-// sweep over n (wave-uniform) steps; rr(j) is this lane's row for step j (its group's row index,
-// or -1: a null row, also for every j >= n).  Software pipeline of depth D: headers 2D steps
-// ahead, the header-dependent parts D steps ahead, in a ring of K = 2D + 1 buffers whose slots
-// are compile-time after unrolling.  The sweep runs whole rounds of K steps (the last round pads
+// sweep over n (wave-uniform) steps; at(R, j) sets R's addresses for step j (a null row for
+// every j past this lane's group's rows).  Software pipeline of depth D: headers 2D steps ahead,
+// the header-dependent parts D steps ahead, in a ring of K = 2D + 1 buffers whose slots are
+// compile-time after unrolling.  The sweep runs whole rounds of K steps (the last round pads
 // with null rows, delta = 0) and issues its read-ahead unconditionally: with no conditional
 // load in the loop the compiler's wait counts are exact (a load that may or may not have been
 // issued on some path makes it wait for everything).
@@ -2545,21 +2553,21 @@ AVR_DI void hdr_of(const S &s, typename S::Row &R) {
     if constexpr (H3) s.hdr3(R);
     else s.hdr(R);
 }
-template <int D, bool H3, class S, class RR, class GO>
-AVR_DI void sweep4(const S &s, int n, const RR &rr, const GO &go) {
+template <int D, bool H3, class S, class AT, class GO>
+AVR_DI void sweep4(const S &s, int n, const AT &at, const GO &go) {
     if (n <= 0) return;
     constexpr int K = 2 * D + 1;
     typename S::Row R[K];
 #pragma unroll
-    for (int q = 0; q < 2 * D; q++) { s.at(R[q], rr(q), 0); hdr_of<D, H3>(s, R[q]); }
+    for (int q = 0; q < 2 * D; q++) { at(R[q], q); hdr_of<D, H3>(s, R[q]); }
 #pragma unroll
-    for (int q = 0; q < D; q++) parts4(s, R[q]);
+    for (int q = 0; q < D; q++) s.parts(R[q]);
     for (int j = 0; j < n; j += K) {
 #pragma unroll
         for (int q = 0; q < K; q++) {
-            s.at(R[(q + 2 * D) % K], rr(j + q + 2 * D), 0);
+            at(R[(q + 2 * D) % K], j + q + 2 * D);
             hdr_of<D, H3>(s, R[(q + 2 * D) % K]);
-            parts4(s, R[(q + D) % K]);
+            s.parts(R[(q + D) % K]);
             go(R[q]);
         }
     }
@@ -2568,47 +2576,33 @@ AVR_DI void sweep4(const S &s, int n, const RR &rr, const GO &go) {
 // friction unit: the two friction rows of one active contact and that contact's normal impulse
 template <class S>
 struct Pair4 { typename S::Row a, b; float in; };
-template <class S>
-AVR_DI void pair_hdr(const S &s, Pair4<S> &X, int r, lds_f *in) {
-    s.at(X.a, r, 0);
-    s.at(X.b, r >= 0 ? r + 1 : -1, 1);
-    s.hdr(X.a); s.hdr2(X.b);
-    const float x = *in;                // (read unconditionally: no branch in the pipeline)
-    X.in = r >= 0 ? x : 0.f;
-}
-template <class S>
-AVR_DI void pair_parts4(const S &s, Pair4<S> &X) {
-    const int slot = s.slot(X.a);
-    const int off = own_of(s.info(X.a));
-    s.own(X.a, off);
-    s.own(X.b, off);
-    X.a.r = s.robot(slot);
-    X.b.r = s.robot(slot >= 0 ? slot + 1 : -1);
-}
 
 template <int DN, int DC, class NS, class CS>
-AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
+AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename NS::Row NR;
     typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
     d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
+    // normal rows in contact order: record j at cn + 64 j, impulse slot ipn + j
+    auto at_n = [&](CR &R, int j) { cs.set(R, j < n_c, cs.cn + CRW * 4 * j, cs.ipn + j); };
     // warm start (normal rows, contact order): delta = cached impulse x warm-start factor, which
     // is also the rows' starting impulse
-    sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-                     [&](const CR &R) { (void)go4<CS::robot_parts>(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
-    const int fr0 = n_nc + n_c;
+    sweep4<DC, true>(cs, nc_max, at_n, [&](const CR &R) { (void)go4<CS::robot_parts>(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
     int units = 0;      // friction units swept (diagnostics)
     for (int it = 0; it < m.iters; it++) {
+        // non-contact rows, the sweep direction alternating per iteration
         const bool fwd = (it & 1) != 0;
-        sweep4<DN, false>(ns, nnc_max, [&](int j) { return j < n_nc ? (fwd ? j : n_nc - 1 - j) : -1; },
+        const int r0 = fwd ? 0 : n_nc - 1, sg = fwd ? 1 : -1;
+        const int ob = ns.eo + r0 * (RWC * 4);
+        lds_f *ib = ns.ip0 + r0;
+        sweep4<DN, false>(ns, nnc_max, [&](NR &R, int j) { ns.set(R, j < n_nc, ob + sg * j * (RWC * 4), ib + sg * j); },
                           [&](const NR &R) { *R.ip = go4<true>(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y); });
-        sweep4<DC, true>(cs, nc_max, [&](int j) { return j < n_c ? n_nc + j : -1; },
-                         [&](const CR &R) { *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
+        sweep4<DC, true>(cs, nc_max, at_n, [&](const CR &R) { *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
         // active contacts (positive normal impulse) of each group, in contact order
         int t = 0;
         for (int c0 = 0; c0 < nc_max; c0 += 16) {
             const int c = c0 + sl;
-            const bool a = c < n_c && imp[n_nc + (c < n_c ? c : 0)] > 0.f;
+            const bool a = c < n_c && cs.ipn[c < n_c ? c : 0] > 0.f;
             const unsigned long long b = __ballot(a);
             const unsigned gm = (unsigned)(b >> (lane_id() & 48)) & 0xffffu;
             if (a) list[t + __popc(gm & ((1u << sl) - 1u))] = c;
@@ -2625,24 +2619,30 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_f *imp, lds_i *
         constexpr int K = 2 * DC + 1;
         Pair4<CS> X[K];
         auto lst = [&](int u) { const int c = list[u < t ? u : 0]; return u < t ? c : -1; };   // (unconditional read)
-        auto hdr = [&](Pair4<CS> &Y, int c) { pair_hdr(cs, Y, c >= 0 ? fr0 + 2 * c : -1, imp + n_nc + (c >= 0 ? c : 0)); };
+        auto hdr = [&](Pair4<CS> &Y, int c) {
+            cs.set(Y.a, c >= 0, cs.cf + 2 * CRW * 4 * c, cs.ipf + 2 * c);
+            cs.hdr(Y.a);
+            cs.hdr2(Y.b, Y.a);
+            const float x = cs.ipn[max(c, 0)];     // (read unconditionally: no branch in the pipeline)
+            Y.in = c >= 0 ? x : 0.f;
+        };
         auto go = [&](const Pair4<CS> &Y) {
             const float lim = Y.a.h.w * Y.in;
-            *Y.a.ip = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
-            *Y.b.ip = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
+            Y.a.ip[0] = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
+            Y.a.ip[1] = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
         };
         // (whole rounds of K units, null units past the end, unconditional read-ahead: sweep4)
         int cn = lst(0);
 #pragma unroll
         for (int q = 0; q < 2 * DC; q++) { hdr(X[q], cn); cn = lst(q + 1); }
 #pragma unroll
-        for (int q = 0; q < DC; q++) pair_parts4(cs, X[q]);
+        for (int q = 0; q < DC; q++) cs.unit_parts(X[q].a, X[q].b);
         for (int u0 = 0; u0 < tmax; u0 += K) {
 #pragma unroll
             for (int q = 0; q < K; q++) {
                 hdr(X[(q + 2 * DC) % K], cn);
                 cn = lst(u0 + q + 2 * DC + 1);
-                pair_parts4(cs, X[(q + DC) % K]);
+                cs.unit_parts(X[(q + DC) % K].a, X[(q + DC) % K].b);
                 go(X[q]);
             }
         }
@@ -2694,14 +2694,14 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     // pack the groups' regions; stage the contact rows when all four fit
     const int szA = al4(n_rows + 2) + al4(n_c), szB = 3 * n_c * CRW + n_rc * ROBW;
     const int t0 = __shfl(szA + szB, 0), t1 = __shfl(szA + szB, 16), t2 = __shfl(szA + szB, 32), t3 = __shfl(szA + szB, 48);
-    const bool in_lds = uni(t0 + t1 + t2 + t3) <= B4_LDSW - LN_GROUPS && !m.b4_global;
+    const bool in_lds = uni(t0 + t1 + t2 + t3) <= B4_LDSW - LN_HEAD && !m.b4_global;
     int base;
     if (in_lds) base = g == 0 ? 0 : g == 1 ? t0 : g == 2 ? t0 + t1 : t0 + t1 + t2;
     else {
         const int a0 = __shfl(szA, 0), a1 = __shfl(szA, 16), a2 = __shfl(szA, 32);
         base = g == 0 ? 0 : g == 1 ? a0 : g == 2 ? a0 + a1 : a0 + a1 + a2;
     }
-    base += LN_GROUPS;
+    base += LN_HEAD;
     lds_f *imp = blk + base;
     lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
     const int cw = base + szA, rw = cw + 3 * n_c * CRW;
@@ -2712,7 +2712,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         const int c = r - n_nc;
         imp[r] = c >= 0 && c < n_c ? cpool[AVR_CP_WORDS * c + AVR_CP_IMP] * m.warmstart : 0.f;
     }
-    if (lane < LN_GROUPS) blk[lane] = 0.f;      // null contact header, zero block
+    if (lane < LN_HEAD) blk[lane] = 0.f;        // null rows, zero parts
     if (in_lds) {   // contact records and robot-contact parts, 8 loads in flight per lane
         const int n4r = 3 * n_c * (CRW / 4), n4s = n_rc * (ROBW / 4);
         const int m4 = wmax(n4r + n4s);
@@ -2732,21 +2732,26 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         }
     }
     __syncthreads();
-    NcSrc ns{rs, eo, ro, imp, n_rows};
+    // impulse slots: rows 0 .. n_rows - 1 (non-contact, normal, friction pairs), then 2 null slots
+    lds_f *const ipn = imp + n_nc, *const ipf = ipn + n_c, *const nullip = imp + n_rows;
+    NcSrc ns{rs, eo, ro, imp, nullip};
     DV d;
     int units, rcb = 0;
     if (in_lds) {
+        // byte addresses: records - 8; robot part of slot s at rw + (s - n_nc) ROBW + 2 sl words
+        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW + 2 * sl);
         if (wmax(n_rc) > 0) {
-            CLds<true> cs{blk, cw, rw, n_nc, imp, n_rows};
-            units = pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
             rcb = 1;
         } else {
-            CLds<false> cs{blk, cw, rw, n_nc, imp, n_rows};
-            units = pgs4<B4_DN, B4_DC>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else {
-        CGlb cs{rs, eo + CR_BASE * 4, ro, n_nc, imp, n_rows};
-        units = pgs4<B4_DN, B4_DG>(m, ns, cs, imp, list, n_nc, n_c, nnc_max, nc_max, d);
+        const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, rob = ro - ROBW * 4 + 8 * sl;
+        CGlb cs{rs, cn, cf, rob, ipn, ipf, nullip};
+        units = pgs4<B4_DN, B4_DG>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
     }
     (void)units; (void)rcb;
     // normal impulses back to the manifold points (warm start + normalForce)
