@@ -2256,64 +2256,130 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
     }
 }
 
-// Sub-step part A2: the narrowphase of every listed shape pair across all envs, in two blocks
-// per env: the sphere-hull list (point-core GJK with refill) and the other pairs (one lane per
-// pair, narrowphase()).  Pairs with a big hull that has no support table, and penetrating pairs
-// that need EPA, are marked rc = 2 and finished by the wave-cooperative path in part A3.  Block b
-// takes env 8 (b / 16) + b % 8 (the XCD of parts A1 and A3 for that env), list (b / 8) % 2.
+// Sub-step part A2: the narrowphase of every listed shape pair across all envs.  A block takes one
+// of the two work lists of NP_ENVS envs, concatenated: the sphere-hull list (point-core GJK, a
+// lane that finishes a pair takes the next item of the concatenation, so the lanes stay busy
+// until the last NP_ENVS-env tail) or the other pairs (one lane per item, narrowphase()).  Pairs
+// with a big hull that has no support table, and penetrating pairs that need EPA, are marked rc =
+// 2 for the cooperative kernel.  Block b takes list (b / 8) % 2 of the envs
+// e = env0 + 8 NP_ENVS (b / 16) + b % 8 + 8 k, k < NP_ENVS: the XCD (b % 8) whose L2 holds their
+// pair lists.  Measured at 4096 envs (env groups on): NP_ENVS 1 / 2 / 4 / 8 give 717k / 703k /
+// 638k / 527k env-steps/s -- fewer, longer waves hide less latency than the shorter refill tail saves.
+#ifndef NP_ENVS
+#define NP_ENVS 1
+#endif
 #ifndef NP_WAVES
 #define NP_WAVES 4
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
                                                              int n_envs) {
-    const int env = env0 + 8 * (blockIdx.x >> 4) + (blockIdx.x & 7);
-    const int list = (blockIdx.x >> 3) & 1;
-    if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
     const int lane = lane_id();
-    float *cs = env_cs(m, env);
+    const int list = (blockIdx.x >> 3) & 1;
+    const int eb = env0 + 8 * NP_ENVS * (blockIdx.x >> 4) + (blockIdx.x & 7);
+    if (eb >= n_envs) return;
+    // items per env (0 past the end or masked out), prefix over the block's envs
+    int pre[NP_ENVS + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < NP_ENVS; k++) {
+        const int e = eb + 8 * k;
+        const bool live = e < n_envs && (!mask || mask[e]);
+        pre[k + 1] = pre[k] + (live ? __float_as_int(env_cs(m, live ? e : eb)[list ? CS_N1 : CS_N0]) : 0);
+    }
+    const int T = pre[NP_ENVS];
+    // item j: env slot k and its position in that env's list (value selects: no indexed register array)
+    auto item = [&](int j, float *&cs) {
+        int k = 0, off = 0;
+#pragma unroll
+        for (int q = 1; q < NP_ENVS; q++)
+            if (j >= pre[q]) { k = q; off = pre[q]; }
+        cs = env_cs(m, eb + 8 * k);
+        return j - off;
+    };
+#ifdef AVR_WAVETIME   // [3][eb] (list-0 block, list-1 block) durations in 100 MHz ticks
+    struct WtNp {
+        const KModel &m; int env, list, n_envs; unsigned long long t0;
+        AVR_DI ~WtNp() {
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            if (m.prof && lane_id() == 0) m.prof[((size_t)3 * n_envs + env) * 2 + list] = t1 - t0;
+        }
+    } wtnp{m, eb, list, n_envs, __builtin_amdgcn_s_memrealtime()};
+#endif
+#ifdef AVR_PROF   // narrowphase counters (tools/prof_phases.py): slots 32-39, the block's totals at env eb
+    unsigned long long *pr = m.prof ? m.prof + (size_t)eb * AVR_PROF_SLOTS : nullptr;
+    auto pcount = [&](int slot, long long v) { if (pr && lane == 0 && v) atomicAdd(pr + slot, (unsigned long long)v); };
+#endif
     if (list == 0) {
-        const int n0 = __float_as_int(cs[CS_N0]);
         PH P;
-        bool act = lane < n0;
-        if (act) ph_init(m, cs, __float_as_int(cs[CS_L0 + lane]), P);
+        float *pcs = nullptr;      // the env of the lane's pair
+        bool act = lane < T;
+        if (act) { const int i = item(lane, pcs); ph_init(m, pcs, __float_as_int(pcs[CS_L0 + i]), P); }
         int next = 64;
+#ifdef AVR_PROF
+        pcount(32, T);
+#endif
         while (__ballot(act)) {
+#ifdef AVR_PROF
+            pcount(34, 1);
+            pcount(35, __popcll(__ballot(act)));
+#endif
             bool done = false;
             int rc = 0;
             v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
             float d = 0.f;
             if (act) {
                 done = ph_step(m, P, rc, nB, pB, d);
-                if (done) np_store(cs, P.k, rc, nB, pB, d);
+                if (done) np_store(pcs, P.k, rc, nB, pB, d);
             }
             const unsigned long long dm = __ballot(done);
             if (done) {
                 const int j = next + __popcll(dm & ((1ull << lane) - 1ull));
-                act = j < n0;
-                if (act) ph_init(m, cs, __float_as_int(cs[CS_L0 + j]), P);
+                act = j < T;
+                if (act) { const int i = item(j, pcs); ph_init(m, pcs, __float_as_int(pcs[CS_L0 + i]), P); }
             }
             next += __popcll(dm);
         }
         return;
     }
-    const int n1 = __float_as_int(cs[CS_N1]);
-    for (int c0 = 0; c0 < n1; c0 += 64) {
-        if (c0 + lane >= n1) continue;
-        const int k = __float_as_int(cs[CS_L1 + c0 + lane]);
-        const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
-        const int sa = key & 0xffff, sb = key >> 16;
-        const int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-        const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
-        int rc = 2;
-        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
-        float d = 0.f;
-        if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
-            int nit, nkind;
-            rc = narrowphase<false>(m, *(EpaBuf *)cs, A, B, thr, nB, pB, d, nit, nkind);   // (the lane path never touches the EPA buffer)
+#ifdef AVR_PROF
+    pcount(33, T);
+#endif
+    for (int c0 = 0; c0 < T; c0 += 64) {
+#ifdef AVR_PROF
+        int pit = 0, pk = -1;
+#endif
+        if (c0 + lane < T) {
+            float *cs;
+            const int i = item(c0 + lane, cs);
+            const int k = __float_as_int(cs[CS_L1 + i]);
+            const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
+            const int sa = key & 0xffff, sb = key >> 16;
+            const int ba = m.shape_body[sa], bb = m.shape_body[sb];
+            const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+            const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+            int rc = 2;
+            v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+            float d = 0.f;
+            if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
+                int nit, nkind;
+                rc = narrowphase<false>(m, *(EpaBuf *)cs, A, B, thr, nB, pB, d, nit, nkind);   // (the lane path never touches the EPA buffer)
+#ifdef AVR_PROF
+                pit = nit; pk = nkind;
+#endif
+            }
+            np_store(cs, k, rc, nB, pB, d);
         }
-        np_store(cs, k, rc, nB, pB, d);
+#ifdef AVR_PROF   // GJK iterations (sum, and the chunk's maximum: what the wave runs), pairs by kind
+        int mx = pit;
+        for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        int sm = pit;
+        for (int o = 32; o; o >>= 1) sm += __shfl_xor(sm, o);
+        pcount(36, sm);
+        pcount(37, mx);
+        pcount(38, __popcll(__ballot(pk == 3)));
+        pcount(39, __popcll(__ballot(pk >= 0 && pk < 3)));
+#endif
     }
 }
 
@@ -2946,7 +3012,7 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
         mark(AVR_K_PAIRS);
         hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
         mark(AVR_K_NARROW);
-        hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 7) / 8)), dim3(64), 0, stream, d_m, mask, env0, env1);
+        hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 8 * NP_ENVS - 1) / (8 * NP_ENVS))), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_COOP);
         hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_A);

@@ -1,7 +1,7 @@
 set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out
-timeout -k 10 200 python3 tools/wavetime.py 4096 > gpurun_out/wt.log 2>&1 && \
-timeout -k 10 200 python3 tools/wavetime.py 2048 > gpurun_out/wt2k.log 2>&1
+AVR_ENV_GROUPS=1 timeout -k 10 200 python3 tools/wavetime.py 4096 > gpurun_out/wt.log 2>&1 && \
+AVR_ENV_GROUPS=1 timeout -k 10 200 python3 tools/wavetime.py 2048 > gpurun_out/wt2k.log 2>&1
 rc=$?
 grep -v amdgpu.ids gpurun_out/wt.log | tail -8
 grep -v amdgpu.ids gpurun_out/wt2k.log | tail -3

@@ -20,8 +20,8 @@ lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100)
 names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-',
          ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '-', '-', '-',
-         '#sph-sph', '#closed form', '#sph-small hull', '#sph-table hull', '#box-hull', '#small-small hull', '#hull-table hull', '#other GJK',
-         '#it sph-sph', '#it closed', '#it sph-small', '#it sph-table', '#it box-hull', '#it small-small', '#it hull-table', '#it other']
+         '#np sph-hull', '#np other', '#np refill trips', '#np ph_steps', '#np GJK it', '#np GJK it max', '#np GJK pairs', '#np closed form',
+         '-', '-', '-', '-', '-', '-', '-', '-']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
