@@ -304,17 +304,42 @@ AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *
 }
 
 // Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping), result in L.h.
-// Forward pass level by level (lane i = link i, temporaries in LDS); the backward force
-// accumulation is summed per DoF instead: the DoF of link j sees the moment about its joint
-// origin of every force in its subtree, h_j = ax_j . sum_k (N_k + (c_k - o_j) x F_k) (revolute;
-// ax_j . sum_k F_k prismatic), which is what the recursion (F_p += F_k, N_p += N_k + (c_k - c_p)
-// x F_k) evaluates.
+// The forward recursion (parent p of link i, joint origin o_i, COM c_i):
+//   om_i = om_p + w_i                       (w_i = axis qd, revolute; 0 otherwise)
+//   al_i = al_p + om_p x w_i
+//   vc_i = ((vc_p + om_p x (o_i - c_p)) + v_i) + om_i x (c_i - o_i)          (v_i = axis qd, prismatic)
+//   ac_i = ((ac_p + (al_p x (o_i - c_p) + om_p x (om_p x (o_i - c_p)))) + 2 om_p x v_i)
+//          + (al_i x (c_i - o_i) + om_i x (om_i x (c_i - o_i)))
+// is a sum of per-link terms over the root-to-i path, so every link forms its own terms once its
+// parent's om (then al) are known and sums its ancestors' terms root first (links are numbered
+// parents first): the same additions in the same order as the level-by-level recursion, in three
+// passes instead of one per tree level.  The backward force accumulation is summed per DoF: the
+// DoF of link j sees the moment about its joint origin of every force in its subtree,
+// h_j = ax_j . sum_k (N_k + (c_k - o_j) x F_k) (revolute; ax_j . sum_k F_k prismatic), which is what
+// the recursion (F_p += F_k, N_p += N_k + (c_k - c_p) x F_k) evaluates.
+AVR_DI v3 anc_sum(const KModel &m, unsigned am, const float (*T)[4], int nla, v3 acc) {
+    for (int k = 0; k < nla; k++) {
+        const f4v t = *(const lds_f4 *)T[k];
+        if ((am >> k) & 1u) acc = add(acc, V(t.x, t.y, t.z));
+    }
+    return acc;
+}
+AVR_DI v3 anc_sum3(const KModel &m, unsigned am, const float (*A)[4], const float (*B)[4], const float (*C)[4], int nla, v3 acc) {
+    for (int k = 0; k < nla; k++) {
+        const f4v a = *(const lds_f4 *)A[k], b = *(const lds_f4 *)B[k], c = *(const lds_f4 *)C[k];
+        if ((am >> k) & 1u) acc = add(add(add(acc, V(a.x, a.y, a.z)), V(b.x, b.y, b.z)), V(c.x, c.y, c.z));
+    }
+    return acc;
+}
+
 AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
-    float (*OM)[4] = L.u.d.rn[0], (*VC)[4] = L.u.d.rn[1], (*AL)[4] = L.u.d.rn[2], (*AC)[4] = L.u.d.rn[3], (*FF)[4] = L.u.d.rn[4], (*NN)[4] = L.u.d.rn[5];
+    float (*R0)[4] = L.u.d.rn[0], (*R1)[4] = L.u.d.rn[1], (*R2)[4] = L.u.d.rn[2], (*R3)[4] = L.u.d.rn[3], (*R4)[4] = L.u.d.rn[4], (*R5)[4] = L.u.d.rn[5];
     const float k1l = m.lin_damp, k1a = m.ang_damp;
     const int i = lane_id();
-    const bool mine = i < L.nla;
-    int p = -3, jt = AVR_J_FIXED, lev = -1;
+    const int nla = L.nla;
+    const bool mine = i < nla;
+    int p = -3, jt = AVR_J_FIXED;
+    unsigned am = 0;
     float mi = 0.f, qd = 0.f;
     v3 I = V(0, 0, 0), o = V(0, 0, 0), c = V(0, 0, 0), axw = V(0, 0, 0);
     qt q = Q(0, 0, 0, 1);
@@ -322,7 +347,7 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
         const int go = lgo(L, m);
         p = m.rl_parent[i];          // < 0: fixed robot base or (-2) the static chest slot
         jt = m.rl_jtype[i];
-        lev = m.rl_level[i];
+        am = m.anc_mask[i];
         const int dof = m.rl_dof[i];
         qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
         o = ld3(L.org[i]); c = ld3(L.cm[i]); axw = ld3(L.ax[i]);
@@ -330,57 +355,58 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
         mi = m.rl_mass[go + i];
         I = ld3(m.rl_inertia + 4 * (go + i));
     }
-    const v3 bp = ld3(m.base);
-    for (int d = 0; d < m.nlev; d++) {
-        if (lev == d) {
-            v3 omp = p < 0 ? V(0, 0, 0) : ld3(OM[p]);
-            v3 vp = p < 0 ? V(0, 0, 0) : ld3(VC[p]);
-            v3 alp = p < 0 ? V(0, 0, 0) : ld3(AL[p]);
-            v3 acp = p < 0 ? V(0, 0, 0) : ld3(AC[p]);
-            v3 cp = p < 0 ? bp : ld3(L.cm[p]);
-            v3 rpo = sub(o, cp), roc = sub(c, o);
-            v3 vo = add(vp, crs(omp, rpo));
-            v3 ao = add(acp, add(crs(alp, rpo), crs(omp, crs(omp, rpo))));
-            v3 om, vc, al, ac;
-            if (jt == AVR_J_REVOLUTE) {
-                v3 wj = scl(axw, qd);
-                om = add(omp, wj);
-                al = add(alp, crs(omp, wj));
-                vc = add(vo, crs(om, roc));
-                ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
-            } else if (jt == AVR_J_PRISMATIC) {
-                v3 vj = scl(axw, qd);
-                om = omp;
-                al = alp;
-                vc = add(add(vo, vj), crs(om, roc));
-                ac = add(add(ao, scl(crs(omp, vj), 2.f)), add(crs(al, roc), crs(om, crs(om, roc))));
-            } else {
-                om = omp;
-                al = alp;
-                vc = add(vo, crs(om, roc));
-                ac = add(ao, add(crs(al, roc), crs(om, crs(om, roc))));
-            }
-            v3 Iw = inertia_mul(q, I, om);
-            float vn = len(vc), wn = len(om);
-            v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
-            v3 tdamp = scl(Iw, -(k1a + k1a * wn));
-            st3(OM[i], om); st3(VC[i], vc); st3(AL[i], al); st3(AC[i], ac);
-            st3(FF[i], sub(scl(ac, mi), fdamp));
-            st3(NN[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
-        }
-        SYNC();
+    const bool rev = jt == AVR_J_REVOLUTE, pri = jt == AVR_J_PRISMATIC;
+    const v3 wj = rev ? scl(axw, qd) : V(0, 0, 0), vj = pri ? scl(axw, qd) : V(0, 0, 0);
+    const v3 cp = p < 0 ? ld3(m.base) : ld3(L.cm[p > 0 ? p : 0]);
+    const v3 rpo = sub(o, cp), roc = sub(c, o);
+    // pass 1: angular velocities
+    if (mine) st3(R1[i], wj);
+    SYNC();
+    const v3 om = anc_sum(m, am, R1, nla, V(0, 0, 0));
+    if (mine) st3(R0[i], om);
+    SYNC();
+    // pass 2: angular accelerations, COM velocities
+    const v3 omp = p < 0 ? V(0, 0, 0) : ld3(R0[p]);
+    if (mine) {
+        st3(R2[i], crs(omp, wj));
+        st3(R3[i], crs(omp, rpo)); st3(R4[i], vj); st3(R5[i], crs(om, roc));
     }
+    SYNC();
+    const v3 al = anc_sum(m, am, R2, nla, V(0, 0, 0));
+    const v3 vc = anc_sum3(m, am, R3, R4, R5, nla, V(0, 0, 0));
+    if (mine) st3(R1[i], al);
+    SYNC();
+    // pass 3: COM accelerations
+    const v3 alp = p < 0 ? V(0, 0, 0) : ld3(R1[p]);
+    SYNC();
+    if (mine) {
+        st3(R2[i], add(crs(alp, rpo), crs(omp, crs(omp, rpo))));
+        st3(R3[i], scl(crs(omp, vj), 2.f));
+        st3(R4[i], add(crs(al, roc), crs(om, crs(om, roc))));
+    }
+    SYNC();
+    const v3 ac = anc_sum3(m, am, R2, R3, R4, nla, V(0, 0, 0));
+    // forces: FF = R1, NN = R5 (every lane is past its pass-3 reads of R2..R4 only after the sync below)
+    if (mine) {
+        const v3 Iw = inertia_mul(q, I, om);
+        const float vn = len(vc), wn = len(om);
+        const v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
+        const v3 tdamp = scl(Iw, -(k1a + k1a * wn));
+        st3(R1[i], sub(scl(ac, mi), fdamp));
+        st3(R5[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
+    }
+    SYNC();
     if (i < MAXD) {
         float h = 0.f;
         if (i < L.nda) {
             const int j = m.dof_link[i];
             const v3 aj = ld3(L.ax[j]), oj = ld3(L.org[j]);
-            const bool rev = m.rl_jtype[j] == AVR_J_REVOLUTE;
+            const bool rj = m.rl_jtype[j] == AVR_J_REVOLUTE;
             v3 acc = V(0, 0, 0);
-            for (int k = 0; k < L.nla; k++) {
+            for (int k = 0; k < nla; k++) {
                 if (!is_ancestor(m, k, j)) continue;
-                const v3 F = ld3(FF[k]);
-                acc = add(acc, rev ? add(ld3(NN[k]), crs(sub(ld3(L.cm[k]), oj), F)) : F);
+                const v3 F = ld3(R1[k]);
+                acc = add(acc, rj ? add(ld3(R5[k]), crs(sub(ld3(L.cm[k]), oj), F)) : F);
             }
             h = dot(aj, acc);
         }
