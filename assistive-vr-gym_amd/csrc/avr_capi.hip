@@ -151,7 +151,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     if (cfg->flags & AVR_CFG_RESERVED_MASK) { int r = fail(s, -1, "avr_config.flags 0x%x: no flag is defined", (unsigned)cfg->flags); *out = s; return r; }
     const int hc = d->hc_n > 0 ? d->hc_n : 0;
     if (d->n_links + hc > AVR_MAX_LINKS || d->n_dof + hc > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
-        d->n_bodies > MAXB || d->n_pairs > 65535 || d->n_shapes > 65535 || d->n_arm > AVR_ACT_DIM || hc > AVR_HC_N) {
+        d->n_bodies > MAXB || d->n_pairs > 65535 || d->n_shapes > MAXSH || d->n_arm > AVR_ACT_DIM || hc > AVR_HC_N) {
         int r = fail(s, -2, "model exceeds compiled capacities");
         *out = s;
         return r;
@@ -364,6 +364,12 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
         unsigned mask = 0;
         for (int q = l; q >= 0; q = par[q]) mask |= 1u << q;
         k.anc_mask[l] = mask;
+    }
+    for (int l = 0; l < nla; l++) {
+        unsigned dm = 0;
+        for (int q = 0; q < nla; q++)
+            if ((k.anc_mask[q] >> l) & 1u) dm |= 1u << q;
+        k.desc_mask[l] = dm;
     }
     // tree levels (parents precede children in DFS order): the kinematics passes run level by level
     k.nlev = 0;

@@ -78,6 +78,7 @@ struct EnvLDS {
 // exist, so the collision scratch overlays them.
 struct PairsLDS {
     float btf[MAXB][8];
+    unsigned short sinfo[MAXSH];   // m.shape_info (13 bits: child index + 1, gender + 1, kind)
     int flags, gender, nla, nda;
 #ifdef AVR_PROF
     unsigned long long prof[AVR_PROF_SLOTS];
@@ -99,6 +100,7 @@ struct PairsLDS {
 };
 #ifndef AVR_PROF
 static_assert(sizeof(PairsLDS) <= 10240, "pair kernel: 16 blocks per CU");
+static_assert(MAXSH % 64 == 0, "shape info staged 64 per pass");
 #endif
 
 #define SYNC() __syncthreads()
@@ -213,8 +215,9 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
             const int la = m.dof_link[a], lb = m.dof_link[b];
             const v3 axa = ld3(L.ax[la]), oa = ld3(L.org[la]), axb = ld3(L.ax[lb]), ob = ld3(L.org[lb]);
             const bool ra = m.rl_jtype[la] == AVR_J_REVOLUTE, rb = m.rl_jtype[lb] == AVR_J_REVOLUTE;
-            for (int i = 0; i < L.nla; i++) {
-                if (!is_ancestor(m, i, la) || !is_ancestor(m, i, lb)) continue;
+            // links in both subtrees, ascending (a per-lane bit loop: no scalar load per link)
+            for (unsigned dm = m.desc_mask[la] & m.desc_mask[lb]; dm; dm &= dm - 1u) {
+                const int i = __builtin_ctz(dm);
                 const float *w = L.u.d.iw[i];
                 const float mi = w[6];
                 if (mi <= 0.f) continue;
@@ -403,8 +406,8 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
             const v3 aj = ld3(L.ax[j]), oj = ld3(L.org[j]);
             const bool rj = m.rl_jtype[j] == AVR_J_REVOLUTE;
             v3 acc = V(0, 0, 0);
-            for (int k = 0; k < nla; k++) {
-                if (!is_ancestor(m, k, j)) continue;
+            for (unsigned dm = m.desc_mask[j]; dm; dm &= dm - 1u) {     // the subtree of j, ascending
+                const int k = __builtin_ctz(dm);
                 const v3 F = ld3(R1[k]);
                 acc = add(acc, rj ? add(ld3(R5[k]), crs(sub(ld3(L.cm[k]), oj), F)) : F);
             }
@@ -1359,7 +1362,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                 if (gcull) {
                     sa = L.u.c.candA[i];
                     sb = L.u.c.candB[j];
-                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
+                    ia = L.sinfo[sa]; ib = L.sinfo[sb];
                     v3 a0, a1, b0, b1;
                     child_aabb(m, L, sa, ia, a0, a1);
                     child_aabb(m, L, sb, ib, b0, b1);
@@ -1367,7 +1370,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                 } else {
                     sa = gsa0 + i;
                     sb = gsb0 + j;
-                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
+                    ia = L.sinfo[sa]; ib = L.sinfo[sb];
                     if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (gbare) act = true;
                         else {
@@ -1392,7 +1395,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                     q = L.u.c.apair[kk];
                     sa = rec.y & 0xffff;
                     sb = rec.z & 0xffff;
-                    ia = m.shape_info[sa]; ib = m.shape_info[sb];
+                    ia = L.sinfo[sa]; ib = L.sinfo[sb];
                     if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (rec.w & 1) act = true;
                         else {
@@ -1425,7 +1428,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                         const int i = base + lane;
                         bool a = false;
                         if (i < na) {
-                            const int ia = m.shape_info[gsa0 + i];
+                            const int ia = L.sinfo[gsa0 + i];
                             if (info_enabled(ia, gender)) {
                                 v3 a0, a1;
                                 child_aabb(m, L, gsa0 + i, ia, a0, a1);
@@ -1442,7 +1445,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                         const int j = base + lane;
                         bool a = false;
                         if (j < nb) {
-                            const int ib = m.shape_info[gsb0 + j];
+                            const int ib = L.sinfo[gsb0 + j];
                             if (info_enabled(ib, gender)) {
                                 v3 b0, b1;
                                 child_aabb(m, L, gsb0 + j, ib, b0, b1);
@@ -1630,25 +1633,34 @@ AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float dt) {
     const int lane = lane_id();
     const float erp = m.erp;
-    // enumerate (uniform loop); each lane keeps the description of its own row
-    int nrow = 0, kind = -1, dof = 0, fix = 0;
+    // enumerate in parallel (lane l = link l: its violated limits, then its motor), number the rows
+    // by ballot prefix and hand each row's description to the lane of that row through LDS
+    int nrow, kind = -1, dof = 0, fix = 0;
     float pen = 0.f;
-    for (int i = 0; i < L.nla; i++) {
-        if (!m.rl_has_limit[i]) continue;
-        const int d = m.rl_dof[i];
-        const float q = L.st[AVR_S_Q + d];
-        for (int side = 0; side < 2; side++) {
-            const float pn = side == 0 ? q - m.rl_lower[i] : m.rl_upper[i] - q;
-            if (pn > 0.f) continue;
-            if (lane == nrow) { kind = side; dof = d; pen = pn; }
-            nrow++;
+    {
+        float (*desc)[4] = L.u.d.rn[0];        // [MAXNC] (kind, dof, pen); the RNEA temporaries are dead
+        const bool lk = lane < L.nla;
+        const int ld = lk ? m.rl_dof[lane] : -1;
+        const bool hl = lk && m.rl_has_limit[lane];
+        float plo = 1.f, phi = 1.f;
+        if (hl) {
+            const float q = L.st[AVR_S_Q + ld];
+            plo = q - m.rl_lower[lane];
+            phi = m.rl_upper[lane] - q;
         }
-    }
-    for (int i = 0; i < L.nla; i++) {
-        const int d = m.rl_dof[i];
-        if (d < 0) continue;
-        if (lane == nrow) { kind = 2; dof = d; }
-        nrow++;
+        const bool vlo = hl && !(plo > 0.f), vhi = hl && !(phi > 0.f), mot = ld >= 0;
+        const unsigned long long blo = __ballot(vlo), bhi = __ballot(vhi), bmo = __ballot(mot), lt = (1ull << lane) - 1ull;
+        const int nlim = __popcll(blo) + __popcll(bhi);
+        const int rlo = __popcll(blo & lt) + __popcll(bhi & lt), rmo = nlim + __popcll(bmo & lt);
+        if (vlo && rlo < MAXNC) st3(desc[rlo], V(0.f, (float)ld, plo));
+        if (vhi && rlo + vlo < MAXNC) st3(desc[rlo + vlo], V(1.f, (float)ld, phi));
+        if (mot && rmo < MAXNC) st3(desc[rmo], V(2.f, (float)ld, 0.f));
+        nrow = nlim + __popcll(bmo);
+        SYNC();
+        if (lane < nrow && lane < MAXNC) {
+            const v3 t = ld3(desc[lane]);
+            kind = (int)t.x; dof = (int)t.y; pen = t.z;
+        }
     }
     if (lane >= nrow && lane < nrow + 6) { kind = 3; fix = lane - nrow; }
     nrow += 6;
@@ -2125,10 +2137,20 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const K
     __shared__ PairsLDS L;
     AVR_ENV_GUARD();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    // the packed shape info, staged in LDS for the pair enumeration (loads issued first, their
+    // LDS stores after the kinematics)
+    int si[MAXSH / 64];
+#pragma unroll
+    for (int q = 0; q < MAXSH / 64; q++) {
+        const int s = lane_id() + 64 * q;
+        si[q] = s < m.ns ? m.shape_info[s] : 0;
+    }
     load_state(m, L, gst);
     PROF_START(ps);
     robot_fk(m, L);
     PROF_STOP(0, ps);
+#pragma unroll
+    for (int q = 0; q < MAXSH / 64; q++) L.sinfo[lane_id() + 64 * q] = (unsigned short)si[q];
     float *cs = env_cs(m, env);
     for (int i = lane_id(); i < L.nla * 8; i += 64) cs[CS_CM + i] = (&L.cm[0][0])[i];
     for (int i = lane_id(); i < L.nla * 4; i += 64) { cs[CS_AX + i] = (&L.ax[0][0])[i]; cs[CS_ORG + i] = (&L.org[0][0])[i]; }

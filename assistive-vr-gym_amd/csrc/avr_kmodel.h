@@ -9,6 +9,7 @@
 #define MAXF AVR_MAX_FREE
 #define MAXB 48
 #define MAXCC 224      // non-static child shapes whose world AABBs are cached per sub-step
+#define MAXSH 320      // shapes (the pair kernel stages their packed info in LDS, 16 bits each)
 #define MAXSP 256
 #define MAXAP 256
 #define MAXNC 32
@@ -88,6 +89,7 @@ struct KModel {
     int env_offset;
     int dof_link[MAXD];        // link owning each DoF
     unsigned anc_mask[MAXL];   // bit k set if link k is on the chain base..link (inclusive)
+    unsigned desc_mask[MAXL];  // bit k set if link k is in the subtree of link (inclusive)
     int rl_level[MAXL];        // depth of each link in the tree (roots 0)
     int nlev;                  // number of levels
     int hc_parent_slot, hc_slot[AVR_HC_N], hc_body[AVR_HC_N];
