@@ -116,12 +116,13 @@ static_assert(MAXSH % 64 == 0, "shape info staged 64 per pass");
 #endif
 
 // --------------------------------------------------------------------------- kinematics
-// robot_fk: link frames published in LDS, level by level (lane i = link i; the joint rotations
-// and the per-link model data are formed in parallel, then each level composes onto its parents'
-// frames).  Under 'tremor' the head chain follows the robot's links: its root hangs off the
-// static chest slot (parent -2) and its link frames (== COM frames) are published into the human
-// slot poses, where collision and the task glue (getLinkState(human, 27), feeding.py:134,254)
-// read them.
+// robot_fk: link frames published in LDS.  Every link (lane i) first publishes its joint's local
+// data (origin frame, joint rotation, axis, displacement); then each lane composes the local
+// frames of its own chain root first -- the same transform products in the same order as a
+// level-by-level pass over the tree, without a barrier per level.  Under 'tremor' the head chain
+// follows the robot's links: its root hangs off the static chest slot (parent -2) and its link
+// frames (== COM frames) are published into the human slot poses, where collision and the task
+// glue (getLinkState(human, 27), feeding.py:134,254) read them.
 template <class LT>
 AVR_DI int lgo(const LT &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
 
@@ -129,37 +130,55 @@ template <class LT>
 AVR_DI void robot_fk(const KModel &m, LT &L) {
     const int i = lane_id();
     const bool mine = i < L.nla;
-    int p = -3, jt = AVR_J_FIXED, lev = -1;
-    tf jo, com;
+    unsigned am = 0;
+    tf com;
     v3 axl = V(0, 0, 0);
-    qt qj = Q(0, 0, 0, 1);
-    float qv = 0.f;
+    // local joint data in LDS (lk: origin frame + displacement in word 7; cm: joint rotation,
+    // axis, joint type), overwritten by the results once every lane has composed its chain
     if (mine) {
         const int go = lgo(L, m);
-        p = m.rl_parent[i];
-        jt = m.rl_jtype[i];
-        lev = m.rl_level[i];
-        jo = ldtf(m.rl_jorig + 8 * (go + i));
+        const int jt = m.rl_jtype[i];
+        am = m.anc_mask[i];
+        const tf jo = ldtf(m.rl_jorig + 8 * (go + i));
         com = ldtf(m.rl_com + 8 * (go + i));
         axl = ld3(m.rl_axis + 4 * i);
         const int dof = m.rl_dof[i];
-        qv = dof >= 0 ? L.st[AVR_S_Q + dof] : 0.f;
-        if (jt == AVR_J_REVOLUTE) qj = qaxis(axl, qv);
+        const float qv = dof >= 0 ? L.st[AVR_S_Q + dof] : 0.f;
+        const qt qj = jt == AVR_J_REVOLUTE ? qaxis(axl, qv) : Q(0, 0, 0, 1);
+        sttf(L.lk[i], jo);
+        L.lk[i][7] = qv;
+        stq(L.cm[i], qj);
+        st3(L.cm[i] + 4, axl);
+        L.cm[i][7] = (float)jt;
     }
-    for (int d = 0; d < m.nlev; d++) {
-        if (lev == d) {
-            const tf par = p == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : p < 0 ? ldtf(m.base) : ldtf(L.lk[p]);
-            tf t = tfmul(par, jo);
-            const v3 axw = qrot(t.q, axl);
-            st3(L.org[i], t.p);
-            st3(L.ax[i], axw);
+    SYNC();
+    tf t;
+    v3 org = V(0, 0, 0), axw = V(0, 0, 0);
+    if (mine) {
+        const int r = __builtin_ctz(am);                       // the chain's root link
+        t = m.rl_parent[r] == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : ldtf(m.base);
+        for (unsigned b = am; b; b &= b - 1u) {
+            const int k = __builtin_ctz(b);
+            const tf jo = ldtf(L.lk[k]);
+            const float qv = L.lk[k][7];
+            const qt qj = ldq(L.cm[k]);
+            const v3 ax = ld3(L.cm[k] + 4);
+            const int jt = (int)L.cm[k][7];
+            t = tfmul(t, jo);
+            const v3 aw = qrot(t.q, ax);
+            if (k == i) { org = t.p; axw = aw; }
             if (jt == AVR_J_REVOLUTE) t.q = qmul(t.q, qj);
-            else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(axw, qv));
-            sttf(L.lk[i], t);
-            sttf(L.cm[i], tfmul(t, com));
+            else if (jt == AVR_J_PRISMATIC) t.p = add(t.p, scl(aw, qv));
         }
-        SYNC();
     }
+    SYNC();
+    if (mine) {
+        st3(L.org[i], org);
+        st3(L.ax[i], axw);
+        sttf(L.lk[i], t);
+        sttf(L.cm[i], tfmul(t, com));
+    }
+    SYNC();
     const int c = i - m.nl;
     if (mine && c >= 0) {
         const int slot = m.hc_slot[c];
@@ -1187,8 +1206,6 @@ AVR_DI void manifold_refresh(lds_f *cp, MfNew &nw, unsigned &pk, int &n, tf ta, 
 // The previous contact pool stays in the env's global state (read, and updated in place by the
 // single lane that owns each point); the new pool is appended to global scratch and copied
 // over the old one at the end.
-#define SCR_EPA 0                                   // EpaBuf
-#define SCR_NEWCP 2560                              // new contact pool [AVR_MAX_CONTACTS][16]
 
 AVR_DI float *env_cs(const KModel &m, int env) { return m.cscr + (size_t)env * CS_WORDS; }
 
@@ -1504,11 +1521,11 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
 
 // Part A3 (avr_substep_a_kernel): manifold update of every listed shape pair from its
 // narrowphase result, 64 pairs at a time, and the new contact pool.  The previous contact pool
-// stays in the env's global state (read, and updated in place by the single lane that owns each
-// point); the new pool is appended to global scratch and copied over the old one at the end.
-AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float *gcp, float *scratch) {
+// is copied into LDS first (read, and updated in place by the single lane that owns each point),
+// so the new pool is appended straight into the env's state.
+AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float *gcp) {
     const int lane = lane_id();
-    float *newcp = scratch + SCR_NEWCP;
+    float *newcp = gcp;
     PROF_START(pt);
     // the previous contact pool in LDS (the manifold update reads and updates it in place) and
     // its keys (matching in the manifold update)
@@ -1519,6 +1536,7 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     for (int i = lane; i < nold; i += 64)
         L.u.k.okey[i] = (int)gp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     if (lane == 0) L.flags |= __float_as_int(cs[CS_FLAGS]);
+    __builtin_amdgcn_s_waitcnt(0);     // (every read of the old pool has returned before the new one overwrites it)
     SYNC();
     const int nsp = __float_as_int(cs[CS_NSP]);
     int nnew = 0;
@@ -1528,8 +1546,6 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     }
     if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
     SYNC();
-    // the new pool replaces the old one
-    for (int i = lane; i < nnew * AVR_CP_WORDS; i += 64) gcp[i] = newcp[i];
     if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
     SYNC();
     PROF_STOP(3, pt);
@@ -1873,7 +1889,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     for (int i = lane; i < L.nla * 4; i += 64) { (&L.ax[0][0])[i] = cs[CS_AX + i]; (&L.org[0][0])[i] = cs[CS_ORG + i]; }
     SYNC();
     PROF_STOP(0, ps);
-    collide_contacts(m, L, cs, gst + AVR_S_CP, rows);
+    collide_contacts(m, L, cs, gst + AVR_S_CP);
     PROF_STOP(13, ps);
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
