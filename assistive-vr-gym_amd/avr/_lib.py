@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get('AVR_LIB') or os.path.join(HERE, 'libavr.so')   # AVR_
 EXPORTS = [
     'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',
     'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
-    'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_state_words', 'avr_abi_version',
+    'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_env_groups', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table',
 ]
@@ -66,6 +66,8 @@ def load(path=LIB_PATH):
     lib.avr_state_device_ptr.argtypes = [vp]
     lib.avr_state_device_ptr.restype = vp
     lib.avr_n_envs.argtypes = [vp]
+    lib.avr_env_groups.argtypes = [vp]
+    lib.avr_env_groups.restype = C.c_int32
     lib.avr_state_words.restype = C.c_int32
     lib.avr_abi_version.restype = C.c_int32
     lib.avr_kernel_info.argtypes = [vp, vp]
@@ -175,6 +177,9 @@ class Sim:
 
     def stream(self):
         return self.lib.avr_stream(self.h)
+
+    def env_groups(self):
+        return int(self.lib.avr_env_groups(self.h))
 
 
 

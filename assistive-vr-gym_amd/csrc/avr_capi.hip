@@ -477,6 +477,7 @@ extern "C" const char *avr_last_error(avr_sim *s) { return s ? s->err : "null ha
 extern "C" void *avr_stream(avr_sim *s) { return s ? (void *)s->stream : nullptr; }
 extern "C" void *avr_state_device_ptr(avr_sim *s) { return s ? (void *)s->d_state : nullptr; }
 extern "C" int32_t avr_n_envs(avr_sim *s) { return s ? s->cfg.n_envs : 0; }
+extern "C" int32_t avr_env_groups(avr_sim *s) { return s ? s->ngroups : 0; }
 
 #define CHECK_SIM(s) \
     if (!(s) || !(s)->d_state) return -1

@@ -191,7 +191,8 @@ def main():
         'config': {'workload': 'FeedingJaco-v0, %d envs/GPU, rigid-only, random actions' % E, 'envs_per_gpu': E,
                    'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
                    'global_envs': world * E, 'substeps_per_env_step': 10, 'solver_iterations': 10,
-                   'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None},
+                   'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None,
+                   'env_groups': sim.env_groups()},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      # the HBM roofline is the bound the contract names; the kernels sit far below
@@ -199,7 +200,9 @@ def main():
                      'limiter': 'valu-issue/latency' if achieved / HBM_PEAK_GBS < 0.05 else 'hbm',
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
                      'scope': 'one env-step = 1 take_step + 10 x (substep_pairs, narrowphase, coop, substep_a, substep_b4) + 1 task launch; '
-                              'achieved = algorithmic bytes of the step / summed launch durations; '
+                              'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
+                              'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
+                              'sequences, so its stream time per step is below the summed durations; '
                               'traffic = PMC HBM bytes of the step (profiles/pmc_traffic.json), traffic_GBs = traffic / summed launch durations',
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(ABI),
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,

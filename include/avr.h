@@ -89,6 +89,10 @@ int avr_sync(avr_sim *sim);
 void *avr_stream(avr_sim *sim);
 void *avr_state_device_ptr(avr_sim *sim);
 int32_t avr_n_envs(avr_sim *sim);
+/* Env groups whose launch sequences run concurrently on separate streams inside each step call
+ * (one per 1024 envs, at most 4; AVR_ENV_GROUPS=1..8 in the environment at avr_create overrides).
+ * Results do not depend on it.  No reference counterpart (diagnostic). */
+int32_t avr_env_groups(avr_sim *sim);
 int32_t avr_state_words(void);
 int32_t avr_abi_version(void);
 /* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of each sub-step kernel, in
