@@ -845,13 +845,21 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
         if (dist - L.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
         int vi = nv++;
         epa_set_vert(L, vi, wv, sa, sb);
-        // visible faces die and leave the horizon edge list: one lane, serial (the order of the
-        // list, with its swap-with-last removals, is that of the CPU restatement)
+        // visible faces die and leave the horizon edge list.  A face's visibility depends on that
+        // face alone, so every lane tests one face; lane 0 then walks the visible faces in face
+        // order and edits the edge list serially (the order of the list, with its swap-with-last
+        // removals, is that of the CPU restatement)
         int ne = 0;
-        if (lane == 0) {
-            for (int f = 0; f < nf; f++) {
-                if (!L.eFi[f][3]) continue;
-                if (dot(ld3(L.eFn[f]), sub(wv, ld3(L.eW[L.eFi[f][0]]))) > 0.f) {
+        for (int base = 0; base < nf; base += 64) {
+            const int fl = base + lane;
+            bool vis = false;
+            if (fl < nf && L.eFi[fl][3]) vis = dot(ld3(L.eFn[fl]), sub(wv, ld3(L.eW[L.eFi[fl][0]]))) > 0.f;
+            unsigned long long vm = __ballot(vis);
+            if (lane != 0) continue;
+            while (vm) {
+                const int f = base + __ffsll((long long)vm) - 1;
+                vm &= vm - 1;
+                {
                     const int fi = L.eFi[f][0], fj = L.eFi[f][1], fk = L.eFi[f][2];
                     L.eFi[f][3] = 0;
                     const int e3[3][2] = {{fi, fj}, {fj, fk}, {fk, fi}};
@@ -1427,15 +1435,20 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                 if (lane == 0) L.prof[4] += run;
 #endif
                 k += run;
-            } else {                                // set up compound pair k (lane 0's record)
+            } else {                                // set up compound pair k (lane 0's record, loaded above)
                 gp = L.u.c.apair[k];
-                const int4 r0 = m.pair_rec[gp];
+                const int4 r0 = make_int4(__builtin_amdgcn_readfirstlane(rec.x), __builtin_amdgcn_readfirstlane(rec.y),
+                                          __builtin_amdgcn_readfirstlane(rec.z), __builtin_amdgcn_readfirstlane(rec.w));
                 const int ba = r0.x & 0xffff, bb = r0.x >> 16;
                 const int na = r0.y >> 16, nb = r0.z >> 16;
                 gsa0 = r0.y & 0xffff;
                 gsb0 = r0.z & 0xffff;
                 gbare = r0.w & 1;
-                gcull = !gbare && na * nb > 1;
+                // a single child against at most 64 (food against the spoon or bowl pieces): its
+                // items are tested directly, in one round, rather than after a culling round.
+                // The same set in the same order: child AABBs lie inside their bodies' fattened
+                // AABBs, so an overlapping child pair passes both body culls
+                gcull = !gbare && na * nb > 1 && !((na == 1 || nb == 1) && na * nb <= 64);
                 int ncA = na, ncB = nb;
                 if (gcull) {
                     const v3 bAmn = ld3(L.u.c.bmin[ba]), bAmx = ld3(L.u.c.bmax[ba]);
@@ -1530,11 +1543,9 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     // the previous contact pool in LDS (the manifold update reads and updates it in place) and
     // its keys (matching in the manifold update)
     const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
-    lds_f *ocp = (lds_f *)L.u.k.ocp;
-    const gfp gp = (gfp)gcp;
-    for (int i = lane; i < nold * AVR_CP_WORDS; i += 64) ocp[i] = gp[i];
+    lds_f *ocp = (lds_f *)L.u.k.ocp;      // (staged by load_a)
     for (int i = lane; i < nold; i += 64)
-        L.u.k.okey[i] = (int)gp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)gp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
+        L.u.k.okey[i] = (int)ocp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)ocp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
     if (lane == 0) L.flags |= __float_as_int(cs[CS_FLAGS]);
     __builtin_amdgcn_s_waitcnt(0);     // (every read of the old pool has returned before the new one overwrites it)
     SYNC();
@@ -1883,11 +1894,8 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
 AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows, const float *cs) {
     const int lane = lane_id();
     PROF_START(ps);
-    // body and link frames from the pair kernel
-    for (int i = lane; i < m.nb * 8; i += 64) (&L.btf[0][0])[i] = cs[CS_BTF + i];
-    for (int i = lane; i < L.nla * 8; i += 64) (&L.cm[0][0])[i] = cs[CS_CM + i];
-    for (int i = lane; i < L.nla * 4; i += 64) { (&L.ax[0][0])[i] = cs[CS_AX + i]; (&L.org[0][0])[i] = cs[CS_ORG + i]; }
-    SYNC();
+    // (the body and link frames from the pair kernel and the previous contact pool were staged
+    // by load_a)
     PROF_STOP(0, ps);
     collide_contacts(m, L, cs, gst + AVR_S_CP);
     PROF_STOP(13, ps);
@@ -2055,20 +2063,82 @@ AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env *
 
 AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[AVR_S_TASK + AVR_T_HDYN] != 0.f; }
 
+// Global -> LDS copies in two halves: g2r issues a lane's loads of words lane, lane + 64, ...
+// (NB of them, indices clamped into [0, n), so every load is unconditional), r2l stores them.  A
+// plain strided copy loop waits for each load before its store -- one memory round trip per 64
+// words -- where the loads of several g2r calls placed ahead of their r2l calls share one.
+template <int NB>
+AVR_DI void g2r(float (&t)[NB], const float *src, int n) {
+    const int lane = lane_id(), l = max(n - 1, 0);
+#pragma unroll
+    for (int q = 0; q < NB; q++) t[q] = src[min(lane + 64 * q, l)];
+}
+template <int NB>
+AVR_DI void r2l(float *dst, const float (&t)[NB], int n) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+        if (lane + 64 * q < n) dst[lane + 64 * q] = t[q];
+}
+#define NB_OF(words) (((words) + 63) / 64)
+
+template <class LT>
+AVR_DI void poison_lds(LT &L) {
+#ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the env's LDS block so that a read of a word this
+                        // kernel did not write shows up (tools/gpu_poison.sh)
+    for (int i = lane_id(); i < (int)(sizeof(LT) / 4); i += 64) ((float *)&L)[i] = __int_as_float(-1);
+    SYNC();
+#else
+    (void)L;
+#endif
+}
+
 template <class LT>
 AVR_DI void load_state(const KModel &m, LT &L, const float *gst) {
     const int lane = lane_id();
-#ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the env's LDS block so that a read of a word this
-                        // kernel did not write shows up (tools/gpu_poison.sh)
-    for (int i = lane; i < (int)(sizeof(LT) / 4); i += 64) ((float *)&L)[i] = __int_as_float(-1);
-    SYNC();
-#endif
-    for (int i = lane; i < AVR_S_CP; i += 64) L.st[i] = gst[i];
+    poison_lds(L);
+    float ts[NB_OF(AVR_S_CP)];
+    g2r(ts, gst, AVR_S_CP);
+    r2l(L.st, ts, AVR_S_CP);
     if (lane == 0) {
         L.flags = 0;
         L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER];
         const bool hd = env_hdyn(m, gst);
         L.nla = hd ? m.nla : m.nl;
+        L.nda = hd ? m.nd + m.hc_n : m.nd;
+    }
+#ifdef AVR_PROF
+    if (lane < AVR_PROF_SLOTS) L.prof[lane] = 0;
+#endif
+    SYNC();
+}
+
+// kernel a's inputs -- the state words, the pair kernel's body and link frames, the previous
+// contact pool -- with every load in flight before the first LDS store
+AVR_DI void load_a(const KModel &m, EnvLDS &L, const float *gst, const float *cs) {
+    const int lane = lane_id();
+    poison_lds(L);
+    const int nold = (int)gst[AVR_S_TASK + AVR_T_NCP];
+    const bool hd = env_hdyn(m, gst);
+    const int nla = hd ? m.nla : m.nl;
+    float ts[NB_OF(AVR_S_CP)], tb[NB_OF(MAXB * 8)], tc[NB_OF(MAXL * 8)], tx[NB_OF(MAXL * 4)], to[NB_OF(MAXL * 4)];
+    float tp[NB_OF(AVR_MAX_CONTACTS * AVR_CP_WORDS)];
+    g2r(ts, gst, AVR_S_CP);
+    g2r(tb, cs + CS_BTF, m.nb * 8);
+    g2r(tc, cs + CS_CM, nla * 8);
+    g2r(tx, cs + CS_AX, nla * 4);
+    g2r(to, cs + CS_ORG, nla * 4);
+    g2r(tp, gst + AVR_S_CP, nold * AVR_CP_WORDS);
+    r2l(L.st, ts, AVR_S_CP);
+    r2l(&L.btf[0][0], tb, m.nb * 8);
+    r2l(&L.cm[0][0], tc, nla * 8);
+    r2l(&L.ax[0][0], tx, nla * 4);
+    r2l(&L.org[0][0], to, nla * 4);
+    r2l(L.u.k.ocp, tp, nold * AVR_CP_WORDS);
+    if (lane == 0) {
+        L.flags = 0;
+        L.gender = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+        L.nla = nla;
         L.nda = hd ? m.nd + m.hc_n : m.nd;
     }
 #ifdef AVR_PROF
@@ -2456,7 +2526,14 @@ __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__
     const KModel &m = *mp;
     __shared__ EpaBuf E;        // the EPA polytope in LDS (9.5 KB; this kernel has no other LDS)
     float *cs = env_cs(m, env);
+#ifdef AVR_WAVETIME   // [4][env] (start, end) in 100 MHz ticks
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     np_coop(m, cs, __float_as_int(cs[CS_NSP]), E);
+#ifdef AVR_WAVETIME
+    const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
+    if (m.prof && lane_id() == 0) { m.prof[((size_t)4 * n_envs + env) * 2] = wt0; m.prof[((size_t)4 * n_envs + env) * 2 + 1] = wt1; }
+#endif
 }
 
 // Sub-step part A3: one 64-lane block per env, state staged in LDS -- manifold update,
@@ -2467,7 +2544,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     AVR_ENV_GUARD();
     WT_START();
     float *gst = state + (size_t)env * AVR_STATE_WORDS;
-    load_state(m, L, gst);
+    load_a(m, L, gst, env_cs(m, env));
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
 #ifdef AVR_PROF
     if (lane_id() == 0) env_ws(m, env)[WS_XCC] = __int_as_float(xcc_id());
@@ -2836,11 +2913,15 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
     const int cw = base + szA, rw = cw + 3 * n_c * CRW;
     // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
-    // warm-start factor; null slots 0
+    // warm-start factor; null slots 0.  The cached impulses are loaded here and stored after the
+    // staging loads below have been issued (one memory round trip for both).
     const gfp cpool = (gfp)(st + AVR_S_CP);
+    float wimp[AVR_MAX_CONTACTS / 16];
+#pragma unroll
+    for (int q = 0; q < AVR_MAX_CONTACTS / 16; q++) wimp[q] = cpool[AVR_CP_WORDS * min(sl + 16 * q, max(n_c - 1, 0)) + AVR_CP_IMP];
     for (int r = sl; r < n_rows + 2; r += 16) {
         const int c = r - n_nc;
-        imp[r] = c >= 0 && c < n_c ? cpool[AVR_CP_WORDS * c + AVR_CP_IMP] * m.warmstart : 0.f;
+        if (!(c >= 0 && c < n_c)) imp[r] = 0.f;
     }
     if (lane < LN_HEAD) blk[lane] = 0.f;        // null rows, zero parts
     if (in_lds) {   // contact records and robot-contact parts, 8 loads in flight per lane
@@ -2861,6 +2942,9 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
             }
         }
     }
+#pragma unroll
+    for (int q = 0; q < AVR_MAX_CONTACTS / 16; q++)
+        if (sl + 16 * q < n_c) imp[n_nc + sl + 16 * q] = wimp[q] * m.warmstart;
     __syncthreads();
     // impulse slots: rows 0 .. n_rows - 1 (non-contact, normal, friction pairs), then 2 null slots
     lds_f *const ipn = imp + n_nc, *const ipf = ipn + n_c, *const nullip = imp + n_rows;

@@ -16,12 +16,12 @@ A = ABI.load_scene(); md = ABI.ModelDesc(A)
 S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
 S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
 sim = _lib.Sim(md, N)
-buf = torch.zeros(4 * N * 2, dtype=torch.int64, device='cuda')
+buf = torch.zeros(5 * N * 2, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, buf.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(20)
 for t in range(3):
     sim.step(_lib.random_actions(1001, np.arange(N), t))
-    raw = buf.cpu().numpy().reshape(4, N, 2)
+    raw = buf.cpu().numpy().reshape(5, N, 2)
     p = raw[:2].astype(np.float64) * 10.0   # 100 MHz ticks -> ns
     for k, nm in enumerate(('A', 'B')):
         sel = p[k, :, 0] > 0        # B: one record per block (its group-0 env)
@@ -47,6 +47,10 @@ for t in range(3):
     npd = raw[3].astype(np.float64) * 10.0 / 1e3
     print('   NP block us: list0 mean %.1f p90 %.1f max %.1f; list1 mean %.1f p90 %.1f max %.1f'
           % (npd[:, 0].mean(), np.percentile(npd[:, 0], 90), npd[:, 0].max(), npd[:, 1].mean(), np.percentile(npd[:, 1], 90), npd[:, 1].max()))
+    cp = raw[4].astype(np.float64) * 10.0 / 1e3
+    cd = cp[:, 1] - cp[:, 0]
+    print('   coop block us: span %.1f, starts spread %.1f, duration mean %.2f p99 %.1f max %.1f, blocks > 3 us: %d'
+          % (cp[:, 1].max() - cp[:, 0].min(), cp[:, 0].max() - cp[:, 0].min(), cd.mean(), np.percentile(cd, 99), cd.max(), int((cd > 3).sum())))
     St = sim.get_state()
 ncp = St[:, ABI.S_TASK + ABI.T_NCP]
 print('ncp of slowest A envs', ncp[order[:6]], 'mean ncp', ncp.mean())
