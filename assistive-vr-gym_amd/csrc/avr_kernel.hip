@@ -33,6 +33,17 @@
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) float lds_f;
+// Model and scratch arrays live in global memory, but a pointer loaded from the KModel is generic
+// to the compiler: its loads become flat loads, whose waits also drain every LDS access in
+// flight.  Hot reads name the address space (gld: global; the model arrays are never written).
+#define AVR_GA __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ T gld(const T *p) { return *(const AVR_GA T *)p; }
+__device__ __forceinline__ int2 gld(const int2 *p) { const AVR_GA int *q = (const AVR_GA int *)p; return make_int2(q[0], q[1]); }
+__device__ __forceinline__ float2 gld(const float2 *p) { const f2v x = *(const AVR_GA f2v *)p; return make_float2(x.x, x.y); }
+__device__ __forceinline__ float4 gld(const float4 *p) { const f4v x = *(const AVR_GA f4v *)p; return make_float4(x.x, x.y, x.z, x.w); }
+__device__ __forceinline__ v3 gld3(const float *p) { const AVR_GA float *q = (const AVR_GA float *)p; return V(q[0], q[1], q[2]); }
+__device__ __forceinline__ qt gldq(const float *p) { const AVR_GA float *q = (const AVR_GA float *)p; return Q(q[0], q[1], q[2], q[3]); }
+__device__ __forceinline__ tf gldtf(const float *p) { tf r; r.p = gld3(p); r.q = gldq(p + 3); return r; }
 typedef __attribute__((address_space(3))) f2v lds_f2;
 typedef __attribute__((address_space(3))) f4v lds_f4;
 typedef __attribute__((address_space(3))) int lds_i;
@@ -137,12 +148,12 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     // axis, joint type), overwritten by the results once every lane has composed its chain
     if (mine) {
         const int go = lgo(L, m);
-        const int jt = m.rl_jtype[i];
-        am = m.anc_mask[i];
-        const tf jo = ldtf(m.rl_jorig + 8 * (go + i));
-        com = ldtf(m.rl_com + 8 * (go + i));
-        axl = ld3(m.rl_axis + 4 * i);
-        const int dof = m.rl_dof[i];
+        const int jt = gld(m.rl_jtype + (i));
+        am = gld(m.anc_mask + (i));
+        const tf jo = gldtf(m.rl_jorig + 8 * (go + i));
+        com = gldtf(m.rl_com + 8 * (go + i));
+        axl = gld3(m.rl_axis + 4 * i);
+        const int dof = gld(m.rl_dof + (i));
         const float qv = dof >= 0 ? L.st[AVR_S_Q + dof] : 0.f;
         const qt qj = jt == AVR_J_REVOLUTE ? qaxis(axl, qv) : Q(0, 0, 0, 1);
         sttf(L.lk[i], jo);
@@ -156,7 +167,7 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     v3 org = V(0, 0, 0), axw = V(0, 0, 0);
     if (mine) {
         const int r = __builtin_ctz(am);                       // the chain's root link
-        t = m.rl_parent[r] == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : ldtf(m.base);
+        t = gld(m.rl_parent + (r)) == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : gldtf(m.base);
         for (unsigned b = am; b; b &= b - 1u) {
             const int k = __builtin_ctz(b);
             const tf jo = ldtf(L.lk[k]);
@@ -181,7 +192,7 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     SYNC();
     const int c = i - m.nl;
     if (mine && c >= 0) {
-        const int slot = m.hc_slot[c];
+        const int slot = gld(m.hc_slot + (c));
         if (slot >= 0) {
             float *h = L.st + AVR_S_HUMAN + 7 * slot;
             st3(h, ld3(L.cm[i]));
@@ -191,11 +202,11 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     SYNC();
 }
 
-AVR_DI bool is_ancestor(const KModel &m, int link, int anc) { return (m.anc_mask[link] >> anc) & 1u; }
+AVR_DI bool is_ancestor(const KModel &m, int link, int anc) { return (gld(m.anc_mask + (link)) >> anc) & 1u; }
 
 AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &ang) {
     v3 a = ld3(L.ax[j]);
-    if (m.rl_jtype[j] == AVR_J_REVOLUTE) {
+    if (gld(m.rl_jtype + (j)) == AVR_J_REVOLUTE) {
         ang = a;
         lin = crs(a, sub(p, ld3(L.org[j])));
     } else {
@@ -215,13 +226,13 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
     const int lane = lane_id();
     if (lane < L.nla) {   // world inertia R diag(I) R^T and mass of link `lane`
         const m3 R = qmat(ldq(L.cm[lane] + 3));
-        const v3 I = ld3(m.rl_inertia + 4 * (go + lane));
+        const v3 I = gld3(m.rl_inertia + 4 * (go + lane));
         float *w = L.u.d.iw[lane];
 #define AVR_IW(a, b) (R.m[a][0] * R.m[b][0] * I.x + R.m[a][1] * R.m[b][1] * I.y + R.m[a][2] * R.m[b][2] * I.z)
         w[0] = AVR_IW(0, 0); w[1] = AVR_IW(1, 1); w[2] = AVR_IW(2, 2);
         w[3] = AVR_IW(0, 1); w[4] = AVR_IW(0, 2); w[5] = AVR_IW(1, 2);
 #undef AVR_IW
-        w[6] = m.rl_mass[go + lane];
+        w[6] = gld(m.rl_mass + (go + lane));
     }
     SYNC();
     const int ne = MAXD * (MAXD + 1) / 2;
@@ -231,11 +242,11 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         int b = rem;
         float s = 0.f;
         if (a < nd && b < nd) {
-            const int la = m.dof_link[a], lb = m.dof_link[b];
+            const int la = gld(m.dof_link + (a)), lb = gld(m.dof_link + (b));
             const v3 axa = ld3(L.ax[la]), oa = ld3(L.org[la]), axb = ld3(L.ax[lb]), ob = ld3(L.org[lb]);
-            const bool ra = m.rl_jtype[la] == AVR_J_REVOLUTE, rb = m.rl_jtype[lb] == AVR_J_REVOLUTE;
+            const bool ra = gld(m.rl_jtype + (la)) == AVR_J_REVOLUTE, rb = gld(m.rl_jtype + (lb)) == AVR_J_REVOLUTE;
             // links in both subtrees, ascending (a per-lane bit loop: no scalar load per link)
-            for (unsigned dm = m.desc_mask[la] & m.desc_mask[lb]; dm; dm &= dm - 1u) {
+            for (unsigned dm = gld(m.desc_mask + (la)) & gld(m.desc_mask + (lb)); dm; dm &= dm - 1u) {
                 const int i = __builtin_ctz(dm);
                 const float *w = L.u.d.iw[i];
                 const float mi = w[6];
@@ -367,19 +378,19 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
     qt q = Q(0, 0, 0, 1);
     if (mine) {
         const int go = lgo(L, m);
-        p = m.rl_parent[i];          // < 0: fixed robot base or (-2) the static chest slot
-        jt = m.rl_jtype[i];
-        am = m.anc_mask[i];
-        const int dof = m.rl_dof[i];
+        p = gld(m.rl_parent + (i));          // < 0: fixed robot base or (-2) the static chest slot
+        jt = gld(m.rl_jtype + (i));
+        am = gld(m.anc_mask + (i));
+        const int dof = gld(m.rl_dof + (i));
         qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
         o = ld3(L.org[i]); c = ld3(L.cm[i]); axw = ld3(L.ax[i]);
         q = ldq(L.cm[i] + 3);
-        mi = m.rl_mass[go + i];
-        I = ld3(m.rl_inertia + 4 * (go + i));
+        mi = gld(m.rl_mass + (go + i));
+        I = gld3(m.rl_inertia + 4 * (go + i));
     }
     const bool rev = jt == AVR_J_REVOLUTE, pri = jt == AVR_J_PRISMATIC;
     const v3 wj = rev ? scl(axw, qd) : V(0, 0, 0), vj = pri ? scl(axw, qd) : V(0, 0, 0);
-    const v3 cp = p < 0 ? ld3(m.base) : ld3(L.cm[p > 0 ? p : 0]);
+    const v3 cp = p < 0 ? gld3(m.base) : ld3(L.cm[p > 0 ? p : 0]);
     const v3 rpo = sub(o, cp), roc = sub(c, o);
     // pass 1: angular velocities
     if (mine) st3(R1[i], wj);
@@ -421,11 +432,11 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
     if (i < MAXD) {
         float h = 0.f;
         if (i < L.nda) {
-            const int j = m.dof_link[i];
+            const int j = gld(m.dof_link + (i));
             const v3 aj = ld3(L.ax[j]), oj = ld3(L.org[j]);
-            const bool rj = m.rl_jtype[j] == AVR_J_REVOLUTE;
+            const bool rj = gld(m.rl_jtype + (j)) == AVR_J_REVOLUTE;
             v3 acc = V(0, 0, 0);
-            for (unsigned dm = m.desc_mask[j]; dm; dm &= dm - 1u) {     // the subtree of j, ascending
+            for (unsigned dm = gld(m.desc_mask + (j)); dm; dm &= dm - 1u) {     // the subtree of j, ascending
                 const int k = __builtin_ctz(dm);
                 const v3 F = ld3(R1[k]);
                 acc = add(acc, rj ? add(ld3(R5[k]), crs(sub(ld3(L.cm[k]), oj), F)) : F);
@@ -447,16 +458,16 @@ struct WShape {
 
 AVR_DI WShape make_wshape(const KModel &m, int s, tf body) {
     WShape w;
-    w.kind = m.shape_kind[s];
-    w.t = tfmul(body, ldtf(m.shape_pose + 8 * s));
-    w.margin = m.shape_margin[s];
-    const float *pa = m.shape_param + 4 * s;
-    if (w.kind == AVR_BOX) w.he = V(fmaxf(pa[0] - w.margin, 0.f), fmaxf(pa[1] - w.margin, 0.f), fmaxf(pa[2] - w.margin, 0.f));
-    else if (w.kind == AVR_CAPSULE) w.he = V(pa[0], pa[1], 0.f);
-    else w.he = V(pa[0], 0.f, 0.f);
-    w.vs = m.shape_hull[4 * s + 0];
-    w.nv = w.kind == AVR_HULL ? m.shape_hull[4 * s + 1] : 0;
-    w.tab = w.kind == AVR_HULL ? m.shape_tab[s] : -1;
+    w.kind = gld(m.shape_kind + (s));
+    w.t = tfmul(body, gldtf(m.shape_pose + 8 * s));
+    w.margin = gld(m.shape_margin + (s));
+    const v3 pa = gld3(m.shape_param + 4 * s);
+    if (w.kind == AVR_BOX) w.he = V(fmaxf(pa.x - w.margin, 0.f), fmaxf(pa.y - w.margin, 0.f), fmaxf(pa.z - w.margin, 0.f));
+    else if (w.kind == AVR_CAPSULE) w.he = V(pa.x, pa.y, 0.f);
+    else w.he = V(pa.x, 0.f, 0.f);
+    w.vs = gld(m.shape_hull + (4 * s + 0));
+    w.nv = w.kind == AVR_HULL ? gld(m.shape_hull + (4 * s + 1)) : 0;
+    w.tab = w.kind == AVR_HULL ? gld(m.shape_tab + (s)) : -1;
     return w;
 }
 
@@ -498,7 +509,7 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
             const float sc = 0.5f * (float)AVR_TAB_G / mx;
             const int i = min(AVR_TAB_G - 1, max(0, (int)((u + mx) * sc)));
             const int j = min(AVR_TAB_G - 1, max(0, (int)((w + mx) * sc)));
-            const int2 oc = m.tab_cell[s.tab + (f * AVR_TAB_G + i) * AVR_TAB_G + j];
+            const int2 oc = gld(m.tab_cell + (s.tab + (f * AVR_TAB_G + i) * AVR_TAB_G + j));
             // batches of 4 candidates in flight; a short last batch re-reads the last candidate,
             // which cannot displace an earlier winner under the strict ">" (exact)
             float best = -BIGF;
@@ -561,6 +572,54 @@ AVR_DI v3 support(const KModel &m, const WShape &s, v3 d) {
         }
     }
     return tfpt(s.t, r);
+}
+
+// cube-map cell of a table hull for the local direction l (support(): mx > 0)
+AVR_DI int2 tab_cell_of(const KModel &m, int tab, v3 l, float mx) {
+    const float ax = fabsf(l.x), ay = fabsf(l.y), az = fabsf(l.z);
+    int f;
+    float u, w;
+    if (ax >= ay && ax >= az) { f = l.x < 0.f; u = l.y; w = l.z; }
+    else if (ay >= az) { f = 2 + (l.y < 0.f); u = l.x; w = l.z; }
+    else { f = 4 + (l.z < 0.f); u = l.x; w = l.y; }
+    const float sc = 0.5f * (float)AVR_TAB_G / mx;
+    const int i = min(AVR_TAB_G - 1, max(0, (int)((u + mx) * sc)));
+    const int j = min(AVR_TAB_G - 1, max(0, (int)((w + mx) * sc)));
+    return gld(m.tab_cell + (tab + (f * AVR_TAB_G + i) * AVR_TAB_G + j));
+}
+
+// support(A, da) and support(B, db) together: when both are table hulls, the two cell lookups
+// and then the two candidate scans are issued side by side (two dependent round trips instead of
+// four).  Exactly support()'s results: the same candidates, the same strict ">" in ascending
+// order, and a scan past a list's end re-reads its last candidate, which cannot displace a winner.
+template <bool COOP>
+AVR_DI void support2(const KModel &m, const WShape &A, v3 da, const WShape &B, v3 db, v3 &ra, v3 &rb) {
+    const v3 la = qrot(qconj(A.t.q), da), lb = qrot(qconj(B.t.q), db);
+    const float mxa = fmaxf(fabsf(la.x), fmaxf(fabsf(la.y), fabsf(la.z))), mxb = fmaxf(fabsf(lb.x), fmaxf(fabsf(lb.y), fabsf(lb.z)));
+    if (!(A.tab >= 0 && B.tab >= 0 && mxa > 0.f && mxb > 0.f)) {
+        ra = support<COOP>(m, A, da);
+        rb = support<COOP>(m, B, db);
+        return;
+    }
+    const GlobalF4 tv{m.tab_vert};
+    const int2 ca = tab_cell_of(m, A.tab, la, mxa), cb = tab_cell_of(m, B.tab, lb, mxb);
+    float besta = -BIGF, bestb = -BIGF;
+    float4 bva = tv[ca.x], bvb = tv[cb.x];
+    const int lasta = ca.x + ca.y - 1, lastb = cb.x + cb.y - 1, n = max(ca.y, cb.y);
+    for (int k = 0; k < n; k += 4) {
+        float4 va[4], vb[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) { va[q] = tv[min(ca.x + k + q, lasta)]; vb[q] = tv[min(cb.x + k + q, lastb)]; }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float d1 = la.x * va[q].x + la.y * va[q].y + la.z * va[q].z;
+            if (d1 > besta) { besta = d1; bva = va[q]; }
+            const float d2 = lb.x * vb[q].x + lb.y * vb[q].y + lb.z * vb[q].z;
+            if (d2 > bestb) { bestb = d2; bvb = vb[q]; }
+        }
+    }
+    ra = tfpt(A.t, V(bva.x, bva.y, bva.z));
+    rb = tfpt(B.t, V(bvb.x, bvb.y, bvb.z));
 }
 
 // --------------------------------------------------------------------------- GJK
@@ -716,7 +775,9 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     bool converged = false;
     for (int it = 0; it < max_it; it++) {
         nit = it + 1;
-        v3 sa = support<COOP, GJK_NB>(m, A, scl(v, -1.f)), sb = support<COOP, GJK_NB>(m, B, v);
+        v3 sa, sb;
+        if constexpr (COOP) support2<true>(m, A, scl(v, -1.f), B, v, sa, sb);
+        else { sa = support<COOP, GJK_NB>(m, A, scl(v, -1.f)); sb = support<COOP, GJK_NB>(m, B, v); }
         v3 wv = sub(sa, sb);
         float vv = len2(v), vw = dot(v, wv);
         if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
@@ -801,7 +862,8 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
             if (di & 1) d = scl(d, -1.f);
             if (len2(d) < 1e-24f) continue;
         }
-        v3 sa = support<true>(m, A, d), sb = support<true>(m, B, scl(d, -1.f));
+        v3 sa, sb;
+        support2<true>(m, A, d, B, scl(d, -1.f), sa, sb);
         v3 wv = sub(sa, sb);
         bool dup = false;
         for (int k = 0; k < nv; k++)
@@ -839,7 +901,8 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
         best = bf == 0x7fffffff ? -1 : bf;
         if (best < 0) return -1;
         v3 n = ld3(L.eFn[best]);
-        v3 sa = support<true>(m, A, n), sb = support<true>(m, B, scl(n, -1.f));
+        v3 sa, sb;
+        support2<true>(m, A, n, B, scl(n, -1.f), sa, sb);
         v3 wv = sub(sa, sb);
         float dist = dot(wv, n);
         if (dist - L.eFn[best][3] < EPA_EPS || nv >= EPA_MAX_V) break;
@@ -1050,10 +1113,10 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
 // --------------------------------------------------------------------------- bodies
 template <class LT>
 AVR_DI tf body_tf(const KModel &m, const LT &L, int b) {
-    int kind = m.body_kind[b], idx = m.body_index[b];
+    int kind = gld(m.body_kind + (b)), idx = gld(m.body_index + (b));
     if (kind == AVR_BODY_ROBOT) return ldtf(L.cm[idx]);
     if (kind == AVR_BODY_FREE) return ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * idx);
-    if (kind == AVR_BODY_STATIC) return ldtf(m.st_pose + 8 * idx);
+    if (kind == AVR_BODY_STATIC) return gldtf(m.st_pose + 8 * idx);
     return ldtf(L.st + AVR_S_HUMAN + 7 * idx);
 }
 
@@ -1072,7 +1135,7 @@ AVR_DI bool overlap(v3 a0, v3 a1, v3 b0, v3 b1) {
 }
 
 AVR_DI void shape_aabb(const KModel &m, int s, tf body, v3 &mn, v3 &mx) {
-    tf t = tfmul(body, ldtf(m.shape_pose + 8 * s));
+    tf t = tfmul(body, gldtf(m.shape_pose + 8 * s));
     const float *a = m.shape_aabb + 8 * s;
     aabb_of(t, ld3(a), ld3(a + 4), mn, mx);
 }
@@ -1235,24 +1298,31 @@ AVR_DI bool sphere_hull(int ia, int ib) {
 
 // manifold update for the nq (<= 64) shape pairs k0 .. k0 + nq - 1 of the list, lane q <-> pair
 // k0 + q, from the narrowphase results of avr_narrowphase_kernel
-AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew) {
+// one lane's shape pair k (clamped into the list) and its narrowphase result, loaded a batch
+// ahead of its use so that the loads overlap the previous batch's pool stores
+struct PairIn { float2 kw; float4 r0, r1; };
+AVR_DI void pair_in(const float *cs, int k, int nsp, PairIn &P) {
+    k = min(k, max(nsp - 1, 0));
+    P.kw = gld((const float2 *)(cs + CS_PAIRS) + k);
+    P.r0 = gld((const float4 *)(cs + CS_RES) + 2 * k);
+    P.r1 = gld((const float4 *)(cs + CS_RES) + 2 * k + 1);
+}
+
+AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const PairIn &in, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew) {
     const int lane = lane_id();
     PROF_START(pb);
-    int sa = 0, sb = 0, p = 0;
+    int sa = 0, sb = 0, p = 0, ba = 0, bb = 0;
     int rc = 0;
     v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
     float d = 0.f;
-    bool coop = false;
     if (lane < nq) {
-        const int k = __float_as_int(cs[CS_PAIRS + 2 * (k0 + lane)]);
+        const int k = __float_as_int(in.kw.x);
         sa = k & 0xffff; sb = k >> 16;
-        p = __float_as_int(cs[CS_PAIRS + 2 * (k0 + lane) + 1]);
-        const float4 r0 = ((const float4 *)(cs + CS_RES))[2 * (k0 + lane)], r1 = ((const float4 *)(cs + CS_RES))[2 * (k0 + lane) + 1];
-        rc = __float_as_int(r0.x);
-        nB = V(r0.y, r0.z, r0.w); pB = V(r1.x, r1.y, r1.z); d = r1.w;
-        coop = rc == 2;
+        const int w = __float_as_int(in.kw.y);     // body pair | ba << 16 | bb << 24
+        p = w & 0xffff; ba = (w >> 16) & 0xff; bb = (w >> 24) & 0xff;
+        rc = __float_as_int(in.r0.x);   // (0 or 1: the narrowphase and coop kernels finished every pair)
+        nB = V(in.r0.y, in.r0.z, in.r0.w); pB = V(in.r1.x, in.r1.y, in.r1.z); d = in.r1.w;
     }
-    (void)coop;     // (the narrowphase kernel finished every pair: rc is 0 or 1)
     PROF_STOP(17, pb);
 
     // manifold update (one lane per pair)
@@ -1262,8 +1332,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const float *cs, int k0, i
 #pragma unroll
     for (int k = 0; k < AVR_CP_WORDS; k++) nw.p[k] = 0.f;
     if (lane < nq) {
-        int ba = m.shape_body[sa], bb = m.shape_body[sb];
-        float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+        float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
         const int key = sa | (sb << 16);
         const lds_i *ok = (const lds_i *)L.u.k.okey;
         for (int i = 0; i < nold; i++)      // (no early exit: the key reads stay independent)
@@ -1319,7 +1388,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     if (lane < m.nb) {
         const int b = lane;
         tf t = body_tf(m, L, b);
-        int g = m.body_kind[b] == AVR_BODY_HUMAN ? gender : 0;
+        int g = gld(m.body_kind + (b)) == AVR_BODY_HUMAN ? gender : 0;
         const float *a = m.body_aabb + 12 * b + 6 * g;
         v3 mn, mx;
         aabb_of(t, ld3(a), ld3(a + 3), mn, mx);
@@ -1337,10 +1406,10 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     SYNC();
     // world AABBs of the non-static child shapes
     for (int s = lane; s < m.ns; s += 64) {
-        const int c = m.shape_cidx[s];
+        const int c = gld(m.shape_cidx + (s));
         if (c >= 0) {
             v3 mn, mx;
-            shape_aabb(m, s, ldtf(L.btf[m.shape_body[s]]), mn, mx);
+            shape_aabb(m, s, ldtf(L.btf[gld(m.shape_body + (s))]), mn, mx);
             st3(L.u.c.caabb[c], mn);
             st3(L.u.c.caabb[c] + 3, mx);
         }
@@ -1352,7 +1421,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
         int p = base + lane;
         bool act = false;
         if (p < npe) {
-            int ba = m.pair_a[p], bb = m.pair_b[p];
+            int ba = gld(m.pair_a + (p)), bb = gld(m.pair_b + (p));
             act = overlap(ld3(L.u.c.bmin[ba]), ld3(L.u.c.bmax[ba]), ld3(L.u.c.bmin[bb]), ld3(L.u.c.bmax[bb]));
         }
         int tot;
@@ -1376,9 +1445,10 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     bool gcull = false, gbare = false;
     float grcpB = 1.f;
     int n0 = 0, n1 = 0;                             // sphere-hull / other pairs
+    int gbab = 0;                                   // the compound pair's bodies (ba | bb << 8)
     for (;;) {
         bool act = false, last = false;
-        int sa = 0, sb = 0, q = gp, ia = 0, ib = 0;
+        int sa = 0, sb = 0, q = gp, ia = 0, ib = 0, bab = gbab;
         if (gbase < gn) {                           // the compound pair in progress
             const int it = gbase + lane;
             if (it < gn) {
@@ -1420,6 +1490,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                     q = L.u.c.apair[kk];
                     sa = rec.y & 0xffff;
                     sb = rec.z & 0xffff;
+                    bab = (rec.x & 0xffff) | (rec.x >> 16) << 8;
                     ia = L.sinfo[sa]; ib = L.sinfo[sb];
                     if (info_enabled(ia, gender) && info_enabled(ib, gender)) {
                         if (rec.w & 1) act = true;
@@ -1440,6 +1511,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                 const int4 r0 = make_int4(__builtin_amdgcn_readfirstlane(rec.x), __builtin_amdgcn_readfirstlane(rec.y),
                                           __builtin_amdgcn_readfirstlane(rec.z), __builtin_amdgcn_readfirstlane(rec.w));
                 const int ba = r0.x & 0xffff, bb = r0.x >> 16;
+                gbab = ba | bb << 8;
                 const int na = r0.y >> 16, nb = r0.z >> 16;
                 gsa0 = r0.y & 0xffff;
                 gsb0 = r0.z & 0xffff;
@@ -1508,14 +1580,17 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
         const bool ok = act && kq < MAXSP;
         if (ok) {
             cs[CS_PAIRS + 2 * kq] = __int_as_float(sa | (sb << 16));
-            cs[CS_PAIRS + 2 * kq + 1] = __int_as_float(q);
+            cs[CS_PAIRS + 2 * kq + 1] = __int_as_float(q | bab << 16);
         }
         // the narrowphase kernel's two work lists (pair indices, ascending)
         const bool sh = ok && sphere_hull(ia, ib);
         int t0, t1;
         const int p0 = ballot_prefix(sh, &t0), p1 = ballot_prefix(ok && !sh, &t1);
-        if (sh) cs[CS_L0 + n0 + p0] = __int_as_float(kq);
-        else if (ok) cs[CS_L1 + n1 + p1] = __int_as_float(kq);
+        // (entries carry the shape and body indices, so the narrowphase reads no pair record)
+        if (ok) {
+            const int l = sh ? CS_L0 + 2 * (n0 + p0) : CS_L1 + 2 * (n1 + p1);
+            *(float2 *)(cs + l) = make_float2(__int_as_float(kq | bab << 16), __int_as_float(sa | (sb << 16)));
+        }
         n0 += t0;
         n1 += t1;
         nsp += tot;
@@ -1546,14 +1621,18 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     lds_f *ocp = (lds_f *)L.u.k.ocp;      // (staged by load_a)
     for (int i = lane; i < nold; i += 64)
         L.u.k.okey[i] = (int)ocp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)ocp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
-    if (lane == 0) L.flags |= __float_as_int(cs[CS_FLAGS]);
+    if (lane == 0) L.flags |= __float_as_int(gld(cs + CS_FLAGS));
     __builtin_amdgcn_s_waitcnt(0);     // (every read of the old pool has returned before the new one overwrites it)
     SYNC();
-    const int nsp = __float_as_int(cs[CS_NSP]);
+    const int nsp = __float_as_int(gld(cs + CS_NSP));
     int nnew = 0;
+    PairIn cur, nxt;
+    pair_in(cs, lane, nsp, cur);
     for (int k0 = 0; k0 < nsp; k0 += 64) {
-        collide_batch(m, L, cs, k0, min(64, nsp - k0), ocp, nold, newcp, nnew);
+        pair_in(cs, k0 + 64 + lane, nsp, nxt);
+        collide_batch(m, L, cur, k0, min(64, nsp - k0), ocp, nold, newcp, nnew);
         SYNC();
+        cur = nxt;
     }
     if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
     SYNC();
@@ -1564,12 +1643,12 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
 
 // --------------------------------------------------------------------------- constraint rows
 AVR_DI void robot_jac(const KModel &m, const EnvLDS &L, int link, v3 p, v3 lin, v3 ang, float *J) {
-    const unsigned am = m.anc_mask[link];
+    const unsigned am = gld(m.anc_mask + (link));
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
         float v = 0.f;
         if (d < m.nd + m.hc_n) {           // chain DoFs are never ancestors of a robot link
-            int k = m.dof_link[d];
+            int k = gld(m.dof_link + (d));
             if ((am >> k) & 1u) {
                 v3 cl, ca;
                 dof_col(m, L, k, p, cl, ca);
@@ -1667,13 +1746,13 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     {
         float (*desc)[4] = L.u.d.rn[0];        // [MAXNC] (kind, dof, pen); the RNEA temporaries are dead
         const bool lk = lane < L.nla;
-        const int ld = lk ? m.rl_dof[lane] : -1;
-        const bool hl = lk && m.rl_has_limit[lane];
+        const int ld = lk ? gld(m.rl_dof + (lane)) : -1;
+        const bool hl = lk && gld(m.rl_has_limit + (lane));
         float plo = 1.f, phi = 1.f;
         if (hl) {
             const float q = L.st[AVR_S_Q + ld];
-            plo = q - m.rl_lower[lane];
-            phi = m.rl_upper[lane] - q;
+            plo = q - gld(m.rl_lower + (lane));
+            phi = gld(m.rl_upper + (lane)) - q;
         }
         const bool vlo = hl && !(plo > 0.f), vhi = hl && !(phi > 0.f), mot = ld >= 0;
         const unsigned long long blo = __ballot(vlo), bhi = __ballot(vhi), bmo = __ballot(mot), lt = (1ull << lane) - 1ull;
@@ -1695,7 +1774,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     // fixed constraint robot tool link <-> spoon (uniform geometry)
     const int link = m.tool_link, fb = m.spoon_free;
     const tf ta = ldtf(L.cm[link]);
-    const tf off = ldtf(m.tool_offset);
+    const tf off = gldtf(m.tool_offset);
     const v3 pivA = tfpt(ta, off.p);
     const qt frA = qmul(ta.q, off.q);
     const tf tb = ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * fb);
@@ -1760,7 +1839,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         float den = 0.f, rel = 0.f;
 #pragma unroll
         for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
-        const float im = 1.f / m.fb_mass[fb];
+        const float im = 1.f / gld(m.fb_mass + (fb));
         const v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
         den += dot(jbl, mbl) + dot(jba, mba);
         const float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
@@ -1790,10 +1869,10 @@ AVR_DI void plane_space(v3 n, v3 &p, v3 &q) {
 }
 
 AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, int &idx) {
-    int k = m.body_kind[b];
+    int k = gld(m.body_kind + (b));
     kind = 0; idx = 0;
-    if (k == AVR_BODY_ROBOT) { kind = 1; idx = m.body_index[b]; }
-    else if (k == AVR_BODY_FREE) { kind = 2; idx = m.body_index[b]; }
+    if (k == AVR_BODY_ROBOT) { kind = 1; idx = gld(m.body_index + (b)); }
+    else if (k == AVR_BODY_FREE) { kind = 2; idx = gld(m.body_index + (b)); }
     else if (k == AVR_BODY_HUMAN) {
         for (int c = 0; c < L.nla - m.nl; c++)     // head-chain link under 'tremor'
             if (m.hc_body[c] == b) { kind = 1; idx = m.nl + c; }
@@ -1813,7 +1892,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         int kA = 0, iA = 0, kB = 0, iB = 0;
         const float *c = gcp + AVR_CP_WORDS * (act ? i : 0);
         int sa = (int)c[AVR_CP_SA], sb = (int)c[AVR_CP_SB];
-        int ba = m.shape_body[sa], bb = m.shape_body[sb];
+        int ba = gld(m.shape_body + (sa)), bb = gld(m.shape_body + (sb));
         body_endpoint(m, L, ba, kA, iA);
         body_endpoint(m, L, bb, kB, iB);
         const bool rob = kA == 1 || kB == 1;
@@ -1828,9 +1907,9 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         v3 t1, t2;
         plane_space(n, t1, t2);
         v3 rA = sub(pa, ta.p), rB = sub(pb, tb.p);
-        float fric = fminf(m.body_friction[ba] * m.body_friction[bb], 10.f);
+        float fric = fminf(gld(m.body_friction + (ba)) * gld(m.body_friction + (bb)), 10.f);
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
-        float imA = kA == 2 ? 1.f / m.fb_mass[iA] : 0.f, imB = kB == 2 ? 1.f / m.fb_mass[iB] : 0.f;
+        float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
         for (int k = 0; k < 3; k++) {
             v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
             const int slot = rob ? slot0 + k : -1;
@@ -1924,8 +2003,8 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
         const float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * f;
         v3 v = ld3(fb + 7), om = ld3(fb + 10);
         qt q = ldq(fb + 3);
-        float mass = m.fb_mass[f];
-        v3 I = ld3(m.fb_inertia + 4 * f), g = ld3(m.fb_gravity + 4 * f);
+        float mass = gld(m.fb_mass + (f));
+        v3 I = gld3(m.fb_inertia + 4 * f), g = gld3(m.fb_gravity + 4 * f);
         v3 Iw = inertia_mul(q, I, om);
         v3 F = sub(scl(g, mass), scl(v, mass * (k1l + k1l * len(v))));
         v3 T = sub(scl(Iw, -(k1a + k1a * len(om))), crs(om, Iw));
@@ -1962,7 +2041,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
 AVR_DI void mouth_target(const KModel &m, EnvLDS &L) {
     tf t = ldtf(L.st + AVR_S_HUMAN + 7 * m.head_slot);
     int g = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
-    v3 p = tfpt(t, ld3(m.mouth[g]));
+    v3 p = tfpt(t, gld3(m.mouth[g]));
     SYNC();
     if (lane_id() == 0) st3(L.st + AVR_S_TASK + AVR_T_TARGET, p);
     SYNC();
@@ -1977,8 +2056,8 @@ AVR_DI float contact_sum(const KModel &m, const EnvLDS &L, const float *gcp, int
     int c = 0;
     for (int i = lane; i < n; i += 64) {
         const float *cp = gcp + AVR_CP_WORDS * i;
-        int ba = m.shape_body[(int)cp[AVR_CP_SA]], bb = m.shape_body[(int)cp[AVR_CP_SB]];
-        int ka = m.body_kind[ba], kb = m.body_kind[bb];
+        int ba = gld(m.shape_body + ((int)cp[AVR_CP_SA])), bb = gld(m.shape_body + ((int)cp[AVR_CP_SB]));
+        int ka = gld(m.body_kind + (ba)), kb = gld(m.body_kind + (bb));
         bool hit;
         if (sel == 0) hit = (ka == AVR_BODY_ROBOT && kb == AVR_BODY_HUMAN) || (kb == AVR_BODY_ROBOT && ka == AVR_BODY_HUMAN);
         else if (sel == 1) hit = (ba == m.spoon_body && kb == AVR_BODY_HUMAN) || (bb == m.spoon_body && ka == AVR_BODY_HUMAN);
@@ -2071,7 +2150,7 @@ template <int NB>
 AVR_DI void g2r(float (&t)[NB], const float *src, int n) {
     const int lane = lane_id(), l = max(n - 1, 0);
 #pragma unroll
-    for (int q = 0; q < NB; q++) t[q] = src[min(lane + 64 * q, l)];
+    for (int q = 0; q < NB; q++) t[q] = gld(src + min(lane + 64 * q, l));
 }
 template <int NB>
 AVR_DI void r2l(float *dst, const float (&t)[NB], int n) {
@@ -2229,7 +2308,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const K
 #pragma unroll
     for (int q = 0; q < MAXSH / 64; q++) {
         const int s = lane_id() + 64 * q;
-        si[q] = s < m.ns ? m.shape_info[s] : 0;
+        si[q] = s < m.ns ? gld(m.shape_info + (s)) : 0;
     }
     load_state(m, L, gst);
     PROF_START(ps);
@@ -2275,13 +2354,18 @@ AVR_DI WShape selw(bool c, const WShape &a, const WShape &b) {
     return r;
 }
 
-AVR_DI void ph_init(const KModel &m, const float *cs, int k, PH &P) {
-    const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
-    const int sa = key & 0xffff, sb = key >> 16;
-    const int ba = m.shape_body[sa], bb = m.shape_body[sb];
-    P.k = k;
-    P.thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-    const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+// list entry e: (k | ba << 16 | bb << 24, sa | sb << 16)
+AVR_DI int2 np_entry(const float *cs, int l) {
+    const float2 e = ((const float2 *)(cs + l))[0];
+    return make_int2(__float_as_int(e.x), __float_as_int(e.y));
+}
+
+AVR_DI void ph_init(const KModel &m, const float *btf, int2 e, PH &P) {
+    const int sa = e.y & 0xffff, sb = e.y >> 16;
+    const int ba = (e.x >> 16) & 0xff, bb = (e.x >> 24) & 0xff;
+    P.k = e.x & 0xffff;
+    P.thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
+    const WShape A = make_wshape(m, sa, ldtf(btf + 8 * ba)), B = make_wshape(m, sb, ldtf(btf + 8 * bb));
     P.sw = A.kind != AVR_SPHERE;
     P.c = sel3(P.sw, B.t.p, A.t.p);
     P.H = selw(P.sw, A, B);
@@ -2362,15 +2446,15 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
     const int lane = lane_id();
     for (int c0 = 0; c0 < n; c0 += 64) {
         const int k = c0 + lane < n ? c0 + lane : -1;
-        unsigned long long cm = __ballot(k >= 0 && __float_as_int(cs[CS_RES + 8 * (k >= 0 ? k : 0)]) == 2);
+        unsigned long long cm = __ballot(k >= 0 && __float_as_int(gld(cs + CS_RES + 8 * (k >= 0 ? k : 0))) == 2);
         while (cm) {
             const int j = __ffsll((long long)cm) - 1;
             cm &= cm - 1;
             const int kj = __shfl(k, j, 64);
-            const int key = __float_as_int(cs[CS_PAIRS + 2 * kj]);
+            const int key = __float_as_int(gld(cs + CS_PAIRS + 2 * kj)), w = __float_as_int(gld(cs + CS_PAIRS + 2 * kj + 1));
             const int sa = key & 0xffff, sb = key >> 16;
-            const int ba = m.shape_body[sa], bb = m.shape_body[sb];
-            const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
+            const int ba = (w >> 16) & 0xff, bb = (w >> 24) & 0xff;
+            const float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
             const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
             v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
             float d2 = 0.f;
@@ -2419,7 +2503,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
     for (int k = 0; k < NP_ENVS; k++) {
         const int e = eb + 8 * k;
         const bool live = e < n_envs && (!mask || mask[e]);
-        pre[k + 1] = pre[k] + (live ? __float_as_int(env_cs(m, live ? e : eb)[list ? CS_N1 : CS_N0]) : 0);
+        pre[k + 1] = pre[k] + (live ? __float_as_int(gld(env_cs(m, live ? e : eb) + (list ? CS_N1 : CS_N0))) : 0);
     }
     const int T = pre[NP_ENVS];
     // item j: env slot k and its position in that env's list (value selects: no indexed register array)
@@ -2431,6 +2515,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
         cs = env_cs(m, eb + 8 * k);
         return j - off;
     };
+    auto slot_of = [&](int j) {
+        int k = 0;
+#pragma unroll
+        for (int q = 1; q < NP_ENVS; q++)
+            if (j >= pre[q]) k = q;
+        return k;
+    };
+    // the block's list entries (concatenated over its envs) and its envs' body frames, staged in
+    // LDS in one round trip: a refill then reads its entry and frames from LDS
+    __shared__ float2 ent[NP_ENVS * MAXSP];
+    __shared__ float btfs[NP_ENVS][MAXB * 8];
+#pragma unroll
+    for (int k = 0; k < NP_ENVS; k++) {
+        const int e = eb + 8 * k;
+        const float *ck = env_cs(m, e < n_envs ? e : eb);
+        const int nk = pre[k + 1] - pre[k];
+        float te[NB_OF(2 * MAXSP)], tb[NB_OF(MAXB * 8)];
+        g2r(te, ck + (list ? CS_L1 : CS_L0), 2 * nk);
+        g2r(tb, ck + CS_BTF, m.nb * 8);
+        r2l((float *)ent + 2 * pre[k], te, 2 * nk);
+        r2l(btfs[k], tb, m.nb * 8);
+    }
+    __syncthreads();
+    auto entry = [&](int j) { const float2 x = ent[j]; return make_int2(__float_as_int(x.x), __float_as_int(x.y)); };
 #ifdef AVR_WAVETIME   // [3][eb] (list-0 block, list-1 block) durations in 100 MHz ticks
     struct WtNp {
         const KModel &m; int env, list, n_envs; unsigned long long t0;
@@ -2448,7 +2556,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
         PH P;
         float *pcs = nullptr;      // the env of the lane's pair
         bool act = lane < T;
-        if (act) { const int i = item(lane, pcs); ph_init(m, pcs, __float_as_int(pcs[CS_L0 + i]), P); }
+        if (act) { (void)item(lane, pcs); ph_init(m, btfs[slot_of(lane)], entry(lane), P); }
         int next = 64;
 #ifdef AVR_PROF
         pcount(32, T);
@@ -2470,7 +2578,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
             if (done) {
                 const int j = next + __popcll(dm & ((1ull << lane) - 1ull));
                 act = j < T;
-                if (act) { const int i = item(j, pcs); ph_init(m, pcs, __float_as_int(pcs[CS_L0 + i]), P); }
+                if (act) { (void)item(j, pcs); ph_init(m, btfs[slot_of(j)], entry(j), P); }
             }
             next += __popcll(dm);
         }
@@ -2485,13 +2593,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
 #endif
         if (c0 + lane < T) {
             float *cs;
-            const int i = item(c0 + lane, cs);
-            const int k = __float_as_int(cs[CS_L1 + i]);
-            const int key = __float_as_int(cs[CS_PAIRS + 2 * k]);
-            const int sa = key & 0xffff, sb = key >> 16;
-            const int ba = m.shape_body[sa], bb = m.shape_body[sb];
-            const float thr = fminf(m.body_threshold[ba], m.body_threshold[bb]);
-            const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+            (void)item(c0 + lane, cs);
+            const int2 e = entry(c0 + lane);
+            const float *bt = btfs[slot_of(c0 + lane)];
+            const int k = e.x & 0xffff;
+            const int sa = e.y & 0xffff, sb = e.y >> 16;
+            const int ba = (e.x >> 16) & 0xff, bb = (e.x >> 24) & 0xff;
+            const float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
+            const WShape A = make_wshape(m, sa, ldtf(bt + 8 * ba)), B = make_wshape(m, sb, ldtf(bt + 8 * bb));
             int rc = 2;
             v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
             float d = 0.f;
@@ -2529,7 +2638,7 @@ __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__
 #ifdef AVR_WAVETIME   // [4][env] (start, end) in 100 MHz ticks
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    np_coop(m, cs, __float_as_int(cs[CS_NSP]), E);
+    np_coop(m, cs, __float_as_int(gld(cs + CS_NSP)), E);
 #ifdef AVR_WAVETIME
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
     if (m.prof && lane_id() == 0) { m.prof[((size_t)4 * n_envs + env) * 2] = wt0; m.prof[((size_t)4 * n_envs + env) * 2 + 1] = wt1; }
@@ -2987,8 +3096,8 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
     if (sl < m.nf) {
         const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * sl + 3);
-        const v3 I = ld3(m.fb_inertia + 4 * sl);
-        const float rs = 1.f / sqrtf(m.fb_mass[sl]);
+        const v3 I = gld3(m.fb_inertia + 4 * sl);
+        const float rs = 1.f / sqrtf(gld(m.fb_mass + (sl)));
         const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
         const v3 w = qrot(q, V(d.wx * sd.x, d.wy * sd.y, d.wz * sd.z));
         d.vx *= rs; d.vy *= rs; d.vz *= rs;
@@ -3001,7 +3110,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         float q = st[AVR_S_Q + sl] + dt * v;
         if (frame_end && sl >= m.nd) {
             // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
-            const float lo = m.hc_lower[sl - m.nd], hi = m.hc_upper[sl - m.nd];
+            const float lo = gld(m.hc_lower + (sl - m.nd)), hi = gld(m.hc_upper + (sl - m.nd));
             if (q < lo) { q = lo; v = 0.f; }
             else if (q > hi) { q = hi; v = 0.f; }
         }

@@ -42,9 +42,10 @@
 #define CS_CM (CS_BTF + 8 * MAXB)                   // [MAXL][8] link COM frames
 #define CS_AX (CS_CM + 8 * MAXL)                    // [MAXL][4] joint axes (world)
 #define CS_ORG (CS_AX + 4 * MAXL)                   // [MAXL][4] joint origins (world)
-#define CS_L0 (CS_ORG + 4 * MAXL)                   // [MAXSP] indices of the sphere-hull pairs, ascending
-#define CS_L1 (CS_L0 + MAXSP)                       // [MAXSP] indices of the other pairs, ascending
-#define CS_WORDS (CS_L1 + MAXSP)
+#define CS_L0 (CS_ORG + 4 * MAXL)                   // [MAXSP][2] the sphere-hull pairs, ascending: (k | ba << 16 | bb << 24, sa | sb << 16)
+#define CS_L1 (CS_L0 + 2 * MAXSP)                   // [MAXSP][2] the other pairs, ascending, the same entries
+#define CS_WORDS (CS_L1 + 2 * MAXSP)
+static_assert(MAXB <= 256 && MAXSP <= 65536, "narrowphase list entries pack k (16 bits) and two body indices (8 bits each)");
 
 // Articulated links: the robot's nl links, then (impairment 'tremor') the head/neck chain's
 // hc_n links with DoFs nd .. nd + hc_n - 1; nla = nl + hc_n.  The chain root's parent is -2:

@@ -55,7 +55,7 @@ def test_kernel_resources(lib_and_scene):
     sim = make_sim(md, 4)
     ki = sim.kernel_info()
     assert all(k['scratch_bytes'] == 0 for k in ki.values())     # no spills to scratch on gfx950
-    assert ki['narrowphase']['lds_bytes'] == 0
+    assert ki['narrowphase']['lds_bytes'] <= 4 * 1024     # staged list entries + body frames: 16 blocks per CU
     assert ki['a']['lds_bytes'] <= 20 * 1024 and ki['pairs']['lds_bytes'] <= 20 * 1024    # 8 env blocks per CU
     assert ki['b']['lds_bytes'] <= 40 * 1024            # part B (four envs per wave): 4 blocks per CU, all resident
     sim.close()
