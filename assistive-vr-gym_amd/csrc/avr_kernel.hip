@@ -1516,10 +1516,11 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
                 gsa0 = r0.y & 0xffff;
                 gsb0 = r0.z & 0xffff;
                 gbare = r0.w & 1;
-                // a single child against at most 64 (food against the spoon or bowl pieces): its
-                // items are tested directly, in one round, rather than after a culling round.
-                // The same set in the same order: child AABBs lie inside their bodies' fattened
-                // AABBs, so an overlapping child pair passes both body culls
+                // a single child against at most 64 (food against the spoon pieces): its items are
+                // tested directly, in one round, rather than after a culling round.  The same set
+                // in the same order: child AABBs lie inside their bodies' fattened AABBs, so an
+                // overlapping child pair passes both body culls.  (Measured: extending this to 128
+                // children -- the bowl, the wheelchair -- made the kernel slower, 0.080 -> 0.083 ms.)
                 gcull = !gbare && na * nb > 1 && !((na == 1 || nb == 1) && na * nb <= 64);
                 int ncA = na, ncB = nb;
                 if (gcull) {

@@ -51,28 +51,37 @@ def counters(c, names):
     return res
 
 
-def per_step(cnt, name):
-    """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS); None unless
-    every step kernel has the counter."""
+def per_step(cnt, name, groups=1):
+    """sum over the kernels of one env-step (launch multiplicities of STEP_KERNELS, once per env
+    group); None unless every step kernel has the counter."""
     if not cnt or any(name not in cnt.get(k, {}) for k in STEP_KERNELS):
         return None
-    return sum(cnt[k][name] * STEP_KERNELS[k] for k in STEP_KERNELS)
+    return sum(cnt[k][name] * STEP_KERNELS[k] * groups for k in STEP_KERNELS)
 
 
-def main(pdir, tag, envs=4096):
+def main(pdir, tag, envs=4096, groups=None):
+    # the bench runs min(4, envs / 1024) env groups: every kernel of the step is dispatched once
+    # per group, over that group's share of the envs
+    groups = groups or max(1, min(4, envs // 1024))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    prof = os.path.join(root, 'profiles')
+    prof = os.environ.get('AVR_PROF_OUT') or os.path.join(root, 'profiles')   # (on the GPU box: a gpurun_out/ dir)
     os.makedirs(prof, exist_ok=True)
-    c = db(os.path.join(pdir, 'kt'))
-    if c:
+    # kt: the bench as the driver runs it (env groups); kt1: the same bench with one env group,
+    # whose launches are the ones bench.py's per-kernel event pass times
+    for sub, name in (('kt', '%s_kernel_stats.csv'), ('kt1', '%s_kernel_stats_1group.csv')):
+        c = db(os.path.join(pdir, sub))
+        if not c:
+            continue
         st = kernel_stats(c)
-        with open(os.path.join(prof, '%s_kernel_stats.csv' % tag), 'w') as f:
+        with open(os.path.join(prof, name % tag), 'w') as f:
             f.write('kernel,calls,total_ns,avg_ns,median_ns,min_ns,max_ns,pct\n')
             for r in st:
                 f.write('%s,%d,%.0f,%.1f,%.1f,%.0f,%.0f,%.2f\n' % r)
+        print(name % tag)
         for r in st:
             print('%-28s calls %4d avg %10.3f ms  median %10.3f ms  %5.1f%%' % (r[0], r[1], r[3] / 1e6, r[4] / 1e6, r[7]))
-    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs}   # (only kernels that run in a step)
+    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs, 'env_groups': groups,
+           'dispatches_per_step': {k: v * groups for k, v in STEP_KERNELS.items()}}   # (only kernels that run in a step)
     cf, cw, cs = db(os.path.join(pdir, 'fetch')), db(os.path.join(pdir, 'write')), db(os.path.join(pdir, 'sq'))
     fetch = counters(cf, ['FETCH_SIZE']) if cf else {}
     write = counters(cw, ['WRITE_SIZE']) if cw else {}
@@ -81,14 +90,14 @@ def main(pdir, tag, envs=4096):
     if cs:
         out['sq_per_launch'] = counters(cs, ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_INSTS_LDS', 'SQ_WAIT_ANY',
                                              'SQ_ACTIVE_INST_ANY', 'SQ_WAVE_CYCLES'])
-    f_step, w_step = per_step(fetch, 'FETCH_SIZE'), per_step(write, 'WRITE_SIZE')
+    f_step, w_step = per_step(fetch, 'FETCH_SIZE', groups), per_step(write, 'WRITE_SIZE', groups)
     if f_step is not None and w_step is not None:
         fb, wb = 2 * f_step * 1024, w_step * 1024
         out['hbm_read_bytes_per_step'] = fb
         out['hbm_write_bytes_per_step'] = wb
         out['hbm_bytes_per_step'] = fb + wb
         out['hbm_bytes_per_env_step'] = (fb + wb) / envs
-        out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x launches per step'
+        out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x dispatches per step (launches x env groups)'
         json.dump(out, open(os.path.join(prof, 'pmc_traffic.json'), 'w'), indent=1)
     json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
     print(json.dumps(out, indent=1))
