@@ -1137,7 +1137,7 @@ AVR_DI bool overlap(v3 a0, v3 a1, v3 b0, v3 b1) {
 AVR_DI void shape_aabb(const KModel &m, int s, tf body, v3 &mn, v3 &mx) {
     tf t = tfmul(body, gldtf(m.shape_pose + 8 * s));
     const float *a = m.shape_aabb + 8 * s;
-    aabb_of(t, ld3(a), ld3(a + 4), mn, mx);
+    aabb_of(t, gld3(a), gld3(a + 4), mn, mx);
 }
 
 AVR_DI bool shape_enabled(const KModel &m, int s, int gender) {
@@ -1404,30 +1404,45 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
         st3(L.u.c.bmax[lane], bmx);
     }
     SYNC();
-    // world AABBs of the non-static child shapes
-    for (int s = lane; s < m.ns; s += 64) {
-        const int c = gld(m.shape_cidx + (s));
+    // world AABBs of the non-static child shapes (child index from the staged shape info; the
+    // shape records are read unconditionally, clamped into the table, so the unrolled passes'
+    // loads are not held behind each other's branches)
+#pragma unroll
+    for (int q = 0; q < MAXSH / 64; q++) {
+        const int s = lane + 64 * q, sc = min(s, m.ns - 1);
+        const int c = s < m.ns ? (int)(L.sinfo[sc] & 511) - 1 : -1;
+        v3 mn, mx;
+        shape_aabb(m, sc, ldtf(L.btf[gld(m.shape_body + sc)]), mn, mx);
         if (c >= 0) {
-            v3 mn, mx;
-            shape_aabb(m, s, ldtf(L.btf[gld(m.shape_body + (s))]), mn, mx);
             st3(L.u.c.caabb[c], mn);
             st3(L.u.c.caabb[c] + 3, mx);
         }
     }
-    // broadphase over the candidate pair list, order-preserving compaction
+    // broadphase over the candidate pair list, order-preserving compaction; the body indices of
+    // BP_BATCH rounds of 64 pairs are loaded together (one round trip per batch, not per round)
     int nap = 0;
     const int npe = L.nla > m.nl ? m.np : m.np_base;   // chain-vs-static pairs: 'tremor' envs only
-    for (int base = 0; base < npe; base += 64) {
-        int p = base + lane;
-        bool act = false;
-        if (p < npe) {
-            int ba = gld(m.pair_a + (p)), bb = gld(m.pair_b + (p));
-            act = overlap(ld3(L.u.c.bmin[ba]), ld3(L.u.c.bmax[ba]), ld3(L.u.c.bmin[bb]), ld3(L.u.c.bmax[bb]));
+    constexpr int BP_BATCH = 8;
+    for (int b0 = 0; b0 < npe; b0 += 64 * BP_BATCH) {
+        int pa[BP_BATCH], pb[BP_BATCH];
+#pragma unroll
+        for (int q = 0; q < BP_BATCH; q++) {
+            const int p = min(b0 + 64 * q + lane, npe - 1);
+            pa[q] = gld(m.pair_a + p);
+            pb[q] = gld(m.pair_b + p);
         }
-        int tot;
-        int pre = ballot_prefix(act, &tot);
-        if (act && nap + pre < MAXAP) L.u.c.apair[nap + pre] = p;
-        nap += tot;
+#pragma unroll
+        for (int q = 0; q < BP_BATCH; q++) {
+            const int base = b0 + 64 * q;
+            if (base >= npe) break;
+            const int p = base + lane;
+            const int ba = pa[q], bb = pb[q];
+            const bool act = p < npe && overlap(ld3(L.u.c.bmin[ba]), ld3(L.u.c.bmax[ba]), ld3(L.u.c.bmin[bb]), ld3(L.u.c.bmax[bb]));
+            int tot;
+            int pre = ballot_prefix(act, &tot);
+            if (act && nap + pre < MAXAP) L.u.c.apair[nap + pre] = p;
+            nap += tot;
+        }
     }
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
