@@ -11,7 +11,11 @@ import numpy as np
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # ---- capacities / offsets (must match include/avr_model.h) ----
-ABI_VERSION = 2
+ABI_VERSION = 3
+TASK_FEEDING, TASK_SCRATCH = 0, 1
+DESC_HC = 8                               # avr_model_desc hc_* capacity
+BODY_ROBOT, BODY_FREE, BODY_STATIC, BODY_HUMAN, BODY_RSTATIC = 0, 1, 2, 3, 4
+# FeedingJaco-v0 layout (module-level names; the ScratchItchPR2-v0 layout is `SI` below)
 MAX_LINKS, MAX_DOF, MAX_FREE, MAX_HUMAN, MAX_CONTACTS, HC_N = 20, 14, 10, 20, 96, 4
 MAX_FOOD, ACT_DIM, OBS_DIM, INFO_DIM = 8, 7, 25, 2
 FB_WORDS, CP_WORDS = 13, 16
@@ -28,6 +32,45 @@ S_HCH = S_HUMAN + MAX_HUMAN * 7          # [HC_N] target_human_joint_positions, 
 S_CP = S_HCH + 2 * HC_N
 STATE_WORDS = S_CP + MAX_CONTACTS * CP_WORDS
 CP_SA, CP_SB, CP_LA, CP_LB, CP_N, CP_DIST, CP_IMP, CP_LIFE, CP_PAIR = 0, 1, 2, 5, 8, 11, 12, 13, 14
+
+
+class _Layout:
+    """State layout of one task (include/avr_model.h), attribute names as the module-level ones."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+FEEDING = _Layout(TASK=TASK_FEEDING, MAX_LINKS=MAX_LINKS, MAX_DOF=MAX_DOF, MAX_FREE=MAX_FREE, MAX_HUMAN=MAX_HUMAN,
+                  MAX_CONTACTS=MAX_CONTACTS, HC_N=HC_N, ACT_DIM=ACT_DIM, OBS_DIM=OBS_DIM, INFO_DIM=INFO_DIM,
+                  S_Q=S_Q, S_QD=S_QD, S_QTGT=S_QTGT, S_KP=S_KP, S_MAXIMP=S_MAXIMP, S_FREE=S_FREE, S_TASK=S_TASK,
+                  T_TARGET=T_TARGET, T_ITER=T_ITER, T_SUCCESS=T_SUCCESS, T_ALIVE=T_ALIVE, T_HIT=T_HIT, T_GENDER=T_GENDER,
+                  T_FLAGS=T_FLAGS, T_NCP=T_NCP, T_HDYN=T_HDYN, T_WORDS=T_WORDS, S_HUMAN=S_HUMAN, S_HCH=S_HCH, S_CP=S_CP,
+                  STATE_WORDS=STATE_WORDS)
+
+
+def _scratch_layout():
+    L = dict(TASK=TASK_SCRATCH, MAX_LINKS=32, MAX_DOF=24, HC_N=8, MAX_FREE=1, MAX_HUMAN=20, MAX_CONTACTS=64,
+             ACT_DIM=7, OBS_DIM=30, INFO_DIM=2)
+    L['S_Q'] = 0
+    L['S_QD'] = L['S_Q'] + L['MAX_DOF']
+    L['S_QTGT'] = L['S_QD'] + L['MAX_DOF']
+    L['S_KP'] = L['S_QTGT'] + L['MAX_DOF']
+    L['S_MAXIMP'] = L['S_KP'] + L['MAX_DOF']
+    L['S_FREE'] = L['S_MAXIMP'] + L['MAX_DOF']
+    L['S_RBASE'] = L['S_FREE'] + L['MAX_FREE'] * FB_WORDS
+    L['S_TASK'] = L['S_RBASE'] + 8
+    L.update(T_TARGET=0, T_ITER=3, T_SUCCESS=4, T_LIMB=5, T_STRENGTH=6, T_GENDER=7, T_FLAGS=8, T_NCP=9, T_HDYN=10,
+             T_PREV=11, T_TREMOR=14, T_ONARM=16, T_WORDS=24)
+    L['S_HUMAN'] = L['S_TASK'] + L['T_WORDS']
+    L['S_HCH'] = L['S_HUMAN'] + L['MAX_HUMAN'] * 7      # [HC_N] targets, tremors, lower, upper limits
+    L['S_CP'] = L['S_HCH'] + 4 * L['HC_N']
+    L['STATE_WORDS'] = L['S_CP'] + L['MAX_CONTACTS'] * CP_WORDS
+    return _Layout(**L)
+
+
+SI = _scratch_layout()
+LAYOUTS = {TASK_FEEDING: FEEDING, TASK_SCRATCH: SI}
 
 PI32 = C.POINTER(C.c_int32)
 PF64 = C.POINTER(C.c_double)
@@ -80,13 +123,18 @@ class avr_model_desc(C.Structure):
         ('w_velocity', C.c_double), ('w_force_nontarget', C.c_double), ('w_high_forces', C.c_double),
         ('w_food_hit', C.c_double), ('w_food_velocities', C.c_double), ('task_success_threshold', C.c_double),
         ('hc_n', C.c_int32), ('hc_parent_slot', C.c_int32),
-        ('hc_slot', C.c_int32 * HC_N), ('hc_body', C.c_int32 * HC_N),
-        ('hc_jpos', ((C.c_double * 3) * HC_N) * 2),
-        ('hc_axis', (C.c_double * 3) * HC_N),
-        ('hc_mass', (C.c_double * HC_N) * 2), ('hc_inertia', ((C.c_double * 3) * HC_N) * 2),
-        ('hc_lower', C.c_double * HC_N), ('hc_upper', C.c_double * HC_N),
+        ('hc_slot', C.c_int32 * DESC_HC), ('hc_body', C.c_int32 * DESC_HC),
+        ('hc_jpos', ((C.c_double * 3) * DESC_HC) * 2),
+        ('hc_axis', (C.c_double * 3) * DESC_HC),
+        ('hc_mass', (C.c_double * DESC_HC) * 2), ('hc_inertia', ((C.c_double * 3) * DESC_HC) * 2),
+        ('hc_lower', C.c_double * DESC_HC), ('hc_upper', C.c_double * DESC_HC),
         ('human_gain', C.c_double), ('human_force', C.c_double),
         ('n_pairs_base', C.c_int32),
+        # ABI 3
+        ('task', C.c_int32), ('n_rstatic', C.c_int32),
+        ('human_gravity', C.c_double * 3), ('fix_pivot_b', C.c_double * 3), ('tool_tip', C.c_double * 3),
+        ('torso_com', C.c_double * 3), ('tool_handle_shapes', C.c_int32),
+        ('w_tool_force', C.c_double), ('w_scratch', C.c_double),
     ]
 
 
@@ -119,17 +167,55 @@ FEEDING_PARAMS = dict(
 )
 
 
+# ScratchItchPR2 physics / task constants ([ext]: assumed Bullet/PyBullet defaults, as above)
+SCRATCH_PARAMS = dict(
+    time_step=0.02,              # world_creation.py:75
+    num_sub_steps=0,             # scratch_itch.py:258 (0: one step of time_step)
+    frame_skip=5,                # scratch_itch.py:18
+    solver_iterations=50,        # scratch_itch.py:258
+    max_episode_steps=200,       # assistive_gym/__init__.py (ScratchItchPR2-v0)
+    erp=0.2, warmstart=0.85, linear_damping=0.04, angular_damping=0.04, max_coord_vel=100.0,   # [ext]
+    default_motor_impulse=1.0,   # [ext]
+    robot_gain=0.05,             # config.ini:5 (scratch_itch robot_gains)
+    robot_force=1.0,             # config.ini:4
+    finger_gain=0.05,            # world_creation.py:328
+    finger_force=500.0,          # world_creation.py:328
+    finger_target=0.25,          # scratch_itch.py:192 set_gripper_open_position(position=0.25)
+    fixed_max_force=500.0,       # world_creation.py:364
+    w_distance=1.0, w_action=0.01, w_food=0.0,                       # config.ini:6-7
+    w_tool_force=0.01, w_scratch=2.0,                                # config.ini:8-9
+    w_velocity=0.25, w_force_nontarget=0.01, w_high_forces=0.05,     # config.ini:37-39
+    w_food_hit=0.0, w_food_velocities=0.0,
+    task_success_threshold=25.0,                                     # config.ini:10
+    human_gain=0.05,             # scratch_itch.py:45 take_step(..., human_gains=0.05) under 'tremor'
+    human_force=1.0,             # env.py:274 take_step default human_forces (x human_strength)
+    reactive_gain=0.01,          # scratch_itch.py:263 human_reactive_gain (not a descriptor field)
+    reactive_force=1.0,          # scratch_itch.py:263 human_reactive_force (x human_strength)
+)
+
+SCENES = {TASK_FEEDING: 'feeding_jaco', TASK_SCRATCH: 'scratch_itch_pr2'}
+
+
 def load_scene(name='feeding_jaco'):
+    if isinstance(name, int):
+        name = SCENES[name]
     return dict(np.load(os.path.join(DATA_DIR, name + '.npz')))
+
+
+def scene_task(A):
+    return TASK_SCRATCH if 'n_rstatic' in A else TASK_FEEDING
 
 
 class ModelDesc:
     """Owns the arrays behind an `avr_model_desc`."""
 
     def __init__(self, A, params=None):
-        P = dict(FEEDING_PARAMS)
+        task = scene_task(A)
+        P = dict(SCRATCH_PARAMS if task == TASK_SCRATCH else FEEDING_PARAMS)
         if params:
             P.update(params)
+        self.task = task
+        self.layout = LAYOUTS[task]
         self.A = {}
         self.params = P
         d = avr_model_desc()
@@ -182,22 +268,39 @@ class ModelDesc:
         for i, x in enumerate(fin):
             d.finger_dofs[i] = x
         d.tool_link = int(A['task_tool_link'])
-        d.torso_link = int(A['task_torso_link'])
-        d.head_slot = int(A['task_head_slot'])
-        d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, 1, 2, 8
-        d.table_body = int(A['task_table_body'])
-        d.bowl_body = int(A['task_bowl_body'])
-        d.spoon_body = int(A['task_spoon_body'])
-        d.food_body0 = int(A['task_food_body0'])
+        if task == TASK_FEEDING:
+            d.torso_link = int(A['task_torso_link'])
+            d.head_slot = int(A['task_head_slot'])
+        d.task = task
+        if task == TASK_SCRATCH:
+            d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, -1, -1, 0
+            d.table_body = d.bowl_body = d.food_body0 = -1
+            d.spoon_body = int(A['task_tool_body'])
+            d.n_rstatic = int(A['n_rstatic'])
+            d.human_gravity[2] = -1.0                    # scratch_itch.py:260
+            for i in range(3):
+                d.fix_pivot_b[i] = float(A['task_tool_pivot'][i])
+                d.tool_tip[i] = float(A['task_tool_tip'][i])
+                d.torso_com[i] = float(A['task_torso_com'][i])
+            d.tool_handle_shapes = int(A['task_tool_handle_shapes'])
+            d.torso_link = -1
+            d.head_slot = -1
+        else:
+            d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, 1, 2, 8
+            d.table_body = int(A['task_table_body'])
+            d.bowl_body = int(A['task_bowl_body'])
+            d.spoon_body = int(A['task_spoon_body'])
+            d.food_body0 = int(A['task_food_body0'])
         d.human_body0 = int(A['task_human_body0'])
         d.n_human_bodies = int(np.sum(A['body_kind'] == 3))
         d.robot_body0 = 0
         d.n_robot_bodies = int(np.sum(A['body_kind'] == 0))
         for i, x in enumerate(A['task_tool_offset']):
             d.tool_offset[i] = float(x)
-        for i in range(3):
-            d.mouth_offset[0][i] = float(A['task_mouth_male'][i])
-            d.mouth_offset[1][i] = float(A['task_mouth_female'][i])
+        if task == TASK_FEEDING:
+            for i in range(3):
+                d.mouth_offset[0][i] = float(A['task_mouth_male'][i])
+                d.mouth_offset[1][i] = float(A['task_mouth_female'][i])
         # take_step limit zeroing uses getJointInfo limits; continuous joints -> +-1e10
         # (world_creation.py:122-124)
         dof_link = {int(A['rl_dof'][l]): l for l in range(int(A['n_links'])) if A['rl_dof'][l] >= 0}
@@ -207,10 +310,11 @@ class ModelDesc:
                 d.arm_lower[i], d.arm_upper[i] = float(A['rl_lower'][l]), float(A['rl_upper'][l])
             else:
                 d.arm_lower[i], d.arm_upper[i] = -1e10, 1e10
-        if 'hc_slot' in A:                 # tremor head/neck chain (model_compiler.head_chain)
-            d.hc_n = HC_N
+        if 'hc_slot' in A:                 # articulated human chain (model_compiler.head_chain)
+            nhc = int(A['hc_n']) if 'hc_n' in A else HC_N
+            d.hc_n = nhc
             d.hc_parent_slot = int(A['hc_parent_slot'])
-            for k in range(HC_N):
+            for k in range(nhc):
                 d.hc_slot[k] = int(A['hc_slot'][k])
                 d.hc_body[k] = int(A['hc_body'][k])
                 d.hc_lower[k] = float(A['hc_lower'][k])
@@ -223,6 +327,8 @@ class ModelDesc:
                         d.hc_jpos[g][k][i] = float(A['hc_jpos'][g][k][i])
                         d.hc_inertia[g][k][i] = float(A['hc_inertia'][g][k][i])
         for k, v in P.items():
+            if k in ('reactive_gain', 'reactive_force'):
+                continue
             setattr(d, k, v)
         self.desc = d
         self.n_dof = d.n_dof

@@ -18,7 +18,8 @@ EXPORTS = [
     'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_env_groups', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
-    'avr_hull_support_table',
+    'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
+    'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary',
 ]
 
 
@@ -77,9 +78,19 @@ def load(path=LIB_PATH):
     lib.avr_reset.argtypes = [vp, vp, vp, C.c_int32, vp]
     lib.avr_profile_kernels.argtypes = [vp, C.c_int32]
     lib.avr_kernel_times.argtypes = [vp, vp, vp]
-    if lib.avr_abi_version() != ABI.ABI_VERSION or lib.avr_state_words() != ABI.STATE_WORDS:
-        raise RuntimeError('%s: ABI %d / %d state words, this package expects ABI %d / %d (rebuild)'
-                           % (path, lib.avr_abi_version(), lib.avr_state_words(), ABI.ABI_VERSION, ABI.STATE_WORDS))
+    lib.avr_task.argtypes = [vp]
+    lib.avr_n_dof.argtypes = [vp]
+    for f in ('avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim'):
+        getattr(lib, f).argtypes = [C.c_int32]
+        getattr(lib, f).restype = C.c_int32
+    lib.avr_get_q.argtypes = [vp, vp, vp]
+    lib.avr_get_link_pose.argtypes = [vp, C.c_int32, vp]
+    lib.avr_get_contact_summary.argtypes = [vp, vp]
+    if lib.avr_abi_version() != ABI.ABI_VERSION or any(
+            lib.avr_task_state_words(t) != L.STATE_WORDS or lib.avr_task_obs_dim(t) != L.OBS_DIM or lib.avr_task_act_dim(t) != L.ACT_DIM
+            for t, L in ABI.LAYOUTS.items()):
+        raise RuntimeError('%s: ABI %d / state layouts differ from this package (ABI %d); rebuild'
+                           % (path, lib.avr_abi_version(), ABI.ABI_VERSION))
     _LIB = lib
     return lib
 
@@ -104,7 +115,10 @@ class Sim:
                 self.lib.avr_destroy(h)
                 self.h = None
             raise RuntimeError('avr_create failed (%d): %s' % (rc, msg))
-        self.words = self.lib.avr_state_words()
+        self.task = int(self.lib.avr_task(h))
+        self.L = ABI.LAYOUTS[self.task]
+        self.words = self.lib.avr_task_state_words(self.task)
+        self.obs_dim, self.act_dim = self.L.OBS_DIM, self.L.ACT_DIM
 
     def _chk(self, rc):
         if rc:
@@ -136,7 +150,7 @@ class Sim:
         return S
 
     def settle(self, frames=100):
-        obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         self._chk(self.lib.avr_settle(self.h, frames, obs.ctypes.data))
         return obs
 
@@ -145,8 +159,8 @@ class Sim:
         S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.n)
         if obs is None:
-            obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
-        assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.shape == (self.n, ABI.OBS_DIM)
+            obs = np.zeros((self.n, self.obs_dim), np.float32)
+        assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.shape == (self.n, self.obs_dim)
         self._chk(self.lib.avr_reset(self.h, None if m is None else m.ctypes.data, S.ctypes.data, int(frames), obs.ctypes.data))
         return obs
 
@@ -154,8 +168,8 @@ class Sim:
         self._chk(self.lib.avr_substep(self.h, dt))
 
     def step(self, act):
-        act = np.ascontiguousarray(act, np.float32).reshape(self.n, ABI.ACT_DIM)
-        obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        act = np.ascontiguousarray(act, np.float32).reshape(self.n, self.act_dim)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
         done = np.zeros(self.n, np.uint8)
         info = np.zeros((self.n, ABI.INFO_DIM), np.float32)
@@ -193,11 +207,35 @@ class Sim:
         self._chk(self.lib.avr_kernel_times(self.h, ms.ctypes.data, n.ctypes.data))
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.kernel_kinds)}
 
+    # ---- state queries (include/avr.h avr_get_*)
+    def n_dof(self):
+        return int(self.lib.avr_n_dof(self.h))
+
+    def get_q(self):
+        """(q, qd), each (n_envs, n_dof): robot DoFs, then the articulated human chain's."""
+        nd = self.n_dof()
+        q = np.zeros((self.n, nd), np.float32)
+        qd = np.zeros((self.n, nd), np.float32)
+        self._chk(self.lib.avr_get_q(self.h, q.ctypes.data, qd.ctypes.data))
+        return q, qd
+
+    def get_link_pose(self, link):
+        """(n_envs, 7) world COM frame of articulated link `link` (-1: robot base)."""
+        out = np.zeros((self.n, 7), np.float32)
+        self._chk(self.lib.avr_get_link_pose(self.h, int(link), out.ctypes.data))
+        return out
+
+    def get_contact_summary(self):
+        """(n_envs, 4): contact points, sum of normal force, robot-human, tool-human."""
+        out = np.zeros((self.n, 4), np.float32)
+        self._chk(self.lib.avr_get_contact_summary(self.h, out.ctypes.data))
+        return out
+
     def kernel_info(self):
-        """{kernel: dict(vgprs, lds_bytes, scratch_bytes)} of the four sub-step kernels."""
-        out = np.zeros(16, np.int32)
+        """{kernel: dict(vgprs, lds_bytes, scratch_bytes)} of the five sub-step kernels."""
+        out = np.zeros(20, np.int32)
         self._chk(self.lib.avr_kernel_info(self.h, out.ctypes.data))
-        names = ('pairs', 'narrowphase', 'a', 'b')
+        names = ('pairs', 'narrowphase', 'coop', 'a', 'b')
         return {n: dict(vgprs=int(out[4 * i]), lds_bytes=int(out[4 * i + 2]), scratch_bytes=int(out[4 * i + 3])) for i, n in enumerate(names)}
 
 

@@ -14,8 +14,11 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(HERE, 'libavr.so')
 ARCH = os.environ.get('AVR_OFFLOAD_ARCH', 'gfx950')
-SOURCES = ['avr_kernel.hip', 'avr_capi.hip', 'avr_hulltab.cpp']
-HEADERS = ['avr_math.h', 'avr_kmodel.h']
+# one translation unit per task (the shared kernel / C-ABI sources instantiated in a namespace,
+# csrc/avr_task_tu.h), the extern "C" dispatcher, the hull support tables
+SOURCES = ['avr_task_feeding.hip', 'avr_task_scratch.hip', 'avr_api.cpp', 'avr_hulltab.cpp']
+HEADERS = ['avr_math.h', 'avr_kmodel.h', 'avr_task.h', 'avr_task_tu.h', 'avr_kernel.hip', 'avr_capi.hip', 'avr_glue_scratch.hip']
+OBJDIR = os.path.join(PKG, 'build')
 
 
 def _hipcc():
@@ -38,11 +41,19 @@ def _stale(target, deps, cmd):
 
 
 _PROBED = {}
+_PROBE_CACHE = os.path.join(HERE, '.hipcc_probe')     # probe results survive across processes
 
 
 def _supported(flags):
-    """True if hipcc accepts `flags` (probed once per flag set on an empty gfx950 kernel)."""
+    """True if hipcc accepts `flags` (probed once per flag set on an empty gfx950 kernel; the result
+    is cached on disk next to the library, keyed by the hipcc path and the flags)."""
     key = tuple(flags)
+    ckey = '%s %s' % (_hipcc(), ' '.join(flags))
+    if key not in _PROBED and os.path.exists(_PROBE_CACHE):
+        for line in open(_PROBE_CACHE):
+            k, _, v = line.rstrip('\n').rpartition('\t')
+            if k == ckey:
+                _PROBED[key] = v == '1'
     if key not in _PROBED:
         import tempfile
         with tempfile.TemporaryDirectory() as d:
@@ -51,30 +62,49 @@ def _supported(flags):
             r = subprocess.run([_hipcc(), '--offload-arch=%s' % ARCH, '--cuda-device-only', '-c', '-o', os.path.join(d, 'p.o'), src] + list(flags),
                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             _PROBED[key] = r.returncode == 0
+        with open(_PROBE_CACHE, 'a') as f:
+            f.write('%s\t%d\n' % (ckey, int(_PROBED[key])))
     return _PROBED[key]
 
 
 # AMDGPU register-pressure trackers in the scheduler: part B 0.590 -> 0.564 ms, A 0.552 -> 0.560 ms,
-# 356k -> 361k env-steps/s (round 1, tools/gpu_flags.sh VARIANTS=trackers).  An internal LLVM
-# option: dropped (with a warning) when this hipcc does not know it.
+# 356k -> 361k env-steps/s (round 1 flag sweep; tools/build_variants.py + tools/gpu_variants.sh
+# rerun such sweeps).  An internal LLVM option: dropped (with a warning) when this hipcc does not
+# know it.
 TRACKERS = ('-mllvm', '-amdgpu-use-amdgpu-trackers=1')
 
 
-def lib_cmd(extra=(), out=LIB):
-    cmd = [_hipcc(), '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared', '-Wno-unused-result', '-fno-slp-vectorize']
+def lib_flags(extra=()):
+    flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result', '-fno-slp-vectorize']
     if _supported(TRACKERS):
-        cmd += list(TRACKERS)
+        flags += list(TRACKERS)
     else:
         sys.stderr.write('avr.build: hipcc does not accept %s; building without it\n' % ' '.join(TRACKERS))
-    return cmd + ['-o', out] + [os.path.join(CSRC, f) for f in SOURCES] + list(extra)
+    return flags + list(extra)
+
+
+def lib_cmd(extra=(), out=LIB):
+    """The full build as one command line (recorded in <lib>.cmd: a flag change rebuilds)."""
+    return [_hipcc()] + lib_flags(extra) + ['-shared', '-o', out] + [os.path.join(CSRC, f) for f in SOURCES]
 
 
 def build_lib(force=False, extra=(), out=LIB):
+    """Compile the translation units in parallel (one hipcc per TU), then link libavr*.so."""
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')] + [os.path.abspath(__file__)]
     cmd = lib_cmd(extra, out)
     if not force and not _stale(out, deps, cmd):
         return out
-    subprocess.check_call(cmd)
+    tag = os.path.splitext(os.path.basename(out))[0]
+    os.makedirs(OBJDIR, exist_ok=True)
+    flags = lib_flags(extra)
+    procs, objs = [], []
+    for f in SOURCES:
+        o = os.path.join(OBJDIR, '%s.%s.o' % (tag, os.path.splitext(f)[0]))
+        objs.append(o)
+        procs.append(subprocess.Popen([_hipcc()] + flags + ['-c', '-o', o, os.path.join(CSRC, f)]))
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, 'hipcc (%s)' % out)
+    subprocess.check_call([_hipcc(), '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out] + objs)
     open(out + '.cmd', 'w').write(' '.join(cmd))
     return out
 

@@ -19,6 +19,7 @@ ships.  Nothing here is on the step path.  What it restates, with reference cita
 """
 import os
 import re
+import struct
 import xml.etree.ElementTree as ET
 
 import numpy as np
@@ -33,7 +34,7 @@ URDF_MARGIN = 0.001          # gUrdfDefaultCollisionMargin (assumed Bullet defau
 CONTACT_BREAKING = 0.02      # gContactBreakingThreshold (assumed Bullet default)
 
 SPHERE, CAPSULE, BOX, HULL = 0, 1, 2, 3
-KIND_ROBOT, KIND_FREE, KIND_STATIC, KIND_HUMAN = 0, 1, 2, 3
+KIND_ROBOT, KIND_FREE, KIND_STATIC, KIND_HUMAN, KIND_RSTATIC = 0, 1, 2, 3, 4
 J_FIXED, J_REVOLUTE, J_PRISMATIC = 0, 1, 2
 
 
@@ -44,6 +45,30 @@ def dae_vertices(path):
     for m in re.finditer(r'<float_array id="[^"]*positions-array" count="(\d+)">([^<]*)<', s):
         out.append(np.array(m.group(2).split(), float).reshape(-1, 3))
     return np.concatenate(out, 0)
+
+
+def stl_vertices(path):
+    """Vertices of an STL mesh (binary or ASCII), duplicates removed."""
+    data = open(path, 'rb').read()
+    n = struct.unpack('<I', data[80:84])[0] if len(data) >= 84 else 0
+    if len(data) == 84 + 50 * n:
+        rec = np.frombuffer(data, dtype=np.dtype([('n', '<f4', 3), ('v', '<f4', (3, 3)), ('a', '<u2')]), count=n, offset=84)
+        v = rec['v'].reshape(-1, 3).astype(float)
+    else:
+        v = np.array([[float(x) for x in m.groups()] for m in
+                      re.finditer(rb'vertex\s+(\S+)\s+(\S+)\s+(\S+)', data)], float)
+    return np.unique(v, axis=0)
+
+
+def cylinder_vertices(radius, length):
+    """URDF cylinder as Bullet's URDF importer builds it without URDF_USE_IMPLICIT_CYLINDER: a
+    convex hull of two 32-gons at z = +-length/2 (BulletUrdfImporter, [ext] SURVEY A.7)."""
+    out = []
+    for i in range(32):
+        a = 2.0 * np.pi * i / 32.0
+        for z in (0.5 * length, -0.5 * length):
+            out.append([radius * np.sin(a), radius * np.cos(a), z])
+    return np.array(out)
 
 
 def obj_groups(path):
@@ -163,9 +188,14 @@ def parse_urdf(path):
         L = Link()
         L.name = le.get('name')
         ine = le.find('inertial')
+        L.tensor = np.zeros((3, 3))
         if ine is not None:
             L.mass = float(ine.find('mass').get('value'))
             L.com_pos, L.com_quat = _origin(ine.find('origin'))
+            it = ine.find('inertia')
+            if it is not None:
+                g = lambda k: float(it.get(k, 0.0))
+                L.tensor = np.array([[g('ixx'), g('ixy'), g('ixz')], [g('ixy'), g('iyy'), g('iyz')], [g('ixz'), g('iyz'), g('izz')]])
         else:
             L.mass = 0.0
             L.com_pos, L.com_quat = np.zeros(3), np.array([0, 0, 0, 1.0])
@@ -173,8 +203,10 @@ def parse_urdf(path):
         for ce in le.findall('collision'):
             pos, quat = _origin(ce.find('origin'))
             ge = ce.find('geometry')
-            me, be, se = ge.find('mesh'), ge.find('box'), ge.find('sphere')
-            if me is not None:
+            me, be, se, ce = ge.find('mesh'), ge.find('box'), ge.find('sphere'), ge.find('cylinder')
+            if ce is not None:
+                L.collisions.append(('cylinder', float(ce.get('radius')), float(ce.get('length')), pos, quat))
+            elif me is not None:
                 scale = np.array([float(x) for x in me.get('scale', '1 1 1').split()])
                 L.collisions.append(('mesh', os.path.join(base_dir, me.get('filename')), scale, pos, quat))
             elif be is not None:
@@ -228,6 +260,8 @@ def urdf_shapes(L, scale_override=None):
             path, scale = a, b
             if path.endswith('.dae'):
                 shapes.append(Shape(HULL, p, q, hull=Hull(dae_vertices(path) * scale)))
+            elif path.lower().endswith('.stl'):
+                shapes.append(Shape(HULL, p, q, hull=Hull(stl_vertices(path) * scale)))
             else:
                 for g in obj_groups(path):
                     shapes.append(Shape(HULL, p, q, hull=Hull(g * scale)))
@@ -235,6 +269,8 @@ def urdf_shapes(L, scale_override=None):
             shapes.append(Shape(BOX, p, q, half_extents=0.5 * a))
         elif kind == 'sphere':
             shapes.append(Shape(SPHERE, p, q, radius=a))
+        elif kind == 'cylinder':
+            shapes.append(Shape(HULL, p, q, hull=Hull(cylinder_vertices(a, b))))
     return shapes
 
 
@@ -382,21 +418,27 @@ def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
 
 
 HEAD_CHAIN = (24, 25, 26, 27)    # human joints driven under 'tremor' (feeding.py:219, env.py:307-337)
+ARM_CHAIN = (7, 8, 9, 10, 11, 12, 13)   # ScratchItch: the right arm's revolute joints (controllable 4..13, scratch_itch.py:191; 4..6 are fixed)
+HC_CAP = 8                        # avr_model_desc hc_* capacity (AVR_DESC_HC)
 
 
-def head_chain(S):
-    """Arrays of the tremor head/neck chain (include/avr_model.h hc_*): joint origins, axes,
-    masses and inertias per gender (human_creation.py:195-207; inertia from the collision
-    shapes' compound AABB as for every other link), limits (limit_scale 1: 'tremor' is not
-    'limits', world_creation.py:71), and the human slot / collision body of each link."""
-    out = dict(hc_jpos=np.zeros((2, 4, 3)), hc_axis=np.zeros((4, 3)), hc_mass=np.zeros((2, 4)),
-               hc_inertia=np.zeros((2, 4, 3)), hc_lower=np.zeros(4), hc_upper=np.zeros(4),
-               hc_slot=np.full(4, -1, np.int32), hc_body=np.full(4, -1, np.int32))
+def head_chain(S, joints=HEAD_CHAIN, cap=HC_CAP):
+    """Arrays of an articulated human chain (include/avr_model.h hc_*): joint origins, axes,
+    masses and inertias per gender (human_creation.py:163-274; inertia from the collision
+    shapes' compound AABB as for every other link), limits at limit_scale 1, and the human slot /
+    collision body of each link.  Feeding's tremor head/neck chain is joints 24..27
+    (human_creation.py:195-207); ScratchItch's is the right arm, joints 7..13
+    (human_creation.py:214-226).  The arrays are padded to `cap` links."""
+    n = len(joints)
+    out = dict(hc_jpos=np.zeros((2, cap, 3)), hc_axis=np.zeros((cap, 3)), hc_mass=np.zeros((2, cap)),
+               hc_inertia=np.zeros((2, cap, 3)), hc_lower=np.zeros(cap), hc_upper=np.zeros(cap),
+               hc_slot=np.full(cap, -1, np.int32), hc_body=np.full(cap, -1, np.int32), hc_n=np.int32(n),
+               hc_joint=np.full(cap, -1, np.int32))
     for g, gender in enumerate(('male', 'female')):
         hl = S.human[gender][1]
-        for k, li in enumerate(HEAD_CHAIN):
+        for k, li in enumerate(joints):
             L = hl[li]
-            assert L['jtype'] == J_REVOLUTE and L['parent'] == (hl[HEAD_CHAIN[0]]['parent'] if k == 0 else li - 1)
+            assert L['jtype'] == J_REVOLUTE and L['parent'] == (hl[joints[0]]['parent'] if k == 0 else li - 1)
             out['hc_jpos'][g, k] = L['pos']
             out['hc_mass'][g, k] = L['mass']
             if L['shapes'] and L['mass'] > 0:
@@ -404,8 +446,9 @@ def head_chain(S):
                 out['hc_inertia'][g, k] = box_inertia(L['mass'], lo, hi)
             out['hc_axis'][k] = L['axis']
             out['hc_lower'][k], out['hc_upper'][k] = L['lower'], L['upper']
-    out['hc_parent_slot'] = np.int32(S.human_slots.index(S.human['male'][1][HEAD_CHAIN[0]]['parent']))
-    for k, li in enumerate(HEAD_CHAIN):
+            out['hc_joint'][k] = li
+    out['hc_parent_slot'] = np.int32(S.human_slots.index(S.human['male'][1][joints[0]]['parent']))
+    for k, li in enumerate(joints):
         if li in S.human_slots:
             out['hc_slot'][k] = S.human_slots.index(li)
             out['hc_body'][k] = S.human_body[li]
@@ -604,6 +647,256 @@ def compile_feeding_jaco():
     return S
 
 
+# ----------------------------------------------------------------------------- ScratchItchPR2
+PR2_URDF = 'PR2/pr2_no_torso_lift_tall.urdf'
+PR2_LEFT_ROOT = 64                                       # l_shoulder_pan_joint (DFS index)
+PR2_LEFT_ARM = (64, 65, 66, 68, 69, 71, 72)             # world_creation.py:189
+PR2_RIGHT_ARM = (42, 43, 44, 46, 47, 49, 50)            # world_creation.py:188
+PR2_RIGHT_ARM_RESET = (-1.75, 1.25, -1.5, -0.5, -1, 0, -1)   # env.py:459-460 (reset_robot_joints)
+PR2_LEFT_FINGERS = (79, 80, 81, 82)                     # world_creation.py:311
+PR2_TOOL_LINK = 76                                       # l_gripper_tool_frame (world_creation.py:332,363)
+PR2_TORSO_LINK = 15                                      # scratch_itch.py:105 (obs origin)
+PR2_TOOL_FILTER = range(71, 86)                          # world_creation.py:357-360: tool vs these links off
+# static PR2 links (not in the left arm's subtree), grouped into robot-fixed bodies: base +
+# casters, torso + head + laser, right arm
+PR2_STATIC_GROUPS = (('pr2_base', range(0, 15)), ('pr2_torso', list(range(15, 42)) + [86]), ('pr2_right_arm', range(42, 64)))
+
+
+def principal_frame(L):
+    """URDF_USE_INERTIA_FROM_FILE (world_creation.py:187): Bullet diagonalises the file inertia
+    tensor and turns the link's inertial frame onto its principal axes [ext, SURVEY A.2].
+    Returns (principal moments, inertial-frame quaternion)."""
+    T = L.tensor
+    if not np.any(T):
+        return np.zeros(3), L.com_quat
+    w, V = np.linalg.eigh(T)
+    if np.linalg.det(V) < 0:
+        V[:, 2] = -V[:, 2]
+    # rotation matrix -> quaternion (x, y, z, w)
+    R = V
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0:
+        S4 = np.sqrt(tr + 1.0) * 2
+        q = np.array([(R[2, 1] - R[1, 2]) / S4, (R[0, 2] - R[2, 0]) / S4, (R[1, 0] - R[0, 1]) / S4, 0.25 * S4])
+    else:
+        i = int(np.argmax([R[0, 0], R[1, 1], R[2, 2]]))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        S4 = np.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2
+        q = np.zeros(4)
+        q[i] = 0.25 * S4
+        q[j] = (R[j, i] + R[i, j]) / S4
+        q[k] = (R[k, i] + R[i, k]) / S4
+        q[3] = (R[k, j] - R[j, k]) / S4
+    q = q / np.linalg.norm(q)
+    return w, G.quat_mul(L.com_quat, q)
+
+
+def pr2_fk(dfs, q_of):
+    """URDF link frames of every PR2 link in the base_footprint frame for joint values q_of[i]."""
+    n = len(dfs)
+    P = np.zeros((n, 3)); Q = np.zeros((n, 4))
+    for i, (J, parent) in enumerate(dfs):
+        pp, pq = (np.zeros(3), np.array([0, 0, 0, 1.0])) if parent < 0 else (P[parent], Q[parent])
+        p, qq = G.tf_mul(pp, pq, J['pos'], J['quat'])
+        ax = J['axis'] / max(np.linalg.norm(J['axis']), 1e-12)
+        v = q_of.get(i, 0.0)
+        if J['type'] in ('revolute', 'continuous'):
+            qq = G.quat_mul(qq, G.quat_axis_angle(ax, v))
+        elif J['type'] == 'prismatic':
+            p = p + G.quat_rotate(qq, ax) * v
+        P[i], Q[i] = p, qq
+    return P, Q
+
+
+def build_pr2():
+    """The PR2 as ScratchItchPR2-v0 simulates it (world_creation.py:181-217, env.py:450-464):
+    fixed base, inertia from file, no self-collision.  Its articulated part is the left arm's
+    subtree (links 64..85, 14 DoF); every other link keeps the pose of reset_robot_joints
+    (zeros, right arm tucked) for the whole episode -- zero gravity (scratch_itch.py:259), no
+    motor target change and no contact pushes them -- and collides as robot-fixed geometry."""
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, PR2_URDF))
+    for J, _ in dfs:
+        L = links[J['child']]
+        L.inertia, L.com_quat = principal_frame(L)
+    rootL = links[root]
+    rootL.inertia, rootL.com_quat = principal_frame(rootL)
+    q_of = {j: v for j, v in zip(PR2_RIGHT_ARM, PR2_RIGHT_ARM_RESET)}
+    P, Q = pr2_fk(dfs, q_of)
+    # subtree of the left arm root, in DFS order
+    sub = [PR2_LEFT_ROOT]
+    for i in range(PR2_LEFT_ROOT + 1, len(dfs)):
+        if dfs[i][1] in sub:
+            sub.append(i)
+    rob = dict(name=[], parent=[], jtype=[], dof=[], jpos=[], jquat=[], axis=[], com_pos=[], com_quat=[],
+               mass=[], inertia=[], lower=[], upper=[], has_limit=[], shapes=[], friction=[], urdf=[])
+    ndof = 0
+    for i in sub:
+        J, parent = dfs[i]
+        L = links[J['child']]
+        t = {'fixed': J_FIXED, 'revolute': J_REVOLUTE, 'continuous': J_REVOLUTE, 'prismatic': J_PRISMATIC}[J['type']]
+        rob['urdf'].append(i)
+        rob['name'].append(L.name)
+        if i == PR2_LEFT_ROOT:
+            rob['parent'].append(-1)
+            jp, jq = G.tf_mul(P[parent], Q[parent], J['pos'], J['quat'])   # torso_lift_link (static) x joint origin
+        else:
+            rob['parent'].append(sub.index(parent))
+            jp, jq = J['pos'], J['quat']
+        rob['jtype'].append(t)
+        rob['dof'].append(ndof if t != J_FIXED else -1)
+        if t != J_FIXED:
+            ndof += 1
+        rob['jpos'].append(np.asarray(jp))
+        rob['jquat'].append(np.asarray(jq))
+        rob['axis'].append(J['axis'] / max(np.linalg.norm(J['axis']), 1e-12) if t != J_FIXED else np.zeros(3))
+        rob['com_pos'].append(L.com_pos)
+        rob['com_quat'].append(L.com_quat)
+        rob['mass'].append(L.mass)
+        rob['inertia'].append(L.inertia)
+        rob['shapes'].append(urdf_shapes(L))
+        lim = J['type'] in ('revolute', 'prismatic') and J['lower'] <= J['upper']
+        rob['lower'].append(J['lower'] if lim else 0.0)
+        rob['upper'].append(J['upper'] if lim else -1.0)
+        rob['has_limit'].append(1 if lim else 0)
+        rob['friction'].append(L.friction)
+    rob['ndof'] = ndof
+    # robot-fixed geometry: shapes of the static links placed in the base_footprint frame
+    groups = []
+    for name, members in PR2_STATIC_GROUPS:
+        shapes = []
+        for i in members:
+            if i in sub:
+                continue
+            L = links[dfs[i][0]['child']]
+            cp, cq = G.tf_mul(P[i], Q[i], L.com_pos, L.com_quat)
+            for s in urdf_shapes(L):
+                s.pos, s.quat = G.tf_mul(cp, cq, s.pos, s.quat)
+                shapes.append(s)
+        groups.append((name, shapes))
+    L15 = links[dfs[PR2_TORSO_LINK][0]['child']]
+    torso_com = G.tf_mul(P[PR2_TORSO_LINK], Q[PR2_TORSO_LINK], L15.com_pos, L15.com_quat)[0]
+    # base_footprint: inertial origin 0, so PyBullet's base (COM) pose is the URDF root frame
+    assert np.allclose(rootL.com_pos, 0)
+    return rob, groups, torso_com, sub
+
+
+def build_scratcher():
+    """tool_scratch.urdf (world_creation.py:344): handle (base) + tool cylinder + tip sphere,
+    welded by fixed joints, loaded without URDF_USE_INERTIA_FROM_FILE (inertia per link from its
+    collision AABB).  A floating base with only fixed links moves as one rigid body: the three
+    links are composed into one free body at the composite COM, axes those of the handle (every
+    link's principal axes are the handle's).  Returns the body plus the offsets, in that body
+    frame, of the handle origin (the fixed constraint's child pivot, world_creation.py:363) and of
+    tool link 1's COM (getLinkState(tool, 1), scratch_itch.py:51,106)."""
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, 'scratcher', 'tool_scratch.urdf'))
+    parts = [(links[root], np.zeros(3), np.array([0, 0, 0, 1.0]))]
+    frames = {root: (np.zeros(3), np.array([0, 0, 0, 1.0]))}
+    for J, parent in dfs:
+        pp, pq = frames[J['parent']]
+        frames[J['child']] = G.tf_mul(pp, pq, J['pos'], J['quat'])
+        parts.append((links[J['child']],) + frames[J['child']])
+    mass = sum(L.mass for L, _, _ in parts)
+    coms = [G.tf_mul(p, q, L.com_pos, L.com_quat)[0] for L, p, q in parts]
+    c = sum(L.mass * cm for (L, _, _), cm in zip(parts, coms)) / mass
+    I = np.zeros(3)
+    shapes = []
+    for (L, p, q), cm in zip(parts, coms):
+        sh = urdf_shapes(L)
+        lo, hi = compound_aabb(sh)
+        Ii = box_inertia(L.mass, lo, hi)
+        assert np.allclose(q, [0, 0, 0, 1]) and np.allclose(L.com_quat, [0, 0, 0, 1])
+        d = cm - c
+        I += Ii + L.mass * (np.dot(d, d) - d * d)        # parallel axes (offsets along the handle axes)
+        lp, lq = G.tf_mul(p, q, L.com_pos, L.com_quat)
+        for s in sh:
+            s.pos, s.quat = G.tf_mul(lp - c, lq, s.pos, s.quat)
+            shapes.append(s)
+    tip = frames['tool_tip'][0] + links['tool_tip'].com_pos
+    return dict(mass=mass, inertia=I, shapes=shapes, friction=links[root].friction,
+                pivot=-c, tip=tip - c, handle_shapes=len(urdf_shapes(links[root])))
+
+
+def compile_scratch_pr2():
+    """ScratchItchPR2-v0 scene (scratch_itch.py:130-273 + world_creation.py:27-93,181-217,
+    330-365): plane, wheelchair, the human (right arm 7..13 articulated: controllable joints
+    4..13 keep their masses, world_creation.py:157-161), the PR2 and the scratcher."""
+    S = Scene()
+    rob, groups, torso_com, sub = build_pr2()
+    S.robot = rob
+    S.robot_base_pos = np.zeros(3)                 # per env (position_robot_toc): lives in the state
+    S.robot_base_quat = np.array([0, 0, 0, 1.0])
+    robot_body = {}
+    for i in range(len(rob['name'])):
+        if rob['shapes'][i]:
+            robot_body[i] = S.add_body(KIND_ROBOT, i, rob['shapes'][i], rob['friction'][i], rob['name'][i])
+    rstatic_body = [S.add_body(KIND_RSTATIC, k, shapes, 0.5, name) for k, (name, shapes) in enumerate(groups)]
+    tool = build_scratcher()
+    S.free = [dict(name='scratcher', mass=tool['mass'], inertia=tool['inertia'], gravity=np.zeros(3))]
+    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'scratcher')
+    plane = build_static_urdf('plane/plane.urdf')
+    chair = build_static_urdf('wheelchair/wheelchair.urdf')
+    S.static = [dict(name='plane', pos=np.zeros(3), quat=np.array([0, 0, 0, 1.0])),
+                dict(name='wheelchair', pos=np.array([0.0, 0.09, -0.01]),
+                     quat=G.quat_from_euler([np.pi / 2.0, 0, -np.pi / 2.0 - 0.05]))]
+    static_body = [S.add_body(KIND_STATIC, 0, plane['shapes'], plane['friction'], 'plane'),
+                   S.add_body(KIND_STATIC, 1, chair['shapes'], chair['friction'], 'wheelchair')]
+    S.human = {}
+    human_body = {}
+    for gender in ('male', 'female'):
+        S.human[gender] = build_human(gender)
+    slot_links = [-1] + [i for i, L in enumerate(S.human['male'][1]) if L['shapes']]
+    S.human_slots = slot_links
+    for si, li in enumerate(slot_links):
+        shapes = []
+        for gi, gender in enumerate(('male', 'female')):
+            base_shapes, hl = S.human[gender]
+            for s in (base_shapes if li < 0 else hl[li]['shapes']):
+                s.gender = gi
+                shapes.append(s)
+        human_body[li] = S.add_body(KIND_HUMAN, si, shapes, 0.5, 'human%d' % li)
+    chain = [human_body[li] for li in ARM_CHAIN if li in human_body]
+    # right arm self-collision partners (human_creation.py:283-285: links 7..13 vs -1..3, 14..41)
+    arm_partners = [human_body[li] for li in slot_links if li < 4 or li >= 14]
+    pairs = []
+    for li, b in sorted(robot_body.items()):
+        if not (PR2_LEFT_ROOT + li in PR2_TOOL_FILTER):
+            pairs.append((b, tool_body))
+        for sb in static_body:
+            pairs.append((b, sb))
+        for h in slot_links:
+            pairs.append((b, human_body[h]))
+    for rb in rstatic_body:                        # robot-fixed geometry vs the moving bodies
+        pairs.append((rb, tool_body))
+        for hb in chain:
+            pairs.append((rb, hb))
+    for sb in static_body:
+        pairs.append((tool_body, sb))
+    for h in slot_links:
+        pairs.append((tool_body, human_body[h]))
+    for hb in chain:
+        for sb in static_body:
+            pairs.append((hb, sb))
+        for pb in arm_partners:
+            pairs.append((hb, pb))
+    S.n_pairs_base = len(pairs)
+    S.pairs = pairs
+    S.robot_body = robot_body
+    S.free_body = [tool_body]
+    S.static_body = static_body
+    S.human_body = human_body
+    S.rstatic = groups
+    S.task = dict(
+        arm_dofs=[rob['dof'][sub.index(j)] for j in PR2_LEFT_ARM],
+        finger_dofs=[rob['dof'][sub.index(j)] for j in PR2_LEFT_FINGERS],
+        tool_link=sub.index(PR2_TOOL_LINK), torso_com=torso_com,
+        tool_pos_offset=np.zeros(3), tool_orient_offset=np.array([0, 0, 0, 1.0]),   # scratch_itch.py:193
+        tool_pivot=tool['pivot'], tool_tip=tool['tip'], tool_handle_shapes=tool['handle_shapes'],
+        # generate_target (scratch_itch.py:275-287): limb link, capsule length and radius per gender
+        limbs={'male': [(9, 0.279, 0.043), (11, 0.257, 0.033)], 'female': [(9, 0.264, 0.0355), (11, 0.234, 0.027)]},
+    )
+    return S
+
+
 def to_arrays(S):
     """Flatten a Scene into the arrays of include/avr_model.h (float64 / int32)."""
     rob = S.robot
@@ -689,11 +982,8 @@ def to_arrays(S):
     return A
 
 
-def compile_all(out_dir=DATA_DIR):
-    os.makedirs(out_dir, exist_ok=True)
-    S = compile_feeding_jaco()
-    A = to_arrays(S)
-    # human kinematic tables (host reset path) for both genders
+def _human_tables(S, A):
+    """Human kinematic tables for the host reset path, both genders."""
     for gender in ('male', 'female'):
         base_shapes, hl = S.human[gender]
         A['human_%s_parent' % gender] = np.array([L['parent'] for L in hl], np.int32)
@@ -704,7 +994,14 @@ def compile_all(out_dir=DATA_DIR):
         A['human_%s_upper' % gender] = np.array([L['upper'] for L in hl])
     A['human_slot_link'] = np.array(S.human_slots, np.int32)
     A['n_pairs_base'] = np.int32(S.n_pairs_base)
-    A.update(head_chain(S))
+
+
+def compile_feeding(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    S = compile_feeding_jaco()
+    A = to_arrays(S)
+    _human_tables(S, A)
+    A.update(head_chain(S, HEAD_CHAIN, cap=4))
     t = S.task
     A['task_arm_dofs'] = np.array(t['arm_dofs'], np.int32)
     A['task_finger_dofs'] = np.array(t['finger_dofs'], np.int32)
@@ -725,8 +1022,40 @@ def compile_all(out_dir=DATA_DIR):
     return path, A
 
 
+def compile_scratch(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    S = compile_scratch_pr2()
+    A = to_arrays(S)
+    _human_tables(S, A)
+    A.update(head_chain(S, ARM_CHAIN, cap=HC_CAP))
+    t = S.task
+    A['task_arm_dofs'] = np.array(t['arm_dofs'], np.int32)
+    A['task_finger_dofs'] = np.array(t['finger_dofs'], np.int32)
+    A['task_tool_link'] = np.int32(t['tool_link'])
+    A['task_tool_offset'] = np.concatenate([t['tool_pos_offset'], t['tool_orient_offset']])
+    A['task_torso_com'] = np.asarray(t['torso_com'], float)
+    A['task_tool_pivot'] = np.asarray(t['tool_pivot'], float)
+    A['task_tool_tip'] = np.asarray(t['tool_tip'], float)
+    A['task_tool_handle_shapes'] = np.int32(t['tool_handle_shapes'])
+    A['task_tool_body'] = np.int32(S.free_body[0])
+    A['task_human_body0'] = np.int32(S.human_body[S.human_slots[0]])
+    A['task_limbs'] = np.array([[[li, ln, r] for li, ln, r in t['limbs'][g]] for g in ('male', 'female')], float)
+    A['n_rstatic'] = np.int32(len(S.rstatic))
+    A['rl_urdf'] = np.array(S.robot['urdf'], np.int32)
+    path = os.path.join(out_dir, 'scratch_itch_pr2.npz')
+    np.savez_compressed(path, **A)
+    return path, A
+
+
+def compile_all(out_dir=DATA_DIR):
+    """Both compiled scenes; returns the FeedingJaco one (path, arrays) first."""
+    out = compile_feeding(out_dir)
+    compile_scratch(out_dir)
+    return out
+
+
 if __name__ == '__main__':
-    path, A = compile_all()
-    print(path)
-    for k, v in A.items():
-        print('%-24s %s %s' % (k, getattr(v, 'shape', ()), getattr(v, 'dtype', type(v))))
+    for path, A in (compile_feeding(), compile_scratch()):
+        print(path)
+        for k, v in A.items():
+            print('%-24s %s %s' % (k, getattr(v, 'shape', ()), getattr(v, 'dtype', type(v))))

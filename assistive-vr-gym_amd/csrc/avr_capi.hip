@@ -1,4 +1,6 @@
-// avr_capi.hip -- C-ABI of libavr.so (include/avr.h): device arenas, scene upload, launches.
+// avr_capi.hip -- body of the C-ABI of libavr.so (include/avr.h) for one task: device arenas, scene
+// upload, launches.  Included once per task inside that task's namespace (avr_task_*.hip); the
+// extern "C" entry points in avr_api.cpp dispatch to it by the handle's task.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -11,19 +13,6 @@
 #include <cmath>
 
 #include "../../include/avr.h"
-
-// KModel is defined in avr_kernel.hip; it is mirrored here field by field via a shared header
-// section to keep one definition.
-#define AVR_KMODEL_ONLY
-#include "avr_kmodel.h"
-
-extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
-                                      unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int env0,
-                                      int env1, hipStream_t stream, avr_evlog *log);
-extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st);
-extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
-                                                hipStream_t stream);
-extern "C" hipError_t avr_kernel_attrs(int *out16);
 
 #define AVR_MAX_GROUPS 8
 
@@ -51,6 +40,8 @@ struct avr_sim {
     std::vector<int> evkind;
     double kt_ms[AVR_K_KINDS];
     long long kt_n[AVR_K_KINDS];
+    float *d_query;                        // device scratch of the state queries (avr_get_*)
+    size_t qcap;
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -138,10 +129,8 @@ static std::vector<float> poses(const double *pos, const double *quat, int n) {
     return v;
 }
 
-extern "C" int32_t avr_state_words(void) { return AVR_STATE_WORDS; }
-extern "C" int32_t avr_abi_version(void) { return AVR_ABI_VERSION; }
 
-extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
+int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     if (!cfg || !d || !out) return -1;
     *out = nullptr;
     avr_sim *s = new avr_sim();
@@ -150,12 +139,21 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     if (cfg->n_envs <= 0) { int r = fail(s, -1, "n_envs must be > 0"); *out = s; return r; }
     if (cfg->flags & AVR_CFG_RESERVED_MASK) { int r = fail(s, -1, "avr_config.flags 0x%x: no flag is defined", (unsigned)cfg->flags); *out = s; return r; }
     const int hc = d->hc_n > 0 ? d->hc_n : 0;
-    if (d->n_links + hc > AVR_MAX_LINKS || d->n_dof + hc > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE || d->n_human > AVR_MAX_HUMAN ||
-        d->n_bodies > MAXB || d->n_pairs > 65535 || d->n_shapes > MAXSH || d->n_arm > AVR_ACT_DIM || hc > AVR_HC_N) {
+    if (d->task != AVR_TASK) { int r = fail(s, -2, "model task %d does not match this instantiation (%d)", (int)d->task, (int)AVR_TASK); *out = s; return r; }
+    if (d->n_links + hc > K_MAX_LINKS || d->n_dof + hc > K_MAX_DOF || d->n_free > K_MAX_FREE || d->n_human > K_MAX_HUMAN ||
+        d->n_bodies > MAXB || d->n_pairs > 65535 || d->n_shapes > MAXSH || d->n_arm > K_ACT_DIM || hc > K_HC_N || hc > AVR_DESC_HC ||
+        d->n_free < 1) {
         int r = fail(s, -2, "model exceeds compiled capacities");
         *out = s;
         return r;
     }
+    for (int b = 0; b < d->n_bodies; b++)
+        if (d->body_shape_count[b] > 128 || d->body_shape_count[b] < 0) {
+            // the pair kernel's culled child lists (candA / candB) hold 128 entries
+            int r = fail(s, -2, "body %d has %d shapes (> 128)", b, (int)d->body_shape_count[b]);
+            *out = s;
+            return r;
+        }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) { int r = fail(s, -4, "no HIP device available (%s)", hipGetErrorString(e)); *out = s; return r; }
@@ -228,6 +226,14 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     }
     k.hc_parent_slot = d->hc_parent_slot;
     k.human_gain = (float)d->human_gain; k.human_force = (float)d->human_force;
+    for (int q = 0; q < 3; q++) {
+        k.hc_grav[q] = (float)d->human_gravity[q];
+        k.fix_pivot_b[q] = (float)d->fix_pivot_b[q];
+        k.tool_tip[q] = (float)d->tool_tip[q];
+        k.torso_com[q] = (float)d->torso_com[q];
+    }
+    k.tool_handle_shapes = d->tool_handle_shapes;
+    k.w_tool_force = (float)d->w_tool_force; k.w_scratch = (float)d->w_scratch;
     int r;
     if ((r = upload(s, par, &k.rl_parent))) return r;
     if ((r = upload(s, jt, &k.rl_jtype))) return r;
@@ -342,7 +348,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     k.tool_link = d->tool_link; k.torso_link = d->torso_link; k.head_slot = d->head_slot;
     k.spoon_free = d->spoon_free; k.bowl_free = d->bowl_free; k.food_free0 = d->food_free0; k.n_food = d->n_food;
     k.table_body = d->table_body; k.bowl_body = d->bowl_body; k.spoon_body = d->spoon_body; k.food_body0 = d->food_body0;
-    k.tool_body = -1;
+    k.tool_body = d->spoon_body;     // the tool on the fixed constraint (spoon / scratcher)
     for (int i = 0; i < 7; i++) k.tool_offset[i] = (float)d->tool_offset[i];
     for (int g = 0; g < 2; g++)
         for (int i = 0; i < 3; i++) k.mouth[g][i] = (float)d->mouth_offset[g][i];
@@ -357,7 +363,7 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     k.task_success_threshold = (float)d->task_success_threshold;
     k.seed = cfg->seed;
     k.env_offset = cfg->env_offset;
-    for (int i = 0; i < AVR_MAX_DOF; i++) k.dof_link[i] = 0;
+    for (int i = 0; i < K_MAX_DOF; i++) k.dof_link[i] = 0;
     for (int l = 0; l < nla; l++)
         if (dofv[l] >= 0) k.dof_link[dofv[l]] = l;
     for (int l = 0; l < nla; l++) {
@@ -379,10 +385,10 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     }
     size_t E = (size_t)cfg->n_envs;
     // per-env constraint-row scratch (written and read inside each sub-step)
-    k.rowcap = MAXNC + 3 * AVR_MAX_CONTACTS;
+    k.rowcap = MAXNC + 3 * K_MAX_CONTACTS;
     // records [rowcap][20] then robot parts [rowcap][32]; part B reads the whole row buffer
     // through one buffer resource with 32-bit byte offsets below B4_OOB (avr_kernel.hip)
-    k.rowstride = 52 * k.rowcap;
+    k.rowstride = (RWC + ROBW) * k.rowcap;
     k.rows_envs = (int)E;
     k.b4_global = getenv("AVR_B4_GLOBAL") && getenv("AVR_B4_GLOBAL")[0] == '1';
     if (E * (size_t)k.rowstride * sizeof(float) >= 0x7fff0000ull) {
@@ -409,14 +415,14 @@ extern "C" int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_si
     }
     HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
-    HIPCHK(s, hipMalloc(&s->d_state, E * AVR_STATE_WORDS * sizeof(float)));
-    HIPCHK(s, hipMemset(s->d_state, 0, E * AVR_STATE_WORDS * sizeof(float)));
-    HIPCHK(s, hipMalloc(&s->d_act, E * AVR_ACT_DIM * sizeof(float)));
-    HIPCHK(s, hipMalloc(&s->d_obs, E * AVR_OBS_DIM * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_state, E * K_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMemset(s->d_state, 0, E * K_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_act, E * K_ACT_DIM * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_obs, E * K_OBS_DIM * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_rew, E * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_done, E));
     HIPCHK(s, hipMalloc(&s->d_info, E * AVR_INFO_DIM * sizeof(float)));
-    HIPCHK(s, hipMalloc(&s->d_stage, E * AVR_STATE_WORDS * sizeof(float)));
+    HIPCHK(s, hipMalloc(&s->d_stage, E * K_STATE_WORDS * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_mask, E));
     return 0;
 }
@@ -449,7 +455,7 @@ static hipError_t run_step(avr_sim *s, float *state, const float *act, float *ob
     return hipSuccess;
 }
 
-extern "C" int avr_destroy(avr_sim *s) {
+int avr_destroy(avr_sim *s) {
     if (!s) return -1;
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void *p : s->allocs) (void)hipFree(p);
@@ -462,6 +468,7 @@ extern "C" int avr_destroy(avr_sim *s) {
     if (s->d_info) (void)hipFree(s->d_info);
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->d_mask) (void)hipFree(s->d_mask);
+    if (s->d_query) (void)hipFree(s->d_query);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     for (int i = 0; i < s->ngroups; i++) {
         if (s->gstream[i]) (void)hipStreamDestroy(s->gstream[i]);
@@ -473,18 +480,18 @@ extern "C" int avr_destroy(avr_sim *s) {
     return 0;
 }
 
-extern "C" const char *avr_last_error(avr_sim *s) { return s ? s->err : "null handle"; }
-extern "C" void *avr_stream(avr_sim *s) { return s ? (void *)s->stream : nullptr; }
-extern "C" void *avr_state_device_ptr(avr_sim *s) { return s ? (void *)s->d_state : nullptr; }
-extern "C" int32_t avr_n_envs(avr_sim *s) { return s ? s->cfg.n_envs : 0; }
-extern "C" int32_t avr_env_groups(avr_sim *s) { return s ? s->ngroups : 0; }
+const char *avr_last_error(avr_sim *s) { return s ? s->err : "null handle"; }
+void *avr_stream(avr_sim *s) { return s ? (void *)s->stream : nullptr; }
+void *avr_state_device_ptr(avr_sim *s) { return s ? (void *)s->d_state : nullptr; }
+int32_t avr_n_envs(avr_sim *s) { return s ? s->cfg.n_envs : 0; }
+int32_t avr_env_groups(avr_sim *s) { return s ? s->ngroups : 0; }
 
 #define CHECK_SIM(s) \
     if (!(s) || !(s)->d_state) return -1
 
-extern "C" int avr_set_state(avr_sim *s, const float *h) {
+int avr_set_state(avr_sim *s, const float *h) {
     CHECK_SIM(s);
-    HIPCHK(s, hipMemcpyAsync(s->d_state, h, (size_t)s->cfg.n_envs * AVR_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(s->d_state, h, (size_t)s->cfg.n_envs * K_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
@@ -493,13 +500,13 @@ extern "C" int avr_set_state(avr_sim *s, const float *h) {
 // selected env rows (one transfer instead of one per env).
 static int upload_masked(avr_sim *s, const uint8_t *mask, const float *h) {
     const size_t E = (size_t)s->cfg.n_envs;
-    HIPCHK(s, hipMemcpyAsync(s->d_stage, h, E * AVR_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(s->d_stage, h, E * K_STATE_WORDS * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, hipMemcpyAsync(s->d_mask, mask, E, hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, avr_launch_copy_masked(s->d_state, s->d_stage, s->d_mask, s->cfg.n_envs, s->stream));
     return 0;
 }
 
-extern "C" int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float *h) {
+int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float *h) {
     CHECK_SIM(s);
     if (!mask) return avr_set_state(s, h);
     if (upload_masked(s, mask, h)) return -2;
@@ -507,7 +514,7 @@ extern "C" int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float
     return 0;
 }
 
-extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_t n_frames, float *host_obs) {
+int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
     const size_t E = (size_t)s->cfg.n_envs;
     std::vector<uint8_t> all;
@@ -517,32 +524,32 @@ extern "C" int avr_reset(avr_sim *s, const uint8_t *mask, const float *h, int32_
     if (upload_masked(s, mask, h)) return -2;
     HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames));
     if (host_obs) {
-        std::vector<float> o(E * AVR_OBS_DIM);
-        HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+        std::vector<float> o(E * K_OBS_DIM);
+        HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * K_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
         HIPCHK(s, hipStreamSynchronize(s->stream));
         for (size_t e = 0; e < E; e++)
-            if (mask[e]) memcpy(host_obs + e * AVR_OBS_DIM, o.data() + e * AVR_OBS_DIM, AVR_OBS_DIM * sizeof(float));
+            if (mask[e]) memcpy(host_obs + e * K_OBS_DIM, o.data() + e * K_OBS_DIM, K_OBS_DIM * sizeof(float));
     }
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
-extern "C" int avr_get_state(avr_sim *s, float *h) {
+int avr_get_state(avr_sim *s, float *h) {
     CHECK_SIM(s);
-    HIPCHK(s, hipMemcpyAsync(h, s->d_state, (size_t)s->cfg.n_envs * AVR_STATE_WORDS * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(h, s->d_state, (size_t)s->cfg.n_envs * K_STATE_WORDS * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
-extern "C" int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
+int avr_settle(avr_sim *s, int32_t n_frames, float *host_obs) {
     CHECK_SIM(s);
     HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 2, n_frames));
-    if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (host_obs) HIPCHK(s, hipMemcpyAsync(host_obs, s->d_obs, (size_t)s->cfg.n_envs * K_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
-extern "C" int avr_substep(avr_sim *s, float dt) {
+int avr_substep(avr_sim *s, float dt) {
     CHECK_SIM(s);
     long long t = 0;
     memcpy(&t, &dt, sizeof(float));
@@ -551,31 +558,31 @@ extern "C" int avr_substep(avr_sim *s, float dt) {
     return 0;
 }
 
-extern "C" int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
+int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
     HIPCHK(s, run_step(s, s->d_state, d_act, d_obs, d_rew, d_done, d_info, nullptr, 0, 0));
     return 0;
 }
 
-extern "C" int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
+int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
     HIPCHK(s, run_step(s, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
                               d_info ? d_info : s->d_info, nullptr, 1, t));
     return 0;
 }
 
-extern "C" int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {
+int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {
     CHECK_SIM(s);
     HIPCHK(s, avr_launch_random_actions(s->cfg.seed, s->cfg.env_offset, t, d_act, s->cfg.n_envs, s->km.n_arm, s->stream));
     return 0;
 }
 
-extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
+int avr_step(avr_sim *s, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
     CHECK_SIM(s);
     size_t E = (size_t)s->cfg.n_envs;
-    HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * AVR_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(s->d_act, act, E * K_ACT_DIM * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, run_step(s, s->d_state, s->d_act, s->d_obs, s->d_rew, s->d_done, s->d_info, nullptr, 0, 0));
-    HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * AVR_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(obs, s->d_obs, E * K_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(rew, s->d_rew, E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(done, s->d_done, E, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipMemcpyAsync(info, s->d_info, E * AVR_INFO_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
@@ -583,23 +590,23 @@ extern "C" int avr_step(avr_sim *s, const float *act, float *obs, float *rew, ui
     return 0;
 }
 
-extern "C" int avr_sync(avr_sim *s) {
+int avr_sync(avr_sim *s) {
     CHECK_SIM(s);
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
 
 // Diagnostic builds (-DAVR_PROF): attach a device buffer [n_envs][16] of per-phase cycle counters.
-extern "C" int avr_set_profile_buffer(avr_sim *s, void *d_prof) {
+int avr_set_profile_buffer(avr_sim *s, void *d_prof) {
     CHECK_SIM(s);
     s->km.prof = (unsigned long long *)d_prof;
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
     return 0;
 }
 
-extern "C" int avr_kernel_info(avr_sim *s, int32_t *out16) {
+int avr_kernel_info(avr_sim *s, int32_t *out20) {
     (void)s;
-    hipError_t e = avr_kernel_attrs(out16);
+    hipError_t e = avr_kernel_attrs(out20);
     return e == hipSuccess ? 0 : -3;
 }
 
@@ -620,7 +627,7 @@ static int drain_evlog(avr_sim *s) {
     return 0;
 }
 
-extern "C" int avr_profile_kernels(avr_sim *s, int32_t enable) {
+int avr_profile_kernels(avr_sim *s, int32_t enable) {
     CHECK_SIM(s);
     if (drain_evlog(s)) return -3;
     for (int k = 0; k < AVR_K_KINDS; k++) { s->kt_ms[k] = 0; s->kt_n[k] = 0; }
@@ -636,9 +643,63 @@ extern "C" int avr_profile_kernels(avr_sim *s, int32_t enable) {
     return 0;
 }
 
-extern "C" int avr_kernel_times(avr_sim *s, double *ms8, int64_t *count8) {
+int avr_kernel_times(avr_sim *s, double *ms8, int64_t *count8) {
     CHECK_SIM(s);
     if (drain_evlog(s)) return -3;
     for (int k = 0; k < AVR_K_KINDS; k++) { ms8[k] = s->kt_ms[k]; count8[k] = s->kt_n[k]; }
+    return 0;
+}
+
+// ------------------------------------------------------------------ state queries
+int32_t avr_n_dof(avr_sim *s) { return s ? s->km.nd + s->km.hc_n : 0; }
+
+// device scratch for the getters: one buffer, grown on demand
+static int query_buf(avr_sim *s, size_t floats, float **out) {
+    if (floats > s->qcap) {
+        if (s->d_query) HIPCHK(s, hipFree(s->d_query));
+        s->d_query = nullptr;
+        s->qcap = 0;
+        HIPCHK(s, hipMalloc(&s->d_query, floats * sizeof(float)));
+        s->qcap = floats;
+    }
+    *out = s->d_query;
+    return 0;
+}
+
+int avr_get_q(avr_sim *s, float *q, float *qd) {
+    CHECK_SIM(s);
+    const int nd = avr_n_dof(s), E = s->cfg.n_envs;
+    const size_t n = (size_t)nd * E;
+    float *d = nullptr;
+    if (query_buf(s, 2 * n, &d)) return -3;
+    HIPCHK(s, avr_launch_get_q(s->d_state, q ? d : nullptr, qd ? d + n : nullptr, nd, E, s->stream));
+    if (q) HIPCHK(s, hipMemcpyAsync(q, d, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (qd) HIPCHK(s, hipMemcpyAsync(qd, d + n, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+int avr_get_link_pose(avr_sim *s, int32_t link, float *out7) {
+    CHECK_SIM(s);
+    if (!out7) return fail(s, -1, "avr_get_link_pose: out7 is NULL");
+    if (link >= s->km.nla) return fail(s, -1, "avr_get_link_pose: link %d out of range (%d articulated links)", (int)link, s->km.nla);
+    const int E = s->cfg.n_envs;
+    float *d = nullptr;
+    if (query_buf(s, (size_t)7 * E, &d)) return -3;
+    HIPCHK(s, avr_launch_link_pose(s->d_km, s->d_state, d, link < 0 ? -1 : link, E, s->stream));
+    HIPCHK(s, hipMemcpyAsync(out7, d, (size_t)7 * E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+int avr_get_contact_summary(avr_sim *s, float *out4) {
+    CHECK_SIM(s);
+    if (!out4) return fail(s, -1, "avr_get_contact_summary: out4 is NULL");
+    const int E = s->cfg.n_envs;
+    float *d = nullptr;
+    if (query_buf(s, (size_t)4 * E, &d)) return -3;
+    HIPCHK(s, avr_launch_contact_summary(s->d_km, s->d_state, d, E, s->stream));
+    HIPCHK(s, hipMemcpyAsync(out4, d, (size_t)4 * E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }

@@ -57,7 +57,7 @@ typedef const __attribute__((address_space(1))) f2v *gf2p;
 // --------------------------------------------------------------------------- LDS layout
 #define AVR_PROF_SLOTS 48   // diagnostic build: per-env cycle / event counters (tools/prof_phases.py)
 struct EnvLDS {
-    float st[AVR_S_CP];     // state words before the contact cache; the cache lives in global memory
+    float st[S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
     float btf[MAXB][8];
     float Mi[MAXD][MAXD];   // Cholesky factor of the mass matrix (lower)
@@ -74,8 +74,8 @@ struct EnvLDS {
 #endif
     union __attribute__((aligned(16))) {
         struct {                           // contact update (part A3)
-            float ocp[AVR_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
-            int okey[AVR_MAX_CONTACTS];                   // its (sa | sb << 16) keys
+            float ocp[K_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
+            int okey[K_MAX_CONTACTS];                   // its (sa | sb << 16) keys
         } k;
         struct {
             float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
@@ -96,7 +96,7 @@ struct PairsLDS {
 #endif
     union __attribute__((aligned(16))) {
         struct {                           // forward kinematics and body frames
-            float st[AVR_S_CP];
+            float st[S_CP];
             float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
         };
         struct {
@@ -154,7 +154,7 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
         com = gldtf(m.rl_com + 8 * (go + i));
         axl = gld3(m.rl_axis + 4 * i);
         const int dof = gld(m.rl_dof + (i));
-        const float qv = dof >= 0 ? L.st[AVR_S_Q + dof] : 0.f;
+        const float qv = dof >= 0 ? L.st[S_Q + dof] : 0.f;
         const qt qj = jt == AVR_J_REVOLUTE ? qaxis(axl, qv) : Q(0, 0, 0, 1);
         sttf(L.lk[i], jo);
         L.lk[i][7] = qv;
@@ -167,7 +167,11 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     v3 org = V(0, 0, 0), axw = V(0, 0, 0);
     if (mine) {
         const int r = __builtin_ctz(am);                       // the chain's root link
-        t = gld(m.rl_parent + (r)) == -2 ? ldtf(L.st + AVR_S_HUMAN + 7 * m.hc_parent_slot) : gldtf(m.base);
+#if K_RBASE_IN_STATE
+        t = gld(m.rl_parent + (r)) == -2 ? ldtf(L.st + S_HUMAN + 7 * m.hc_parent_slot) : ldtf(L.st + S_RBASE);
+#else
+        t = gld(m.rl_parent + (r)) == -2 ? ldtf(L.st + S_HUMAN + 7 * m.hc_parent_slot) : gldtf(m.base);
+#endif
         for (unsigned b = am; b; b &= b - 1u) {
             const int k = __builtin_ctz(b);
             const tf jo = ldtf(L.lk[k]);
@@ -194,7 +198,7 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     if (mine && c >= 0) {
         const int slot = gld(m.hc_slot + (c));
         if (slot >= 0) {
-            float *h = L.st + AVR_S_HUMAN + 7 * slot;
+            float *h = L.st + S_HUMAN + 7 * slot;
             st3(h, ld3(L.cm[i]));
             stq(h + 3, ldq(L.cm[i] + 3));
         }
@@ -382,7 +386,7 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
         jt = gld(m.rl_jtype + (i));
         am = gld(m.anc_mask + (i));
         const int dof = gld(m.rl_dof + (i));
-        qd = dof >= 0 ? L.st[AVR_S_QD + dof] : 0.f;
+        qd = dof >= 0 ? L.st[S_QD + dof] : 0.f;
         o = ld3(L.org[i]); c = ld3(L.cm[i]); axw = ld3(L.ax[i]);
         q = ldq(L.cm[i] + 3);
         mi = gld(m.rl_mass + (go + i));
@@ -425,7 +429,13 @@ AVR_DI void robot_bias(const KModel &m, EnvLDS &L) {
         const float vn = len(vc), wn = len(om);
         const v3 fdamp = scl(vc, -mi * (k1l + k1l * vn));
         const v3 tdamp = scl(Iw, -(k1a + k1a * wn));
+#if K_HUMAN_GRAVITY
+        // gravity of the articulated human chain (its links follow the robot's): F = m (a - g)
+        const v3 ga = i >= m.nl ? V(ac.x - m.hc_grav[0], ac.y - m.hc_grav[1], ac.z - m.hc_grav[2]) : ac;
+        st3(R1[i], sub(scl(ga, mi), fdamp));
+#else
         st3(R1[i], sub(scl(ac, mi), fdamp));
+#endif
         st3(R5[i], sub(add(inertia_mul(q, I, al), crs(om, Iw)), tdamp));
     }
     SYNC();
@@ -1115,9 +1125,12 @@ template <class LT>
 AVR_DI tf body_tf(const KModel &m, const LT &L, int b) {
     int kind = gld(m.body_kind + (b)), idx = gld(m.body_index + (b));
     if (kind == AVR_BODY_ROBOT) return ldtf(L.cm[idx]);
-    if (kind == AVR_BODY_FREE) return ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * idx);
+    if (kind == AVR_BODY_FREE) return ldtf(L.st + S_FREE + AVR_FB_WORDS * idx);
     if (kind == AVR_BODY_STATIC) return gldtf(m.st_pose + 8 * idx);
-    return ldtf(L.st + AVR_S_HUMAN + 7 * idx);
+#if K_RBASE_IN_STATE
+    if (kind == AVR_BODY_RSTATIC) return ldtf(L.st + S_RBASE);
+#endif
+    return ldtf(L.st + S_HUMAN + 7 * idx);
 }
 
 AVR_DI void aabb_of(tf t, v3 c, v3 h, v3 &mn, v3 &mx) {
@@ -1353,7 +1366,7 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const PairIn &in, int k0, 
         if (k < n) {
             int dst = nnew + excl + k;
             int id = mf_idx(pk, k);
-            if (dst < AVR_MAX_CONTACTS) {
+            if (dst < K_MAX_CONTACTS) {
                 // 16-word point record: the new point from registers or an old one from memory
                 float4 *o = (float4 *)(newcp + AVR_CP_WORDS * dst);
                 if (id == MF_NEW) {
@@ -1633,7 +1646,7 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
     PROF_START(pt);
     // the previous contact pool in LDS (the manifold update reads and updates it in place) and
     // its keys (matching in the manifold update)
-    const int nold = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    const int nold = (int)L.st[S_TASK + T_NCP];
     lds_f *ocp = (lds_f *)L.u.k.ocp;      // (staged by load_a)
     for (int i = lane; i < nold; i += 64)
         L.u.k.okey[i] = (int)ocp[AVR_CP_WORDS * i + AVR_CP_SA] | ((int)ocp[AVR_CP_WORDS * i + AVR_CP_SB] << 16);
@@ -1650,9 +1663,9 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
         SYNC();
         cur = nxt;
     }
-    if (nnew > AVR_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = AVR_MAX_CONTACTS; }
+    if (nnew > K_MAX_CONTACTS) { if (lane == 0) L.flags |= 2; nnew = K_MAX_CONTACTS; }
     SYNC();
-    if (lane == 0) L.st[AVR_S_TASK + AVR_T_NCP] = (float)nnew;
+    if (lane == 0) L.st[S_TASK + T_NCP] = (float)nnew;
     SYNC();
     PROF_STOP(3, pt);
 }
@@ -1707,7 +1720,11 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define CRW 16      // words per contact record
 #define CR_BASE (MAXNC * RWC)
 #define CI_SLOT 20  // contact header word 0: robot slot + 1 from this bit
-#define ROBW 32     // words per robot part
+#if NDL == 2
+#define ROBW 64     // words per robot part: lane sl's (J, M^-1 J^T) of DoFs sl and sl + 16
+#else
+#define ROBW 32     // words per robot part: lane sl's (J, M^-1 J^T) of DoF sl
+#endif
 // per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
 #define WS_WORDS 128
 #define WS_NNC 0     // int bits: non-contact rows
@@ -1716,11 +1733,12 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_XCC 3     // diagnostic builds: XCD that ran part A
 #define WS_NROB 4    // int bits: robot parts (slots) of the row set
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
-#define WS_FV 32     // [MAXF][4] unconstrained free-body linear velocities
-#define WS_FW 72     // [MAXF][4] angular
+#define WS_FV (WS_VQ + 16 * NDL)     // [MAXF][4] unconstrained free-body linear velocities
+#define WS_FW (WS_FV + 4 * MAXF)     // [MAXF][4] angular
+static_assert(MAXD <= 16 * NDL && WS_FW + 4 * MAXF <= WS_WORDS, "workspace layout");
 // A row's ownership mask: 2 bits per free body f (= part-B lane f): 1 endpoint A, 2 endpoint B
 AVR_DI int own_mask(int fa, int fb) { return (fa >= 0 ? 1 << (2 * fa) : 0) | (fb >= 0 ? 2 << (2 * fb) : 0); }
-static_assert(CR_BASE + 3 * AVR_MAX_CONTACTS * CRW <= (MAXNC + 3 * AVR_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
+static_assert(CR_BASE + 3 * K_MAX_CONTACTS * CRW <= (MAXNC + 3 * K_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
 
 AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RWC; }
 AVR_DI float *row_crec(float *base, int k) { return base + CR_BASE + k * CRW; }
@@ -1732,7 +1750,7 @@ AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.
 // one 6-vector per endpoint serves both halves of a row resolve.
 AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
     const float *g = L.gsc[f];
-    const qt q = ldq(L.st + AVR_S_FREE + AVR_FB_WORDS * f + 3);
+    const qt q = ldq(L.st + S_FREE + AVR_FB_WORDS * f + 3);
     const v3 b = qrot(qconj(q), ja);
     w[0] = jl.x * g[0]; w[1] = jl.y * g[0]; w[2] = jl.z * g[0];
     w[3] = b.x * g[1]; w[4] = b.y * g[2]; w[5] = b.z * g[3];
@@ -1745,8 +1763,16 @@ AVR_DI void put_hdr(float *w, int info, float inv, float rhs, float lo, float hi
     w[0] = __int_as_float(info); w[1] = __int_as_float(slot + 1); w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = 0.f; w[7] = 0.f;
 }
 AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
+#if NDL == 2
+#pragma unroll
+    for (int d = 0; d < 16; d++) {
+        w[4 * d] = J[d]; w[4 * d + 1] = MJ[d];
+        w[4 * d + 2] = d + 16 < MAXD ? J[d + 16] : 0.f; w[4 * d + 3] = d + 16 < MAXD ? MJ[d + 16] : 0.f;
+    }
+#else
 #pragma unroll
     for (int d = 0; d < 16; d++) { w[2 * d] = d < MAXD ? J[d] : 0.f; w[2 * d + 1] = d < MAXD ? MJ[d] : 0.f; }
+#endif
 }
 
 // Non-contact rows (limits, motors, fixed constraint), one lane per row.
@@ -1766,9 +1792,16 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         const bool hl = lk && gld(m.rl_has_limit + (lane));
         float plo = 1.f, phi = 1.f;
         if (hl) {
-            const float q = L.st[AVR_S_Q + ld];
+            const float q = L.st[S_Q + ld];
+#if K_CHAIN_LIMITS_IN_STATE
+            // the human chain's limits carry the env's limit_scale (state); the robot's are the model's
+            const int c = lane - m.nl;
+            plo = q - (c >= 0 ? L.st[S_HCH + 2 * K_HC_N + c] : gld(m.rl_lower + (lane)));
+            phi = (c >= 0 ? L.st[S_HCH + 3 * K_HC_N + c] : gld(m.rl_upper + (lane))) - q;
+#else
             plo = q - gld(m.rl_lower + (lane));
             phi = gld(m.rl_upper + (lane)) - q;
+#endif
         }
         const bool vlo = hl && !(plo > 0.f), vhi = hl && !(phi > 0.f), mot = ld >= 0;
         const unsigned long long blo = __ballot(vlo), bhi = __ballot(vhi), bmo = __ballot(mot), lt = (1ull << lane) - 1ull;
@@ -1793,8 +1826,12 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     const tf off = gldtf(m.tool_offset);
     const v3 pivA = tfpt(ta, off.p);
     const qt frA = qmul(ta.q, off.q);
-    const tf tb = ldtf(L.st + AVR_S_FREE + AVR_FB_WORDS * fb);
+    const tf tb = ldtf(L.st + S_FREE + AVR_FB_WORDS * fb);
+#if K_TOOL_PIVOT
+    const v3 pivB = tfpt(tb, V(m.fix_pivot_b[0], m.fix_pivot_b[1], m.fix_pivot_b[2]));   // the tool's base COM (handle)
+#else
     const v3 pivB = tb.p;
+#endif
     const m3 FA = qmat(frA), FB = qmat(tb.q);
     if (kind == 0 || kind == 1 || kind == 2) {
         // J = +-e_dof: M^-1 J^T is a signed column of M^-1
@@ -1809,10 +1846,10 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         if (kind < 2) {
             put_hdr(w, 0, inv, (-pen * erp / dt - rel) * inv, 0.f, 100.f, lane);
         } else {
-            const float q = L.st[AVR_S_Q + dof], cur = L.vq[dof];
-            const float kp = L.st[AVR_S_KP + dof], kd = 1.f;
-            const float desired = kp * (L.st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
-            const float mi = L.st[AVR_S_MAXIMP + dof];
+            const float q = L.st[S_Q + dof], cur = L.vq[dof];
+            const float kp = L.st[S_KP + dof], kd = 1.f;
+            const float desired = kp * (L.st[S_QTGT + dof] - q) / dt + cur + kd * (0.f - cur);
+            const float mi = L.st[S_MAXIMP + dof];
             put_hdr(w, 0, inv, (desired - rel) * inv, -mi, mi, lane);
         }
         put_free_zero(w + 8); put_free_zero(w + 14);
@@ -1899,7 +1936,7 @@ AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, in
 // n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions).
 AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
-    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    const int ncp = (int)L.st[S_TASK + T_NCP];
     const float erp = m.erp;
     int nrob = n_nc;                                 // robot parts: nc rows first, then 3 per robot contact
     for (int base = 0; base < ncp; base += 64) {
@@ -1992,7 +2029,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     // (the body and link frames from the pair kernel and the previous contact pool were staged
     // by load_a)
     PROF_STOP(0, ps);
-    collide_contacts(m, L, cs, gst + AVR_S_CP);
+    collide_contacts(m, L, cs, gst + S_CP);
     PROF_STOP(13, ps);
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
@@ -2010,13 +2047,13 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     // slot left over from another kernel's LDS (NaN bit patterns included) would turn those
     // zero-Jacobian terms into NaN (0 * NaN) -- inactive slots (d >= nda) hold 0
     if (lane < MAXD) {
-        const float v = L.st[AVR_S_QD + lane] + dt * L.qdd[lane];
+        const float v = L.st[S_QD + lane] + dt * L.qdd[lane];
         L.vq[lane] = lane < L.nda ? clampf(v, -vmax, vmax) : 0.f;
     }
     const float k1l = m.lin_damp, k1a = m.ang_damp;
     if (lane < m.nf) {
         int f = lane;
-        const float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * f;
+        const float *fb = L.st + S_FREE + AVR_FB_WORDS * f;
         v3 v = ld3(fb + 7), om = ld3(fb + 10);
         qt q = ldq(fb + 3);
         float mass = gld(m.fb_mass + (f));
@@ -2040,7 +2077,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     PROF_STOP(6, ps);
     const int n_nc = build_noncontact_rows(m, L, rows, dt);
     PROF_STOP(7, ps);
-    const int n_rob = build_contact_rows(m, L, gst + AVR_S_CP, rows, n_nc, dt);
+    const int n_rob = build_contact_rows(m, L, gst + S_CP, rows, n_nc, dt);
     SYNC();
     PROF_STOP(8, ps);
     // hand-over to part B
@@ -2054,12 +2091,13 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
 }
 
 // --------------------------------------------------------------------------- task glue
+#if AVR_TASK == AVR_TASK_FEEDING
 AVR_DI void mouth_target(const KModel &m, EnvLDS &L) {
-    tf t = ldtf(L.st + AVR_S_HUMAN + 7 * m.head_slot);
-    int g = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+    tf t = ldtf(L.st + S_HUMAN + 7 * m.head_slot);
+    int g = (int)L.st[S_TASK + T_GENDER];
     v3 p = tfpt(t, gld3(m.mouth[g]));
     SYNC();
-    if (lane_id() == 0) st3(L.st + AVR_S_TASK + AVR_T_TARGET, p);
+    if (lane_id() == 0) st3(L.st + S_TASK + T_TARGET, p);
     SYNC();
 }
 
@@ -2067,7 +2105,7 @@ AVR_DI void mouth_target(const KModel &m, EnvLDS &L) {
 // sel: 0 robot-human, 1 spoon-human, 2 body X vs body Y, 3 body X vs human
 AVR_DI float contact_sum(const KModel &m, const EnvLDS &L, const float *gcp, int sel, int X, int Y, int &count) {
     const int lane = lane_id();
-    int n = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    int n = (int)L.st[S_TASK + T_NCP];
     float s = 0.f;
     int c = 0;
     for (int i = lane; i < n; i += 64) {
@@ -2093,23 +2131,25 @@ AVR_DI void observe(const KModel &m, EnvLDS &L, float spoon_force, float *obs_ou
     robot_fk(m, L);
     if (lane_id() == 0) {
         v3 torso = ld3(L.cm[m.torso_link]);
-        const float *sp = L.st + AVR_S_FREE + AVR_FB_WORDS * m.spoon_free;
+        const float *sp = L.st + S_FREE + AVR_FB_WORDS * m.spoon_free;
         v3 spos = ld3(sp);
-        v3 tgt = ld3(L.st + AVR_S_TASK + AVR_T_TARGET);
-        const float *h = L.st + AVR_S_HUMAN + 7 * m.head_slot;
+        v3 tgt = ld3(L.st + S_TASK + T_TARGET);
+        const float *h = L.st + S_HUMAN + 7 * m.head_slot;
         int k = 0;
         v3 a = sub(spos, torso);
         obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
         for (int i = 0; i < 4; i++) obs_out[k++] = sp[3 + i];
         a = sub(spos, tgt);
         obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
-        for (int i = 0; i < m.n_arm; i++) obs_out[k++] = L.st[AVR_S_Q + m.arm_dofs[i]];
+        for (int i = 0; i < m.n_arm; i++) obs_out[k++] = L.st[S_Q + m.arm_dofs[i]];
         a = sub(ld3(h), torso);
         obs_out[k++] = a.x; obs_out[k++] = a.y; obs_out[k++] = a.z;
         for (int i = 0; i < 4; i++) obs_out[k++] = h[3 + i];
         obs_out[k++] = spoon_force;
     }
 }
+
+#endif  // AVR_TASK_FEEDING
 
 // Philox4x32-10 (Salmon et al. 2011): counter (env, step, j, 0), key (seed lo, seed hi)
 AVR_DI void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1) {
@@ -2156,7 +2196,7 @@ AVR_DI int xcc_id() {   // XCD of the executing CU (HW_REG_XCC_ID, id 20, bits 3
 AVR_DI float *env_ws(const KModel &m, int env) { return m.ws + (size_t)env * WS_WORDS; }
 AVR_DI float *env_rows(const KModel &m, int env) { return m.rows + (size_t)env * (size_t)m.rowstride; }
 
-AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[AVR_S_TASK + AVR_T_HDYN] != 0.f; }
+AVR_DI bool env_hdyn(const KModel &m, const float *gst) { return m.hc_n > 0 && gst[S_TASK + T_HDYN] != 0.f; }
 
 // Global -> LDS copies in two halves: g2r issues a lane's loads of words lane, lane + 64, ...
 // (NB of them, indices clamped into [0, n), so every load is unconditional), r2l stores them.  A
@@ -2192,12 +2232,12 @@ template <class LT>
 AVR_DI void load_state(const KModel &m, LT &L, const float *gst) {
     const int lane = lane_id();
     poison_lds(L);
-    float ts[NB_OF(AVR_S_CP)];
-    g2r(ts, gst, AVR_S_CP);
-    r2l(L.st, ts, AVR_S_CP);
+    float ts[NB_OF(S_CP)];
+    g2r(ts, gst, S_CP);
+    r2l(L.st, ts, S_CP);
     if (lane == 0) {
         L.flags = 0;
-        L.gender = (int)gst[AVR_S_TASK + AVR_T_GENDER];
+        L.gender = (int)gst[S_TASK + T_GENDER];
         const bool hd = env_hdyn(m, gst);
         L.nla = hd ? m.nla : m.nl;
         L.nda = hd ? m.nd + m.hc_n : m.nd;
@@ -2213,18 +2253,18 @@ AVR_DI void load_state(const KModel &m, LT &L, const float *gst) {
 AVR_DI void load_a(const KModel &m, EnvLDS &L, const float *gst, const float *cs) {
     const int lane = lane_id();
     poison_lds(L);
-    const int nold = (int)gst[AVR_S_TASK + AVR_T_NCP];
+    const int nold = (int)gst[S_TASK + T_NCP];
     const bool hd = env_hdyn(m, gst);
     const int nla = hd ? m.nla : m.nl;
-    float ts[NB_OF(AVR_S_CP)], tb[NB_OF(MAXB * 8)], tc[NB_OF(MAXL * 8)], tx[NB_OF(MAXL * 4)], to[NB_OF(MAXL * 4)];
-    float tp[NB_OF(AVR_MAX_CONTACTS * AVR_CP_WORDS)];
-    g2r(ts, gst, AVR_S_CP);
+    float ts[NB_OF(S_CP)], tb[NB_OF(MAXB * 8)], tc[NB_OF(MAXL * 8)], tx[NB_OF(MAXL * 4)], to[NB_OF(MAXL * 4)];
+    float tp[NB_OF(K_MAX_CONTACTS * AVR_CP_WORDS)];
+    g2r(ts, gst, S_CP);
     g2r(tb, cs + CS_BTF, m.nb * 8);
     g2r(tc, cs + CS_CM, nla * 8);
     g2r(tx, cs + CS_AX, nla * 4);
     g2r(to, cs + CS_ORG, nla * 4);
-    g2r(tp, gst + AVR_S_CP, nold * AVR_CP_WORDS);
-    r2l(L.st, ts, AVR_S_CP);
+    g2r(tp, gst + S_CP, nold * AVR_CP_WORDS);
+    r2l(L.st, ts, S_CP);
     r2l(&L.btf[0][0], tb, m.nb * 8);
     r2l(&L.cm[0][0], tc, nla * 8);
     r2l(&L.ax[0][0], tx, nla * 4);
@@ -2232,7 +2272,7 @@ AVR_DI void load_a(const KModel &m, EnvLDS &L, const float *gst, const float *cs
     r2l(L.u.k.ocp, tp, nold * AVR_CP_WORDS);
     if (lane == 0) {
         L.flags = 0;
-        L.gender = (int)L.st[AVR_S_TASK + AVR_T_GENDER];
+        L.gender = (int)L.st[S_TASK + T_GENDER];
         L.nla = nla;
         L.nda = hd ? m.nd + m.hc_n : m.nd;
     }
@@ -2252,6 +2292,7 @@ AVR_DI void prof_flush(const KModel &m, LT &L, int env) {
 #endif
 }
 
+#if AVR_TASK == AVR_TASK_FEEDING
 // take_step (env.py:274-337): clip, scale, 5x limit-respecting accumulation, motor targets.
 // One thread per env.
 __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const float *__restrict__ act,
@@ -2261,38 +2302,40 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const int env = env0 + 512 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
-    float *st = state + (size_t)env * AVR_STATE_WORDS;
+    float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
     float asq = 0.f;
     for (int i = 0; i < m.n_arm; i++) {
-        float a_raw = mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * AVR_ACT_DIM + i];
+        float a_raw = mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * K_ACT_DIM + i];
         asq += a_raw * a_raw;                    // reward_action uses the caller's action (feeding.py:69)
         float a = clampf(a_raw, -1.f, 1.f) * 0.05f;
         const int d = m.arm_dofs[i];
-        float qn = st[AVR_S_Q + d];
+        float qn = st[S_Q + d];
         for (int it = 0; it < m.frame_skip; it++) {
             if (qn + a < m.arm_lower[i]) a = 0.f;
             if (qn + a > m.arm_upper[i]) a = 0.f;
             qn += a;
         }
-        st[AVR_S_QTGT + d] = qn;
-        st[AVR_S_KP + d] = m.robot_gain;
-        st[AVR_S_MAXIMP + d] = m.robot_force * m.time_step;
+        st[S_QTGT + d] = qn;
+        st[S_KP + d] = m.robot_gain;
+        st[S_MAXIMP + d] = m.robot_force * m.time_step;
     }
     if (env_hdyn(m, st)) {
         // tremor (env.py:327-337): targets target_human_joint_positions + human_tremors with the
         // tremor's sign alternating with self.iteration, gains human_gains, forces human_forces
         // (x human_strength = 1: 'tremor' is not 'weakness')
-        const float sg = ((int)st[AVR_S_TASK + AVR_T_ITER] & 1) ? -1.f : 1.f;
+        const float sg = ((int)st[S_TASK + T_ITER] & 1) ? -1.f : 1.f;
         for (int c = 0; c < m.hc_n; c++) {
             const int d = m.nd + c;
-            st[AVR_S_QTGT + d] = st[AVR_S_HCH + c] + st[AVR_S_HCH + AVR_HC_N + c] * sg;
-            st[AVR_S_KP + d] = m.human_gain;
-            st[AVR_S_MAXIMP + d] = m.human_force * m.time_step;
+            st[S_QTGT + d] = st[S_HCH + c] + st[S_HCH + K_HC_N + c] * sg;
+            st[S_KP + d] = m.human_gain;
+            st[S_MAXIMP + d] = m.human_force * m.time_step;
         }
     }
     ws[WS_ASQ] = asq;
 }
+
+#endif  // AVR_TASK_FEEDING
 
 // Diagnostic wave timeline (-DAVR_WAVETIME builds only): global 100 MHz stamps at the start and
 // end of every wave of the last A / B launch, [2][n_envs][2] u64 in m.prof (tools/wavetime.py).
@@ -2317,7 +2360,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const K
                                                                          const unsigned char *__restrict__ mask, int env0, int n_envs) {
     __shared__ PairsLDS L;
     AVR_ENV_GUARD();
-    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    float *gst = state + (size_t)env * K_STATE_WORDS;
     // the packed shape info, staged in LDS for the pair enumeration (loads issued first, their
     // LDS stores after the kinematics)
     int si[MAXSH / 64];
@@ -2668,7 +2711,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     WT_START();
-    float *gst = state + (size_t)env * AVR_STATE_WORDS;
+    float *gst = state + (size_t)env * K_STATE_WORDS;
     load_a(m, L, gst, env_cs(m, env));
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
 #ifdef AVR_PROF
@@ -2676,11 +2719,11 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 #endif
     if (lane_id() == 0 && !ok) L.flags |= 1;
     SYNC();
-    if (lane_id() == 0) L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)((int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags);
+    if (lane_id() == 0) L.st[S_TASK + T_FLAGS] = (float)((int)L.st[S_TASK + T_FLAGS] | L.flags);
     SYNC();
     // write back what part A changes in LDS: contact count and flags (the pool itself was
     // written to global memory by collide_contacts)
-    if (lane_id() < 16) gst[AVR_S_TASK + lane_id()] = L.st[AVR_S_TASK + lane_id()];
+    if (lane_id() < 16) gst[S_TASK + lane_id()] = L.st[S_TASK + lane_id()];
     prof_flush(m, L, env);
     WT_END(0);
 }
@@ -2705,7 +2748,7 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 // select: the waits the compiler places for a row then count only that row's loads, and the
 // software pipeline's read-ahead (headers 2D rows ahead, the header-dependent parts D ahead)
 // stays in flight.
-struct DV { float rq, vx, vy, vz, wx, wy, wz; };
+struct DV { float rq, rq2, vx, vy, vz, wx, wy, wz; };   // rq2: DoF sl + 16 (NDL 2)
 
 AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -2721,6 +2764,16 @@ typedef unsigned u3v __attribute__((ext_vector_type(3)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 AVR_DI f4v bld4(rsrc_t r, int o) { u4v x = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0); return *(f4v *)&x; }
 AVR_DI f2v bld2(rsrc_t r, int o) { u2v x = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0); return *(f2v *)&x; }
+#if NDL == 2
+typedef f4v rv_t;           // a lane's robot-part words: (J, M^-1 J^T) of DoF sl, then of DoF sl + 16
+#define RVB 16              // bytes per lane in a robot part
+#define rload bld4
+#else
+typedef f2v rv_t;           // (J, M^-1 J^T) of DoF sl
+#define RVB 8
+#define rload bld2
+#endif
+typedef __attribute__((address_space(3))) rv_t lds_rv;
 AVR_DI f4v bld3(rsrc_t r, int o) {
     u3v x = __builtin_amdgcn_raw_buffer_load_b96(r, o, 0, 0);
     f4v y = {__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), 0.f};
@@ -2745,7 +2798,7 @@ AVR_DI int own_of(int mask) {
     const int sl = lane_id() & 15;
     return (int)__builtin_amdgcn_ubfe((unsigned)mask, sl < MAXF ? 2 * sl : 30, 2);
 }
-static_assert(2 * MAXF <= CI_SLOT && MAXNC + 3 * AVR_MAX_CONTACTS < (1 << (30 - CI_SLOT)), "own mask and slot bit fields");
+static_assert(2 * MAXF <= CI_SLOT && MAXNC + 3 * K_MAX_CONTACTS < (1 << (30 - CI_SLOT)), "own mask and slot bit fields");
 
 // Row sources.  A sweep step sets a row's addresses with set(R, valid, address, impulse slot)
 // from per-lane bases plus a wave-uniform step offset (an invalid step is a null row), reads its
@@ -2754,7 +2807,7 @@ static_assert(2 * MAXF <= CI_SLOT && MAXNC + 3 * AVR_MAX_CONTACTS < (1 << (30 - 
 // impulse slots: the second row's loads are the first's plus immediate offsets.
 
 // non-contact rows: buffer loads (they stay L2-resident)
-struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2, r; };
+struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2; rv_t r; };
 struct NcSrc {
     typedef NcRow Row;
     static constexpr bool robot_parts = true;
@@ -2768,7 +2821,7 @@ struct NcSrc {
         const int b = o ? R.o + 8 + 24 * o : B4_OOB;
         R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16);
         const int slot = __float_as_int(R.h0.y) - 1;
-        R.r = bld2(rs, slot >= 0 ? ro + slot * (ROBW * 4) + 8 * (lane_id() & 15) : B4_OOB);
+        R.r = rload(rs, slot >= 0 ? ro + slot * (ROBW * 4) + RVB * (lane_id() & 15) : B4_OOB);
     }
 };
 
@@ -2777,11 +2830,11 @@ struct NcSrc {
 // parts come from the block's zero-filled head (LN_HEAD words): the null record's headers at
 // words 8-11 and 24-27 (a null friction unit), zero parts at words 12-17 and 28-33, zero robot
 // parts at words 12-13 and 44-45.
-#define LN_HEAD 48
+#define LN_HEAD (NDL == 2 ? 80 : 48)   // NDL 2: zero robot parts at words 12-15 and 76-79
 #define LNB_NULL 24                // null record - 8 (bytes)
 #define LNB_ZERO 48                // zero block (bytes)
 typedef __attribute__((address_space(3))) char lds_c;
-struct CRowL { unsigned wb; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+struct CRowL { unsigned wb; lds_f *ip; f4v h; float imp; f2v j0, j1, j2; rv_t r; };
 template <bool RC>             // RC: the block has robot contacts (otherwise no contact row has a robot part)
 struct CLds {
     typedef CRowL Row;
@@ -2805,10 +2858,10 @@ struct CLds {
     }
     AVR_DI unsigned own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.wb + 24 * o : LNB_ZERO; }
     AVR_DI void own_at(Row &R, unsigned b) const { const lds_f2 *q = (const lds_f2 *)(blk + b); R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2]; }
-    AVR_DI unsigned rob_b(const Row &R) const { const unsigned s = (unsigned)__float_as_int(R.h.x) >> CI_SLOT; return s ? rob + 128 * s : LNB_ZERO; }
-    AVR_DI f2v rob_at(unsigned b) const {
-        if constexpr (!RC) { (void)b; return f2v{0.f, 0.f}; }
-        return *(const lds_f2 *)(blk + b);
+    AVR_DI unsigned rob_b(const Row &R) const { const unsigned s = (unsigned)__float_as_int(R.h.x) >> CI_SLOT; return s ? rob + ROBW * 4 * s : LNB_ZERO; }
+    AVR_DI rv_t rob_at(unsigned b) const {
+        if constexpr (!RC) { (void)b; return rv_t{}; }
+        return *(const lds_rv *)(blk + b);
     }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
@@ -2820,7 +2873,7 @@ struct CLds {
 
 // contact rows, buffer loads (blocks whose four envs do not fit the LDS); a null row or part
 // reads at B4_OOB (+ immediate offsets), past the buffer: zeros
-struct CRowG { int o; lds_f *ip; f4v h; float imp; f2v j0, j1, j2, r; };
+struct CRowG { int o; lds_f *ip; f4v h; float imp; f2v j0, j1, j2; rv_t r; };
 struct CGlb {
     typedef CRowG Row;
     static constexpr bool robot_parts = true;
@@ -2834,8 +2887,8 @@ struct CGlb {
     AVR_DI void hdr2(Row &B, const Row &A) const { const f2v a = bld2(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.imp = A.ip[1]; }
     AVR_DI int own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.o - 8 + 24 * o : B4_OOB; }
     AVR_DI void own_at(Row &R, int b) const { R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16); }
-    AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + 128 * s : B4_OOB; }
-    AVR_DI f2v rob_at(int b) const { return bld2(rs, b); }
+    AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + ROBW * 4 * s : B4_OOB; }
+    AVR_DI rv_t rob_at(int b) const { return rload(rs, b); }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
         const int b = own_b(A), r = rob_b(A);
@@ -2862,14 +2915,22 @@ template <bool RP, class R>
 AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi) {
 #pragma clang fp contract(off)
     const float p = fmaf(X.j1.x, d.vz, fmaf(X.j0.y, d.vy, X.j0.x * d.vx));
+#if NDL == 2
+    const float q = RP ? fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.z, d.rq2, fmaf(X.r.x, d.rq, X.j1.y * d.wx))))
+                       : fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, X.j1.y * d.wx));
+#else
     const float q = RP ? fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.x, d.rq, X.j1.y * d.wx)))
                        : fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, X.j1.y * d.wx));
+#endif
     const float dv = row16_sum(p + q);
     const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
     const float delta = ni - imp;
     d.vx = fmaf(X.j0.x, delta, d.vx); d.vy = fmaf(X.j0.y, delta, d.vy); d.vz = fmaf(X.j1.x, delta, d.vz);
     d.wx = fmaf(X.j1.y, delta, d.wx); d.wy = fmaf(X.j2.x, delta, d.wy); d.wz = fmaf(X.j2.y, delta, d.wz);
     if (RP) d.rq = fmaf(X.r.y, delta, d.rq);
+#if NDL == 2
+    if (RP) d.rq2 = fmaf(X.r.w, delta, d.rq2);
+#endif
     return ni;
 }
 
@@ -2914,7 +2975,7 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
     typedef typename NS::Row NR;
     typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
-    d.rq = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
+    d.rq = d.rq2 = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
     // normal rows in contact order: record j at cn + 64 j, impulse slot ipn + j
     auto at_n = [&](CR &R, int j) { cs.set(R, j < n_c, cs.cn + CRW * 4 * j, cs.ipn + j); };
     // warm start (normal rows, contact order): delta = cached impulse x warm-start factor, which
@@ -3010,7 +3071,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     const bool live = env < n_envs && (!mask || mask[env]);
     const int ev = live ? env : env0;
     const gfp wsg = (gfp)env_ws(m, ev);
-    float *st = state + (size_t)ev * AVR_STATE_WORDS;
+    float *st = state + (size_t)ev * K_STATE_WORDS;
     const int n_nc = live ? __float_as_int(wsg[WS_NNC]) : 0, n_c = live ? __float_as_int(wsg[WS_NC]) : 0;
     const int n_rob = live ? __float_as_int(wsg[WS_NROB]) : 0;
     const int n_rows = n_nc + 3 * n_c, n_rc = max(n_rob - n_nc, 0);
@@ -3040,15 +3101,15 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
     // warm-start factor; null slots 0.  The cached impulses are loaded here and stored after the
     // staging loads below have been issued (one memory round trip for both).
-    const gfp cpool = (gfp)(st + AVR_S_CP);
-    float wimp[AVR_MAX_CONTACTS / 16];
+    const gfp cpool = (gfp)(st + S_CP);
+    float wimp[K_MAX_CONTACTS / 16];
 #pragma unroll
-    for (int q = 0; q < AVR_MAX_CONTACTS / 16; q++) wimp[q] = cpool[AVR_CP_WORDS * min(sl + 16 * q, max(n_c - 1, 0)) + AVR_CP_IMP];
+    for (int q = 0; q < K_MAX_CONTACTS / 16; q++) wimp[q] = cpool[AVR_CP_WORDS * min(sl + 16 * q, max(n_c - 1, 0)) + AVR_CP_IMP];
     for (int r = sl; r < n_rows + 2; r += 16) {
         const int c = r - n_nc;
         if (!(c >= 0 && c < n_c)) imp[r] = 0.f;
     }
-    if (lane < LN_HEAD) blk[lane] = 0.f;        // null rows, zero parts
+    for (int i = lane; i < LN_HEAD; i += 64) blk[i] = 0.f;        // null rows, zero parts
     if (in_lds) {   // contact records and robot-contact parts, 8 loads in flight per lane
         const int n4r = 3 * n_c * (CRW / 4), n4s = n_rc * (ROBW / 4);
         const int m4 = wmax(n4r + n4s);
@@ -3068,7 +3129,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         }
     }
 #pragma unroll
-    for (int q = 0; q < AVR_MAX_CONTACTS / 16; q++)
+    for (int q = 0; q < K_MAX_CONTACTS / 16; q++)
         if (sl + 16 * q < n_c) imp[n_nc + sl + 16 * q] = wimp[q] * m.warmstart;
     __syncthreads();
     // impulse slots: rows 0 .. n_rows - 1 (non-contact, normal, friction pairs), then 2 null slots
@@ -3078,7 +3139,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     int units, rcb = 0;
     if (in_lds) {
         // byte addresses: records - 8; robot part of slot s at rw + (s - n_nc) ROBW + 2 sl words
-        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW + 2 * sl);
+        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW) + RVB * sl;
         if (wmax(n_rc) > 0) {
             CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
             units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
@@ -3088,13 +3149,13 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
             units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else {
-        const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, rob = ro - ROBW * 4 + 8 * sl;
+        const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, rob = ro - ROBW * 4 + RVB * sl;
         CGlb cs{rs, cn, cf, rob, ipn, ipf, nullip};
         units = pgs4<B4_DN, B4_DG>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
     }
     (void)units; (void)rcb;
     // normal impulses back to the manifold points (warm start + normalForce)
-    for (int c = sl; c < n_c; c += 16) st[AVR_S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = imp[n_nc + c];
+    for (int c = sl; c < n_c; c += 16) st[S_CP + AVR_CP_WORDS * c + AVR_CP_IMP] = imp[n_nc + c];
 #ifdef AVR_WAVETIME   // block timeline at its group-0 env: [1][env] (start, end); [2][env] (sweep lengths, LDS path, friction units)
     {
         const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
@@ -3111,7 +3172,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     const float *ws = env_ws(m, ev);
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
     if (sl < m.nf) {
-        const qt q = ldq(st + AVR_S_FREE + AVR_FB_WORDS * sl + 3);
+        const qt q = ldq(st + S_FREE + AVR_FB_WORDS * sl + 3);
         const v3 I = gld3(m.fb_inertia + 4 * sl);
         const float rs = 1.f / sqrtf(gld(m.fb_mass + (sl)));
         const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
@@ -3121,20 +3182,28 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     }
     const float vmax = m.max_vel;
     const int nda = env_hdyn(m, st) ? m.nd + m.hc_n : m.nd;
-    if (sl < nda) {
-        float v = clampf(ws[WS_VQ + sl] + d.rq, -vmax, vmax);
-        float q = st[AVR_S_Q + sl] + dt * v;
-        if (frame_end && sl >= m.nd) {
-            // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
-            const float lo = gld(m.hc_lower + (sl - m.nd)), hi = gld(m.hc_upper + (sl - m.nd));
-            if (q < lo) { q = lo; v = 0.f; }
-            else if (q > hi) { q = hi; v = 0.f; }
+#pragma unroll
+    for (int k = 0; k < NDL; k++) {
+        const int dof = sl + 16 * k;
+        if (dof < nda) {
+            float v = clampf(ws[WS_VQ + dof] + (k == 0 ? d.rq : d.rq2), -vmax, vmax);
+            float q = st[S_Q + dof] + dt * v;
+            if (frame_end && dof >= m.nd) {
+                // enforce_hard_human_joint_limits (env.py:389-410): resetJointState onto the limit, qd = 0
+#if K_CHAIN_LIMITS_IN_STATE
+                const float lo = st[S_HCH + 2 * K_HC_N + (dof - m.nd)], hi = st[S_HCH + 3 * K_HC_N + (dof - m.nd)];
+#else
+                const float lo = gld(m.hc_lower + (dof - m.nd)), hi = gld(m.hc_upper + (dof - m.nd));
+#endif
+                if (q < lo) { q = lo; v = 0.f; }
+                else if (q > hi) { q = hi; v = 0.f; }
+            }
+            st[S_QD + dof] = v;
+            st[S_Q + dof] = q;
         }
-        st[AVR_S_QD + sl] = v;
-        st[AVR_S_Q + sl] = q;
     }
     if (sl < m.nf) {
-        float *fb = st + AVR_S_FREE + AVR_FB_WORDS * sl;
+        float *fb = st + S_FREE + AVR_FB_WORDS * sl;
         v3 v = clamp3(add(ld3(ws + WS_FV + 4 * sl), V(d.vx, d.vy, d.vz)), vmax);
         v3 om = clamp3(add(ld3(ws + WS_FW + 4 * sl), V(d.wx, d.wy, d.wz)), vmax);
         st3(fb + 7, v);
@@ -3150,6 +3219,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     }
 }
 
+#if AVR_TASK == AVR_TASK_FEEDING
 // Task glue after the frames: update_targets (feeding.py:345-349), iteration count,
 // get_total_force (83-90), get_food_rewards (92-121), _get_obs (123-142), reward (56-77),
 // TimeLimit; SETTLE mode: target + reset observation only.  NaN guard for every mode.
@@ -3159,27 +3229,27 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     const int lane = lane_id();
-    float *gst = state + (size_t)env * AVR_STATE_WORDS;
-    const float *gcp = gst + AVR_S_CP;
+    float *gst = state + (size_t)env * K_STATE_WORDS;
+    const float *gcp = gst + S_CP;
     load_state(m, L, gst);
     PROF_START(ptask);
     if (L.nla > m.nl) robot_fk(m, L);    // head pose after the last sub-step (update_targets)
     mouth_target(m, L);
     if (mode == MODE_SETTLE) {
-        if (obs) observe(m, L, 0.f, obs + (size_t)env * AVR_OBS_DIM);
+        if (obs) observe(m, L, 0.f, obs + (size_t)env * K_OBS_DIM);
     } else if (mode == MODE_STEP || mode == MODE_STEP_RANDOM) {
-        if (lane == 0) L.st[AVR_S_TASK + AVR_T_ITER] += 1.f;
+        if (lane == 0) L.st[S_TASK + T_ITER] += 1.f;
         SYNC();
         int dummy;
         float robot_force = contact_sum(m, L, gcp, 0, 0, 0, dummy);
         float spoon_force = contact_sum(m, L, gcp, 1, 0, 0, dummy);
         float food_reward = 0.f, hit_reward = 0.f, mouth_vel = 0.f;
-        int alive = (int)L.st[AVR_S_TASK + AVR_T_ALIVE], hit = (int)L.st[AVR_S_TASK + AVR_T_HIT];
-        float succ = L.st[AVR_S_TASK + AVR_T_SUCCESS];
-        v3 tgt = ld3(L.st + AVR_S_TASK + AVR_T_TARGET);
+        int alive = (int)L.st[S_TASK + T_ALIVE], hit = (int)L.st[S_TASK + T_HIT];
+        float succ = L.st[S_TASK + T_SUCCESS];
+        v3 tgt = ld3(L.st + S_TASK + T_TARGET);
         for (int k = 0; k < m.n_food; k++) {
             if (!(alive >> k & 1)) continue;
-            float *fb = L.st + AVR_S_FREE + AVR_FB_WORDS * (m.food_free0 + k);
+            float *fb = L.st + S_FREE + AVR_FB_WORDS * (m.food_free0 + k);
             v3 fp = ld3(fb);
             int fbody = m.food_body0 + k;
             if (len(sub(tgt, fp)) < 0.02f) {
@@ -3205,14 +3275,14 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
         }
         SYNC();
         if (lane == 0) {
-            L.st[AVR_S_TASK + AVR_T_ALIVE] = (float)alive;
-            L.st[AVR_S_TASK + AVR_T_HIT] = (float)hit;
-            L.st[AVR_S_TASK + AVR_T_SUCCESS] = succ;
+            L.st[S_TASK + T_ALIVE] = (float)alive;
+            L.st[S_TASK + T_HIT] = (float)hit;
+            L.st[S_TASK + T_SUCCESS] = succ;
         }
         SYNC();
-        const float *sp = L.st + AVR_S_FREE + AVR_FB_WORDS * m.spoon_free;
+        const float *sp = L.st + S_FREE + AVR_FB_WORDS * m.spoon_free;
         float ee_vel = len(ld3(sp + 7));
-        observe(m, L, spoon_force, obs + (size_t)env * AVR_OBS_DIM);
+        observe(m, L, spoon_force, obs + (size_t)env * K_OBS_DIM);
         float prefs = m.w_velocity * (-ee_vel) + m.w_force_nontarget * (-robot_force) +
                       m.w_high_forces * (spoon_force < 10.f ? 0.f : -spoon_force) + m.w_food_hit * hit_reward +
                       m.w_food_velocities * (-mouth_vel);
@@ -3221,7 +3291,7 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
         float r = m.w_distance * (-dist) + m.w_action * (-asq) + m.w_food * food_reward + prefs;
         if (lane == 0) {
             rew[env] = r;
-            int itn = (int)L.st[AVR_S_TASK + AVR_T_ITER];
+            int itn = (int)L.st[S_TASK + T_ITER];
             done[env] = (unsigned char)(itn >= m.max_steps);
             info[(size_t)env * AVR_INFO_DIM + 0] = robot_force + spoon_force;
             info[(size_t)env * AVR_INFO_DIM + 1] = succ >= (float)m.n_food * m.task_success_threshold ? 1.f : 0.f;
@@ -3230,27 +3300,31 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     SYNC();
     // NaN guard + flags, then write the state back
     bool bad = false;
-    for (int i = lane; i < AVR_S_CP; i += 64) bad |= !(L.st[i] == L.st[i]);
-    const int ncp = (int)L.st[AVR_S_TASK + AVR_T_NCP];
+    for (int i = lane; i < S_CP; i += 64) bad |= !(L.st[i] == L.st[i]);
+    const int ncp = (int)L.st[S_TASK + T_NCP];
     for (int i = lane; i < ncp * AVR_CP_WORDS; i += 64) bad |= !(gcp[i] == gcp[i]);
     bad = __any(bad);
     if (lane == 0) {
-        int fl = (int)L.st[AVR_S_TASK + AVR_T_FLAGS] | L.flags | (bad ? 1 : 0);
-        L.st[AVR_S_TASK + AVR_T_FLAGS] = (float)fl;
+        int fl = (int)L.st[S_TASK + T_FLAGS] | L.flags | (bad ? 1 : 0);
+        L.st[S_TASK + T_FLAGS] = (float)fl;
     }
     SYNC();
-    for (int i = lane; i < AVR_S_CP; i += 64) gst[i] = L.st[i];
+    for (int i = lane; i < S_CP; i += 64) gst[i] = L.st[i];
     PROF_STOP(12, ptask);
     prof_flush(m, L, env);
 }
+
+#else
+#include "avr_glue_scratch.hip"
+#endif  // AVR_TASK
 
 // state[e] = src[e] for the envs whose mask byte is set (masked reset upload)
 __global__ void avr_copy_masked_kernel(float *state, const float *src, const unsigned char *mask, int n_envs) {
     const int e = blockIdx.x;
     if (e >= n_envs || !mask[e]) return;
-    for (int i = threadIdx.x; i < AVR_STATE_WORDS; i += blockDim.x) state[(size_t)e * AVR_STATE_WORDS + i] = src[(size_t)e * AVR_STATE_WORDS + i];
+    for (int i = threadIdx.x; i < K_STATE_WORDS; i += blockDim.x) state[(size_t)e * K_STATE_WORDS + i] = src[(size_t)e * K_STATE_WORDS + i];
 }
-extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st) {
+hipError_t avr_launch_copy_masked(float *state, const float *src, const unsigned char *mask, int n_envs, hipStream_t st) {
     if (n_envs <= 0) return hipSuccess;
     hipLaunchKernelGGL(avr_copy_masked_kernel, dim3(n_envs), dim3(256), 0, st, state, src, mask, n_envs);
     return hipGetLastError();
@@ -3258,8 +3332,8 @@ extern "C" hipError_t avr_launch_copy_masked(float *state, const float *src, con
 
 __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_envs * AVR_ACT_DIM) return;
-    int e = i / AVR_ACT_DIM, j = i % AVR_ACT_DIM;
+    if (i >= n_envs * K_ACT_DIM) return;
+    int e = i / K_ACT_DIM, j = i % K_ACT_DIM;
     act[i] = j < n_arm ? philox_action(seed, env_offset + e, t, j) : 0.f;
 }
 
@@ -3269,7 +3343,7 @@ __global__ void avr_random_actions_kernel(unsigned long long seed, int env_offse
 //   t frames x nsub x (substep_a, substep_b) -> task (settle obs)        (SETTLE)
 //   substep_a, substep_b with dt = bit-cast(t)                           (SUBSTEP)
 // envs [env0, env1) of the handle; n_envs arguments of the kernels are the end bound env1
-extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
+hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, const float *act, float *obs, float *rew,
                                       unsigned char *done, float *info, const unsigned char *mask, int mode, long long t, int env0,
                                       int env1, hipStream_t stream, avr_evlog *log) {
     const int n_envs = env1 - env0;
@@ -3315,27 +3389,95 @@ extern "C" hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, floa
     return hipGetLastError();
 }
 
-extern "C" hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
+hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, long long t, float *act, int n_envs, int n_arm,
                                                 hipStream_t stream) {
-    int n = n_envs * AVR_ACT_DIM;
+    int n = n_envs * K_ACT_DIM;
     hipLaunchKernelGGL(avr_random_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, seed, env_offset, t, act, n_envs, n_arm);
     return hipGetLastError();
 }
 
-// [vgprs, 0, lds bytes, scratch bytes] of each sub-step kernel: pairs, narrowphase, a, b4
-extern "C" hipError_t avr_kernel_attrs(int *out16) {
-    const void *k[4] = {(const void *)avr_substep_pairs_kernel, (const void *)avr_narrowphase_kernel, (const void *)avr_substep_a_kernel,
-                        (const void *)avr_substep_b4_kernel};
-    for (int i = 0; i < 4; i++) {
+// [vgprs, 0, lds bytes, scratch bytes] of each sub-step kernel: pairs, narrowphase, coop, a, b4
+hipError_t avr_kernel_attrs(int *out20) {
+    const void *k[5] = {(const void *)avr_substep_pairs_kernel, (const void *)avr_narrowphase_kernel, (const void *)avr_coop_kernel,
+                        (const void *)avr_substep_a_kernel, (const void *)avr_substep_b4_kernel};
+    for (int i = 0; i < 5; i++) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, k[i]);
         if (e != hipSuccess) return e;
-        out16[4 * i + 0] = a.numRegs;
-        out16[4 * i + 1] = 0;
-        out16[4 * i + 2] = (int)a.sharedSizeBytes;
-        out16[4 * i + 3] = (int)a.localSizeBytes;
+        out20[4 * i + 0] = a.numRegs;
+        out20[4 * i + 1] = 0;
+        out20[4 * i + 2] = (int)a.sharedSizeBytes;
+        out20[4 * i + 3] = (int)a.localSizeBytes;
     }
     return hipSuccess;
 }
 
-extern "C" size_t avr_kmodel_size(void) { return sizeof(KModel); }
+// ---------------------------------------------------------------------------- state queries
+// (avr_get_q / avr_get_link_pose / avr_get_contact_summary, include/avr.h)
+__global__ void avr_get_q_kernel(const float *__restrict__ state, float *__restrict__ q, float *__restrict__ qd, int nd, int n_envs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_envs * nd) return;
+    const int e = i / nd, j = i - e * nd;
+    if (q) q[i] = state[(size_t)e * K_STATE_WORDS + S_Q + j];
+    if (qd) qd[i] = state[(size_t)e * K_STATE_WORDS + S_QD + j];
+}
+
+// COM frame of articulated link `link` (< 0: the robot base) by forward kinematics on the current
+// joint positions, one block per env
+__global__ __launch_bounds__(64) void avr_link_pose_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ out, int link,
+                                                           int n_envs) {
+    __shared__ PairsLDS L;
+    const int env = blockIdx.x;
+    if (env >= n_envs) return;
+    const KModel &m = *mp;
+    load_state(m, L, state + (size_t)env * K_STATE_WORDS);
+    robot_fk(m, L);
+    if (lane_id() == 0) {
+#if K_RBASE_IN_STATE
+        const tf t = link < 0 ? ldtf(L.st + S_RBASE) : ldtf(L.cm[link]);
+#else
+        const tf t = link < 0 ? tf{V(m.base[0], m.base[1], m.base[2]), Q(m.base[3], m.base[4], m.base[5], m.base[6])} : ldtf(L.cm[link]);
+#endif
+        float *o = out + (size_t)env * 7;
+        o[0] = t.p.x; o[1] = t.p.y; o[2] = t.p.z; o[3] = t.q.x; o[4] = t.q.y; o[5] = t.q.z; o[6] = t.q.w;
+    }
+}
+
+// {points, sum normalForce, robot-human, tool-human} of each env's contact pool
+__global__ void avr_contact_summary_kernel(const KModel *__restrict__ mp, const float *__restrict__ state, float *__restrict__ out, int n_envs) {
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= n_envs) return;
+    const KModel &m = *mp;
+    const float *st = state + (size_t)env * K_STATE_WORDS;
+    const int n = (int)st[S_TASK + T_NCP];
+    float all = 0.f, rh = 0.f, th = 0.f;
+    for (int i = 0; i < n; i++) {
+        const float *cp = st + S_CP + AVR_CP_WORDS * i;
+        const int ba = m.shape_body[(int)cp[AVR_CP_SA]], bb = m.shape_body[(int)cp[AVR_CP_SB]];
+        const int ka = m.body_kind[ba], kb = m.body_kind[bb];
+        const float f = cp[AVR_CP_IMP] / m.time_step;
+        const bool ha = ka == AVR_BODY_HUMAN, hb = kb == AVR_BODY_HUMAN;
+        const bool ra = ka == AVR_BODY_ROBOT || ka == AVR_BODY_RSTATIC, rb = kb == AVR_BODY_ROBOT || kb == AVR_BODY_RSTATIC;
+        all += f;
+        if ((ra && hb) || (rb && ha)) rh += f;
+        if ((ba == m.tool_body && hb) || (bb == m.tool_body && ha)) th += f;
+    }
+    float *o = out + (size_t)env * 4;
+    o[0] = (float)n; o[1] = all; o[2] = rh; o[3] = th;
+}
+
+hipError_t avr_launch_get_q(const float *state, float *q, float *qd, int nd, int n_envs, hipStream_t st) {
+    const int n = nd * n_envs;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_get_q_kernel, dim3((n + 255) / 256), dim3(256), 0, st, state, q, qd, nd, n_envs);
+    return hipGetLastError();
+}
+hipError_t avr_launch_link_pose(const KModel *d_m, float *state, float *out, int link, int n_envs, hipStream_t st) {
+    hipLaunchKernelGGL(avr_link_pose_kernel, dim3(n_envs), dim3(64), 0, st, d_m, state, out, link, n_envs);
+    return hipGetLastError();
+}
+hipError_t avr_launch_contact_summary(const KModel *d_m, const float *state, float *out, int n_envs, hipStream_t st) {
+    hipLaunchKernelGGL(avr_contact_summary_kernel, dim3((n_envs + 63) / 64), dim3(64), 0, st, d_m, state, out, n_envs);
+    return hipGetLastError();
+}
+

@@ -3,16 +3,24 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "../../include/avr_model.h"
+#include "avr_task.h"
 
-#define MAXL AVR_MAX_LINKS
-#define MAXD AVR_MAX_DOF
-#define MAXF AVR_MAX_FREE
+#define MAXL K_MAX_LINKS
+#define MAXD K_MAX_DOF
+#define MAXF K_MAX_FREE
 #define MAXB 48
 #define MAXCC 224      // non-static child shapes whose world AABBs are cached per sub-step
 #define MAXSH 320      // shapes (the pair kernel stages their packed info in LDS, 16 bits each)
 #define MAXSP 256
 #define MAXAP 256
+#if AVR_TASK == AVR_TASK_SCRATCH
+#define MAXNC 48       // non-contact rows: 21 motors, the 6-row tool weld, violated limits
+#else
 #define MAXNC 32
+#endif
+// DoF slots per part-B lane: lane sl (0..15) of an env group holds DoFs sl and (NDL 2) sl + 16
+#define NDL (MAXD > 16 ? 2 : 1)
+static_assert(MAXD <= 16 * NDL && MAXL <= 32, "DoF slots per lane / 32-bit link masks");
 #ifndef SMALL_NV
 #define SMALL_NV 64     // hulls with more vertices and no support table take the wave-cooperative narrowphase
 #endif
@@ -93,10 +101,16 @@ struct KModel {
     unsigned desc_mask[MAXL];  // bit k set if link k is in the subtree of link (inclusive)
     int rl_level[MAXL];        // depth of each link in the tree (roots 0)
     int nlev;                  // number of levels
-    int hc_parent_slot, hc_slot[AVR_HC_N], hc_body[AVR_HC_N];
-    float hc_lower[AVR_HC_N], hc_upper[AVR_HC_N], human_gain, human_force;
+    int hc_parent_slot, hc_slot[K_HC_N], hc_body[K_HC_N];
+    float hc_lower[K_HC_N], hc_upper[K_HC_N], human_gain, human_force;
+    float hc_grav[4];          // gravity on the articulated human chain (K_HUMAN_GRAVITY)
+    float fix_pivot_b[4];      // fixed constraint: child pivot in the tool body frame
+    float tool_tip[4];         // ScratchItch: tool link 1 COM in the tool body frame
+    float torso_com[4];        // ScratchItch: PR2 torso link COM in the base frame
+    int tool_handle_shapes;    // ScratchItch: leading tool shapes that belong to the handle (link -1)
+    float w_tool_force, w_scratch;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
-    int rowcap;                // rows per env = MAXNC + 3 * AVR_MAX_CONTACTS
+    int rowcap;                // rows per env = MAXNC + 3 * K_MAX_CONTACTS
     int rowstride;             // floats between consecutive envs' row buffers
     int rows_envs;             // envs covered by the row buffer (the handle's n_envs)
     int b4_global;             // diagnostic (AVR_B4_GLOBAL=1): part B reads every row from global memory

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 2
+#define AVR_ABI_VERSION 3      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters */
 
 typedef struct avr_config {
     int32_t n_envs;        /* envs owned by this handle (one GPU)                          */
@@ -50,11 +50,14 @@ typedef struct avr_config {
 typedef struct avr_sim avr_sim;
 
 /* Create a handle: copies the compiled scene to the device.  (replaces p.connect + the
- * loadURDF/createMultiBody/createConstraint scene build of world_creation.py:27-93) */
+ * loadURDF/createMultiBody/createConstraint scene build of world_creation.py:27-93)
+ * model->task selects the task (AVR_TASK_FEEDING: FeedingJaco-v0, feeding.py; AVR_TASK_SCRATCH:
+ * ScratchItchPR2-v0, scratch_itch.py) and with it the state layout (avr_model.h), the action and
+ * observation sizes and the task glue. */
 int avr_create(const avr_config *cfg, const avr_model_desc *model, avr_sim **out);
 int avr_destroy(avr_sim *sim);
 
-/* Per-env state blocks (n_envs x AVR_STATE_WORDS floats, layout in avr_model.h).
+/* Per-env state blocks (n_envs x avr_task_state_words(task) floats, layout in avr_model.h).
  * (replaces resetJointState / resetBasePositionAndOrientation of the reset path) */
 int avr_set_state(avr_sim *sim, const float *host_state);
 int avr_get_state(avr_sim *sim, float *host_state);
@@ -72,8 +75,10 @@ int avr_settle(avr_sim *sim, int32_t n_frames, float *host_obs);
  * Unmasked envs and their host_obs rows are left untouched.  Replaces FeedingEnv.reset(). */
 int avr_reset(avr_sim *sim, const uint8_t *env_mask, const float *host_state, int32_t n_frames, float *host_obs);
 
-/* One gym step for every env: act[n_envs*7] -> obs[n_envs*25], rew[n_envs],
- * done[n_envs] (TimeLimit 200), info[n_envs*2] = {total_force_on_human, task_success}. */
+/* One gym step for every env: act[n_envs*act_dim] -> obs[n_envs*obs_dim], rew[n_envs],
+ * done[n_envs] (TimeLimit 200), info[n_envs*2] = {total_force_on_human, task_success}
+ * (FeedingJaco: act 7, obs 25, feeding.py:30-81; ScratchItchPR2: act 7, obs 30,
+ * scratch_itch.py:30-82). */
 int avr_step(avr_sim *sim, const float *act, float *obs, float *rew, uint8_t *done, float *info);
 int avr_step_device(avr_sim *sim, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
 /* Same, with synthetic actions a[e,t] ~ U(-1,1)^7 drawn on the device from Philox4x32-10
@@ -93,12 +98,40 @@ int32_t avr_n_envs(avr_sim *sim);
  * (one per 1024 envs, at most 4; AVR_ENV_GROUPS=1..8 in the environment at avr_create overrides).
  * Results do not depend on it.  No reference counterpart (diagnostic). */
 int32_t avr_env_groups(avr_sim *sim);
-int32_t avr_state_words(void);
+int32_t avr_state_words(void);          /* FeedingJaco's: avr_task_state_words(AVR_TASK_FEEDING) */
 int32_t avr_abi_version(void);
+/* Per-task sizes (-1 for an unknown task) and the handle's task. */
+int32_t avr_task_state_words(int32_t task);
+int32_t avr_task_obs_dim(int32_t task);
+int32_t avr_task_act_dim(int32_t task);
+int32_t avr_task(avr_sim *sim);
 /* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of each sub-step kernel, in
- * launch order: pairs (kinematics, broadphase, shape-pair list), narrowphase, a (manifolds,
- * dynamics, constraint rows), b (PGS + integration). */
-int avr_kernel_info(avr_sim *sim, int32_t *out16);
+ * launch order: pairs (kinematics, broadphase, shape-pair list), narrowphase, coop (the
+ * wave-cooperative GJK/EPA), a (manifolds, dynamics, constraint rows), b (PGS + integration):
+ * out20 holds 5 x 4 ints. */
+int avr_kernel_info(avr_sim *sim, int32_t *out20);
+
+/* ---- state queries (device-side gathers; host buffers; block until done) ----
+ * The reference reads these through PyBullet every step; here they come out of the state without
+ * copying the whole state block to the host.
+ * avr_get_q: joint positions / velocities of every articulated DoF, q[n_envs*n_dof],
+ *   qd[n_envs*n_dof] (either may be NULL), n_dof = avr_n_dof(sim): the robot's DoFs in URDF DFS
+ *   order, then the articulated human chain's (zeros while that chain is static).
+ *   Replaces p.getJointStates(robot | human, ...)[0:2] (env.py:320-321, feeding.py:126,
+ *   scratch_itch.py:109). */
+int32_t avr_n_dof(avr_sim *sim);
+int avr_get_q(avr_sim *sim, float *q, float *qd);
+/* avr_get_link_pose: world COM frame (x y z, qx qy qz qw) of articulated link `link` of every
+ *   env, out7[n_envs*7]; link < 0 selects the robot base.  Forward kinematics on the current
+ *   joint positions, as p.getLinkState(robot, link, computeForwardKinematics=True)[0:2]
+ *   (feeding.py:124, scratch_itch.py:105; link indices are the compiled robot's, URDF DFS order
+ *   within the simulated subtree). */
+int avr_get_link_pose(avr_sim *sim, int32_t link, float *out7);
+/* avr_get_contact_summary: per env, out4[n_envs*4] = {contact points, sum of normalForce over all
+ *   points, over robot-human points, over tool-human points} of the last sub-step's contact set:
+ *   the sums p.getContactPoints(...)[9] feeds to get_total_force (feeding.py:83-90,
+ *   scratch_itch.py:84-102). */
+int avr_get_contact_summary(avr_sim *sim, float *out4);
 const char *avr_last_error(avr_sim *sim);
 
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is

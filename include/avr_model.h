@@ -17,6 +17,11 @@
 extern "C" {
 #endif
 
+/* ---- tasks: one compiled scene and one state layout each ---- */
+enum { AVR_TASK_FEEDING = 0,     /* FeedingJaco-v0   (feeding.py, feeding_robots.py:7-9)       */
+       AVR_TASK_SCRATCH = 1 };   /* ScratchItchPR2-v0 (scratch_itch.py, scratch_itch_robots.py) */
+
+/* ==== FeedingJaco-v0 layout ==== */
 /* ---- capacities (compile-time; checked against the model at create time) ---- */
 #define AVR_MAX_LINKS 20        /* articulated links: robot (Jaco: 15) + head chain  */
 #define AVR_MAX_DOF 14          /* robot DoF (Jaco: 10) + head chain DoF (4)        */
@@ -34,7 +39,11 @@ extern "C" {
 
 /* shape / body kinds */
 enum { AVR_SPHERE = 0, AVR_CAPSULE = 1, AVR_BOX = 2, AVR_HULL = 3 };
-enum { AVR_BODY_ROBOT = 0, AVR_BODY_FREE = 1, AVR_BODY_STATIC = 2, AVR_BODY_HUMAN = 3 };
+/* ROBOT: an articulated robot link; FREE: a floating body; STATIC: fixed world pose; HUMAN: a
+ * per-env human slot (pose in the state; links of an articulated human chain are written there by
+ * the kinematics); RSTATIC: robot-fixed geometry, pose = the env's robot base frame (ScratchItch:
+ * the PR2 links outside the simulated left-arm subtree) */
+enum { AVR_BODY_ROBOT = 0, AVR_BODY_FREE = 1, AVR_BODY_STATIC = 2, AVR_BODY_HUMAN = 3, AVR_BODY_RSTATIC = 4 };
 enum { AVR_J_FIXED = 0, AVR_J_REVOLUTE = 1, AVR_J_PRISMATIC = 2 };
 
 /* ---- per-env state block (words) ---- */
@@ -75,7 +84,44 @@ enum { AVR_J_FIXED = 0, AVR_J_REVOLUTE = 1, AVR_J_PRISMATIC = 2 };
 #define AVR_CP_PAIR    14     /* body-pair index (candidate list)                    */
 #define AVR_CP_SLOT    15     /* reserved                                            */
 
+/* ==== ScratchItchPR2-v0 layout ====
+ * Articulated: the PR2's left-arm subtree (URDF links 64..85, 14 DoF; the rest of the PR2 is
+ * robot-fixed geometry at the reset joint values) and the human's right arm (joints 7..13, 7 DoF:
+ * the controllable joints 4..13 of scratch_itch.py:191 minus the fixed 4..6), always articulated:
+ * every impairment keeps these masses and drives them with reactive / tremor motors. */
+#define AVR_SI_MAX_LINKS 32       /* PR2 subtree 22 + human arm 7 (32-bit link masks)          */
+#define AVR_SI_MAX_DOF 24         /* 14 + 7, padded                                             */
+#define AVR_SI_HC_N 8             /* human arm chain slots (7 used)                             */
+#define AVR_SI_MAX_FREE 1         /* the scratcher                                              */
+#define AVR_SI_MAX_HUMAN 20
+#define AVR_SI_MAX_CONTACTS 64
+#define AVR_SI_ACT_DIM 7
+#define AVR_SI_OBS_DIM 30         /* scratch_itch.py:122                                        */
+#define AVR_SI_S_Q        0
+#define AVR_SI_S_QD       (AVR_SI_S_Q + AVR_SI_MAX_DOF)
+#define AVR_SI_S_QTGT     (AVR_SI_S_QD + AVR_SI_MAX_DOF)
+#define AVR_SI_S_KP       (AVR_SI_S_QTGT + AVR_SI_MAX_DOF)
+#define AVR_SI_S_MAXIMP   (AVR_SI_S_KP + AVR_SI_MAX_DOF)
+#define AVR_SI_S_FREE     (AVR_SI_S_MAXIMP + AVR_SI_MAX_DOF)
+#define AVR_SI_S_RBASE    (AVR_SI_S_FREE + AVR_SI_MAX_FREE * AVR_FB_WORDS)   /* PR2 base_footprint pose [7] (position_robot_toc) */
+#define AVR_SI_S_TASK     (AVR_SI_S_RBASE + 8)
+/* task words: 0-2, 3, 4, 7-10 as in FeedingJaco (target, iteration, task_success, gender, flags,
+ * contact count, articulated human chain = 1) */
+#define AVR_SI_T_LIMB     5       /* chain link index of the target limb (2: upper arm 9, 4: forearm 11) */
+#define AVR_SI_T_STRENGTH 6       /* human_strength (world_creation.py:72)                     */
+#define AVR_SI_T_PREV     11      /* prev_target_contact_pos [3] (scratch_itch.py:65,150)      */
+#define AVR_SI_T_TREMOR   14      /* 1: impairment 'tremor' (take_step drives the arm, env.py:327-337) */
+#define AVR_SI_T_ONARM    16      /* target_on_arm [3] in the limb frame (scratch_itch.py:281)  */
+#define AVR_SI_T_WORDS    24
+#define AVR_SI_S_HUMAN    (AVR_SI_S_TASK + AVR_SI_T_WORDS)
+/* human arm chain: [HC_N] target_human_joint_positions, [HC_N] human_tremors, [HC_N] lower and
+ * [HC_N] upper joint limits (x limit_scale per env, human_creation.py:226) */
+#define AVR_SI_S_HCH      (AVR_SI_S_HUMAN + AVR_SI_MAX_HUMAN * 7)
+#define AVR_SI_S_CP       (AVR_SI_S_HCH + 4 * AVR_SI_HC_N)
+#define AVR_SI_STATE_WORDS (AVR_SI_S_CP + AVR_SI_MAX_CONTACTS * AVR_CP_WORDS)
+
 /* ---- compiled scene (host arrays; row-major) ---- */
+#define AVR_DESC_HC 8             /* capacity of the hc_* arrays below                          */
 typedef struct avr_model_desc {
     /* robot articulation, fixed base, DFS link order */
     int32_t n_links, n_dof;
@@ -137,15 +183,26 @@ typedef struct avr_model_desc {
      * follow the robot's links; the chain hangs off the static human slot hc_parent_slot.
      * hc_n = 0: no chain.  Per-gender arrays are [male, female]. */
     int32_t hc_n, hc_parent_slot;
-    int32_t hc_slot[AVR_HC_N];             /* human slot of each chain link (-1: no shape)  */
-    int32_t hc_body[AVR_HC_N];             /* collision body of each chain link (-1: none)  */
-    double hc_jpos[2][AVR_HC_N][3];        /* joint origin in the parent link frame         */
-    double hc_axis[AVR_HC_N][3];
-    double hc_mass[2][AVR_HC_N], hc_inertia[2][AVR_HC_N][3];
-    double hc_lower[AVR_HC_N], hc_upper[AVR_HC_N];
+    int32_t hc_slot[AVR_DESC_HC];          /* human slot of each chain link (-1: no shape)  */
+    int32_t hc_body[AVR_DESC_HC];          /* collision body of each chain link (-1: none)  */
+    double hc_jpos[2][AVR_DESC_HC][3];     /* joint origin in the parent link frame         */
+    double hc_axis[AVR_DESC_HC][3];
+    double hc_mass[2][AVR_DESC_HC], hc_inertia[2][AVR_DESC_HC][3];
+    double hc_lower[AVR_DESC_HC], hc_upper[AVR_DESC_HC];
     double human_gain, human_force;        /* feeding.py:48 human_gains, feeding.py:17 human_forces */
     int32_t n_pairs_base;                  /* pairs [n_pairs_base, n_pairs): chain bodies vs static
                                               bodies, active in 'tremor' envs only              */
+    /* ---- ABI 3 ---- */
+    int32_t task;                          /* AVR_TASK_*: selects the state layout and task glue */
+    int32_t n_rstatic;                     /* AVR_BODY_RSTATIC bodies                          */
+    double human_gravity[3];               /* gravity on the articulated human chain (ScratchItch
+                                              -1 z, scratch_itch.py:260; FeedingJaco 0, feeding.py:286) */
+    double fix_pivot_b[3];                 /* fixed constraint: child pivot in the tool's body frame
+                                              (the child's base COM, world_creation.py:363)     */
+    double tool_tip[3];                    /* ScratchItch: tool link 1 COM in the tool body frame   */
+    double torso_com[3];                   /* ScratchItch: PR2 link 15 COM in the base frame        */
+    int32_t tool_handle_shapes;            /* ScratchItch: tool shapes of the handle (link -1)      */
+    double w_tool_force, w_scratch;        /* config.ini:7-8 tool_force_weight, scratch_reward_weight */
 } avr_model_desc;
 
 #ifdef __cplusplus
