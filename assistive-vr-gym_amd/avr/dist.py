@@ -11,7 +11,12 @@ import torch
 
 from . import _abi as ABI
 
-ROLL_WIDTH = ABI.OBS_DIM + 1 + ABI.INFO_DIM + 1   # obs, reward, info, done
+ROLL_WIDTH = ABI.OBS_DIM + 1 + ABI.INFO_DIM + 1   # FeedingJaco: obs, reward, info, done
+
+
+def roll_width(obs_dim):
+    """Columns of one env's rollout row: obs, reward, info, done."""
+    return obs_dim + 1 + ABI.INFO_DIM + 1
 
 
 def shard(envs_per_rank, rank):
@@ -20,10 +25,11 @@ def shard(envs_per_rank, rank):
 
 
 def pack_rollout(roll, j, obs, rew, info, done):
-    """roll[j] (E, ROLL_WIDTH) <- one step of outputs (device tensors, no host sync)."""
-    roll[j, :, :ABI.OBS_DIM] = obs
-    roll[j, :, ABI.OBS_DIM] = rew
-    roll[j, :, ABI.OBS_DIM + 1:ABI.OBS_DIM + 1 + ABI.INFO_DIM] = info
+    """roll[j] (E, W) <- one step of outputs (device tensors, no host sync); W = roll_width(obs_dim)."""
+    od = obs.shape[1]
+    roll[j, :, :od] = obs
+    roll[j, :, od] = rew
+    roll[j, :, od + 1:od + 1 + ABI.INFO_DIM] = info
     roll[j, :, -1] = done.to(roll.dtype)
 
 

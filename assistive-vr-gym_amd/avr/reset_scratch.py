@@ -1,0 +1,309 @@
+"""Host-side reset path for ScratchItchPR2-v0 (ScratchItchEnv.reset, scratch_itch.py:130-273).
+
+It produces the initial per-env state block (ScratchItch layout, `_abi.SI`) the device step
+consumes:
+  * gender, impairment (world_creation.py:66-72: limit_scale, human_strength, human_tremors);
+  * the human pose: setup_human_joints with the ScratchItch joint targets (scratch_itch.py:257-259;
+    world_creation.py:135-179) clamped by the (scaled) joint limits; the right arm (controllable
+    joints 4..13; its revolute joints 7..13 are the articulated chain) keeps its masses and gets
+    reactive position motors (gain 0.01, force human_strength) or, under 'tremor', the take_step
+    tremor motors;
+  * the PR2: reset_robot_joints (env.py:450-464), then position_robot_toc (env.py:489-585): random
+    base poses, IK of the left gripper tool frame (link 76) to the start goal and to the human's
+    shoulder / elbow / wrist, best base by goals reached then joint-limit-weighted manipulability
+    (JLWKI, env.py:466-477,536-553).  p.calculateInverseKinematics is a Bullet internal: it is
+    restated as damped least squares with a random rest pose per attempt (util.py:76-105);
+  * the gripper open at 0.25 (world_creation.py:309-328), the scratcher on link 76's COM frame
+    (world_creation.py:330-365), and the target (generate_target, scratch_itch.py:275-287;
+    util.point_on_capsule, util.py:112-132).
+ScratchItch's reset runs no settling frames after the tool is attached.
+
+Per-env randomness: numpy Generator keyed by (seed, env_id[, episode]) as in reset.py; the
+reference's single np_random stream cannot be reproduced draw for draw.
+"""
+import numpy as np
+
+from . import _abi as ABI
+from . import geom as G
+from .reset import _cross, _impairment, _qaxis, _qmul, _qrot, _rng, human_link_poses
+
+SI = ABI.SI
+HUMAN_SCALED = set(range(7, 14)) | set(range(17, 24)) | set(range(24, 28))   # limit_scale joints (human_creation.py)
+ARM_CHAIN = (7, 8, 9, 10, 11, 12, 13)
+CONTROLLABLE = tuple(range(4, 14))            # scratch_itch.py:191
+JOINT_TARGETS = [(7, 30), (10, -90), (20, -90), (28, -90), (31, 80), (35, -90), (38, 80)]   # scratch_itch.py:257
+LEFT_ARM_RESET = (1.75, 1.25, 1.5, -0.5, 1, 0, 1)     # env.py:456-457
+
+
+# ----------------------------------------------------------------------------- human
+def human_joint_angles(A, gender, limit_scale=1.0):
+    """(q[42], scaled lower, scaled upper): setup_human_joints + enforce_joint_limits."""
+    n = len(A['human_%s_parent' % gender])
+    q = np.zeros(n)
+    for j, ang in JOINT_TARGETS:
+        q[j] = np.deg2rad(ang)
+    lo = A['human_%s_lower' % gender].copy()
+    hi = A['human_%s_upper' % gender].copy()
+    for j in HUMAN_SCALED:
+        lo[j] *= limit_scale
+        hi[j] *= limit_scale
+    jt = A['human_%s_jtype' % gender]
+    for j in range(n):
+        if jt[j] == 1 and not (lo[j] == 0 and hi[j] == -1):
+            q[j] = min(max(q[j], lo[j]), hi[j])
+    return q, lo, hi
+
+
+def point_on_capsule(rng, length, radius):
+    """util.point_on_capsule(p1=0, p2=[0, 0, -length], radius, theta in [0, 2 pi))."""
+    axis = np.array([0.0, 0.0, -1.0])
+    L = rng.uniform(radius, length)
+    m = int(np.argmax(np.abs(axis)))
+    y = np.zeros(3)
+    y[(m + 1) % 3] = 1
+    ortho = np.cross(axis, y)
+    ortho /= np.linalg.norm(ortho)
+    normal = np.cross(axis, ortho)
+    th = rng.uniform(0, 2 * np.pi)
+    return L * axis + radius * np.cos(th) * ortho + radius * np.sin(th) * normal
+
+
+# ----------------------------------------------------------------------------- PR2 arm FK / IK
+def arm_fk(A, Q, bp, bq, links=None):
+    """Batched FK of the compiled robot (the PR2 left-arm subtree) on per-row bases (N, 3/4):
+    COM positions/quaternions and joint axes/origins, (N, nl, .).  `links` (ascending, closed
+    under parents) restricts the work to those links; the others stay zero."""
+    N = Q.shape[0]
+    nl = int(A['n_links'])
+    LP = np.zeros((N, nl, 3)); LQ = np.zeros((N, nl, 4))
+    CP = np.zeros((N, nl, 3)); CQ = np.zeros((N, nl, 4))
+    AX = np.zeros((N, nl, 3)); OR = np.zeros((N, nl, 3))
+    for i in (range(nl) if links is None else links):
+        p = A['rl_parent'][i]
+        pp, pq = (bp, bq) if p < 0 else (LP[:, p], LQ[:, p])
+        tp = pp + _qrot(pq, np.broadcast_to(A['rl_jpos'][i], (N, 3)))
+        tq = _qmul(pq, np.broadcast_to(A['rl_jquat'][i], (N, 4)))
+        OR[:, i] = tp
+        AX[:, i] = _qrot(tq, np.broadcast_to(A['rl_axis'][i], (N, 3)))
+        dof = A['rl_dof'][i]
+        if A['rl_jtype'][i] == 1:
+            tq = _qmul(tq, _qaxis(np.broadcast_to(A['rl_axis'][i], (N, 3)), Q[:, dof]))
+        elif A['rl_jtype'][i] == 2:
+            tp = tp + AX[:, i] * Q[:, dof][:, None]
+        LP[:, i], LQ[:, i] = tp, tq
+        CP[:, i] = tp + _qrot(tq, np.broadcast_to(A['rl_com_pos'][i], (N, 3)))
+        CQ[:, i] = _qmul(tq, np.broadcast_to(A['rl_com_quat'][i], (N, 4)))
+    return CP, CQ, AX, OR
+
+
+def _chain(A, link):
+    out = []
+    k = link
+    while k >= 0:
+        out.append(k)
+        k = A['rl_parent'][k]
+    return sorted(out)
+
+
+def _chain_cols(A, link, dofs):
+    chain = _chain(A, link)
+    cols = []
+    for d in dofs:
+        l = [k for k in chain if A['rl_dof'][k] == d]
+        cols.append(l[0] if l else -1)
+    return cols
+
+
+def arm_jacobian(A, link, cols, CP, AX, OR):
+    N = CP.shape[0]
+    J = np.zeros((N, 6, len(cols)))
+    for c, l in enumerate(cols):
+        if l < 0:
+            continue
+        J[:, :3, c] = _cross(AX[:, l], CP[:, link] - OR[:, l])
+        J[:, 3:, c] = AX[:, l]
+    return J
+
+
+def ik_dls(A, link, Q0, bp, bq, tp, tq, dofs, lower, upper, iters):
+    """Damped least squares on the rows of Q0 (N, nd) towards positions tp (N, 3) and, when tq is
+    not None, orientations tq (N, 4) of link's COM frame (FK of link's chain only; rows that have
+    converged stop moving, and the loop ends once all have)."""
+    Q = Q0.copy()
+    chain = _chain(A, link)
+    cols = _chain_cols(A, link, dofs)
+    for it in range(iters):
+        CP, CQ, AX, OR = arm_fk(A, Q, bp, bq, chain)
+        ep = tp - CP[:, link]
+        J = arm_jacobian(A, link, cols, CP, AX, OR)
+        if tq is not None:
+            dq = _qmul(tq, CQ[:, link] * np.array([-1, -1, -1, 1.0]))
+            dq = np.where(dq[:, 3:4] < 0, -dq, dq)
+            s = np.linalg.norm(dq[:, :3], axis=1)
+            ang = 2.0 * np.arctan2(s, dq[:, 3])
+            er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
+            err = np.concatenate([ep, er], 1)
+            Jr = J
+        else:
+            err = ep
+            Jr = J[:, :3]
+        if it % 10 == 9 and np.all(np.abs(err) < 1e-6):
+            break
+        k = Jr.shape[1]
+        JJ = Jr @ np.transpose(Jr, (0, 2, 1)) + 1e-4 * np.eye(k)[None]
+        step = np.transpose(Jr, (0, 2, 1)) @ np.linalg.solve(JJ, err[..., None])
+        Q[:, dofs] = np.clip(Q[:, dofs] + step[..., 0], lower, upper)
+    CP, CQ, AX, OR = arm_fk(A, Q, bp, bq, chain)
+    return Q, CP, CQ, AX, OR
+
+
+def jlwki(J, q, lower, upper):
+    """Joint-limit-weighted kinematic isotropy (env.py:466-477, 548-553), rows of J (N, 6, 7)."""
+    phi, lam = 0.5, 0.05
+    qr = 0.5 * (upper - lower)
+    w = 1.0 - np.power(phi, (qr - np.abs(qr - q + lower)) / (lam * qr) + 1)
+    w = np.maximum(w, 0.001)
+    M = J @ (w[:, :, None] * np.transpose(J, (0, 2, 1)))
+    det = np.maximum(np.linalg.det(M), 0.0)
+    return np.power(det, 1.0 / 6.0) / (np.trace(M, axis1=1, axis2=2) / 6.0)
+
+
+def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200):
+    """Batched position_robot_toc for the PR2 (env.py:489-585; scratch_itch.py:189-190): per env,
+    `attempts` random base poses; at each the start goal (link 76 to target_pos with identity
+    orientation, base offset pos_offset=[0.1, 0, 0]) must be reached (0.03 on position and
+    quaternion), then the shoulder / elbow / wrist positions count as further goals; the best
+    base maximises goals reached, then summed manipulability.  Returns (base_pos, base_quat,
+    arm q, start target, ok) per env."""
+    N = len(rngs)
+    nd = int(A['n_dof'])
+    arm = np.array(md.arm_dofs)
+    link = int(A['task_tool_link'])
+    lo = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
+    hi = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
+    # draws per env: the start goal, then per attempt the base pose and the IK rest pose
+    tstart = np.stack([np.array([-0.55, 0, 0.8]) + r.uniform(-0.05, 0.05, size=3) for r in rngs])
+    M = N * attempts
+    bp = np.zeros((M, 3)); yaw = np.zeros(M); rest = np.zeros((M, len(arm)))
+    for e, r in enumerate(rngs):
+        for a in range(attempts):
+            k = e * attempts + a
+            bp[k] = np.array([-0.85, -0.4, 0]) + np.array([0.1, 0, 0]) + np.array([r.uniform(-0.5, 0), r.uniform(-0.5, 0.5), 0])
+            yaw[k] = np.deg2rad(r.uniform(-30, 30))
+            rest[k] = r.uniform(lo, hi)
+    bq = np.stack([np.zeros(M), np.zeros(M), np.sin(0.5 * yaw), np.cos(0.5 * yaw)], 1)
+    Q0 = np.zeros((M, nd))
+    for i, d in enumerate(arm):
+        Q0[:, d] = rest[:, i]
+    for d in md.finger_dofs:
+        Q0[:, d] = md.params['finger_target']
+    tp = np.repeat(tstart, attempts, 0)
+    tq = np.tile(np.array([0, 0, 0, 1.0]), (M, 1))
+    Qs, CP, CQ, AX, OR = ik_dls(A, link, Q0, bp, bq, tp, tq, arm, lo, hi, iters)
+    pe = np.linalg.norm(tp - CP[:, link], axis=1)
+    qe = np.linalg.norm(tq - CQ[:, link], axis=1)
+    ok0 = (pe < 0.03) & ((qe < 0.03) | (np.abs(qe - 2) < 0.03))
+    cols = _chain_cols(A, link, arm)
+    manip = np.where(ok0, jlwki(arm_jacobian(A, link, cols, CP, AX, OR), Qs[:, arm], lo, hi), 0.0)
+    goals = ok0.astype(int)
+    for g in range(3):                                   # shoulder, elbow, wrist (position only)
+        hp = np.repeat(human_goals[:, g], attempts, 0)
+        Qg, CPg, _, AXg, ORg = ik_dls(A, link, np.where(ok0[:, None], Q0, Q0), bp, bq, hp, None, arm, lo, hi, iters)
+        okg = ok0 & (np.linalg.norm(hp - CPg[:, link], axis=1) < 0.03)
+        manip = manip + np.where(okg, jlwki(arm_jacobian(A, link, cols, CPg, AXg, ORg), Qg[:, arm], lo, hi), 0.0)
+        goals = goals + okg.astype(int)
+    goals = np.where(ok0, goals, -1).reshape(N, attempts)
+    manip = manip.reshape(N, attempts)
+    out_bp, out_bq, out_q, ok = np.zeros((N, 3)), np.zeros((N, 4)), np.zeros((N, nd)), np.zeros(N, bool)
+    for e in range(N):
+        best = None
+        for a in range(attempts):
+            g, mm = goals[e, a], manip[e, a]
+            if g > 0 and (best is None or g > goals[e, best] or (g == goals[e, best] and mm > manip[e, best])):
+                best = a
+        if best is None:                                  # no start goal reached: the closest attempt
+            best = int(np.argmin(pe.reshape(N, attempts)[e]))
+        else:
+            ok[e] = True
+        k = e * attempts + best
+        out_bp[e], out_bq[e], out_q[e] = bp[k], bq[k], Qs[k]
+    return out_bp, out_bq, out_q, tstart, ok
+
+
+# ----------------------------------------------------------------------------- full reset
+def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100, iters=200):
+    """Initial ScratchItch state blocks (float64 (N, SI.STATE_WORDS)) and per-env metadata."""
+    env_ids = list(env_ids)
+    N = len(env_ids)
+    eps = [0] * N if episodes is None else list(episodes)
+    rngs = [_rng(seed, e, ep) for e, ep in zip(env_ids, eps)]
+    S = np.zeros((N, SI.STATE_WORDS))
+    nd = int(A['n_dof'])
+    hc = int(A['hc_n'])
+    meta = []
+    goals = np.zeros((N, 3, 3))
+    slot_link = A['human_slot_link']
+    for k in range(N):
+        rng = rngs[k]
+        g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')   # scratch_itch.py:163
+        imp = _impairment(rng, impairment)
+        ls = rng.uniform(0.5, 1.0) if imp == 'limits' else 1.0          # world_creation.py:71
+        strength = rng.uniform(0.25, 1.0) if imp == 'weakness' else 1.0  # world_creation.py:72
+        tremors = rng.uniform(np.deg2rad(-10), np.deg2rad(10), size=len(CONTROLLABLE)) if imp == 'tremor' else np.zeros(len(CONTROLLABLE))
+        qh, lo, hi = human_joint_angles(A, g, ls)
+        base_p, base_q, P, Q = human_link_poses(A, g, qh)
+        st = S[k]
+        for s, l in enumerate(slot_link):
+            st[SI.S_HUMAN + 7 * s:SI.S_HUMAN + 7 * s + 7] = np.concatenate([base_p, base_q]) if l < 0 else np.concatenate([P[l], Q[l]])
+        goals[k] = P[[9, 11, 13]]                                       # shoulder, elbow, wrist (scratch_itch.py:187-190)
+        for c, j in enumerate(ARM_CHAIN):
+            st[SI.S_Q + nd + c] = qh[j]
+            st[SI.S_HCH + c] = qh[j]                                    # target_human_joint_positions
+            st[SI.S_HCH + SI.HC_N + c] = tremors[CONTROLLABLE.index(j)]
+            st[SI.S_HCH + 2 * SI.HC_N + c] = lo[j]
+            st[SI.S_HCH + 3 * SI.HC_N + c] = hi[j]
+            # reactive motors (world_creation.py:171-179), replaced by take_step's under 'tremor'
+            st[SI.S_QTGT + nd + c] = qh[j]
+            st[SI.S_KP + nd + c] = md.params['reactive_gain']
+            st[SI.S_MAXIMP + nd + c] = md.params['reactive_force'] * strength * md.params['time_step']
+        t = SI.S_TASK
+        st[t + SI.T_GENDER] = 0 if g == 'male' else 1
+        st[t + SI.T_HDYN] = 1.0
+        st[t + SI.T_TREMOR] = 1.0 if imp == 'tremor' else 0.0
+        st[t + SI.T_STRENGTH] = strength
+        meta.append(dict(gender=g, impairment=imp, limit_scale=ls, strength=strength))
+    bp, bq, Qa, tstart, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters)
+    CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
+    link = int(A['task_tool_link'])
+    piv = A['task_tool_pivot']
+    gidx = {'male': 0, 'female': 1}
+    for k in range(N):
+        st = S[k]
+        rng = rngs[k]
+        st[SI.S_RBASE:SI.S_RBASE + 3] = bp[k]
+        st[SI.S_RBASE + 3:SI.S_RBASE + 7] = bq[k]
+        st[SI.S_Q:SI.S_Q + nd] = Qa[k]
+        for d in range(nd):                          # default velocity motors (PyBullet createJointMotors)
+            st[SI.S_KP + d] = 0.0
+            st[SI.S_QTGT + d] = 0.0
+            st[SI.S_MAXIMP + d] = md.params['default_motor_impulse']
+        for d in md.finger_dofs:                     # set_gripper_open_position(0.25) (world_creation.py:323-328)
+            st[SI.S_KP + d] = md.params['finger_gain']
+            st[SI.S_QTGT + d] = md.params['finger_target']
+            st[SI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+        # scratcher: its base (handle) COM on link 76's COM frame; the body frame is the composite COM
+        hq = CQ[k, link]
+        st[SI.S_FREE:SI.S_FREE + 3] = CP[k, link] - G.quat_rotate(hq, piv)
+        st[SI.S_FREE + 3:SI.S_FREE + 7] = hq
+        # generate_target (scratch_itch.py:275-287)
+        g = meta[k]['gender']
+        li, ln, rad = A['task_limbs'][gidx[g]][int(rng.integers(2))]
+        on_arm = point_on_capsule(rng, ln, rad)
+        t = SI.S_TASK
+        ck = ARM_CHAIN.index(int(li))
+        st[t + SI.T_LIMB] = ck
+        st[t + SI.T_ONARM:t + SI.T_ONARM + 3] = on_arm
+        lp = st[SI.S_HUMAN + 7 * list(slot_link).index(int(li)):][:7]
+        st[t + SI.T_TARGET:t + SI.T_TARGET + 3] = G.tf_mul(lp[:3], lp[3:], on_arm, [0, 0, 0, 1])[0]
+        meta[k].update(base_ok=bool(ok[k]), limb=int(li), start_goal=tstart[k])
+    return S, meta

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
-"""Benchmark: FeedingJaco-v0 env-steps/s on MI355X (BASELINE.json configs[1]).
+"""Benchmark: env-steps/s on MI355X.  Default: FeedingJaco-v0 at 4096 envs (BASELINE.json
+configs[1]); --task ScratchItchPR2-v0 runs configs[2].
 
-One "step" = one gym step of every env (take_step + 5 x stepSimulation x 2 sub-steps + task
-glue) = one launch of the gfx950 step kernel.  Synthetic random actions are drawn on the device
-(Philox4x32-10 keyed by (seed=1001, global env id, step), examples/random_actions.py semantics).
-Inputs are resident in HBM before the timed region; host buffers are not touched inside it.
+One "step" = one gym step of every env (take_step + 5 x stepSimulation (FeedingJaco: 2 sub-steps
+each, ScratchItch: 1) + task glue) = one launch sequence of the gfx950 kernels.  Synthetic random
+actions are drawn on the device (Philox4x32-10 keyed by (seed=1001, global env id, step),
+examples/random_actions.py semantics).  Inputs are resident in HBM before the timed region; host
+buffers are not touched inside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E_per_gpu]
+  python bench.py [--task T] [--gpus N] [--steps K] [--warmup W] [--envs E_per_gpu]
   torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Multi-GPU: envs shard across ranks (global env id = rank*E + e, independent units -> weak
@@ -26,29 +28,45 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-# algorithmic bytes per FeedingJaco env-step = persistent state read + written once
-# (605 words, 2420 B each way) + read-only per-env params (144 B) + action in (28 B) + obs,
-# reward, done, info out (116 B).
-ALGO_BYTES_PER_ENV_STEP = 2420 * 2 + 144 + 28 + 116      # 5128
+# algorithmic bytes per env-step = persistent state read + written once + read-only
+# per-env params + action in + obs, reward, done, info out.  FeedingJaco: 605 words (2420 B) each
+# way + 144 + 28 + 116 = 5128 B.  ScratchItchPR2: 563 words (2252 B) each way + 120 + 28 + 136.
+TASKS = {
+    'FeedingJaco-v0': dict(task=0, bytes=2420 * 2 + 144 + 28 + 116, settle=100, substeps=10, iters=10, pool=1024,
+                           workload='FeedingJaco-v0, %d envs/GPU, rigid-only, random actions'),
+    'ScratchItchPR2-v0': dict(task=1, bytes=2252 * 2 + 120 + 28 + 136, settle=0, substeps=5, iters=50, pool=128,
+                              workload='ScratchItchPR2-v0, %d envs/GPU, human-capsule contact + tool force reward, random actions'),
+}
+VALU_CYC = 2.0          # v_fma_f32 wave64 issue throughput, cycles (MI355X_MICROARCH.md cycle table)
+SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
-def layout_bytes_per_env_step(ABI):
+def layout_bytes_per_env_step(L):
     """What this build's state layout actually moves per env-step (state block in and out once,
-    it stays in LDS across the 10 sub-steps; actions are generated on the device)."""
-    return 2 * ABI.STATE_WORDS * 4 + (ABI.OBS_DIM + 1 + ABI.INFO_DIM) * 4 + 1
+    it stays resident across the sub-steps; actions are generated on the device)."""
+    return 2 * L.STATE_WORDS * 4 + (L.OBS_DIM + 1 + L.INFO_DIM) * 4 + 1
 
 
-def cpu_baseline(md, A, RS, seconds, threads, impairment):
-    """Oracle (the CPU restatement, fp64) on the host cores; bounded sample."""
+def reset_pool(task, A, md, ids, impairment):
+    if task == 1:
+        from avr import reset_scratch as RSS
+        return RSS.batch_reset_states(A, md, 1001, ids, impairment=impairment, attempts=25, iters=100)
+    from avr import reset as RS
+    return RS.batch_reset_states_fast(A, md, 1001, ids, impairment=impairment)
+
+
+def cpu_baseline(name, md, A, seconds, threads, impairment):
+    """Oracle (the CPU restatement, fp64) on the host cores; bounded sample of 4 envs per thread."""
     import numpy as np
     from oracle.oracle import Oracle
     from avr import _lib
-    n = max(threads * 2, 8)
-    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)), impairment=impairment)
+    T = TASKS[name]
+    n = max(threads * 4, 8)
+    S, _ = reset_pool(T['task'], A, md, list(range(n)), impairment)
     o = Oracle(md, n)
     o.set_threads(threads)
     o.set_state(S)
-    o.settle(100)
+    o.settle(T['settle'])
     steps = 0
     t0 = time.perf_counter()
     while True:
@@ -58,29 +76,62 @@ def cpu_baseline(md, A, RS, seconds, threads, impairment):
         el = time.perf_counter() - t0
         if el >= seconds and steps >= 2:
             break
-    return dict(value=n * steps / el, unit='env-steps/s', cores=threads, kind='port',
-                sample='FeedingJaco-v0, %d envs x %d gym steps (%.1f s) after a 100-frame settle; fp64 oracle, OpenMP over envs' % (n, steps, el))
+    return dict(value=n * steps / el, unit='env-steps/s', cores=threads, host_cpus=os.cpu_count(), kind='port',
+                sample='%s, %d envs x %d gym steps (%.1f s) after a %d-frame settle; fp64 oracle, OpenMP over envs on %d threads '
+                       '(the GPU box\'s CPU share, OMP_NUM_THREADS; os.cpu_count() reports the whole host)' % (
+                           name, n, steps, el, T['settle'], threads))
+
+
+def pmc_summary(task, kernels, ms_per_step, E):
+    """HBM traffic and SQ issue figures from the committed rocprofv3 PMC summary of this task's
+    bench (profiles/pmc_<task>.json, tools/rocpd_summary.py), if its kernel set and env count match."""
+    name = {0: 'pmc_traffic.json', 1: 'pmc_scratch.json'}[task]
+    path = os.path.join(ROOT, 'profiles', name)
+    if not os.path.exists(path):
+        return None
+    try:
+        tj = json.load(open(path))
+    except Exception:
+        return None
+    if tj.get('envs') != E or tj.get('task', 0) != task or set(tj.get('kernels_per_step', {})) != set(kernels):
+        return None
+    out = dict(traffic=tj.get('hbm_bytes_per_step'), source='profiles/' + name)
+    sq = tj.get('sq_per_launch', {})
+    disp = tj.get('dispatches_per_step', {})
+    if sq and disp:
+        valu = sum(sq[k]['SQ_INSTS_VALU'] * disp.get(k, 0) for k in sq)
+        out['valu_busy_chip'] = valu * VALU_CYC / (SIMDS * CLOCK_HZ * ms_per_step * 1e-3)
+        per = {}
+        for k, c in sq.items():
+            wc = max(c.get('SQ_WAVE_CYCLES', 0.0), 1.0)
+            per[k] = dict(issue_frac=c.get('SQ_ACTIVE_INST_ANY', 0.0) / wc, wait_frac=c.get('SQ_WAIT_ANY', 0.0) / wc,
+                          valu_insts_per_wave=c['SQ_INSTS_VALU'] / max(c.get('SQ_WAVES', 1.0), 1.0))
+        out['sq'] = per
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument('--task', default='FeedingJaco-v0', choices=sorted(TASKS))
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
-    ap.add_argument('--settle', type=int, default=100)
+    ap.add_argument('--settle', type=int, default=None, help='reset settle frames (FeedingJaco 100, ScratchItch 0)')
     ap.add_argument('--gather-every', type=int, default=16)
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--reset-pool', type=int, default=1024,
-                    help='distinct host reset states, tiled over the envs (IK is host-side)')
+    ap.add_argument('--reset-pool', type=int, default=None,
+                    help='distinct host reset states, tiled over the envs (IK is host-side; FeedingJaco 1024, ScratchItch 128)')
     ap.add_argument('--impairment', default='random',
-                    help="human impairment per env: 'random' is FeedingJaco-v0's own setting (feeding.py:175)")
+                    help="human impairment per env: 'random' is the tasks' own setting (feeding.py:175, scratch_itch.py:178)")
     args = ap.parse_args()
+    T = TASKS[args.task]
+    settle = T['settle'] if args.settle is None else args.settle
 
     import numpy as np
     import torch
-    from avr import _abi as ABI, reset as RS, _lib
+    from avr import _abi as ABI, _lib
     from avr import dist as D
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -93,29 +144,31 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
-    A = ABI.load_scene()
+    A = ABI.load_scene(T['task'])
     md = ABI.ModelDesc(A)
+    L = md.layout
     E = args.envs
     # reset pool: distinct initial states for global env ids; tiled if pool < E
-    pool = min(args.reset_pool, E)
+    pool = min(args.reset_pool or T['pool'], E)
     base_id, _ = D.shard(E, rank)
-    S_pool, meta = RS.batch_reset_states_fast(A, md, 1001, [base_id + i for i in range(pool)], impairment=args.impairment)
+    S_pool, meta = reset_pool(T['task'], A, md, [base_id + i for i in range(pool)], args.impairment)
     n_tremor = sum(m['impairment'] == 'tremor' for m in meta)
     import hashlib
     pool_sha = hashlib.sha1(S_pool.astype(np.float32).tobytes()).hexdigest()[:12]
     S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
     sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
     sim.set_state(S.astype(np.float32))
-    sim.settle(args.settle)
+    sim.settle(settle)
 
-    obs = torch.zeros(E, ABI.OBS_DIM, device=dev)
+    obs = torch.zeros(E, L.OBS_DIM, device=dev)
     rew = torch.zeros(E, device=dev)
     done = torch.zeros(E, dtype=torch.uint8, device=dev)
-    info = torch.zeros(E, ABI.INFO_DIM, device=dev)
+    info = torch.zeros(E, L.INFO_DIM, device=dev)
     ext = torch.cuda.ExternalStream(sim.stream(), device=dev)
     G = args.gather_every
-    roll = torch.zeros(G, E, D.ROLL_WIDTH, device=dev)
-    gathered = torch.zeros(world * G * E * D.ROLL_WIDTH, device=dev) if world > 1 else None
+    W = D.roll_width(L.OBS_DIM)
+    roll = torch.zeros(G, E, W, device=dev)
+    gathered = torch.zeros(world * G * E * W, device=dev) if world > 1 else None
 
     def one_step(t, k):
         sim.step_random_device(t, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr())
@@ -161,20 +214,24 @@ def main():
     step_kernel_ms = sum(v['ms_per_step'] for v in kernels.values())
     dominant = max(kernels, key=lambda k: kernels[k]['ms_per_step'])
     St = sim.get_state()
-    flags = St[:, ABI.S_TASK + ABI.T_FLAGS].astype(np.int64)
+    flags = St[:, L.S_TASK + L.T_FLAGS].astype(np.int64)
     value = world * E * args.steps / el
-    bpe = ALGO_BYTES_PER_ENV_STEP
+    bpe = T['bytes']
     achieved = bpe * E / (step_kernel_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            # only a profile of this build's kernel set counts (kernels_per_step names them)
-            if tj.get('envs') == E and set(tj.get('kernels_per_step', {})) == set(sim.kernel_kinds):
-                traffic = tj.get('hbm_bytes_per_step')
-        except Exception:
-            traffic = None
+    ms_per_step = el / args.steps * 1e3
+    pmc = pmc_summary(T['task'], sim.kernel_kinds, ms_per_step, E)
+    traffic = pmc['traffic'] if pmc else None
+    # the bound: the larger of the two roofline fractions the path could sit on (HBM bytes vs the
+    # dense matrix-core peak; the path issues no MFMA, so its MFMA fraction is 0)
+    fracs = {'hbm': achieved / HBM_PEAK_GBS, 'mfma': 0.0}
+    bound = max(fracs, key=fracs.get)
+    # what actually limits the kernels, from the PMC SQ counters of the dominant kernel: issue-
+    # or wait-dominated wave lifetime (None without a matching PMC summary)
+    limiter = None
+    if pmc and pmc.get('sq', {}).get(dominant):
+        q = pmc['sq'][dominant]
+        limiter = 'latency (waves waiting %.0f%% of their cycles, issuing %.0f%%)' % (100 * q['wait_frac'], 100 * q['issue_frac']) \
+            if q['wait_frac'] > q['issue_frac'] else 'instruction issue (%.0f%% of wave cycles)' % (100 * q['issue_frac'])
     out = {
         'metric': 'env-steps/sec at N parallel envs, 1/2/4/8 MI355X; max |dq| vs PyBullet',
         'value': value,
@@ -182,29 +239,31 @@ def main():
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': el / args.steps * 1e3,
+        'ms_per_step': ms_per_step,
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
         'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the host IK path (%d distinct per GPU, tiled)' % pool,
-        'config': {'workload': 'FeedingJaco-v0, %d envs/GPU, rigid-only, random actions' % E, 'envs_per_gpu': E,
+        'config': {'workload': T['workload'] % E, 'task': args.task, 'envs_per_gpu': E,
                    'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
-                   'global_envs': world * E, 'substeps_per_env_step': 10, 'solver_iterations': 10,
+                   'global_envs': world * E, 'substeps_per_env_step': T['substeps'], 'solver_iterations': T['iters'],
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None,
                    'env_groups': sim.env_groups()},
-        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'roofline': {'bound': bound, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     # the HBM roofline is the bound the contract names; the kernels sit far below
-                     # it and are limited by VALU issue and memory latency
-                     'limiter': 'valu-issue/latency' if achieved / HBM_PEAK_GBS < 0.05 else 'hbm',
+                     'fracs': fracs, 'limiter': limiter,
+                     'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
+                     'sq_by_kernel': pmc.get('sq') if pmc else None,
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': 'one env-step = 1 take_step + 10 x (substep_pairs, narrowphase, coop, substep_a, substep_b4) + 1 task launch; '
+                     'scope': 'one env-step = 1 take_step + %d x (substep_pairs, narrowphase, coop, substep_a, substep_b4) + 1 task launch; '
                               'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
                               'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
-                              'sequences, so its stream time per step is below the summed durations; '
-                              'traffic = PMC HBM bytes of the step (profiles/pmc_traffic.json), traffic_GBs = traffic / summed launch durations',
-                     'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(ABI),
+                              'sequences, so its stream time per step is below the summed durations; traffic = PMC HBM bytes of the '
+                              'step and valu_busy = PMC VALU instructions x %.0f cycles / (%d SIMDs x %.1f GHz x ms_per_step), both from '
+                              'the task\'s committed rocprofv3 summary (%s)' % (
+                                  T['substeps'], VALU_CYC, SIMDS, CLOCK_HZ / 1e9, pmc['source'] if pmc else 'none matching'),
+                     'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(L),
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
                      'dominant_kernel': dominant, 'kernels': kernels},
         'nan_or_overflow_envs': int(np.count_nonzero(flags)),
@@ -213,9 +272,10 @@ def main():
         'reset_pool_sha1': pool_sha,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the host threads this process may use: OMP_NUM_THREADS (the GPU box's CPU share, 16 per
+        # GPU; os.cpu_count() reports the whole machine there), else every CPU of this host
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-        threads = max(1, min(threads, 16))
-        out['cpu_baseline'] = cpu_baseline(md, A, RS, args.cpu_seconds, threads, args.impairment)
+        out['cpu_baseline'] = cpu_baseline(args.task, md, A, args.cpu_seconds, max(1, threads), args.impairment)
     elif rank == 0:
         out['cpu_baseline'] = None
     if rank == 0:

@@ -18,8 +18,8 @@ extern "C" {
 #endif
 
 /* ---- tasks: one compiled scene and one state layout each ---- */
-enum { AVR_TASK_FEEDING = 0,     /* FeedingJaco-v0   (feeding.py, feeding_robots.py:7-9)       */
-       AVR_TASK_SCRATCH = 1 };   /* ScratchItchPR2-v0 (scratch_itch.py, scratch_itch_robots.py) */
+#define AVR_TASK_FEEDING 0       /* FeedingJaco-v0   (feeding.py, feeding_robots.py:7-9)       */
+#define AVR_TASK_SCRATCH 1       /* ScratchItchPR2-v0 (scratch_itch.py, scratch_itch_robots.py) */
 
 /* ==== FeedingJaco-v0 layout ==== */
 /* ---- capacities (compile-time; checked against the model at create time) ---- */

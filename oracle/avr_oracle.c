@@ -27,6 +27,68 @@
 
 #include "../include/avr_model.h"
 
+/* Task layout (include/avr_model.h): one build per task, AVR_TASK selects it (Makefile). */
+#ifndef AVR_TASK
+#define AVR_TASK AVR_TASK_FEEDING
+#endif
+#define T_TARGET 0
+#define T_ITER 3
+#define T_SUCCESS 4
+#define T_GENDER 7
+#define T_FLAGS 8
+#define T_NCP 9
+#define T_HDYN 10
+#if AVR_TASK == AVR_TASK_FEEDING
+#define K_MAX_LINKS AVR_MAX_LINKS
+#define K_MAX_DOF AVR_MAX_DOF
+#define K_HC_N AVR_HC_N
+#define K_MAX_FREE AVR_MAX_FREE
+#define K_MAX_HUMAN AVR_MAX_HUMAN
+#define K_MAX_CONTACTS AVR_MAX_CONTACTS
+#define K_ACT_DIM AVR_ACT_DIM
+#define K_OBS_DIM AVR_OBS_DIM
+#define S_Q AVR_S_Q
+#define S_QD AVR_S_QD
+#define S_QTGT AVR_S_QTGT
+#define S_KP AVR_S_KP
+#define S_MAXIMP AVR_S_MAXIMP
+#define S_FREE AVR_S_FREE
+#define S_TASK AVR_S_TASK
+#define S_HUMAN AVR_S_HUMAN
+#define S_HCH AVR_S_HCH
+#define S_CP AVR_S_CP
+#define K_STATE_WORDS AVR_STATE_WORDS
+#define T_ALIVE AVR_T_ALIVE
+#define T_HIT AVR_T_HIT
+#else
+#define K_MAX_LINKS AVR_SI_MAX_LINKS
+#define K_MAX_DOF AVR_SI_MAX_DOF
+#define K_HC_N AVR_SI_HC_N
+#define K_MAX_FREE AVR_SI_MAX_FREE
+#define K_MAX_HUMAN AVR_SI_MAX_HUMAN
+#define K_MAX_CONTACTS AVR_SI_MAX_CONTACTS
+#define K_ACT_DIM AVR_SI_ACT_DIM
+#define K_OBS_DIM AVR_SI_OBS_DIM
+#define S_Q AVR_SI_S_Q
+#define S_QD AVR_SI_S_QD
+#define S_QTGT AVR_SI_S_QTGT
+#define S_KP AVR_SI_S_KP
+#define S_MAXIMP AVR_SI_S_MAXIMP
+#define S_FREE AVR_SI_S_FREE
+#define S_RBASE AVR_SI_S_RBASE
+#define S_TASK AVR_SI_S_TASK
+#define S_HUMAN AVR_SI_S_HUMAN
+#define S_HCH AVR_SI_S_HCH
+#define S_CP AVR_SI_S_CP
+#define K_STATE_WORDS AVR_SI_STATE_WORDS
+#define T_LIMB AVR_SI_T_LIMB
+#define T_STRENGTH AVR_SI_T_STRENGTH
+#define T_PREV AVR_SI_T_PREV
+#define T_TREMOR AVR_SI_T_TREMOR
+#define T_ONARM AVR_SI_T_ONARM
+#endif
+#define SCRATCH (AVR_TASK == AVR_TASK_SCRATCH)
+
 #ifdef AVR_ORACLE_FLOAT
 typedef float real;
 #define R(x) ((float)(x))
@@ -127,12 +189,12 @@ typedef struct {
     avr_model_desc d;                 /* arrays point into the copies below */
     int nl, nd, nf, nb, ns, np;
     int nl_robot, nd_robot, hc;       /* hc: this view articulates the head chain */
-    int parent[AVR_MAX_LINKS], jtype[AVR_MAX_LINKS], dof[AVR_MAX_LINKS], has_limit[AVR_MAX_LINKS];
-    real lower[AVR_MAX_LINKS], upper[AVR_MAX_LINKS];
+    int parent[K_MAX_LINKS], jtype[K_MAX_LINKS], dof[K_MAX_LINKS], has_limit[K_MAX_LINKS];
+    real lower[K_MAX_LINKS], upper[K_MAX_LINKS];
     int body_link[MAX_BODIES];        /* articulated link of a collision body, -1 if none */
-    tf jorig[AVR_MAX_LINKS], com[AVR_MAX_LINKS];
-    v3 axis[AVR_MAX_LINKS], inertia[AVR_MAX_LINKS];
-    real mass[AVR_MAX_LINKS];
+    tf jorig[K_MAX_LINKS], com[K_MAX_LINKS];
+    v3 axis[K_MAX_LINKS], inertia[K_MAX_LINKS];
+    real mass[K_MAX_LINKS];
     tf base;
     real *hv;                         /* hull verts (real) */
     real *hp;                         /* hull planes       */
@@ -145,31 +207,31 @@ typedef struct {
 
 typedef struct {
     int kindA, idxA, kindB, idxB;     /* endpoint kind: 0 none, 1 robot, 2 free */
-    real JA[AVR_MAX_DOF], JB[AVR_MAX_DOF];      /* robot: ndof entries; free: 6 (lin, ang) */
-    real MA[AVR_MAX_DOF], MB[AVR_MAX_DOF];      /* M^-1 J^T */
+    real JA[K_MAX_DOF], JB[K_MAX_DOF];      /* robot: ndof entries; free: 6 (lin, ang) */
+    real MA[K_MAX_DOF], MB[K_MAX_DOF];      /* M^-1 J^T */
     real inv, rhs, lo, hi, imp, fric;
     int normal_row;                   /* friction rows: index into normal rows */
     int cp;                           /* contact point index (normal rows)     */
 } row_t;
 
 typedef struct {
-    tf lk[AVR_MAX_LINKS];             /* link (URDF) frames */
-    tf cm[AVR_MAX_LINKS];             /* COM frames         */
-    v3 ax[AVR_MAX_LINKS], org[AVR_MAX_LINKS];
+    tf lk[K_MAX_LINKS];             /* link (URDF) frames */
+    tf cm[K_MAX_LINKS];             /* COM frames         */
+    v3 ax[K_MAX_LINKS], org[K_MAX_LINKS];
     tf body[MAX_BODIES];
     v3 bmin[MAX_BODIES], bmax[MAX_BODIES];
-    real Mi[AVR_MAX_DOF][AVR_MAX_DOF];    /* Cholesky factor of M */
-    real vq[AVR_MAX_DOF];                 /* robot velocity (post unconstrained) */
-    v3 fv[AVR_MAX_FREE], fw[AVR_MAX_FREE];
-    real dq[AVR_MAX_DOF];                 /* solver delta velocities */
-    v3 dfv[AVR_MAX_FREE], dfw[AVR_MAX_FREE];
+    real Mi[K_MAX_DOF][K_MAX_DOF];    /* Cholesky factor of M */
+    real vq[K_MAX_DOF];                 /* robot velocity (post unconstrained) */
+    v3 fv[K_MAX_FREE], fw[K_MAX_FREE];
+    real dq[K_MAX_DOF];                 /* solver delta velocities */
+    v3 dfv[K_MAX_FREE], dfw[K_MAX_FREE];
     row_t rows[MAX_ROWS];
     int nrows, n_nc, n_nrm, n_fr;
     int nc_idx[64], nrm_idx[MAX_ROWS / 3 + 8], fr_idx[MAX_ROWS];
     int sp_a[MAX_SPAIRS], sp_b[MAX_SPAIRS], sp_pair[MAX_SPAIRS];
     int nsp;
     int gender;
-    real oldcp[AVR_MAX_CONTACTS * AVR_CP_WORDS];
+    real oldcp[K_MAX_CONTACTS * AVR_CP_WORDS];
     long long stats_gjk, stats_epa, stats_rows;
 } ws_t;
 
@@ -177,7 +239,7 @@ typedef struct avr_oracle {
     model m;             /* view 0 (static human) */
     model mv[2];         /* tremor views: male, female */
     int n_envs;
-    real *state;         /* n_envs * AVR_STATE_WORDS */
+    real *state;         /* n_envs * K_STATE_WORDS */
     ws_t *ws;
     char err[256];
     int threads;
@@ -185,13 +247,13 @@ typedef struct avr_oracle {
 
 /* the view an env simulates: T_HDYN (impairment 'tremor') selects the head-chain view */
 static const model *oview(const avr_oracle *o, const real *st) {
-    if (o->m.d.hc_n > 0 && st[AVR_S_TASK + AVR_T_HDYN] != 0) return &o->mv[(int)st[AVR_S_TASK + AVR_T_GENDER] ? 1 : 0];
+    if (o->m.d.hc_n > 0 && st[S_TASK + T_HDYN] != 0) return &o->mv[(int)st[S_TASK + T_GENDER] ? 1 : 0];
     return &o->m;
 }
 
 /* ---------------------------------------------------------------- kinematics */
 static tf slot_pose(const real *st, int slot) {
-    const real *h = st + AVR_S_HUMAN + 7 * slot;
+    const real *h = st + S_HUMAN + 7 * slot;
     tf t; t.p = ld3(h); t.q = ldq(h + 3);
     return t;
 }
@@ -202,13 +264,18 @@ static tf slot_pose(const real *st, int slot) {
 static void robot_fk(const model *m, real *st, ws_t *w) {
     for (int i = 0; i < m->nl; i++) {
         int p = m->parent[i];
-        tf par = p == -2 ? slot_pose(st, m->d.hc_parent_slot) : p < 0 ? m->base : w->lk[p];
+#if SCRATCH
+        tf base; base.p = ld3(st + S_RBASE); base.q = ldq(st + S_RBASE + 3);   /* position_robot_toc: per env */
+#else
+        tf base = m->base;
+#endif
+        tf par = p == -2 ? slot_pose(st, m->d.hc_parent_slot) : p < 0 ? base : w->lk[p];
         tf t = tfmul(par, m->jorig[i]);
         w->org[i] = t.p;
         w->ax[i] = qrot(t.q, m->axis[i]);
         int dof = m->dof[i];
-        if (m->jtype[i] == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(m->axis[i], st[AVR_S_Q + dof]));
-        else if (m->jtype[i] == AVR_J_PRISMATIC) t.p = add(t.p, scl(w->ax[i], st[AVR_S_Q + dof]));
+        if (m->jtype[i] == AVR_J_REVOLUTE) t.q = qmul(t.q, qaxis(m->axis[i], st[S_Q + dof]));
+        else if (m->jtype[i] == AVR_J_PRISMATIC) t.p = add(t.p, scl(w->ax[i], st[S_Q + dof]));
         w->lk[i] = t;
         w->cm[i] = tfmul(t, m->com[i]);
     }
@@ -216,7 +283,7 @@ static void robot_fk(const model *m, real *st, ws_t *w) {
         for (int k = 0; k < m->d.hc_n; k++) {
             int slot = m->d.hc_slot[k];
             if (slot < 0) continue;
-            real *h = st + AVR_S_HUMAN + 7 * slot;
+            real *h = st + S_HUMAN + 7 * slot;
             st3(h, w->cm[m->nl_robot + k].p);
             stq(h + 3, w->cm[m->nl_robot + k].q);
         }
@@ -243,17 +310,17 @@ static void dof_col(const model *m, const ws_t *w, int j, v3 p, v3 *lin, v3 *ang
  * btMultiBody's ABA solve for the same articulated inertia (fixed base). */
 static int robot_mass_matrix(const model *m, ws_t *w) {
     int nd = m->nd;
-    real M[AVR_MAX_DOF][AVR_MAX_DOF];
+    real M[K_MAX_DOF][K_MAX_DOF];
     memset(M, 0, sizeof(M));
-    int dl[AVR_MAX_DOF];
+    int dl[K_MAX_DOF];
     for (int j = 0; j < m->nl; j++)
         if (m->dof[j] >= 0) dl[m->dof[j]] = j;
     for (int i = 0; i < m->nl; i++) {
         real mi = m->mass[i];
         if (mi <= 0) continue;
         v3 c = w->cm[i].p;
-        v3 lin[AVR_MAX_DOF], ang[AVR_MAX_DOF];
-        int use[AVR_MAX_DOF];
+        v3 lin[K_MAX_DOF], ang[K_MAX_DOF];
+        int use[K_MAX_DOF];
         for (int a = 0; a < nd; a++) {
             use[a] = is_ancestor_dof(m, i, dl[a]);
             if (use[a]) dof_col(m, w, dl[a], c, &lin[a], &ang[a]);
@@ -285,7 +352,7 @@ static int robot_mass_matrix(const model *m, ws_t *w) {
 
 static void chol_solve(const model *m, const ws_t *w, const real *b, real *x) {
     int nd = m->nd;
-    real y[AVR_MAX_DOF];
+    real y[K_MAX_DOF];
     for (int i = 0; i < nd; i++) {
         real s = b[i];
         for (int k = 0; k < i; k++) s -= w->Mi[i][k] * y[k];
@@ -303,8 +370,8 @@ static void chol_solve(const model *m, const ws_t *w, const real *b, real *x) {
  * zeroed per body in Feeding, feeding.py:285). */
 static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
     int nl = m->nl;
-    v3 om[AVR_MAX_LINKS], vc[AVR_MAX_LINKS], al[AVR_MAX_LINKS], ac[AVR_MAX_LINKS];
-    v3 F[AVR_MAX_LINKS], N[AVR_MAX_LINKS];
+    v3 om[K_MAX_LINKS], vc[K_MAX_LINKS], al[K_MAX_LINKS], ac[K_MAX_LINKS];
+    v3 F[K_MAX_LINKS], N[K_MAX_LINKS];
     real k1l = R(m->d.linear_damping), k1a = R(m->d.angular_damping);
     for (int i = 0; i < nl; i++) {
         int p = m->parent[i];
@@ -314,7 +381,7 @@ static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
         v3 acp = p < 0 ? V(0, 0, 0) : ac[p];
         v3 cp = p < 0 ? m->base.p : w->cm[p].p;
         int dof = m->dof[i];
-        real qd = dof >= 0 ? st[AVR_S_QD + dof] : 0;
+        real qd = dof >= 0 ? st[S_QD + dof] : 0;
         v3 o = w->org[i], c = w->cm[i].p;
         v3 rpo = sub(o, cp), roc = sub(c, o);
         v3 vo = add(vp, crs(omp, rpo));                               /* joint point velocity */
@@ -343,7 +410,13 @@ static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
         real vn = len(vc[i]), wn = len(om[i]);
         v3 fdamp = scl(vc[i], -mi * (k1l + k1l * vn));
         v3 tdamp = scl(Iw, -(k1a + k1a * wn));
+#if SCRATCH
+        /* gravity of the articulated human chain (links after the robot's): F = m (a - g) */
+        v3 ga = i >= m->nl_robot ? sub(ac[i], ld3d(m->d.human_gravity)) : ac[i];
+        F[i] = sub(scl(ga, mi), fdamp);
+#else
         F[i] = sub(scl(ac[i], mi), fdamp);
+#endif
         N[i] = sub(add(inertia_mul(q, m->inertia[i], al[i]), crs(om[i], Iw)), tdamp);
     }
     for (int d = 0; d < m->nd; d++) h[d] = 0;
@@ -744,12 +817,15 @@ static tf body_tf(const model *m, const real *st, const ws_t *w, int b) {
     tf t;
     if (kind == AVR_BODY_ROBOT) return w->cm[idx];
     if (kind == AVR_BODY_FREE) {
-        const real *f = st + AVR_S_FREE + AVR_FB_WORDS * idx;
+        const real *f = st + S_FREE + AVR_FB_WORDS * idx;
         t.p = ld3(f); t.q = ldq(f + 3);
         return t;
     }
     if (kind == AVR_BODY_STATIC) return ldtf(m->d.st_pose + 7 * idx);
-    const real *h = st + AVR_S_HUMAN + 7 * idx;
+#if SCRATCH
+    if (kind == AVR_BODY_RSTATIC) { t.p = ld3(st + S_RBASE); t.q = ldq(st + S_RBASE + 3); return t; }
+#endif
+    const real *h = st + S_HUMAN + 7 * idx;
     t.p = ld3(h); t.q = ldq(h + 3);
     return t;
 }
@@ -780,7 +856,7 @@ static void shape_aabb(const model *m, int s, tf body, v3 *mn, v3 *mx) {
 }
 
 /* ---------------------------------------------------------------- contact manifolds */
-static real *cp_ptr(real *st, int i) { return st + AVR_S_CP + AVR_CP_WORDS * i; }
+static real *cp_ptr(real *st, int i) { return st + S_CP + AVR_CP_WORDS * i; }
 
 /* One btPersistentManifold (<= 4 points) of a shape pair, held locally while it is updated. */
 typedef struct { real p[AVR_MANIFOLD_POINTS][AVR_CP_WORDS]; int n; } manifold_t;
@@ -882,7 +958,7 @@ static void row_endpoint(const model *m, const real *st, ws_t *w, row_t *r, int 
         chol_solve(m, w, J, MJ);
     } else if (kind == AVR_BODY_FREE) {
         *pk = 2; *pi = idx;
-        const real *f = st + AVR_S_FREE + AVR_FB_WORDS * idx;
+        const real *f = st + S_FREE + AVR_FB_WORDS * idx;
         v3 c = ld3(f);
         qt q = ldq(f + 3);
         v3 angt = add(crs(sub(p, c), lin), ang);
@@ -949,9 +1025,16 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
     for (int i = 0; i < m->nl; i++) {
         if (!m->has_limit[i]) continue;
         int dof = m->dof[i];
-        real q = st[AVR_S_Q + dof];
+        real q = st[S_Q + dof];
+        real lo = m->lower[i], hi = m->upper[i];
+#if SCRATCH
+        if (i >= m->nl_robot) {   /* human arm limits x the env's limit_scale (human_creation.py:226) */
+            lo = st[S_HCH + 2 * K_HC_N + (i - m->nl_robot)];
+            hi = st[S_HCH + 3 * K_HC_N + (i - m->nl_robot)];
+        }
+#endif
         for (int side = 0; side < 2; side++) {
-            real pen = side == 0 ? q - m->lower[i] : m->upper[i] - q;
+            real pen = side == 0 ? q - lo : hi - q;
             if (pen > 0) continue;
             row_t *r = new_row(w);
             r->kindA = 1; r->idxA = i;
@@ -976,12 +1059,12 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
         r->JA[dof] = 1;
         chol_solve(m, w, r->JA, r->MA);
         row_finish(m, w, r);
-        real q = st[AVR_S_Q + dof], cur = w->vq[dof];
-        real kp = st[AVR_S_KP + dof], kd = 1;                  /* pybullet default velocityGain 1 */
-        real desired = kp * (st[AVR_S_QTGT + dof] - q) / dt + cur + kd * (0 - cur);
+        real q = st[S_Q + dof], cur = w->vq[dof];
+        real kp = st[S_KP + dof], kd = 1;                  /* pybullet default velocityGain 1 */
+        real desired = kp * (st[S_QTGT + dof] - q) / dt + cur + kd * (0 - cur);
         real rel = row_relvel(m, w, r);
         r->rhs = (desired - rel) * r->inv;
-        real mi = st[AVR_S_MAXIMP + dof];
+        real mi = st[S_MAXIMP + dof];
         r->lo = -mi; r->hi = mi;
         w->nc_idx[w->n_nc++] = w->nrows - 1;
     }
@@ -993,9 +1076,13 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
         tf off = ldtf(m->d.tool_offset);
         v3 pivA = tfpt(ta, off.p);
         qt frA = qmul(ta.q, off.q);
-        const real *f = st + AVR_S_FREE + AVR_FB_WORDS * fb;
+        const real *f = st + S_FREE + AVR_FB_WORDS * fb;
         tf tb; tb.p = ld3(f); tb.q = ldq(f + 3);
+#if SCRATCH
+        v3 pivB = tfpt(tb, ld3d(m->d.fix_pivot_b));   /* the composite tool's base (handle) COM */
+#else
         v3 pivB = tb.p;
+#endif
         m3 FA = qmat(frA), FB = qmat(tb.q);
         /* relRot = FA^-1 FB; matrixToEulerXYZ with btGetMatrixElem(mat, i) = mat[i%3][i/3] */
         m3 rr;
@@ -1038,7 +1125,7 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
                 st3(r->JB, V(0, 0, 0));
                 st3(r->JB + 3, scl(an, -1));
                 {
-                    const real *ff = st + AVR_S_FREE + AVR_FB_WORDS * fb;
+                    const real *ff = st + S_FREE + AVR_FB_WORDS * fb;
                     st3(r->MB, V(0, 0, 0));
                     st3(r->MB + 3, inertia_inv_mul(ldq(ff + 3), ld3d(m->d.fb_inertia + 3 * fb), scl(an, -1)));
                 }
@@ -1066,7 +1153,7 @@ static void plane_space(v3 n, v3 *p, v3 *q) {
 }
 
 static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
-    int ncp = (int)st[AVR_S_TASK + AVR_T_NCP];
+    int ncp = (int)st[S_TASK + T_NCP];
     real erp = R(m->d.erp), ws = R(m->d.warmstart);
     for (int i = 0; i < ncp; i++) {
         real *c = cp_ptr(st, i);
@@ -1187,9 +1274,9 @@ static void collide(avr_oracle *o, real *st, ws_t *w) {
     /* Rebuild the contact pool: for each overlapping shape pair, in order, take its old
      * manifold (points in slot order), run narrowphase + add + refresh, append the survivors.
      * Points of pairs that stopped overlapping are dropped (child algorithm destroyed). */
-    int nold = (int)st[AVR_S_TASK + AVR_T_NCP];
+    int nold = (int)st[S_TASK + T_NCP];
     real *oldcp = w->oldcp;
-    memcpy(oldcp, st + AVR_S_CP, sizeof(real) * AVR_CP_WORDS * nold);
+    memcpy(oldcp, st + S_CP, sizeof(real) * AVR_CP_WORDS * nold);
     int nnew = 0;
     for (int q = 0; q < w->nsp; q++) {
         int sa = w->sp_a[q], sb = w->sp_b[q], p = w->sp_pair[q];
@@ -1207,11 +1294,11 @@ static void collide(avr_oracle *o, real *st, ws_t *w) {
         if (narrowphase(w, &A, &B, thr, &nB, &pB, &d)) manifold_add(&M, sa, sb, p, w->body[ba], w->body[bb], nB, pB, d, thr);
         manifold_refresh(&M, w->body[ba], w->body[bb], thr);
         for (int k = 0; k < M.n; k++) {
-            if (nnew >= AVR_MAX_CONTACTS) { st[AVR_S_TASK + AVR_T_FLAGS] = (real)((int)st[AVR_S_TASK + AVR_T_FLAGS] | 2); break; }
+            if (nnew >= K_MAX_CONTACTS) { st[S_TASK + T_FLAGS] = (real)((int)st[S_TASK + T_FLAGS] | 2); break; }
             memcpy(cp_ptr(st, nnew++), M.p[k], sizeof(real) * AVR_CP_WORDS);
         }
     }
-    st[AVR_S_TASK + AVR_T_NCP] = (real)nnew;
+    st[S_TASK + T_NCP] = (real)nnew;
 }
 
 /* ---------------------------------------------------------------- one Bullet sub-step */
@@ -1221,19 +1308,19 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
     collide(o, st, w);
     /* unconstrained velocities (btMultiBody::computeAccelerationsArticulatedBodyAlgorithmMultiDof) */
     if (robot_mass_matrix(m, w)) return -1;
-    real h[AVR_MAX_DOF] = {0}, qdd[AVR_MAX_DOF] = {0}, nh[AVR_MAX_DOF] = {0};
+    real h[K_MAX_DOF] = {0}, qdd[K_MAX_DOF] = {0}, nh[K_MAX_DOF] = {0};
     robot_bias(m, st, w, h);
     for (int d = 0; d < m->nd; d++) nh[d] = -h[d];
     chol_solve(m, w, nh, qdd);
     real vmax = R(m->d.max_coord_vel);
     for (int d = 0; d < m->nd; d++) {
-        real v = st[AVR_S_QD + d] + dt * qdd[d];
+        real v = st[S_QD + d] + dt * qdd[d];
         w->vq[d] = fmin(vmax, fmax(-vmax, v));
         w->dq[d] = 0;
     }
     real k1l = R(m->d.linear_damping), k1a = R(m->d.angular_damping);
     for (int f = 0; f < m->nf; f++) {
-        const real *fb = st + AVR_S_FREE + AVR_FB_WORDS * f;
+        const real *fb = st + S_FREE + AVR_FB_WORDS * f;
         v3 v = ld3(fb + 7), om = ld3(fb + 10);
         qt q = ldq(fb + 3);
         real mass = R(m->d.fb_mass[f]);
@@ -1262,11 +1349,11 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
     for (int d = 0; d < m->nd; d++) {
         real v = w->vq[d] + w->dq[d];
         v = fmin(vmax, fmax(-vmax, v));
-        st[AVR_S_QD + d] = v;
-        st[AVR_S_Q + d] += dt * v;
+        st[S_QD + d] = v;
+        st[S_Q + d] += dt * v;
     }
     for (int f = 0; f < m->nf; f++) {
-        real *fb = st + AVR_S_FREE + AVR_FB_WORDS * f;
+        real *fb = st + S_FREE + AVR_FB_WORDS * f;
         v3 v = add(w->fv[f], w->dfv[f]), om = add(w->fw[f], w->dfw[f]);
         v = V(fmin(vmax, fmax(-vmax, v.x)), fmin(vmax, fmax(-vmax, v.y)), fmin(vmax, fmax(-vmax, v.z)));
         om = V(fmin(vmax, fmax(-vmax, om.x)), fmin(vmax, fmax(-vmax, om.y)), fmin(vmax, fmax(-vmax, om.z)));
@@ -1287,7 +1374,7 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
 
 /* ---------------------------------------------------------------- task glue (FeedingJaco) */
 static real contact_force(const model *m, real *st, int (*pred)(const model *, int, int, void *), void *ctx, int *count) {
-    int n = (int)st[AVR_S_TASK + AVR_T_NCP];
+    int n = (int)st[S_TASK + T_NCP];
     real s = 0;
     int c = 0;
     for (int i = 0; i < n; i++) {
@@ -1299,6 +1386,7 @@ static real contact_force(const model *m, real *st, int (*pred)(const model *, i
     return s;
 }
 
+#if !SCRATCH
 static int is_robot(const model *m, int b) { return m->d.body_kind[b] == AVR_BODY_ROBOT; }
 static int is_human(const model *m, int b) { return m->d.body_kind[b] == AVR_BODY_HUMAN; }
 static int pred_robot_human(const model *m, int a, int b, void *c) { (void)c; return (is_robot(m, a) && is_human(m, b)) || (is_robot(m, b) && is_human(m, a)); }
@@ -1307,9 +1395,9 @@ static int pred_body_pair(const model *m, int a, int b, void *c) { int *p = (int
 static int pred_body_human(const model *m, int a, int b, void *c) { int f = *(int *)c; return (a == f && is_human(m, b)) || (b == f && is_human(m, a)); }
 
 static void mouth_target(const model *m, const real *st, real *out) {
-    const real *h = st + AVR_S_HUMAN + 7 * m->d.head_slot;
+    const real *h = st + S_HUMAN + 7 * m->d.head_slot;
     tf t; t.p = ld3(h); t.q = ldq(h + 3);
-    int g = (int)st[AVR_S_TASK + AVR_T_GENDER];
+    int g = (int)st[S_TASK + T_GENDER];
     v3 p = tfpt(t, ld3d(m->d.mouth_offset[g]));
     st3(out, p);
 }
@@ -1317,39 +1405,46 @@ static void mouth_target(const model *m, const real *st, real *out) {
 static void observe(const model *m, real *st, ws_t *w, float spoon_force, float *obs) {
     robot_fk(m, st, w);
     v3 torso = w->cm[m->d.torso_link].p;
-    const real *sp = st + AVR_S_FREE + AVR_FB_WORDS * m->d.spoon_free;
+    const real *sp = st + S_FREE + AVR_FB_WORDS * m->d.spoon_free;
     v3 spos = ld3(sp);
-    v3 tgt = ld3(st + AVR_S_TASK + AVR_T_TARGET);
-    const real *h = st + AVR_S_HUMAN + 7 * m->d.head_slot;
+    v3 tgt = ld3(st + S_TASK + T_TARGET);
+    const real *h = st + S_HUMAN + 7 * m->d.head_slot;
     int k = 0;
     v3 a = sub(spos, torso);
     obs[k++] = (float)a.x; obs[k++] = (float)a.y; obs[k++] = (float)a.z;
     for (int i = 0; i < 4; i++) obs[k++] = (float)sp[3 + i];
     a = sub(spos, tgt);
     obs[k++] = (float)a.x; obs[k++] = (float)a.y; obs[k++] = (float)a.z;
-    for (int i = 0; i < m->d.n_arm; i++) obs[k++] = (float)st[AVR_S_Q + m->d.arm_dofs[i]];
+    for (int i = 0; i < m->d.n_arm; i++) obs[k++] = (float)st[S_Q + m->d.arm_dofs[i]];
     a = sub(ld3(h), torso);
     obs[k++] = (float)a.x; obs[k++] = (float)a.y; obs[k++] = (float)a.z;
     for (int i = 0; i < 4; i++) obs[k++] = (float)h[3 + i];
     obs[k++] = spoon_force;
 }
 
+#endif
+
 /* enforce_hard_human_joint_limits (env.py:389-410): after every stepSimulation a head-chain
  * joint outside its limits is reset onto the limit with zero velocity (resetJointState). */
 static void hard_limits(const model *m, real *st) {
     for (int k = 0; k < m->d.hc_n; k++) {
         int d = m->nd_robot + k;
+#if SCRATCH
+        real lo = st[S_HCH + 2 * K_HC_N + k], hi = st[S_HCH + 3 * K_HC_N + k];
+#else
         real lo = R(m->d.hc_lower[k]), hi = R(m->d.hc_upper[k]);
-        if (st[AVR_S_Q + d] < lo) { st[AVR_S_Q + d] = lo; st[AVR_S_QD + d] = 0; }
-        else if (st[AVR_S_Q + d] > hi) { st[AVR_S_Q + d] = hi; st[AVR_S_QD + d] = 0; }
+#endif
+        if (st[S_Q + d] < lo) { st[S_Q + d] = lo; st[S_QD + d] = 0; }
+        else if (st[S_Q + d] > hi) { st[S_Q + d] = hi; st[S_QD + d] = 0; }
     }
 }
 
+#if !SCRATCH
 static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
-    real *st = o->state + (size_t)e * AVR_STATE_WORDS;
+    real *st = o->state + (size_t)e * K_STATE_WORDS;
     const model *m = oview(o, st);
     ws_t *w = &o->ws[e];
-    w->gender = (int)st[AVR_S_TASK + AVR_T_GENDER];
+    w->gender = (int)st[S_TASK + T_GENDER];
     real dt = R(m->d.time_step) / (m->d.num_sub_steps > 0 ? m->d.num_sub_steps : 1);
     int nsub = m->d.num_sub_steps > 0 ? m->d.num_sub_steps : 1;
     /* take_step (env.py:274-337) */
@@ -1358,7 +1453,7 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
         real x = act[i];
         x = x < -1 ? -1 : x > 1 ? 1 : x;
         a[i] = (real)((float)x * 0.05f);                  /* float32 action space */
-        qn[i] = st[AVR_S_Q + m->d.arm_dofs[i]];
+        qn[i] = st[S_Q + m->d.arm_dofs[i]];
     }
     for (int it = 0; it < m->d.frame_skip; it++)
         for (int i = 0; i < m->d.n_arm; i++) {
@@ -1368,20 +1463,20 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
         }
     for (int i = 0; i < m->d.n_arm; i++) {
         int d = m->d.arm_dofs[i];
-        st[AVR_S_QTGT + d] = qn[i];
-        st[AVR_S_KP + d] = R(m->d.robot_gain);
-        st[AVR_S_MAXIMP + d] = R(m->d.robot_force * m->d.time_step);
+        st[S_QTGT + d] = qn[i];
+        st[S_KP + d] = R(m->d.robot_gain);
+        st[S_MAXIMP + d] = R(m->d.robot_force * m->d.time_step);
     }
     if (m->hc) {
         /* tremor (env.py:327-337): position targets target_human_joint_positions + human_tremors,
            the tremor's sign alternating with self.iteration; gains human_gains, forces
            human_forces * human_strength (strength 1: 'tremor' is not 'weakness') */
-        real sg = ((int)st[AVR_S_TASK + AVR_T_ITER] % 2 == 0) ? 1 : -1;
+        real sg = ((int)st[S_TASK + T_ITER] % 2 == 0) ? 1 : -1;
         for (int k = 0; k < m->d.hc_n; k++) {
             int d = m->nd_robot + k;
-            st[AVR_S_QTGT + d] = st[AVR_S_HCH + k] + st[AVR_S_HCH + AVR_HC_N + k] * sg;
-            st[AVR_S_KP + d] = R(m->d.human_gain);
-            st[AVR_S_MAXIMP + d] = R(m->d.human_force * m->d.time_step);
+            st[S_QTGT + d] = st[S_HCH + k] + st[S_HCH + K_HC_N + k] * sg;
+            st[S_KP + d] = R(m->d.human_gain);
+            st[S_MAXIMP + d] = R(m->d.human_force * m->d.time_step);
         }
     }
     for (int fr = 0; fr < m->d.frame_skip; fr++) {
@@ -1393,24 +1488,24 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
             hard_limits(m, st);
             robot_fk(m, st, w);
         }
-        mouth_target(m, st, st + AVR_S_TASK + AVR_T_TARGET);
+        mouth_target(m, st, st + S_TASK + T_TARGET);
     }
-    st[AVR_S_TASK + AVR_T_ITER] += 1;
+    st[S_TASK + T_ITER] += 1;
     /* get_total_force (feeding.py:83-90) */
     real robot_force = contact_force(m, st, pred_robot_human, 0, 0);
     real spoon_force = contact_force(m, st, pred_spoon_human, 0, 0);
     /* get_food_rewards (feeding.py:92-121) */
     real food_reward = 0, hit_reward = 0, mouth_vel = 0;
-    int alive = (int)st[AVR_S_TASK + AVR_T_ALIVE], hit = (int)st[AVR_S_TASK + AVR_T_HIT];
-    v3 tgt = ld3(st + AVR_S_TASK + AVR_T_TARGET);
+    int alive = (int)st[S_TASK + T_ALIVE], hit = (int)st[S_TASK + T_HIT];
+    v3 tgt = ld3(st + S_TASK + T_TARGET);
     for (int k = 0; k < m->d.n_food; k++) {
         if (!(alive >> k & 1)) continue;
-        real *fb = st + AVR_S_FREE + AVR_FB_WORDS * (m->d.food_free0 + k);
+        real *fb = st + S_FREE + AVR_FB_WORDS * (m->d.food_free0 + k);
         v3 fp = ld3(fb);
         int fbody = m->d.food_body0 + k;
         if (len(sub(tgt, fp)) < R(0.02)) {
             food_reward += 20;
-            st[AVR_S_TASK + AVR_T_SUCCESS] += 1;
+            st[S_TASK + T_SUCCESS] += 1;
             mouth_vel += len(ld3(fb + 7));
             alive &= ~(1 << k);
             /* teleported far away (feeding.py:109); the draw U(1000,2000) is replaced by a fixed spot */
@@ -1429,9 +1524,9 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
         contact_force(m, st, pred_body_human, &fbody, &chum);
         if (chum > 0 && !(hit >> k & 1)) { hit |= 1 << k; hit_reward -= 1; }
     }
-    st[AVR_S_TASK + AVR_T_ALIVE] = (real)alive;
-    st[AVR_S_TASK + AVR_T_HIT] = (real)hit;
-    const real *sp = st + AVR_S_FREE + AVR_FB_WORDS * m->d.spoon_free;
+    st[S_TASK + T_ALIVE] = (real)alive;
+    st[S_TASK + T_HIT] = (real)hit;
+    const real *sp = st + S_FREE + AVR_FB_WORDS * m->d.spoon_free;
     real ee_vel = len(ld3(sp + 7));
     observe(m, st, w, (float)spoon_force, obs);
     /* human_preferences (env.py:412-448), feeding branch */
@@ -1443,14 +1538,18 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
     for (int i = 0; i < m->d.n_arm; i++) asq += (real)act[i] * (real)act[i];    /* unclipped (feeding.py:69) */
     real r = R(m->d.w_distance) * (-dist) + R(m->d.w_action) * (-asq) + R(m->d.w_food) * food_reward + prefs;
     *rew = (float)r;
-    int it = (int)st[AVR_S_TASK + AVR_T_ITER];
+    int it = (int)st[S_TASK + T_ITER];
     *done = (uint8_t)(it >= m->d.max_episode_steps);
     info[0] = (float)(robot_force + spoon_force);
-    info[1] = (float)(st[AVR_S_TASK + AVR_T_SUCCESS] >= R(m->d.n_food) * R(m->d.task_success_threshold) ? 1 : 0);
-    for (int i = 0; i < AVR_STATE_WORDS; i++)
-        if (st[i] != st[i]) { st[AVR_S_TASK + AVR_T_FLAGS] = (real)((int)st[AVR_S_TASK + AVR_T_FLAGS] | 1); break; }
+    info[1] = (float)(st[S_TASK + T_SUCCESS] >= R(m->d.n_food) * R(m->d.task_success_threshold) ? 1 : 0);
+    for (int i = 0; i < K_STATE_WORDS; i++)
+        if (st[i] != st[i]) { st[S_TASK + T_FLAGS] = (real)((int)st[S_TASK + T_FLAGS] | 1); break; }
     return 0;
 }
+
+#else
+#include "avr_oracle_scratch.c"
+#endif
 
 /* ---------------------------------------------------------------- public API */
 #define EXPORT __attribute__((visibility("default")))
@@ -1463,8 +1562,8 @@ static void *dupa(const void *p, size_t n) {
 
 EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **out) {
     if (!d || !out || n_envs <= 0) return -1;
-    if (d->n_links + d->hc_n > AVR_MAX_LINKS || d->n_dof + d->hc_n > AVR_MAX_DOF || d->n_free > AVR_MAX_FREE ||
-        d->n_human > AVR_MAX_HUMAN || d->n_bodies > MAX_BODIES || d->n_shapes > MAX_SHAPES || d->hc_n > AVR_HC_N)
+    if (d->n_links + d->hc_n > K_MAX_LINKS || d->n_dof + d->hc_n > K_MAX_DOF || d->n_free > K_MAX_FREE ||
+        d->n_human > K_MAX_HUMAN || d->n_bodies > MAX_BODIES || d->n_shapes > MAX_SHAPES || d->hc_n > K_HC_N)
         return -2;
     avr_oracle *o = (avr_oracle *)calloc(1, sizeof(avr_oracle));
     model *m = &o->m;
@@ -1525,7 +1624,7 @@ EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **o
     }
     o->n_envs = n_envs;
     o->threads = 1;
-    o->state = (real *)calloc((size_t)n_envs * AVR_STATE_WORDS, sizeof(real));
+    o->state = (real *)calloc((size_t)n_envs * K_STATE_WORDS, sizeof(real));
     o->ws = (ws_t *)calloc((size_t)n_envs, sizeof(ws_t));
     *out = o;
     return 0;
@@ -1551,15 +1650,15 @@ EXPORT int avr_oracle_destroy(avr_oracle *o) {
     return 0;
 }
 
-EXPORT int avr_oracle_state_words(void) { return AVR_STATE_WORDS; }
+EXPORT int avr_oracle_state_words(void) { return K_STATE_WORDS; }
 
 EXPORT int avr_oracle_set_state(avr_oracle *o, const double *state) {
-    for (size_t i = 0; i < (size_t)o->n_envs * AVR_STATE_WORDS; i++) o->state[i] = R(state[i]);
+    for (size_t i = 0; i < (size_t)o->n_envs * K_STATE_WORDS; i++) o->state[i] = R(state[i]);
     return 0;
 }
 
 EXPORT int avr_oracle_get_state(avr_oracle *o, double *state) {
-    for (size_t i = 0; i < (size_t)o->n_envs * AVR_STATE_WORDS; i++) state[i] = (double)o->state[i];
+    for (size_t i = 0; i < (size_t)o->n_envs * K_STATE_WORDS; i++) state[i] = (double)o->state[i];
     return 0;
 }
 
@@ -1570,17 +1669,22 @@ EXPORT int avr_oracle_settle(avr_oracle *o, int n_frames, float *obs) {
     real dt = R(m0->d.time_step) / (m0->d.num_sub_steps > 0 ? m0->d.num_sub_steps : 1);
     int nsub = m0->d.num_sub_steps > 0 ? m0->d.num_sub_steps : 1;
     for (int e = 0; e < o->n_envs; e++) {
-        real *st = o->state + (size_t)e * AVR_STATE_WORDS;
+        real *st = o->state + (size_t)e * K_STATE_WORDS;
         const model *m = oview(o, st);
         ws_t *w = &o->ws[e];
-        w->gender = (int)st[AVR_S_TASK + AVR_T_GENDER];
+        w->gender = (int)st[S_TASK + T_GENDER];
         for (int f = 0; f < n_frames; f++)
             for (int s = 0; s < nsub; s++)
                 if (substep(o, st, w, dt)) return -1;
         /* reset drops the food with plain stepSimulation calls: no hard human limits here */
         robot_fk(m, st, w);
-        mouth_target(m, st, st + AVR_S_TASK + AVR_T_TARGET);
-        if (obs) observe(m, st, w, 0.0f, obs + (size_t)e * AVR_OBS_DIM);
+#if SCRATCH
+        scratch_target(m, st, w);
+        if (obs) scratch_observe(m, st, w, 0.0f, obs + (size_t)e * K_OBS_DIM);   /* _get_obs([0], [0, 0]) */
+#else
+        mouth_target(m, st, st + S_TASK + T_TARGET);
+        if (obs) observe(m, st, w, 0.0f, obs + (size_t)e * K_OBS_DIM);
+#endif
     }
     return 0;
 }
@@ -1589,7 +1693,7 @@ EXPORT int avr_oracle_step(avr_oracle *o, const float *act, float *obs, float *r
     int bad = -1;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(o->threads) if (o->threads > 1)
     for (int e = 0; e < o->n_envs; e++)
-        if (env_step(o, e, act + (size_t)e * AVR_ACT_DIM, obs + (size_t)e * AVR_OBS_DIM, rew + e, done + e, info + (size_t)e * AVR_INFO_DIM))
+        if (env_step(o, e, act + (size_t)e * K_ACT_DIM, obs + (size_t)e * K_OBS_DIM, rew + e, done + e, info + (size_t)e * AVR_INFO_DIM))
             bad = e;
     if (bad >= 0) {
         snprintf(o->err, sizeof(o->err), "env %d: mass matrix not positive definite", bad);
@@ -1601,8 +1705,8 @@ EXPORT int avr_oracle_step(avr_oracle *o, const float *act, float *obs, float *r
 /* single sub-step without task glue (KAT tests) */
 EXPORT int avr_oracle_substep(avr_oracle *o, double dt) {
     for (int e = 0; e < o->n_envs; e++) {
-        real *st = o->state + (size_t)e * AVR_STATE_WORDS;
-        o->ws[e].gender = (int)st[AVR_S_TASK + AVR_T_GENDER];
+        real *st = o->state + (size_t)e * K_STATE_WORDS;
+        o->ws[e].gender = (int)st[S_TASK + T_GENDER];
         if (substep(o, st, &o->ws[e], R(dt))) return -1;
     }
     return 0;
@@ -1630,7 +1734,7 @@ EXPORT int avr_oracle_narrowphase(avr_oracle *o, int sa, const double *pa, int s
 /* forward kinematics for tests: COM frames of robot links -> out[n_links*7] */
 EXPORT int avr_oracle_robot_fk(avr_oracle *o, int env, double *out) {
     ws_t *w = &o->ws[env];
-    real *st = o->state + (size_t)env * AVR_STATE_WORDS;
+    real *st = o->state + (size_t)env * K_STATE_WORDS;
     robot_fk(oview(o, st), st, w);
     for (int i = 0; i < o->m.nl_robot; i++) {
         out[7 * i + 0] = w->cm[i].p.x; out[7 * i + 1] = w->cm[i].p.y; out[7 * i + 2] = w->cm[i].p.z;

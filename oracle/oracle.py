@@ -18,8 +18,8 @@ def build():
     subprocess.check_call(['make', '-s', '-C', HERE])
 
 
-def _load(precision):
-    name = 'libavr_oracle.so' if precision == 'f64' else 'libavr_oracle_f32.so'
+def _load(precision, task=0):
+    name = 'libavr_oracle%s%s.so' % ('_scratch' if task == 1 else '', '' if precision == 'f64' else '_f32')
     path = os.path.join(HERE, name)
     if not os.path.exists(path):
         build()
@@ -45,15 +45,18 @@ def _load(precision):
 _LIBS = {}
 
 
-def lib(precision='f64'):
-    if precision not in _LIBS:
-        _LIBS[precision] = _load(precision)
-    return _LIBS[precision]
+def lib(precision='f64', task=0):
+    """The oracle build for `task` (0 FeedingJaco, 1 ScratchItchPR2; avr_model.h AVR_TASK_*)."""
+    key = (precision, task)
+    if key not in _LIBS:
+        _LIBS[key] = _load(precision, task)
+    return _LIBS[key]
 
 
 class Oracle:
     def __init__(self, md, n_envs, precision='f64'):
-        self.lib = lib(precision)
+        self.task = getattr(md, 'task', 0)
+        self.lib = lib(precision, self.task)
         self.md = md
         self.n = n_envs
         h = C.c_void_p()
@@ -62,6 +65,7 @@ class Oracle:
             raise RuntimeError('avr_oracle_create failed: %d' % rc)
         self.h = h
         self.words = self.lib.avr_oracle_state_words()
+        self.obs_dim = 30 if self.task == 1 else 25
 
     def set_threads(self, n):
         self.lib.avr_oracle_set_threads(self.h, int(n))
@@ -87,14 +91,14 @@ class Oracle:
         return S
 
     def settle(self, frames=100):
-        obs = np.zeros((self.n, 25), np.float32)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         if self.lib.avr_oracle_settle(self.h, frames, obs.ctypes.data):
             raise RuntimeError(self.lib.avr_oracle_last_error(self.h).decode())
         return obs
 
     def step(self, act):
         act = np.ascontiguousarray(act, np.float32).reshape(self.n, 7)
-        obs = np.zeros((self.n, 25), np.float32)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
         done = np.zeros(self.n, np.uint8)
         info = np.zeros((self.n, 2), np.float32)
