@@ -135,6 +135,7 @@ class avr_model_desc(C.Structure):
         ('human_gravity', C.c_double * 3), ('fix_pivot_b', C.c_double * 3), ('tool_tip', C.c_double * 3),
         ('torso_com', C.c_double * 3), ('tool_handle_shapes', C.c_int32),
         ('w_tool_force', C.c_double), ('w_scratch', C.c_double),
+        ('robot_gravity', C.c_double * 3),
     ]
 
 
@@ -328,6 +329,10 @@ class ModelDesc:
                         d.hc_inertia[g][k][i] = float(A['hc_inertia'][g][k][i])
         for k, v in P.items():
             if k in ('reactive_gain', 'reactive_force'):
+                continue
+            if k == 'robot_gravity':
+                for i in range(3):
+                    d.robot_gravity[i] = float(v[i])
                 continue
             setattr(d, k, v)
         self.desc = d

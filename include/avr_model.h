@@ -203,6 +203,9 @@ typedef struct avr_model_desc {
     double torso_com[3];                   /* ScratchItch: PR2 link 15 COM in the base frame        */
     int32_t tool_handle_shapes;            /* ScratchItch: tool shapes of the handle (link -1)      */
     double w_tool_force, w_scratch;        /* config.ini:7-8 tool_force_weight, scratch_reward_weight */
+    double robot_gravity[3];               /* gravity on the robot's links: 0 in both tasks (feeding.py:285,
+                                              scratch_itch.py:259); the kernels reject anything else,
+                                              the oracle honours it (known-answer tests) */
 } avr_model_desc;
 
 #ifdef __cplusplus

@@ -410,13 +410,10 @@ static void robot_bias(const model *m, const real *st, ws_t *w, real *h) {
         real vn = len(vc[i]), wn = len(om[i]);
         v3 fdamp = scl(vc[i], -mi * (k1l + k1l * vn));
         v3 tdamp = scl(Iw, -(k1a + k1a * wn));
-#if SCRATCH
-        /* gravity of the articulated human chain (links after the robot's): F = m (a - g) */
-        v3 ga = i >= m->nl_robot ? sub(ac[i], ld3d(m->d.human_gravity)) : ac[i];
-        F[i] = sub(scl(ga, mi), fdamp);
-#else
-        F[i] = sub(scl(ac[i], mi), fdamp);
-#endif
+        /* gravity: F = m (a - g), the human chain's (ScratchItch -1 z) on links after the robot's,
+           the robot's (0 in both tasks; known-answer tests set it) on the robot's */
+        v3 g = i >= m->nl_robot ? ld3d(m->d.human_gravity) : ld3d(m->d.robot_gravity);
+        F[i] = (g.x != 0 || g.y != 0 || g.z != 0) ? sub(scl(sub(ac[i], g), mi), fdamp) : sub(scl(ac[i], mi), fdamp);
         N[i] = sub(add(inertia_mul(q, m->inertia[i], al[i]), crs(om[i], Iw)), tdamp);
     }
     for (int d = 0; d < m->nd; d++) h[d] = 0;

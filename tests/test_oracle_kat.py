@@ -322,3 +322,143 @@ def test_static_human_views_ignore_the_chain(scene, oracle_built):
     assert np.all(St[:, nd:nd + 4] == 0) and np.all(St[:, ABI.S_HCH:ABI.S_CP] == 0)
     h = slice(ABI.S_HUMAN, ABI.S_HCH)
     assert np.array_equal(St[:, h], S[:, h])
+
+
+# ----------------------------------------------------------------------------- dynamics KATs
+# (SURVEY 7 "KATs that need no PyBullet"; synthetic chains from tests/kat_scene.py)
+def _run(md, S, n, dt):
+    from oracle.oracle import Oracle
+    o = Oracle(md, 1)
+    o.set_state(S)
+    out = []
+    for _ in range(n):
+        o.substep(dt)
+        out.append(o.get_state()[0].copy())
+    return np.array(out)
+
+
+def test_motor_row_closed_form(oracle_built):
+    """POSITION_CONTROL motor (btMultiBodyJointMotor): the row's target velocity is
+    kp (q* - q) / dt and, unsaturated and alone, the solve meets it exactly, so
+    q_{n+1} - q* = (1 - kp) (q_n - q*): geometric convergence at rate kp per sub-step."""
+    import kat_scene as K
+    A = K.chain_scene([dict(parent=-1, axis=[0, 0, 1], jpos=[0, 0, 0], com_pos=[0.3, 0, 0], mass=2.0, inertia=[0.01, 0.02, 0.03])])
+    md = K.desc(A)
+    kp, q0, qs, dt = 0.1, 0.2, 1.0, 0.01
+    St = _run(md, K.state(md, [q0], kp=[kp], target=[qs], maximp=[1e6]), 40, dt)
+    q = St[:, ABI.S_Q]
+    want = qs + (q0 - qs) * (1 - kp) ** np.arange(1, 41)
+    assert np.allclose(q, want, rtol=0, atol=1e-12)
+    assert np.allclose(St[:, ABI.S_QD], kp * (np.concatenate([[q0], want[:-1]]) - qs) * -1 / dt, atol=1e-9)
+
+
+def test_motor_impulse_cap(oracle_built):
+    """A saturated motor applies at most its max impulse per sub-step: the joint's velocity grows by
+    maximp / I_axis (I_axis = m r^2 + I_zz about the joint) per sub-step while far from target."""
+    import kat_scene as K
+    m, r, izz = 2.0, 0.3, 0.03
+    A = K.chain_scene([dict(parent=-1, axis=[0, 0, 1], jpos=[0, 0, 0], com_pos=[r, 0, 0], mass=m, inertia=[0.01, 0.02, izz])])
+    md = K.desc(A)
+    imp, dt = 1e-3, 0.01
+    St = _run(md, K.state(md, [0.0], kp=[0.1], target=[100.0], maximp=[imp]), 10, dt)
+    Ia = m * r * r + izz
+    assert np.allclose(St[:, ABI.S_QD], imp / Ia * np.arange(1, 11), rtol=1e-9)
+
+
+def test_pendulum_small_angle_period(oracle_built):
+    """Compound pendulum (point-like bob, no damping, motors off) released at 0.02 rad: its period
+    is 2 pi sqrt(I / (m g r)) to within the time step (semi-implicit Euler)."""
+    import kat_scene as K
+    m, r = 1.0, 0.5
+    A = K.chain_scene([dict(parent=-1, axis=[1, 0, 0], jpos=[0, 0, 1], com_pos=[0, 0, -r], mass=m, inertia=[1e-6, 1e-6, 1e-6])])
+    md = K.desc(A, robot_gravity=(0.0, 0.0, -9.81))
+    dt = 1e-3
+    St = _run(md, K.state(md, [0.02]), 4000, dt)
+    q = St[:, ABI.S_Q]
+    up = np.nonzero((q[:-1] < 0) & (q[1:] >= 0))[0]          # upward zero crossings
+    T = np.diff(up).mean() * dt
+    want = 2 * np.pi * np.sqrt((m * r * r + 1e-6) / (m * 9.81 * r))
+    assert abs(T - want) < 2 * dt, (T, want)
+    assert np.abs(q).max() < 0.0201                           # amplitude kept (no damping)
+
+
+def test_double_pendulum_energy_drift(oracle_built):
+    """Frictionless double pendulum from 1 rad / 0.5 rad over 2 s: the total energy -- kinetic
+    and potential from an independent planar model of the same chain -- deviates by O(dt) only
+    (semi-implicit Euler; measured 0.66 % at dt 1e-3), halving with dt.  A mass-matrix or bias-force
+    error would leave a deviation that does not vanish with dt."""
+    import kat_scene as K
+    m1, m2, l1, l2 = 1.0, 0.7, 0.4, 0.3
+    links = [dict(parent=-1, axis=[1, 0, 0], jpos=[0, 0, 1], com_pos=[0, 0, -l1], mass=m1, inertia=[1e-3, 1e-3, 1e-3]),
+             dict(parent=0, axis=[1, 0, 0], jpos=[0, 0, -l1], com_pos=[0, 0, -l2], mass=m2, inertia=[1e-3, 1e-3, 1e-3])]
+    A = K.chain_scene(links)
+    md = K.desc(A, robot_gravity=(0.0, 0.0, -9.81))
+
+    def energy(q, qd):
+        # planar in y-z; link 1's COM is also joint 2 (jpos l1); R_x(a) (0, 0, -l) = (0, l sin a, -l cos a)
+        a1, a2 = q[0], q[0] + q[1]
+        c1 = np.array([np.sin(a1) * l1, -np.cos(a1) * l1])
+        c2 = c1 + np.array([np.sin(a2) * l2, -np.cos(a2) * l2])
+        w1, w2 = qd[0], qd[0] + qd[1]
+        v1 = w1 * np.array([np.cos(a1), np.sin(a1)]) * l1
+        v2 = v1 + w2 * np.array([np.cos(a2), np.sin(a2)]) * l2
+        T = 0.5 * m1 * v1 @ v1 + 0.5 * m2 * v2 @ v2 + 0.5 * 1e-3 * (w1 * w1 + w2 * w2)
+        return T + 9.81 * (m1 * c1[1] + m2 * c2[1])
+
+    E0 = energy(np.array([1.0, 0.5]), np.zeros(2))
+    errs = []
+    for dt in (1e-3, 5e-4):
+        St = _run(md, K.state(md, [1.0, 0.5]), int(round(2.0 / dt)), dt)
+        errs.append(max(abs(energy(s[ABI.S_Q:ABI.S_Q + 2], s[ABI.S_QD:ABI.S_QD + 2]) - E0) for s in St))
+    assert errs[0] < 1e-2 * abs(E0), errs
+    assert 0.45 < errs[1] / errs[0] < 0.55, errs
+
+
+def test_torque_free_body_keeps_angular_momentum(oracle_built):
+    """A free body with distinct principal inertias spinning about a near-principal axis, no
+    gravity, no damping: its world angular momentum R I R^T w is conserved to 1e-3 over 1 s at
+    dt 1e-3 (explicit gyroscopic term)."""
+    import kat_scene as K
+    I = np.array([0.01, 0.02, 0.03])
+    A = K.chain_scene([dict(parent=-1, axis=[0, 0, 1], jpos=[0, 0, 0], com_pos=[0, 0, 0], mass=1.0, inertia=[1e-3, 1e-3, 1e-3])],
+                      free_inertia=I, free_mass=1.0)
+    md = K.desc(A)
+    S = K.state(md, [0.0])
+    f = ABI.S_FREE
+    S[0, f + 10:f + 13] = [3.0, 0.2, 0.1]
+    St = _run(md, S, 1000, 1e-3)
+
+    def L(s):
+        Rm = G.quat_to_mat(s[f + 3:f + 7])
+        return Rm @ (I * (Rm.T @ s[f + 10:f + 13]))
+
+    L0 = I * np.array([3.0, 0.2, 0.1])
+    drift = max(np.linalg.norm(L(s) - L0) for s in St)
+    assert drift < 1e-3 * np.linalg.norm(L0), drift
+    assert np.allclose(St[-1, f:f + 3], [100, 100, 100], atol=1e-12)     # no linear motion
+
+
+def test_resting_sphere_normal_force_is_weight(scene, oracle_built):
+    """A food sphere at rest on the table (SURVEY 7 'normal force = mg'): the normal impulses of
+    its contact points sum to m g dt per sub-step (getContactPoints normalForce = impulse / dt)."""
+    from oracle.oracle import Oracle
+    A, md, S = _one_env_state(scene)
+    sb = shape_of(A, int(A['task_table_body']), 2)
+    top = A['st_pose'][2][2] + A['shape_pose'][sb][2] + A['shape_param'][sb][2]
+    f = ABI.S_FREE + ABI.FB_WORDS * 3
+    S[0, f:f + 3] = [0.35 + 0.6, -0.9 - 0.4, top + 0.005 + 0.001]
+    S[0, f + 3:f + 7] = [0, 0, 0, 1]
+    S[0, f + 7:f + 13] = 0
+    o = Oracle(md, 1)
+    o.set_state(S)
+    dt = 0.01
+    for _ in range(300):
+        o.substep(dt)
+    St = o.get_state()[0]
+    food_body = int(A['task_food_body0']) + 1
+    imp = 0.0
+    for k in range(int(St[ABI.S_TASK + ABI.T_NCP])):
+        c = St[ABI.S_CP + ABI.CP_WORDS * k:][:ABI.CP_WORDS]
+        if food_body in (A['shape_body'][int(c[ABI.CP_SA])], A['shape_body'][int(c[ABI.CP_SB])]):
+            imp += c[ABI.CP_IMP]
+    assert imp / dt == pytest.approx(0.001 * 9.81, rel=2e-2)
