@@ -82,20 +82,20 @@ def cpu_baseline(name, md, A, seconds, threads, impairment):
                            name, n, steps, el, T['settle'], threads))
 
 
-def pmc_summary(task, kernels, ms_per_step, E):
+def pmc_summary(name, kernels, ms_per_step, E):
     """HBM traffic and SQ issue figures from the committed rocprofv3 PMC summary of this task's
     bench (profiles/pmc_<task>.json, tools/rocpd_summary.py), if its kernel set and env count match."""
-    name = {0: 'pmc_traffic.json', 1: 'pmc_scratch.json'}[task]
-    path = os.path.join(ROOT, 'profiles', name)
+    fname = {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json'}[name]
+    path = os.path.join(ROOT, 'profiles', fname)
     if not os.path.exists(path):
         return None
     try:
         tj = json.load(open(path))
     except Exception:
         return None
-    if tj.get('envs') != E or tj.get('task', 0) != task or set(tj.get('kernels_per_step', {})) != set(kernels):
+    if tj.get('envs') != E or tj.get('task', 'FeedingJaco-v0') != name or set(tj.get('kernels_per_step', {})) != set(kernels):
         return None
-    out = dict(traffic=tj.get('hbm_bytes_per_step'), source='profiles/' + name)
+    out = dict(traffic=tj.get('hbm_bytes_per_step'), source='profiles/' + fname)
     sq = tj.get('sq_per_launch', {})
     disp = tj.get('dispatches_per_step', {})
     if sq and disp:
@@ -219,7 +219,7 @@ def main():
     bpe = T['bytes']
     achieved = bpe * E / (step_kernel_ms * 1e-3) / 1e9
     ms_per_step = el / args.steps * 1e3
-    pmc = pmc_summary(T['task'], sim.kernel_kinds, ms_per_step, E)
+    pmc = pmc_summary(args.task, sim.kernel_kinds, ms_per_step, E)
     traffic = pmc['traffic'] if pmc else None
     # the bound: the larger of the two roofline fractions the path could sit on (HBM bytes vs the
     # dense matrix-core peak; the path issues no MFMA, so its MFMA fraction is 0)

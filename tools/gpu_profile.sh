@@ -3,21 +3,23 @@
 # baseline).  Summaries: python tools/rocpd_summary.py gpurun_out/prof <tag>.
 set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/prof
-B="bench.py --steps 20 --warmup 3 --no-cpu-baseline"
+TASK=${TASK:-FeedingJaco-v0}
+B="bench.py --task $TASK --steps 20 --warmup 3 --no-cpu-baseline"
+B5="bench.py --task $TASK --steps 5 --warmup 1 --no-cpu-baseline"
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_before.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt -- python3 $B > gpurun_out/prof/kt_bench.log 2>&1 && \
 AVR_ENV_GROUPS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt1 -o kt1 -- python3 $B > gpurun_out/prof/kt1_bench.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/fetch.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/write.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/prof/sq -o sq -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/sq.log 2>&1 && \
-timeout -k 10 600 python3 bench.py > gpurun_out/prof/bench_full.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 $B5 > gpurun_out/prof/fetch.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 $B5 > gpurun_out/prof/write.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/prof/sq -o sq -- python3 $B5 > gpurun_out/prof/sq.log 2>&1 && \
+timeout -k 10 600 python3 bench.py --task $TASK > gpurun_out/prof/bench_full.log 2>&1
 rc=$?
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_after.txt
 # summaries on the box (the rocpd databases are too large to copy back), then drop the databases
-mkdir -p gpurun_out/psum && AVR_PROF_OUT=gpurun_out/psum python3 tools/rocpd_summary.py gpurun_out/prof ${TAG:-r02} > gpurun_out/psum/summary.txt 2>&1
-cp gpurun_out/prof/*.txt gpurun_out/prof/*.log gpurun_out/psum/ 2>/dev/null
+PS=gpurun_out/psum_${TAG:-r03}; mkdir -p $PS && AVR_PROF_OUT=$PS python3 tools/rocpd_summary.py gpurun_out/prof ${TAG:-r03} 4096 $TASK > $PS/summary.txt 2>&1
+cp gpurun_out/prof/*.txt gpurun_out/prof/*.log $PS/ 2>/dev/null
 rm -rf gpurun_out/prof
-tail -1 gpurun_out/psum/bench_full.log | cut -c1-600
-head -24 gpurun_out/psum/summary.txt
+tail -1 $PS/bench_full.log | cut -c1-600
+head -24 $PS/summary.txt
 echo rc=$rc
 exit $rc

@@ -1,6 +1,9 @@
 """Summarise rocprofv3 rocpd databases (ROCm 7.2 default output) into profiles/.
 
-    python tools/rocpd_summary.py <prof_dir> <round_tag> [envs]
+    python tools/rocpd_summary.py <prof_dir> <round_tag> [envs] [task]
+
+task: FeedingJaco-v0 (default) or ScratchItchPR2-v0 (launch multiplicities differ: 10 sub-steps
+per env-step vs 5).  Kernel names carry the task namespace (avr_feeding:: / avr_scratch::).
 
 <prof_dir>/kt/*.db     --kernel-trace --stats run  -> profiles/<tag>_kernel_stats.csv
 <prof_dir>/fetch/*.db  --pmc FETCH_SIZE            -> } profiles/pmc_traffic.json and
@@ -17,9 +20,18 @@ import sys
 
 import numpy as np
 
-# launches per env-step (FeedingJaco: 10 sub-steps of four kernels, one take_step, one task launch)
-STEP_KERNELS = {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': 10, 'avr_narrowphase_kernel': 10, 'avr_coop_kernel': 10, 'avr_substep_a_kernel': 10,
-                'avr_substep_b4_kernel': 10, 'avr_task_kernel': 1}
+# launches per env-step: one take_step, one task launch and, per sub-step, the five sub-step kernels
+# (FeedingJaco: 5 frames x 2 sub-steps; ScratchItchPR2: 5 frames x 1 sub-step)
+SUBSTEPS = {'FeedingJaco-v0': 10, 'ScratchItchPR2-v0': 5}
+
+
+def step_kernels(task):
+    n = SUBSTEPS[task]
+    return {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n, 'avr_coop_kernel': n,
+            'avr_substep_a_kernel': n, 'avr_substep_b4_kernel': n, 'avr_task_kernel': 1}
+
+
+STEP_KERNELS = step_kernels('FeedingJaco-v0')
 
 
 def db(d):
@@ -45,7 +57,8 @@ def counters(c, names):
     res = {}
     for k in STEP_KERNELS:
         for n in names:
-            v = [r[0] for r in c.execute("select value from counters_collection where counter_name=? and kernel_name like ?", (n, k + '%'))]
+            v = [r[0] for r in c.execute("select value from counters_collection where counter_name=? and (kernel_name like ? or kernel_name like ?)",
+                                         (n, k + '(%', '%::' + k + '(%'))]
             if v:
                 res.setdefault(k, {})[n] = float(np.median(v))
     return res
@@ -59,7 +72,9 @@ def per_step(cnt, name, groups=1):
     return sum(cnt[k][name] * STEP_KERNELS[k] * groups for k in STEP_KERNELS)
 
 
-def main(pdir, tag, envs=4096, groups=None):
+def main(pdir, tag, envs=4096, groups=None, task='FeedingJaco-v0'):
+    global STEP_KERNELS
+    STEP_KERNELS = step_kernels(task)
     # the bench runs min(4, envs / 1024) env groups: every kernel of the step is dispatched once
     # per group, over that group's share of the envs
     groups = groups or max(1, min(4, envs // 1024))
@@ -80,7 +95,7 @@ def main(pdir, tag, envs=4096, groups=None):
         print(name % tag)
         for r in st:
             print('%-28s calls %4d avg %10.3f ms  median %10.3f ms  %5.1f%%' % (r[0], r[1], r[3] / 1e6, r[4] / 1e6, r[7]))
-    out = {'kernels_per_step': STEP_KERNELS, 'envs': envs, 'env_groups': groups,
+    out = {'task': task, 'kernels_per_step': STEP_KERNELS, 'envs': envs, 'env_groups': groups,
            'dispatches_per_step': {k: v * groups for k, v in STEP_KERNELS.items()}}   # (only kernels that run in a step)
     cf, cw, cs = db(os.path.join(pdir, 'fetch')), db(os.path.join(pdir, 'write')), db(os.path.join(pdir, 'sq'))
     fetch = counters(cf, ['FETCH_SIZE']) if cf else {}
@@ -98,10 +113,11 @@ def main(pdir, tag, envs=4096, groups=None):
         out['hbm_bytes_per_step'] = fb + wb
         out['hbm_bytes_per_env_step'] = (fb + wb) / envs
         out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x dispatches per step (launches x env groups)'
-        json.dump(out, open(os.path.join(prof, 'pmc_traffic.json'), 'w'), indent=1)
+        json.dump(out, open(os.path.join(prof, 'pmc_traffic.json' if task == 'FeedingJaco-v0' else 'pmc_scratch.json'), 'w'), indent=1)
     json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4096)
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4096,
+         task=sys.argv[4] if len(sys.argv) > 4 else 'FeedingJaco-v0')
