@@ -19,7 +19,7 @@ EXPORTS = [
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_env_groups', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
-    'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary',
+    'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik',
 ]
 
 
@@ -86,6 +86,8 @@ def load(path=LIB_PATH):
     lib.avr_get_q.argtypes = [vp, vp, vp]
     lib.avr_get_link_pose.argtypes = [vp, C.c_int32, vp]
     lib.avr_get_contact_summary.argtypes = [vp, vp]
+    lib.avr_get_flags.argtypes = [vp, vp]
+    lib.avr_reset_ik.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, C.c_int32, vp, vp]
     if lib.avr_abi_version() != ABI.ABI_VERSION or any(
             lib.avr_task_state_words(t) != L.STATE_WORDS or lib.avr_task_obs_dim(t) != L.OBS_DIM or lib.avr_task_act_dim(t) != L.ACT_DIM
             for t, L in ABI.LAYOUTS.items()):
@@ -164,6 +166,25 @@ class Sim:
         self._chk(self.lib.avr_reset(self.h, None if m is None else m.ctypes.data, S.ctypes.data, int(frames), obs.ctypes.data))
         return obs
 
+    def reset_ik(self, mask, S, target7, init, iters=80, tol=0.01, keepout8=None, frames=100, obs=None):
+        """Masked reset with the IK on the device (include/avr.h avr_reset_ik): S rows without the
+        arm joints, target7 (n_envs, 7), init (n_envs, restarts, n_arm) restart draws.
+        Returns (obs, ok)."""
+        S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
+        t = np.ascontiguousarray(target7, np.float32).reshape(self.n, 7)
+        init = np.ascontiguousarray(init, np.float32)
+        assert init.ndim == 3 and init.shape[0] == self.n
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.n)
+        box = None if keepout8 is None else np.ascontiguousarray(keepout8, np.float32).reshape(8)
+        if obs is None:
+            obs = np.zeros((self.n, self.obs_dim), np.float32)
+        assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.shape == (self.n, self.obs_dim)
+        ok = np.zeros(self.n, np.uint8)
+        self._chk(self.lib.avr_reset_ik(self.h, None if m is None else m.ctypes.data, S.ctypes.data, t.ctypes.data, init.ctypes.data,
+                                        int(init.shape[1]), int(iters), float(tol), None if box is None else box.ctypes.data, int(frames),
+                                        obs.ctypes.data, ok.ctypes.data))
+        return obs, ok.astype(bool)
+
     def substep(self, dt):
         self._chk(self.lib.avr_substep(self.h, dt))
 
@@ -229,6 +250,12 @@ class Sim:
         """(n_envs, 4): contact points, sum of normal force, robot-human, tool-human."""
         out = np.zeros((self.n, 4), np.float32)
         self._chk(self.lib.avr_get_contact_summary(self.h, out.ctypes.data))
+        return out
+
+    def get_flags(self):
+        """(n_envs,) int32 health flags (0 = healthy; bits in include/avr.h avr_get_flags)."""
+        out = np.zeros(self.n, np.int32)
+        self._chk(self.lib.avr_get_flags(self.h, out.ctypes.data))
         return out
 
     def kernel_info(self):

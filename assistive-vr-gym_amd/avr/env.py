@@ -1,18 +1,29 @@
-"""Gym-style facade over libavr: the reference's FeedingJaco-v0 reset/step contract, batched.
+"""Gym-style facade over libavr: the reference's reset/step contract, batched.
 
 Reference contract being mirrored:
-  * ids registered in assistive_gym/__init__.py (FeedingJaco-v0 -> FeedingJacoEnv, TimeLimit 200);
-  * reset() -> obs (25,), feeding.py:144-331 (scene randomisation, IK, 100 food-drop frames);
-  * step(a) -> (obs (25,), reward, done, info) with info keys total_force_on_human,
-    task_success, action_robot_len, action_human_len, obs_robot_len, obs_human_len
-    (feeding.py:76); done at iteration >= 200 (TimeLimit).
-  * observation/action spaces: Box(-1e9, 1e9, (25,)) and Box(-1, 1, (7,)), float32
-    (env.py:34-35 with action_robot_len 7, obs_robot_len 25 for FeedingJaco).
+  * ids registered in assistive_gym/__init__.py (FeedingJaco-v0 -> FeedingJacoEnv,
+    ScratchItchPR2-v0 -> ScratchItchPR2Env; TimeLimit 200);
+  * reset() -> obs: FeedingJaco (25,), feeding.py:144-331 (scene randomisation, IK, 100 food-drop
+    frames); ScratchItchPR2 (30,), scratch_itch.py:130-273 (base-pose search + IK, no settle);
+  * step(a) -> (obs, reward, done, info) with info keys total_force_on_human, task_success,
+    action_robot_len, action_human_len, obs_robot_len, obs_human_len (feeding.py:76,
+    scratch_itch.py:78); done at iteration >= 200 (TimeLimit).
+  * observation/action spaces: Box(-1e9, 1e9, (obs,)) and Box(-1, 1, (7,)), float32 (env.py:34-35).
 
-AVRVecEnv steps all envs of one GPU in one kernel launch; AVREnv is the single-env view
+AVRVecEnv steps all envs of one GPU in one launch sequence (host arrays in/out); AVRTorchVecEnv
+is the same with device tensors (no host copies per step); AVREnv is the single-env view
 (n_envs=1) that reads like `gym.make('FeedingJaco-v0')`.  Physics runs only on the GPU (libavr);
 there is no CPU fallback here.
+
+Episode rollover (auto_reset): FeedingJaco resets run the IK on the device (avr_reset_ik) from
+the host's reset draws (reset.reset_inputs), which a background thread prepares for the next
+episode while the current one steps; ScratchItch resets run the host base-pose search + IK
+(reset_scratch.batch_reset_states), then avr_reset.
 """
+import sys
+import threading
+import time
+
 import numpy as np
 
 from . import _abi as ABI
@@ -20,7 +31,7 @@ from . import _lib
 from . import reset as RS
 
 MAX_EPISODE_STEPS = 200          # assistive_gym/__init__.py TimeLimit
-SETTLE_FRAMES = 100              # feeding.py:318-320
+SETTLE_FRAMES = {ABI.TASK_FEEDING: 100, ABI.TASK_SCRATCH: 0}    # feeding.py:318-320; scratch_itch.py has none
 
 
 class Box:
@@ -45,10 +56,11 @@ class Box:
 
 
 # id -> (task, robot, implemented): every id the reference registers (assistive_gym/__init__.py);
-# this build implements the FeedingJaco-v0 hot path, the rest raise NotImplementedError.
+# this build implements FeedingJaco-v0 and ScratchItchPR2-v0, the rest raise
+# NotImplementedError.
 REGISTRY = {
     'HumanTesting-v0':           ('human_testing', '-', False),
-    'ScratchItchPR2-v0':         ('scratch_itch', 'pr2', False),
+    'ScratchItchPR2-v0':         ('scratch_itch', 'pr2', True),
     'ScratchItchJaco-v0':        ('scratch_itch', 'jaco', False),
     'ScratchItchPR2Human-v0':    ('scratch_itch', 'pr2', False),
     'ScratchItchJacoHuman-v0':   ('scratch_itch', 'jaco', False),
@@ -99,33 +111,78 @@ REGISTRY = {
 }
 
 _SCENES = {}
+_TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH}
 
 
 def _scene(task):
     if task not in _SCENES:
-        A = ABI.load_scene()
+        A = ABI.load_scene(_TASK_OF[task])
         _SCENES[task] = (A, ABI.ModelDesc(A))
     return _SCENES[task]
 
 
+class _Prefetch:
+    """Reset draws of the next episode of a set of envs, prepared on a background thread while
+    the stepping thread keeps the GPU fed.  The stepping thread takes and drops the GIL around
+    every ctypes / torch call; at the default 5 ms switch interval a GIL-bound worker would delay
+    each re-acquisition by up to 5 ms and starve the launches, so the interval is lowered to
+    0.1 ms while the worker runs."""
+
+    def __init__(self, fn):
+        self.fn = fn
+        self.key = None
+        self.result = None
+        self.thread = None
+
+    def start(self, key, *args):
+        self.wait()
+        self.key, self.result = key, None
+
+        def run():
+            old = sys.getswitchinterval()
+            sys.setswitchinterval(1e-4)
+            try:
+                self.result = self.fn(*args)
+            finally:
+                sys.setswitchinterval(old)
+        self.thread = threading.Thread(target=run, daemon=True)
+        self.thread.start()
+
+    def wait(self):
+        if self.thread is not None:
+            self.thread.join()
+            self.thread = None
+
+    def take(self, key):
+        self.wait()
+        if self.key == key and self.result is not None:
+            r, self.key, self.result = self.result, None, None
+            return r
+        return None
+
+
 class AVRVecEnv:
-    """n_envs FeedingJaco-v0 environments on one GPU.
+    """n_envs environments of one task on one GPU; host arrays in and out.
 
     env_offset: global id of env 0 (multi-GPU sharding: rank * n_envs); reset randomness and the
     synthetic action stream are keyed by the global env id, so results do not depend on how
     envs are split over GPUs.
 
-    impairment: 'random' (FeedingJaco-v0's own setting, feeding.py:175: none / limits /
-    weakness / tremor, one draw per episode), a fixed one of those four, or 'no_tremor'.
+    impairment: 'random' (the tasks' own setting, feeding.py:175 / scratch_itch.py:178: none /
+    limits / weakness / tremor, one draw per episode), a fixed one of those four, or 'no_tremor'.
+    reset_ik: 'device' (FeedingJaco default: avr_reset_ik) or 'host' (host IK, then avr_reset).
+    reset_stream: FeedingJaco's reset draws, 'philox' (counter-based, vectorised; default) or
+    'numpy' (the per-env Generator stream of the bench's reset pools and the golden fixtures).
     """
 
     def __init__(self, env_id='FeedingJaco-v0', n_envs=1, device=0, seed=1001, env_offset=0, auto_reset=True,
-                 impairment='random'):
+                 impairment='random', reset_ik='device', prefetch=True, scratch_attempts=100, scratch_iters=200,
+                 reset_stream='philox'):
         if env_id not in REGISTRY:
             raise KeyError('unknown env id %r' % env_id)
         task, robot, ok = REGISTRY[env_id]
         if not ok:
-            raise NotImplementedError('%s: only the FeedingJaco-v0 hot path is built (SURVEY 8)' % env_id)
+            raise NotImplementedError('%s: only FeedingJaco-v0 and ScratchItchPR2-v0 are built (SURVEY 8)' % env_id)
         self.env_id = env_id
         self.n = int(n_envs)
         self.seed = int(seed)
@@ -133,43 +190,92 @@ class AVRVecEnv:
         self.auto_reset = auto_reset
         self.impairment = impairment
         self.A, self.md = _scene(task)
+        self.task = self.md.task
+        self.L = self.md.layout
+        self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'
+        self.scratch_attempts, self.scratch_iters = scratch_attempts, scratch_iters
+        self.reset_stream = reset_stream
         self.sim = _lib.Sim(self.md, self.n, device=device, seed=self.seed, env_offset=self.env_offset)
-        self.observation_space = Box(-1e9, 1e9, (ABI.OBS_DIM,))
-        self.action_space = Box(-1.0, 1.0, (ABI.ACT_DIM,))
+        self.observation_space = Box(-1e9, 1e9, (self.L.OBS_DIM,))
+        self.action_space = Box(-1.0, 1.0, (self.L.ACT_DIM,))
         self.episode = np.zeros(self.n, np.int64)
-        self._obs = np.zeros((self.n, ABI.OBS_DIM), np.float32)
+        # host mirror of the per-env iteration counters: the kernels' done is exactly
+        # T_ITER >= max_steps (TimeLimit), so rollovers are known without reading the device
+        self.iteration = np.zeros(self.n, np.int64)
+        self.max_steps = int(self.md.params['max_episode_steps'])
+        self._obs = np.zeros((self.n, self.L.OBS_DIM), np.float32)
+        self._keepout = RS.keepout_box(self.A) if self.task == ABI.TASK_FEEDING else None
+        self._prefetch = _Prefetch(self._inputs) if (prefetch and self.device_ik) else None
+        self.last_ik_ok = None
+        self.reset_timing = None
 
     # ------------------------------------------------------------------ reset
+    def _inputs(self, idx, episodes):
+        return RS.reset_inputs(self.A, self.md, self.seed, [self.env_offset + int(i) for i in idx],
+                               impairment=self.impairment, episodes=list(episodes), stream=self.reset_stream)
+
     def _reset_rows(self, mask):
         idx = np.nonzero(mask)[0]
-        S = np.zeros((self.n, ABI.STATE_WORDS), np.float32)
-        if len(idx):
-            Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, [self.env_offset + int(i) for i in idx],
-                                               impairment=self.impairment, episodes=self.episode[idx])
+        if not len(idx):
+            return
+        self.iteration[idx] = 0
+        eps = self.episode[idx].copy()
+        S = np.zeros((self.n, self.L.STATE_WORDS), np.float32)
+        frames = SETTLE_FRAMES[self.task]
+        if self.device_ik:
+            t0 = time.perf_counter()
+            key = (tuple(idx.tolist()), tuple(eps.tolist()))
+            got = self._prefetch.take(key) if self._prefetch else None
+            Si, t7, init, _, _ = got if got is not None else self._inputs(idx, eps)
+            t1 = time.perf_counter()
             S[idx] = Si
-        self.sim.reset(mask.astype(np.uint8), S, SETTLE_FRAMES, self._obs)
+            T = np.zeros((self.n, 7), np.float32)
+            T[:, 6] = 1.0
+            T[idx] = t7
+            I = np.zeros((self.n,) + init.shape[1:], np.float32)
+            I[idx] = init
+            t2 = time.perf_counter()
+            _, ok = self.sim.reset_ik(mask.astype(np.uint8), S, T, I, keepout8=self._keepout, frames=frames, obs=self._obs)
+            self.last_ik_ok = ok
+            self.reset_timing = dict(inputs_s=t1 - t0, prefetched=got is not None, pack_s=t2 - t1, device_s=time.perf_counter() - t2)
+            if self._prefetch:           # speculate: the same envs end their next episode together
+                self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
+            return
+        ids = [self.env_offset + int(i) for i in idx]
+        if self.task == ABI.TASK_SCRATCH:
+            from . import reset_scratch as RSS
+            Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, impairment=self.impairment, episodes=eps,
+                                           attempts=self.scratch_attempts, iters=self.scratch_iters)
+        else:
+            Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, impairment=self.impairment, episodes=eps,
+                                               stream=self.reset_stream)
+        S[idx] = Si
+        self.sim.reset(mask.astype(np.uint8), S, frames, self._obs)
 
     def reset(self, mask=None):
-        """Reset all envs (mask None) or the masked ones; returns obs (n_envs, 25) float32."""
+        """Reset all envs (mask None) or the masked ones; returns obs (n_envs, obs_dim) float32."""
         mask = np.ones(self.n, bool) if mask is None else np.asarray(mask, bool)
         self._reset_rows(mask)
         return self._obs.copy()
 
     # ------------------------------------------------------------------ step
+    def _info(self, inf):
+        return {
+            'total_force_on_human': inf[:, 0].copy(),
+            'task_success': inf[:, 1].astype(np.int64),
+            'action_robot_len': self.L.ACT_DIM, 'action_human_len': 0,
+            'obs_robot_len': self.L.OBS_DIM, 'obs_human_len': 0,
+        }
+
     def step(self, actions):
         """actions (n_envs, 7) -> obs, reward (n_envs,), done (n_envs,) bool, info dict of arrays.
 
         With auto_reset, finished envs are reset (next episode stream) and their final
         observation is returned in info['terminal_observation'] (vectorised-gym convention)."""
-        a = np.ascontiguousarray(actions, np.float32).reshape(self.n, ABI.ACT_DIM)
+        a = np.ascontiguousarray(actions, np.float32).reshape(self.n, self.L.ACT_DIM)
         obs, rew, done, inf = self.sim.step(a)
-        info = {
-            'total_force_on_human': inf[:, 0].copy(),
-            'task_success': inf[:, 1].astype(np.int64),
-            'action_robot_len': ABI.ACT_DIM, 'action_human_len': 0,
-            'obs_robot_len': ABI.OBS_DIM, 'obs_human_len': 0,
-            'flags': self.flags(),
-        }
+        self.iteration += 1
+        info = self._info(inf)
         self._obs[:] = obs
         if self.auto_reset and done.any():
             info['terminal_observation'] = obs.copy()
@@ -179,25 +285,80 @@ class AVRVecEnv:
         return obs, rew, done, info
 
     def flags(self):
-        """Per-env health flags (bit0 NaN/failed factorisation, bit1 contact-cache overflow, ...)."""
-        St = self.sim.get_state()
-        return St[:, ABI.S_TASK + ABI.T_FLAGS].astype(np.int64)
+        """Per-env health flags (include/avr.h avr_get_flags; 0 = healthy), without copying the state."""
+        return self.sim.get_flags().astype(np.int64)
 
     def get_state(self):
         return self.sim.get_state()
 
     def set_state(self, S):
         self.sim.set_state(S)
+        self.iteration[:] = np.asarray(S)[:, self.L.S_TASK + self.L.T_ITER].astype(np.int64)
 
     def close(self):
+        if self._prefetch:
+            self._prefetch.wait()
         self.sim.close()
+
+
+class AVRTorchVecEnv(AVRVecEnv):
+    """AVRVecEnv with torch device tensors: step(actions (n, 7) cuda float32) -> obs, reward, done,
+    info as cuda tensors, written by the kernels directly (avr_step_device).  No per-step host
+    traffic or synchronisation: whether a rollover is due follows from the host mirror of the
+    iteration counters (done == T_ITER >= max_steps in the kernels), so launches of consecutive
+    steps queue ahead of the GPU; a rollover step synchronises for the reset."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        import torch
+        self.torch = torch
+        self.dev = torch.device('cuda', kw.get('device', 0))
+        self.ext = torch.cuda.ExternalStream(self.sim.stream(), device=self.dev)
+        n, L = self.n, self.L
+        self.t_obs = torch.zeros(n, L.OBS_DIM, device=self.dev)
+        self.t_rew = torch.zeros(n, device=self.dev)
+        self.t_done = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+        self.t_info = torch.zeros(n, ABI.INFO_DIM, device=self.dev)
+
+    def reset(self, mask=None):
+        obs = super().reset(mask)
+        self.t_obs.copy_(self.torch.from_numpy(obs))
+        return self.t_obs.clone()
+
+    def step(self, actions):
+        torch = self.torch
+        a = actions.to(self.dev, torch.float32).contiguous()
+        assert a.shape == (self.n, self.L.ACT_DIM)
+        self.ext.wait_stream(torch.cuda.current_stream(self.dev))
+        # (the kernels read `a` on the sim stream; torch's stream waits for that stream below, so the
+        # caching allocator cannot hand `a`'s memory to later work before the step has read it)
+        self.sim.step_device(a.data_ptr(), self.t_obs.data_ptr(), self.t_rew.data_ptr(), self.t_done.data_ptr(), self.t_info.data_ptr())
+        torch.cuda.current_stream(self.dev).wait_stream(self.ext)
+        self.iteration += 1
+        obs, rew, done = self.t_obs.clone(), self.t_rew.clone(), self.t_done.bool()
+        info = {'total_force_on_human': self.t_info[:, 0].clone(), 'task_success': self.t_info[:, 1].to(torch.int64),
+                'action_robot_len': self.L.ACT_DIM, 'action_human_len': 0, 'obs_robot_len': self.L.OBS_DIM, 'obs_human_len': 0}
+        if self.auto_reset:
+            dh = self.iteration >= self.max_steps
+            if dh.any():
+                torch.cuda.current_stream(self.dev).synchronize()
+                info['terminal_observation'] = obs
+                self.episode[dh] += 1
+                self._reset_rows(dh)
+                m = torch.from_numpy(dh).to(self.dev)
+                obs = torch.where(m[:, None], torch.from_numpy(self._obs).to(self.dev), obs)
+        return obs, rew, done, info
+
+    def close(self):
+        self.torch.cuda.synchronize(self.dev)
+        super().close()
 
 
 class AVREnv:
     """Single-env view with the reference's gym.Env signatures."""
 
     def __init__(self, env_id='FeedingJaco-v0', device=0, seed=1001, impairment='random'):
-        self.v = AVRVecEnv(env_id, 1, device=device, seed=seed, auto_reset=False, impairment=impairment)
+        self.v = AVRVecEnv(env_id, 1, device=device, seed=seed, auto_reset=False, impairment=impairment, prefetch=False)
         self.observation_space = self.v.observation_space
         self.action_space = self.v.action_space
 
@@ -220,7 +381,10 @@ class AVREnv:
 
 
 def make(env_id, **kw):
-    """gym.make replacement: AVREnv for one env, AVRVecEnv when n_envs is given."""
+    """gym.make replacement: AVREnv for one env, AVRVecEnv when n_envs is given (AVRTorchVecEnv
+    with torch=True)."""
+    if kw.pop('torch', False):
+        return AVRTorchVecEnv(env_id, **kw)
     if 'n_envs' in kw:
         return AVRVecEnv(env_id, **kw)
     return AVREnv(env_id, **kw)

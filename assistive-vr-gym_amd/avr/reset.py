@@ -136,28 +136,36 @@ def ik(A, link, target_pos, target_quat, arm_dofs, lower, upper, rng, q0=None,
 
 
 # ----------------------------------------------------------------------------- human
+_HJ = {}
+
+
+def _human_limits(A, gender):
+    """Per-gender joint-limit tables of human_joint_angles (cached): lower, upper, the
+    limit_scale joint mask and the mask of clamped joints (revolute with a limit)."""
+    if gender not in _HJ:
+        lo = A['human_%s_lower' % gender].astype(float)
+        hi = A['human_%s_upper' % gender].astype(float)
+        n = len(lo)
+        scaled = np.zeros(n, bool)
+        scaled[[j for j in HUMAN_SCALED if j < n]] = True
+        clamp = (A['human_%s_jtype' % gender] == 1)
+        _HJ[gender] = (lo, hi, scaled, clamp)
+    return _HJ[gender]
+
+
 def human_joint_angles(A, gender, rng, limit_scale=1.0):
     """Feeding (non-VR, non-new) human joint setup: fixed arm/leg poses + random head
     (feeding.py:242-245), clamped by enforce_joint_limits (world_creation.py:110-133)."""
-    n = len(A['human_%s_parent' % gender])
-    q = np.zeros(n)
+    lo0, hi0, scaled, clamp = _human_limits(A, gender)
+    q = np.zeros(len(lo0))
     for j, ang in [(10, -90), (20, -90), (28, -90), (31, 80), (35, -90), (38, 80)]:
         q[j] = np.deg2rad(ang)
     for j in (25, 26, 27):
         q[j] = rng.uniform(np.deg2rad(-30), np.deg2rad(30))
-    lo = A['human_%s_lower' % gender].copy()
-    hi = A['human_%s_upper' % gender].copy()
-    for j in HUMAN_SCALED:
-        lo[j] *= limit_scale
-        hi[j] *= limit_scale
-    jt = A['human_%s_jtype' % gender]
-    for j in range(n):
-        if jt[j] != 1:
-            continue
-        l, u = lo[j], hi[j]
-        if l == 0 and u == -1:
-            continue
-        q[j] = min(max(q[j], l), u)
+    lo = np.where(scaled, lo0 * limit_scale, lo0)
+    hi = np.where(scaled, hi0 * limit_scale, hi0)
+    c = clamp & ~((lo == 0) & (hi == -1))
+    q[c] = np.minimum(np.maximum(q[c], lo[c]), hi[c])
     return q
 
 
@@ -315,10 +323,13 @@ def robot_fk_batch(A, Q):
     return CP, CQ, AX, OR
 
 
-def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, restarts=40, tol=0.01):
+def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, tol=0.01):
     """Vectorised DLS IK (same acceptance rule as `ik`), one random restart per round for every
-    env that has not converged yet."""
+    env that has not converged yet.  init (N, restarts, n_arm): the restarts' starting joints,
+    drawn up front from each env's reset stream (reset_inputs).  Restated on the device by
+    avr_reset_ik (csrc/avr_reset_ik.hip), which runs the same rules one env at a time."""
     N = tpos.shape[0]
+    restarts = init.shape[1]
     chain = _chain(A, link)
     cols = []
     for dof in arm_dofs:
@@ -331,7 +342,7 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, rngs, q0, iters=80, r
         if len(idx) == 0:
             break
         Q = np.repeat(q0[None], len(idx), 0)
-        Q[:, arm_dofs] = np.stack([rngs[i].uniform(lower, upper) for i in idx])
+        Q[:, arm_dofs] = init[idx, r]
         tp, tq = tpos[idx], tquat[idx]
         for it in range(iters):
             CP, CQ, AX, OR = robot_fk_batch(A, Q)
@@ -401,15 +412,154 @@ def _rng(seed, env_id, episode=0):
     return np.random.default_rng(key)
 
 
-def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none', episodes=None):
-    """Vectorised equivalent of batch_reset_states (same per-env draws and acceptance rules,
-    IK batched across envs).  episodes[k] selects the k-th env's episode stream (default 0)."""
+def arm_limits(md):
+    """IK joint bounds of the arm: the URDF limits, +-2 pi for continuous joints."""
+    arm = md.arm_dofs
+    lower = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
+    upper = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
+    return lower, upper
+
+
+def keepout_box(A, margin=0.05):
+    """The table box inflated by `margin` (table_clear's screening box) as {center, pad, half
+    extents, pad} -- avr_reset_ik's keepout8."""
+    tb = int(A['task_table_body'])
+    s0 = A['body_shape_start'][tb]
+    c = A['st_pose'][A['body_index'][tb]][:3] + A['shape_pose'][s0][:3]
+    he = A['shape_param'][s0][:3] + margin
+    return np.array([c[0], c[1], c[2], 0.0, he[0], he[1], he[2], 0.0])
+
+
+def human_slot_poses_batch(A, genders, QH):
+    """human_slot_poses for many envs at once: genders (N,) str, QH (N, n_joints) -> (N, MAX_HUMAN, 7)."""
+    N = len(genders)
+    out = np.zeros((N, ABI.MAX_HUMAN, 7))
+    for g in ('male', 'female'):
+        idx = np.array([k for k in range(N) if genders[k] == g], int)
+        if not len(idx):
+            continue
+        Qg = QH[idx]
+        n = len(idx)
+        base_p = np.array([0, 0.03, 0.89 - 0.23725 if g == 'male' else 0.86 - 0.225])
+        par = A['human_%s_parent' % g]
+        jt = A['human_%s_jtype' % g]
+        ax = A['human_%s_axis' % g]
+        pos = A['human_%s_pos' % g]
+        nl = len(par)
+        P = np.zeros((n, nl, 3)); Qq = np.zeros((n, nl, 4))
+        bp = np.broadcast_to(base_p, (n, 3)); bq = np.broadcast_to(np.array([0, 0, 0, 1.0]), (n, 4))
+        for i in range(nl):
+            pp, pq = (bp, bq) if par[i] < 0 else (P[:, par[i]], Qq[:, par[i]])
+            P[:, i] = pp + _qrot(pq, np.broadcast_to(pos[i], (n, 3)))
+            q = pq
+            if jt[i] == 1:
+                q = _qmul(pq, _qaxis(np.broadcast_to(ax[i], (n, 3)), Qg[:, i]))
+            Qq[:, i] = q
+        for s_, l in enumerate(A['human_slot_link']):
+            if l < 0:
+                out[idx, s_, :3] = base_p
+                out[idx, s_, 3:] = [0, 0, 0, 1.0]
+            else:
+                out[idx, s_, :3] = P[:, l]
+                out[idx, s_, 3:] = Qq[:, l]
+    return out
+
+
+# ----------------------------------------------------------------------------- counter-based stream
+# The 'philox' reset stream: draw j of env e's episode ep is uniform (0, 1) from Philox4x32-10
+# (the action generator's family) with key (seed, seed >> 32 ^ 'RSET') and counter
+# (e, ep, j // 4, 0x5EED) -- a pure function of (seed, env, episode, j), so every draw of a batch
+# of resets comes out of a few vectorised numpy passes (no per-env Python, GIL-light), and the
+# same numbers can be generated anywhere.  Fixed draw slots:
+PH_GENDER, PH_IMPAIR, PH_LIMIT, PH_HEAD, PH_TREMOR, PH_BOWL, PH_TARGET, PH_INIT = 0, 1, 2, 3, 6, 14, 16, 24
+_PH_TAG = 0x52534554
+
+
+def philox_uniforms(seed, env_ids, episodes, n):
+    """(N, n) float64 uniforms in (0, 1) of the 'philox' reset stream."""
+    from ._lib import philox4x32_10
+    e = np.asarray(env_ids, np.uint64)
+    ep = np.asarray(episodes, np.uint64)
+    seed = int(seed)
+    out = np.zeros((len(e), 4 * ((n + 3) // 4)))
+    for b in range((n + 3) // 4):
+        c = [e, ep, np.full_like(e, b), np.full_like(e, 0x5EED)]
+        r = philox4x32_10(c, seed & 0xFFFFFFFF, ((seed >> 32) ^ _PH_TAG) & 0xFFFFFFFF)
+        for k in range(4):
+            out[:, 4 * b + k] = (r[k].astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+    return out[:, :n]
+
+
+def human_joint_angles_batch(A, gender, head, limit_scale):
+    """human_joint_angles for many envs of one gender: head (N, 3) angles, limit_scale (N,)."""
+    lo0, hi0, scaled, clamp = _human_limits(A, gender)
+    N = len(head)
+    q = np.zeros((N, len(lo0)))
+    for j, ang in [(10, -90), (20, -90), (28, -90), (31, 80), (35, -90), (38, 80)]:
+        q[:, j] = np.deg2rad(ang)
+    q[:, 25:28] = head
+    ls = np.asarray(limit_scale, float)[:, None]
+    lo = np.where(scaled[None], lo0[None] * ls, lo0[None])
+    hi = np.where(scaled[None], hi0[None] * ls, hi0[None])
+    c = clamp[None] & ~((lo == 0) & (hi == -1))
+    return np.where(c, np.minimum(np.maximum(q, lo), hi), q)
+
+
+def _draws_philox(A, md, seed, env_ids, genders, impairment, episodes, restarts):
+    """The reset draws of the 'philox' stream, vectorised over envs."""
+    N = len(env_ids)
+    lower, upper = arm_limits(md)
+    na = len(md.arm_dofs)
+    U = philox_uniforms(seed, env_ids, episodes, PH_INIT + restarts * na)
+    gl = list(genders) if genders is not None else ['male' if u < 0.5 else 'female' for u in U[:, PH_GENDER]]
+    if impairment == 'random':
+        il = [IMPAIRMENTS[min(3, int(4 * u))] for u in U[:, PH_IMPAIR]]
+    elif impairment == 'no_tremor':
+        il = [IMPAIRMENTS[min(2, int(3 * u))] for u in U[:, PH_IMPAIR]]
+    elif impairment in IMPAIRMENTS:
+        il = [impairment] * N
+    else:
+        raise ValueError('unknown impairment %r' % impairment)
+    lim = np.array([x == 'limits' for x in il])
+    ls = np.where(lim, 0.5 + 0.5 * U[:, PH_LIMIT], 1.0)
+    head = np.deg2rad(-30) + np.deg2rad(60) * U[:, PH_HEAD:PH_HEAD + 3]
+    n_j = max(len(A['human_male_parent']), len(A['human_female_parent']))
+    QH = np.zeros((N, n_j))
+    for g in ('male', 'female'):
+        idx = np.array([k for k in range(N) if gl[k] == g], int)
+        if len(idx):
+            q = human_joint_angles_batch(A, g, head[idx], ls[idx])
+            QH[idx, :q.shape[1]] = q
+    trem = np.deg2rad(-20) + np.deg2rad(40) * U[:, PH_TREMOR:PH_TREMOR + ABI.HC_N]
+    bowl = np.array([-0.15, -0.55, 0.75]) + np.concatenate([-0.05 + 0.1 * U[:, PH_BOWL:PH_BOWL + 2], np.zeros((N, 1))], 1)
+    tpos = bowl + np.array([0, -0.1, 0.4]) + (-0.05 + 0.1 * U[:, PH_TARGET:PH_TARGET + 3])
+    init = lower + (upper - lower) * U[:, PH_INIT:PH_INIT + restarts * na].reshape(N, restarts, na)
+    return gl, il, ls, QH, trem, bowl, tpos, init
+
+
+def reset_inputs(A, md, seed, env_ids, genders=None, impairment='none', episodes=None, restarts=40, vector_fk=True, stream='numpy'):
+    """Everything FeedingEnv.reset draws, for many envs (feeding.py:144-331 minus the IK): state
+    rows without the arm's joints, spoon and food (S, float64), the tool link's IK target
+    (target7: position + quaternion), the restarts' starting joints (init, (N, restarts, n_arm))
+    and per-env meta.  stream 'numpy' (the host reset's per-env Generator; its order: gender,
+    impairment, limit scale, head angles, tremor draws, bowl jitter, target jitter, then the IK
+    restarts) or 'philox' (counter-based, vectorised: philox_uniforms).
+    vector_fk: human link poses by the batched FK (else the per-env one)."""
+    if stream == 'philox':
+        return _inputs_from_draws(A, md, *_draws_philox(A, md, seed, list(env_ids), genders, impairment,
+                                                        [0] * len(env_ids) if episodes is None else list(episodes), restarts))
+    if stream != 'numpy':
+        raise ValueError('unknown reset stream %r' % stream)
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
     rngs = [_rng(seed, e, ep) for e, ep in zip(env_ids, eps)]
     S = np.zeros((N, ABI.STATE_WORDS))
-    gl, il, tpos, bowl = [], [], np.zeros((N, 3)), np.zeros((N, 3))
+    lower, upper = arm_limits(md)
+    arm = md.arm_dofs
+    gl, il, QH = [], [], []
+    tpos, bowl = np.zeros((N, 3)), np.zeros((N, 3))
+    init = np.zeros((N, restarts, len(arm)))
     for k in range(N):
         rng = rngs[k]
         g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
@@ -418,40 +568,110 @@ def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none
         il.append(imp)
         ls = rng.uniform(0.5, 1.0) if imp == 'limits' else 1.0
         qh = human_joint_angles(A, g, rng, ls)
-        S[k, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, g, qh).ravel()
+        QH.append(qh)
+        if not vector_fk:
+            S[k, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses(A, g, qh).ravel()
         if imp == 'tremor':
             _tremor_state(S[k], md, qh, rng)
         bowl[k] = np.array([-0.15, -0.55, 0.75]) + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), 0])
         tpos[k] = bowl[k] + np.array([0, -0.1, 0.4]) + rng.uniform(-0.05, 0.05, size=3)
+        init[k] = rng.uniform(lower, upper, size=(restarts, len(arm)))
+    if vector_fk:
+        nj = max(len(q) for q in QH)
+        QHa = np.zeros((N, nj))
+        for k, q in enumerate(QH):
+            QHa[k, :len(q)] = q
+        S[:, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses_batch(A, gl, QHa).reshape(N, -1)
     tq = np.repeat(G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])[None], N, 0)
-    arm = md.arm_dofs
-    lower = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
-    upper = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
     q0 = np.zeros(int(A['n_dof']))
     for d in md.finger_dofs:
         q0[d] = md.params['finger_target']
+    S[:, ABI.S_Q:ABI.S_Q + len(q0)] = q0
+    for d in arm:
+        S[:, ABI.S_KP + d] = 0.0
+        S[:, ABI.S_QTGT + d] = 0.0
+        S[:, ABI.S_MAXIMP + d] = md.params['default_motor_impulse']
+    for d in md.finger_dofs:
+        S[:, ABI.S_KP + d] = md.params['finger_gain']
+        S[:, ABI.S_QTGT + d] = md.params['finger_target']
+        S[:, ABI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+    b = ABI.S_FREE + ABI.FB_WORDS
+    S[:, b:b + 3] = bowl
+    S[:, b + 3:b + 7] = G.quat_from_euler([np.pi / 2.0, 0, 0])
+    t = ABI.S_TASK
+    gi = np.array([0 if g == 'male' else 1 for g in gl])
+    hs = ABI.S_HUMAN + 7 * int(A['task_head_slot'])
+    for k in range(N):
+        head = S[k, hs:hs + 7]
+        mouth = A['task_mouth_male'] if gi[k] == 0 else A['task_mouth_female']
+        S[k, t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
+    S[:, t + ABI.T_ALIVE] = (1 << 8) - 1
+    S[:, t + ABI.T_GENDER] = gi
+    target7 = np.concatenate([tpos, tq], 1)
+    meta = [dict(gender=gl[k], impairment=il[k], bowl_pos=bowl[k], target_pos=tpos[k]) for k in range(N)]
+    return S, target7, init, q0, meta
+
+
+def _inputs_from_draws(A, md, gl, il, ls, QH, trem, bowl, tpos, init):
+    """reset_inputs' state rows from already-drawn values (the 'philox' stream), vectorised."""
+    N = len(gl)
+    S = np.zeros((N, ABI.STATE_WORDS))
+    S[:, ABI.S_HUMAN:ABI.S_HUMAN + ABI.MAX_HUMAN * 7] = human_slot_poses_batch(A, gl, QH).reshape(N, -1)
+    tr = np.array([x == 'tremor' for x in il])
+    if tr.any():
+        nd = md.n_dof
+        for k, j in enumerate(HEAD_CHAIN):
+            S[tr, ABI.S_Q + nd + k] = QH[tr, j]
+            S[tr, ABI.S_HCH + k] = QH[tr, j]
+        S[tr, ABI.S_HCH + ABI.HC_N:ABI.S_HCH + 2 * ABI.HC_N] = trem[tr]
+        S[tr, ABI.S_TASK + ABI.T_HDYN] = 1.0
+    q0 = np.zeros(int(A['n_dof']))
+    for d in md.finger_dofs:
+        q0[d] = md.params['finger_target']
+    _fill_common(A, md, S, q0, gl, bowl)
+    tq = np.repeat(G.quat_from_euler([np.pi / 2.0, 0, np.pi / 2.0])[None], N, 0)
+    target7 = np.concatenate([tpos, tq], 1)
+    meta = [dict(gender=gl[k], impairment=il[k], limit_scale=float(ls[k]), bowl_pos=bowl[k], target_pos=tpos[k]) for k in range(N)]
+    return S, target7, init, q0, meta
+
+
+def _fill_common(A, md, S, q0, gl, bowl):
+    """Motors, bowl, mouth target, alive mask and gender words of reset state rows."""
+    N = len(S)
+    arm = md.arm_dofs
+    S[:, ABI.S_Q:ABI.S_Q + len(q0)] = q0
+    for d in arm:
+        S[:, ABI.S_KP + d] = 0.0
+        S[:, ABI.S_QTGT + d] = 0.0
+        S[:, ABI.S_MAXIMP + d] = md.params['default_motor_impulse']
+    for d in md.finger_dofs:
+        S[:, ABI.S_KP + d] = md.params['finger_gain']
+        S[:, ABI.S_QTGT + d] = md.params['finger_target']
+        S[:, ABI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+    b = ABI.S_FREE + ABI.FB_WORDS
+    S[:, b:b + 3] = bowl
+    S[:, b + 3:b + 7] = G.quat_from_euler([np.pi / 2.0, 0, 0])
+    t = ABI.S_TASK
+    gi = np.array([0 if g == 'male' else 1 for g in gl])
+    hs = ABI.S_HUMAN + 7 * int(A['task_head_slot'])
+    mouth = np.where(gi[:, None] == 0, A['task_mouth_male'][None], A['task_mouth_female'][None])
+    S[:, t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = S[:, hs:hs + 3] + _qrot(S[:, hs + 3:hs + 7], mouth)
+    S[:, t + ABI.T_ALIVE] = (1 << 8) - 1
+    S[:, t + ABI.T_GENDER] = gi
+
+
+def place_tool_bodies(A, S, Q):
+    """Arm joints Q into S, the spoon on the tool frame (world_creation.py:332-343) and the food
+    spheres above it (feeding.py:291-308) -- what avr_reset_ik does on the device after its IK."""
     tool = int(A['task_tool_link'])
-    Q, ok = ik_batch(A, tool, tpos, tq, arm, lower, upper, rngs, q0)
     CP, CQ, _, _ = robot_fk_batch(A, Q)
     off = A['task_tool_offset']
-    meta = []
-    for k in range(N):
+    for k in range(len(S)):
         st = S[k]
         st[ABI.S_Q:ABI.S_Q + Q.shape[1]] = Q[k]
-        for d in arm:
-            st[ABI.S_KP + d] = 0.0
-            st[ABI.S_QTGT + d] = 0.0
-            st[ABI.S_MAXIMP + d] = md.params['default_motor_impulse']
-        for d in md.finger_dofs:
-            st[ABI.S_KP + d] = md.params['finger_gain']
-            st[ABI.S_QTGT + d] = md.params['finger_target']
-            st[ABI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
         sp, sq = G.tf_mul(CP[k, tool], CQ[k, tool], off[:3], off[3:])
         st[ABI.S_FREE:ABI.S_FREE + 3] = sp
         st[ABI.S_FREE + 3:ABI.S_FREE + 7] = sq
-        b = ABI.S_FREE + ABI.FB_WORDS
-        st[b:b + 3] = bowl[k]
-        st[b + 3:b + 7] = G.quat_from_euler([np.pi / 2.0, 0, 0])
         r = 0.005
         n = 0
         for i in range(2):
@@ -461,12 +681,17 @@ def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none
                     st[f:f + 3] = np.array([i * 2 * r - 0.005, j * 2 * r, kk * 2 * r + 0.02]) + sp
                     st[f + 3:f + 7] = [0, 0, 0, 1]
                     n += 1
-        t = ABI.S_TASK
-        gi = 0 if gl[k] == 'male' else 1
-        head = st[ABI.S_HUMAN + 7 * int(A['task_head_slot']):][:7]
-        mouth = A['task_mouth_male'] if gi == 0 else A['task_mouth_female']
-        st[t + ABI.T_TARGET:t + ABI.T_TARGET + 3] = G.tf_mul(head[:3], head[3:], mouth, [0, 0, 0, 1])[0]
-        st[t + ABI.T_ALIVE] = (1 << 8) - 1
-        st[t + ABI.T_GENDER] = gi
-        meta.append(dict(gender=gl[k], impairment=il[k], ik_ok=bool(ok[k]), bowl_pos=bowl[k], target_pos=tpos[k]))
+    return S
+
+
+def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none', episodes=None, stream='numpy'):
+    """Vectorised equivalent of batch_reset_states (same per-env draws and acceptance rules,
+    IK batched across envs).  episodes[k] selects the k-th env's episode stream (default 0);
+    stream: reset_inputs' draw stream."""
+    S, target7, init, q0, meta = reset_inputs(A, md, seed, env_ids, genders, impairment, episodes, vector_fk=False, stream=stream)
+    lower, upper = arm_limits(md)
+    Q, ok = ik_batch(A, int(A['task_tool_link']), target7[:, :3], target7[:, 3:], md.arm_dofs, lower, upper, init, q0)
+    place_tool_bodies(A, S, Q)
+    for k, m in enumerate(meta):
+        m['ik_ok'] = bool(ok[k])
     return S, meta

@@ -38,6 +38,10 @@
     int avr_get_q(avr_sim *s, float *q, float *qd);                                                                \
     int avr_get_link_pose(avr_sim *s, int32_t link, float *out7);                                                  \
     int avr_get_contact_summary(avr_sim *s, float *out4);                                                          \
+    int avr_get_flags(avr_sim *s, int32_t *flags);                                                                 \
+    int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init,      \
+                     int32_t restarts, int32_t iters, float tol, const float *keepout8, int32_t n_frames,           \
+                     float *host_obs, uint8_t *host_ok);                                                           \
     }
 
 AVR_TASK_DECLS(avr_feeding)
@@ -145,5 +149,10 @@ int avr_set_profile_buffer(avr_sim *s, void *p) { DISPATCH(s, avr_set_profile_bu
 int avr_get_q(avr_sim *s, float *q, float *qd) { DISPATCH(s, avr_get_q(h, q, qd)); }
 int avr_get_link_pose(avr_sim *s, int32_t link, float *o) { DISPATCH(s, avr_get_link_pose(h, link, o)); }
 int avr_get_contact_summary(avr_sim *s, float *o) { DISPATCH(s, avr_get_contact_summary(h, o)); }
+int avr_get_flags(avr_sim *s, int32_t *f) { DISPATCH(s, avr_get_flags(h, f)); }
+int avr_reset_ik(avr_sim *s, const uint8_t *m, const float *p, const float *t7, const float *init, int32_t r, int32_t it, float tol,
+                 const float *box8, int32_t n, float *o, uint8_t *ok) {
+    DISPATCH(s, avr_reset_ik(h, m, p, t7, init, r, it, tol, box8, n, o, ok));
+}
 
 }  // extern "C"

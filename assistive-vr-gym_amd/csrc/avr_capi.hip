@@ -42,6 +42,8 @@ struct avr_sim {
     long long kt_n[AVR_K_KINDS];
     float *d_query;                        // device scratch of the state queries (avr_get_*)
     size_t qcap;
+    float *d_ik;                           // device scratch of avr_reset_ik (targets, restart draws, ok bytes)
+    size_t ikcap;
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -469,6 +471,7 @@ int avr_destroy(avr_sim *s) {
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->d_mask) (void)hipFree(s->d_mask);
     if (s->d_query) (void)hipFree(s->d_query);
+    if (s->d_ik) (void)hipFree(s->d_ik);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     for (int i = 0; i < s->ngroups; i++) {
         if (s->gstream[i]) (void)hipStreamDestroy(s->gstream[i]);
@@ -702,4 +705,67 @@ int avr_get_contact_summary(avr_sim *s, float *out4) {
     HIPCHK(s, hipMemcpyAsync(out4, d, (size_t)4 * E * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
+}
+
+int avr_get_flags(avr_sim *s, int32_t *flags) {
+    CHECK_SIM(s);
+    if (!flags) return fail(s, -1, "avr_get_flags: flags is NULL");
+    const int E = s->cfg.n_envs;
+    float *d = nullptr;
+    if (query_buf(s, (size_t)E, &d)) return -3;
+    HIPCHK(s, avr_launch_get_flags(s->d_state, (int *)d, E, s->stream));
+    HIPCHK(s, hipMemcpyAsync(flags, d, (size_t)E * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ device reset IK
+int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, int32_t restarts, int32_t iters,
+                 float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
+    CHECK_SIM(s);
+#if AVR_TASK != AVR_TASK_FEEDING
+    (void)mask; (void)h; (void)target7; (void)init; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
+    return fail(s, -1, "avr_reset_ik: this task resets through avr_reset (host IK)");
+#else
+    const size_t E = (size_t)s->cfg.n_envs;
+    const int na = s->km.n_arm;
+    if (!h || !target7 || !init) return fail(s, -1, "avr_reset_ik: host_state, target7 and init must be given");
+    if (restarts < 1 || iters < 1 || n_frames < 0 || !(tol > 0.f)) return fail(s, -1, "avr_reset_ik: restarts, iters >= 1, n_frames >= 0, tol > 0");
+    if (na < 1 || na > 8) return fail(s, -1, "avr_reset_ik: %d arm DoFs (1..8 supported)", na);
+    std::vector<uint8_t> all;
+    if (!mask) { all.assign(E, 1); mask = all.data(); }
+    const size_t nt = E * 7, ni = E * (size_t)restarts * na, need = nt + ni + (E + 3) / 4;
+    if (need > s->ikcap) {
+        if (s->d_ik) HIPCHK(s, hipFree(s->d_ik));
+        s->d_ik = nullptr;
+        s->ikcap = 0;
+        HIPCHK(s, hipMalloc(&s->d_ik, need * sizeof(float)));
+        s->ikcap = need;
+    }
+    float *d_t = s->d_ik, *d_i = s->d_ik + nt;
+    unsigned char *d_ok = (unsigned char *)(s->d_ik + nt + ni);
+    if (upload_masked(s, mask, h)) return -2;
+    HIPCHK(s, hipMemcpyAsync(d_t, target7, nt * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(d_i, init, ni * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemsetAsync(d_ok, 0, E, s->stream));
+    HIPCHK(s, avr_launch_reset_ik(s->d_km, s->d_state, s->d_mask, d_t, d_i, restarts, iters, tol, keepout8, d_ok, (int)E, s->stream));
+    if (n_frames > 0) HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames));
+    std::vector<float> o;
+    if (host_obs) {
+        o.resize(E * K_OBS_DIM);
+        HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, E * K_OBS_DIM * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    }
+    std::vector<uint8_t> okh;
+    if (host_ok) {
+        okh.resize(E);
+        HIPCHK(s, hipMemcpyAsync(okh.data(), d_ok, E, hipMemcpyDeviceToHost, s->stream));
+    }
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    for (size_t e = 0; e < E; e++) {
+        if (!mask[e]) continue;
+        if (host_obs) memcpy(host_obs + e * K_OBS_DIM, o.data() + e * K_OBS_DIM, K_OBS_DIM * sizeof(float));
+        if (host_ok) host_ok[e] = okh[e];
+    }
+    return 0;
+#endif
 }

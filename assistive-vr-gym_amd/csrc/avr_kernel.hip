@@ -3466,6 +3466,18 @@ __global__ void avr_contact_summary_kernel(const KModel *__restrict__ mp, const 
     o[0] = (float)n; o[1] = all; o[2] = rh; o[3] = th;
 }
 
+// per-env health flags (T_FLAGS word: bit0 NaN / failed factorisation, bit1 contact pool full, ...)
+__global__ void avr_get_flags_kernel(const float *__restrict__ state, int *__restrict__ out, int n_envs) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n_envs) out[e] = (int)state[(size_t)e * K_STATE_WORDS + S_TASK + T_FLAGS];
+}
+
+hipError_t avr_launch_get_flags(const float *state, int *out, int n_envs, hipStream_t st) {
+    if (n_envs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_get_flags_kernel, dim3((n_envs + 255) / 256), dim3(256), 0, st, state, out, n_envs);
+    return hipGetLastError();
+}
+
 hipError_t avr_launch_get_q(const float *state, float *q, float *qd, int nd, int n_envs, hipStream_t st) {
     const int n = nd * n_envs;
     if (n <= 0) return hipSuccess;

@@ -1,0 +1,189 @@
+// avr_reset_ik.hip -- batched reset IK on the device (avr_reset_ik, include/avr.h).
+//
+// Restates the reset's inverse kinematics with random restarts (util.py:34-105
+// ik_random_restarts; feeding.py:276-278 for FeedingJaco: the tool link's COM frame to the
+// spoon-above-bowl target) as damped least squares, one 64-lane block per env:
+//   per restart r: the arm DoFs start from init[env][r] (the host draws them from the env's
+//   reset stream, so the restart sequence is the host reset's); `iters` DLS updates
+//     dq = J^T (J J^T + 1e-4 I)^-1 [p* - p; rot_err(q*, q)],  q <- clamp(q + dq, lower, upper)
+//   with an early exit at every 10th iteration once |dp| < 1e-5 and |rot_err| < 1e-4; accept
+//   when |p* - p| < tol, min |q* -+ q| < tol and no robot hull vertex lies inside the keep-out
+//   box (the reset's table screening, avr/reset.py table_clear); the last restart's result is
+//   kept when none is accepted.
+// The same rules as the host path's ik_batch (avr/reset.py) run on one env at a time; the host
+// path is the checker of this kernel (tests/test_reset_ik.py).
+// After the IK the task places the tool-attached free bodies (FeedingJaco: the spoon on the
+// tool frame, world_creation.py:330-343, and the food spheres above it, feeding.py:291-308).
+
+struct IkLDS {
+    float J[8][8];     // [arm column][6 rows] (+ pad)
+    float err[8];
+    float y[8];
+    float JJ[36];
+    float pe, qe;
+    int stop, clear;
+};
+
+// |J J^T + 1e-4 I| y = err by Cholesky (6 x 6, lane 0)
+AVR_DI void ik_solve6(const float *A_, const float *b, float *y) {
+    float Lm[36];
+    for (int i = 0; i < 6; i++)
+        for (int j = 0; j <= i; j++) {
+            float s = A_[6 * i + j];
+            for (int k = 0; k < j; k++) s -= Lm[6 * i + k] * Lm[6 * j + k];
+            Lm[6 * i + j] = i == j ? sqrtf(fmaxf(s, 1e-20f)) : s / Lm[6 * j + j];
+        }
+    float z[6];
+    for (int i = 0; i < 6; i++) {
+        float s = b[i];
+        for (int k = 0; k < i; k++) s -= Lm[6 * i + k] * z[k];
+        z[i] = s / Lm[6 * i + i];
+    }
+    for (int i = 5; i >= 0; i--) {
+        float s = z[i];
+        for (int k = i + 1; k < 6; k++) s -= Lm[6 * k + i] * y[k];
+        y[i] = s / Lm[6 * i + i];
+    }
+}
+
+// rotation error of q_cur towards q_tgt as a rotation vector (avr/reset.py _rot_err)
+AVR_DI v3 ik_rot_err(qt tgt, qt cur) {
+    qt d = qmul(tgt, qconj(cur));
+    if (d.w < 0.f) d = Q(-d.x, -d.y, -d.z, -d.w);
+    const float s = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    if (!(s > 1e-12f)) return V(0, 0, 0);
+    const float ang = 2.f * atan2f(s, d.w);
+    return scl(V(d.x, d.y, d.z), ang / s);
+}
+
+__global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const unsigned char *__restrict__ mask,
+                                                          const float *__restrict__ target, const float *__restrict__ init, int R, int iters, float tol,
+                                                          float4 box_c, float4 box_he, unsigned char *__restrict__ ok, int n_envs) {
+    __shared__ PairsLDS L;
+    __shared__ IkLDS K;
+    const int env = blockIdx.x;
+    if (env >= n_envs || !mask[env]) return;     // uniform over the block
+    const KModel &m = *mp;
+    const int lane = lane_id();
+    float *gst = state + (size_t)env * K_STATE_WORDS;
+    load_state(m, L, gst);
+    const int link = m.tool_link, na = m.n_arm;
+    const v3 tp = V(target[7 * env + 0], target[7 * env + 1], target[7 * env + 2]);
+    const qt tq = Q(target[7 * env + 3], target[7 * env + 4], target[7 * env + 5], target[7 * env + 6]);
+    // this lane's arm column: DoF, the link that owns it (if on the tool link's chain), limits
+    int cdof = -1, clink = -1;
+    float lo = 0.f, hi = 0.f;
+    if (lane < na) {
+        cdof = m.arm_dofs[lane];
+        const int l = m.dof_link[cdof];
+        clink = is_ancestor(m, link, l) ? l : -1;
+        lo = m.arm_lower[lane] > -1e9f ? m.arm_lower[lane] : -6.283185307179586f;
+        hi = m.arm_upper[lane] < 1e9f ? m.arm_upper[lane] : 6.283185307179586f;
+    }
+    bool accepted = false;
+    for (int r = 0; r < R; r++) {
+        if (lane < na) L.st[S_Q + cdof] = init[((size_t)env * R + r) * na + lane];
+        SYNC();
+        for (int it = 0; it < iters; it++) {
+            robot_fk(m, L);
+            const v3 cp = ld3(L.cm[link]);
+            if (lane == 0) {
+                const v3 ep = sub(tp, cp);
+                const v3 er = ik_rot_err(tq, ldq(L.cm[link] + 3));
+                K.err[0] = ep.x; K.err[1] = ep.y; K.err[2] = ep.z;
+                K.err[3] = er.x; K.err[4] = er.y; K.err[5] = er.z;
+                K.stop = (it % 10 == 9) && len(ep) < 1e-5f && len(er) < 1e-4f;
+            }
+            if (lane < na) {
+                float *c = K.J[lane];
+                if (clink >= 0) {
+                    const v3 ax = ld3(L.ax[clink]);
+                    st3(c, crs(ax, sub(cp, ld3(L.org[clink]))));
+                    st3(c + 3, ax);
+                } else {
+                    for (int i = 0; i < 6; i++) c[i] = 0.f;
+                }
+            }
+            SYNC();
+            if (K.stop) break;
+            if (lane < 36) {
+                const int i = lane / 6, j = lane - 6 * (lane / 6);
+                float s = i == j ? 1e-4f : 0.f;
+                for (int c = 0; c < na; c++) s += K.J[c][i] * K.J[c][j];
+                K.JJ[lane] = s;
+            }
+            SYNC();
+            if (lane == 0) ik_solve6(K.JJ, K.err, K.y);
+            SYNC();
+            if (lane < na) {
+                float dq = 0.f;
+                for (int i = 0; i < 6; i++) dq += K.J[lane][i] * K.y[i];
+                L.st[S_Q + cdof] = clampf(L.st[S_Q + cdof] + dq, lo, hi);
+            }
+            SYNC();
+        }
+        robot_fk(m, L);
+        if (lane == 0) {
+            const qt cq = ldq(L.cm[link] + 3);
+            K.pe = len(sub(tp, ld3(L.cm[link])));
+            const float d0 = sqrtf((tq.x - cq.x) * (tq.x - cq.x) + (tq.y - cq.y) * (tq.y - cq.y) + (tq.z - cq.z) * (tq.z - cq.z) + (tq.w - cq.w) * (tq.w - cq.w));
+            const float d1 = sqrtf((tq.x + cq.x) * (tq.x + cq.x) + (tq.y + cq.y) * (tq.y + cq.y) + (tq.z + cq.z) * (tq.z + cq.z) + (tq.w + cq.w) * (tq.w + cq.w));
+            K.qe = fminf(d0, d1);
+            K.clear = 1;
+        }
+        SYNC();
+        if (K.pe < tol && K.qe < tol) {
+            // keep-out screening: every hull vertex of every robot link outside the box
+            if (box_he.x >= 0.f) {
+                bool inside = false;
+                for (int b = 0; b < m.nb; b++) {
+                    if (m.body_kind[b] != AVR_BODY_ROBOT) continue;
+                    const tf lc = ldtf(L.cm[m.body_index[b]]);
+                    const int s0 = m.body_shape_start[b], s1 = s0 + m.body_shape_count[b];
+                    for (int s = s0; s < s1; s++) {
+                        if (m.shape_kind[s] != 3) continue;          // convex hulls
+                        const tf w = tfmul(lc, gldtf(m.shape_pose + 8 * s));
+                        const int v0 = m.shape_hull[4 * s], nv = m.shape_hull[4 * s + 1];
+                        for (int v = lane; v < nv; v += 64) {
+                            const float4 hv = m.hull_verts[v0 + v];
+                            const v3 p = tfpt(w, V(hv.x, hv.y, hv.z));
+                            inside |= fabsf(p.x - box_c.x) <= box_he.x && fabsf(p.y - box_c.y) <= box_he.y && fabsf(p.z - box_c.z) <= box_he.z;
+                        }
+                    }
+                }
+                if (inside) K.clear = 0;       // benign race: every writer stores 0
+            }
+            SYNC();
+            accepted = K.clear != 0;
+        }
+        if (accepted) break;
+    }
+    if (lane < na) gst[S_Q + cdof] = L.st[S_Q + cdof];
+    if (lane == 0) ok[env] = accepted ? 1 : 0;
+#if AVR_TASK == AVR_TASK_FEEDING
+    // spoon on the tool frame, food spheres of radius 0.005 stacked above it, all at rest
+    if (lane == 0) {
+        const tf sp = tfmul(ldtf(L.cm[link]), gldtf(m.tool_offset));
+        float *f = gst + S_FREE + AVR_FB_WORDS * m.spoon_free;
+        sttf(f, sp);
+        for (int k = 7; k < AVR_FB_WORDS; k++) f[k] = 0.f;
+        const float r = 0.005f;
+        for (int k = 0; k < m.n_food; k++) {
+            const int i = k >> 2, j = (k >> 1) & 1, kk = k & 1;
+            float *g = gst + S_FREE + AVR_FB_WORDS * (m.food_free0 + k);
+            st3(g, add(sp.p, V(i * 2 * r - 0.005f, j * 2 * r, kk * 2 * r + 0.02f)));
+            stq(g + 3, Q(0, 0, 0, 1));
+            for (int q = 7; q < AVR_FB_WORDS; q++) g[q] = 0.f;
+        }
+    }
+#endif
+}
+
+hipError_t avr_launch_reset_ik(const KModel *d_m, float *state, const unsigned char *mask, const float *target, const float *init, int R, int iters, float tol,
+                               const float *box8, unsigned char *ok, int n_envs, hipStream_t st) {
+    if (n_envs <= 0) return hipSuccess;
+    const float4 c = box8 ? make_float4(box8[0], box8[1], box8[2], 0.f) : make_float4(0, 0, 0, 0);
+    const float4 he = box8 ? make_float4(box8[4], box8[5], box8[6], 0.f) : make_float4(-1, -1, -1, 0);
+    hipLaunchKernelGGL(avr_reset_ik_kernel, dim3(n_envs), dim3(64), 0, st, d_m, state, mask, target, init, R, iters, tol, c, he, ok, n_envs);
+    return hipGetLastError();
+}

@@ -22,5 +22,6 @@ namespace AVR_NS {
 #include "avr_math.h"
 #include "avr_kmodel.h"
 #include "avr_kernel.hip"
+#include "avr_reset_ik.hip"
 #include "avr_capi.hip"
 }  // namespace AVR_NS

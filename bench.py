@@ -110,6 +110,66 @@ def pmc_summary(name, kernels, ms_per_step, E):
     return out
 
 
+def facade_bench(args):
+    """Trainer-side throughput: AVRTorchVecEnv.step with device actions, auto-reset on (every env
+    ends its episode at the 200-step TimeLimit, then resets: FeedingJaco with the device IK whose
+    host draws are prefetched while the previous episode steps).  Reports env-steps/s with the
+    rollovers inside the timed region and the same loop's rate between rollovers."""
+    import numpy as np
+    import torch
+    from avr import env as EV
+    E = args.envs
+    dev = torch.device('cuda', 0)
+    v = EV.AVRTorchVecEnv(args.task, E, device=0, impairment=args.impairment)
+    t0 = time.perf_counter()
+    v.reset()
+    torch.cuda.synchronize(dev)
+    t_reset = time.perf_counter() - t0
+    act = torch.empty(E, v.L.ACT_DIM, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1001)
+    for _ in range(args.warmup):
+        act.uniform_(-1, 1, generator=gen)
+        v.step(act)
+    torch.cuda.synchronize(dev)
+    roll, t_roll = 0, []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        act.uniform_(-1, 1, generator=gen)
+        ts = time.perf_counter()
+        _, _, _, info = v.step(act)
+        if 'terminal_observation' in info:     # (a rollover step synchronises inside step)
+            roll += 1
+            t_roll.append(time.perf_counter() - ts)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    # the same loop over steps that end no episode (synchronised at both ends, after the next
+    # episode's reset draws are ready so that no prefetch runs beside it)
+    if v._prefetch:
+        v._prefetch.wait()
+    K = max(1, min(100, v.max_steps - int(v.iteration.max()) - 1))
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for k in range(K):
+        act.uniform_(-1, 1, generator=gen)
+        v.step(act)
+    torch.cuda.synchronize(dev)
+    no_roll = (time.perf_counter() - t1) / K
+    out = {'metric': 'facade env-steps/sec (AVRTorchVecEnv, auto-reset at the 200-step TimeLimit)', 'value': E * args.steps / el,
+           'unit': 'env-steps/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3,
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'data': 'synthetic: torch uniform(-1, 1) actions on the device; resets drawn per env and episode',
+           'config': {'workload': args.task + ', %d envs, gym facade with rollover' % E, 'task': args.task, 'envs_per_gpu': E,
+                      'impairment': args.impairment, 'reset_ik': 'device' if v.device_ik else 'host'},
+           'rollovers_timed': roll, 'env_steps_per_s_between_rollovers': E / no_roll,
+           'rollover_ms': float(np.mean(t_roll) * 1e3) if roll else None, 'first_reset_s': t_reset,
+           'ik_accept_rate': float(v.last_ik_ok.mean()) if v.last_ik_ok is not None else None,
+           'last_rollover_breakdown_s': v.reset_timing,
+           'flagged_envs': int(np.count_nonzero(v.flags()))}
+    print(json.dumps(out), flush=True)
+    v.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--task', default='FeedingJaco-v0', choices=sorted(TASKS))
@@ -123,9 +183,14 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--reset-pool', type=int, default=None,
                     help='distinct host reset states, tiled over the envs (IK is host-side; FeedingJaco 1024, ScratchItch 128)')
+    ap.add_argument('--facade', action='store_true',
+                    help='time the gym facade (avr.env.AVRTorchVecEnv: device tensors, TimeLimit 200 with auto-reset) '
+                         'instead of the bare step; --steps should span rollovers (e.g. 600)')
     ap.add_argument('--impairment', default='random',
                     help="human impairment per env: 'random' is the tasks' own setting (feeding.py:175, scratch_itch.py:178)")
     args = ap.parse_args()
+    if args.facade:
+        return facade_bench(args)
     T = TASKS[args.task]
     settle = T['settle'] if args.settle is None else args.settle
 

@@ -132,7 +132,29 @@ int avr_get_link_pose(avr_sim *sim, int32_t link, float *out7);
  *   the sums p.getContactPoints(...)[9] feeds to get_total_force (feeding.py:83-90,
  *   scratch_itch.py:84-102). */
 int avr_get_contact_summary(avr_sim *sim, float *out4);
+/* avr_get_flags: per-env health flags, flags[n_envs] (bit0 NaN / failed mass-matrix
+ *   factorisation, bit1 contact pool full, bit2 AABB pair list full, bit3 shape pair list full,
+ *   bit4 non-contact row buffer full); 0 = healthy.  No reference counterpart (PyBullet has no
+ *   such report); a vectorised trainer polls it instead of the whole state block. */
+int avr_get_flags(avr_sim *sim, int32_t *flags);
 const char *avr_last_error(avr_sim *sim);
+
+/* ---- device reset (FeedingJaco) ----
+ * avr_reset_ik: avr_reset with the reset's inverse kinematics on the device.  Replaces the IK of
+ *   FeedingEnv.reset (feeding.py:276-278 -> util.py:34-105 ik_random_restarts) for the masked envs:
+ *   host_state rows carry everything the host reset draws (human pose, bowl, impairment, motors;
+ *   the arm's joints are overwritten); target7[n_envs*7] is the tool link's COM-frame target
+ *   (position, quaternion); init[n_envs*restarts*n_arm] the arm's starting joints of every
+ *   restart (drawn by the host from the env's reset stream).  Per env, restarts run in order
+ *   with `iters` damped-least-squares updates each until one lands within `tol` (position, m, and
+ *   quaternion distance) with no robot hull vertex inside the keep-out box keepout8 = {center xyz,
+ *   pad, half extents xyz, pad} (NULL: no screening); else the last restart's joints are kept.
+ *   The spoon and the food are then placed on the tool frame (world_creation.py:330-343,
+ *   feeding.py:291-308) and n_frames settle frames run (feeding.py:319-320), as in avr_reset.
+ *   host_ok[n_envs] (may be NULL) receives 1 where a restart was accepted.  Returns -1 for tasks
+ *   other than FeedingJaco. */
+int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state, const float *target7, const float *init, int32_t restarts,
+                 int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok);
 
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
  * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times

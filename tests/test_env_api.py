@@ -12,14 +12,15 @@ def test_registry_has_every_reference_id():
     # ids registered by assistive_gym/__init__.py (49 ids: 4 tasks x {PR2, Jaco} x 6 variants + HumanTesting)
     assert len(E.REGISTRY) == 49
     assert E.REGISTRY['FeedingJaco-v0'] == ('feeding', 'jaco', True)
-    assert sum(v[2] for v in E.REGISTRY.values()) == 1
+    assert E.REGISTRY['ScratchItchPR2-v0'] == ('scratch_itch', 'pr2', True)
+    assert sum(v[2] for v in E.REGISTRY.values()) == 2
     for k in E.REGISTRY:
         assert re.match(r'^[A-Za-z0-9]+-v0$', k)
 
 
 def test_unbuilt_ids_raise_not_implemented():
     with pytest.raises(NotImplementedError):
-        E.AVRVecEnv('ScratchItchPR2-v0', 4)
+        E.AVRVecEnv('BedBathingPR2-v0', 4)
     with pytest.raises(KeyError):
         E.AVRVecEnv('NoSuchEnv-v0', 4)
 
@@ -34,8 +35,19 @@ def test_spaces():
 
 def test_constants_follow_reference():
     assert E.MAX_EPISODE_STEPS == 200      # TimeLimit in assistive_gym/__init__.py
-    assert E.SETTLE_FRAMES == 100          # feeding.py:318-320
+    assert E.SETTLE_FRAMES[ABI.TASK_FEEDING] == 100    # feeding.py:318-320
+    assert E.SETTLE_FRAMES[ABI.TASK_SCRATCH] == 0      # scratch_itch.py reset: no settle frames
     P = ABI.FEEDING_PARAMS
     assert P['num_sub_steps'] == 2 and P['solver_iterations'] == 10    # feeding.py:289
     assert P['time_step'] == 0.02                                      # world_creation.py:75
     assert P['frame_skip'] == 5
+
+
+def test_prefetch_returns_only_the_matching_key():
+    calls = []
+    p = E._Prefetch(lambda a, b: calls.append((a, b)) or (a, b))
+    p.start(('k', 1), 3, 4)
+    assert p.take(('k', 2)) is None        # a different key is never handed out
+    p.start(('k', 1), 3, 4)
+    assert p.take(('k', 1)) == (3, 4)
+    assert p.take(('k', 1)) is None        # taken once

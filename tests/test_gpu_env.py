@@ -53,3 +53,78 @@ def test_observation_layout():
     tgt = St[:, ABI.S_TASK + ABI.T_TARGET:ABI.S_TASK + ABI.T_TARGET + 3]
     assert np.allclose(o[:, 7:10], sp - tgt, atol=1e-5)
     v.close()
+
+
+def test_device_reset_ik_and_prefetch_over_two_rollovers():
+    """Auto-reset with the device IK twice in a row: the second rollover uses the prefetched draws
+    of episode 2, which equal a fresh reset_inputs of that episode (same states as computed
+    synchronously)."""
+    from avr import env as E, _lib, _abi as ABI, reset as RS
+    n = 16
+    v = E.AVRVecEnv('FeedingJaco-v0', n)
+    v.reset()
+    assert v.last_ik_ok.mean() > 0.8
+    for ep in range(2):
+        for t in range(E.MAX_EPISODE_STEPS):
+            o, r, d, info = v.step(_lib.random_actions(1001, np.arange(n), ep * 1000 + t))
+        assert d.all() and np.all(v.episode == ep + 1)
+    St = v.get_state()
+    Si, t7, init, q0, meta = RS.reset_inputs(v.A, v.md, v.seed, list(range(n)), impairment='random', episodes=[2] * n, stream='philox')
+    # the human / bowl / task words of episode 2 are the host draws (before the settle moved nothing static)
+    H = slice(ABI.S_HUMAN, ABI.S_HUMAN + 7 * 4)
+    static = [m['impairment'] != 'tremor' for m in meta]
+    assert np.allclose(St[static, H], Si[static, H], atol=1e-5)
+    assert np.all(v.flags() == 0)
+    v.close()
+
+
+def test_torch_vec_env_matches_host_vec_env():
+    import torch
+    from avr import env as E, _lib
+    n = 8
+    h = E.AVRVecEnv('FeedingJaco-v0', n, auto_reset=False)
+    g = E.AVRTorchVecEnv('FeedingJaco-v0', n, auto_reset=False)
+    oh = h.reset()
+    og = g.reset()
+    assert isinstance(og, torch.Tensor) and og.is_cuda
+    np.testing.assert_array_equal(oh, og.cpu().numpy())
+    for t in range(5):
+        a = _lib.random_actions(1001, np.arange(n), t)
+        xh = h.step(a)
+        xg = g.step(torch.from_numpy(a).cuda())
+        assert np.array_equal(xg[2].cpu().numpy(), g.iteration >= g.max_steps)
+        np.testing.assert_array_equal(xh[0], xg[0].cpu().numpy())
+        np.testing.assert_array_equal(xh[1], xg[1].cpu().numpy())
+        np.testing.assert_array_equal(xh[3]['total_force_on_human'], xg[3]['total_force_on_human'].cpu().numpy())
+    h.close(); g.close()
+
+
+def test_scratch_itch_facade():
+    from avr import env as E
+    e = E.make('ScratchItchPR2-v0')
+    o = e.reset()
+    assert o.shape == (30,) and np.all(np.isfinite(o))
+    o, r, d, info = e.step(e.action_space.sample(np.random.default_rng(0)))
+    assert o.shape == (30,) and info['obs_robot_len'] == 30 and info['action_robot_len'] == 7
+    assert np.isfinite(r) and not d
+    e.close()
+
+
+def test_torch_vec_env_rollover_follows_device_done():
+    """The host iteration mirror decides rollovers: at step 200 the device's done is set for every
+    env, the terminal observation is the pre-reset one and the returned obs is the reset's."""
+    import torch
+    from avr import env as E
+    n = 8
+    g = E.AVRTorchVecEnv('FeedingJaco-v0', n)
+    g.reset()
+    gen = torch.Generator(device='cuda'); gen.manual_seed(3)
+    a = torch.empty(n, 7, device='cuda')
+    for t in range(E.MAX_EPISODE_STEPS):
+        a.uniform_(-1, 1, generator=gen)
+        o, r, d, info = g.step(a)
+        assert bool(d.all()) == (t == E.MAX_EPISODE_STEPS - 1) and bool(d.any()) == bool(d.all())
+    assert 'terminal_observation' in info and not torch.equal(info['terminal_observation'], o)
+    assert np.all(g.iteration == 0) and np.all(g.episode == 1)
+    np.testing.assert_array_equal(o.cpu().numpy(), g._obs)
+    g.close()
