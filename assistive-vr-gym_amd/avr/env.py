@@ -198,6 +198,10 @@ class AVRVecEnv:
         self.sim = _lib.Sim(self.md, self.n, device=device, seed=self.seed, env_offset=self.env_offset)
         self.observation_space = Box(-1e9, 1e9, (self.L.OBS_DIM,))
         self.action_space = Box(-1.0, 1.0, (self.L.ACT_DIM,))
+        self.obs_robot_len, self.obs_human_len = self.L.OBS_DIM, 0
+        self.action_robot_len, self.action_human_len = self.L.ACT_DIM, 0
+        self.genders = None                # setup(): fixed gender for every reset
+        self.participant, self.policy_name = -1, ''
         self.episode = np.zeros(self.n, np.int64)
         # host mirror of the per-env iteration counters: the kernels' done is exactly
         # T_ITER >= max_steps (TimeLimit), so rollovers are known without reading the device
@@ -209,9 +213,31 @@ class AVRVecEnv:
         self.last_ik_ok = None
         self.reset_timing = None
 
+    # ------------------------------------------------------------------ setup hook
+    def setup(self, gender, participant, policy_name, hipbone_to_mouth_height=None):
+        """FeedingEnv.setup / ScratchItchEnv.setup (feeding.py:20-28): the evaluation harness fixes
+        the participant's gender (every later reset uses it) and names the policy.  The compiled
+        human has the reference's default proportions (hipbone_to_mouth_height 0.6 male / 0.54
+        female, human_creation.py:60-63); other heights are a VR-calibration feature this build
+        does not model."""
+        default = 0.6 if gender == 'male' else 0.54
+        if gender not in ('male', 'female'):
+            raise ValueError('gender must be male or female')
+        if hipbone_to_mouth_height is not None and abs(float(hipbone_to_mouth_height) - default) > 1e-9:
+            raise NotImplementedError('hipbone_to_mouth_height %.3f: only the default %.2f (%s) is compiled'
+                                      % (hipbone_to_mouth_height, default, gender))
+        self.genders = gender
+        self.participant, self.policy_name = int(participant), str(policy_name)
+        if self._prefetch:
+            self._prefetch.wait()
+            self._prefetch.key = None      # draws prepared before setup() are for the old genders
+
+    def _genders(self, idx):
+        return None if self.genders is None else [self.genders] * len(idx)
+
     # ------------------------------------------------------------------ reset
     def _inputs(self, idx, episodes):
-        return RS.reset_inputs(self.A, self.md, self.seed, [self.env_offset + int(i) for i in idx],
+        return RS.reset_inputs(self.A, self.md, self.seed, [self.env_offset + int(i) for i in idx], genders=self._genders(idx),
                                impairment=self.impairment, episodes=list(episodes), stream=self.reset_stream)
 
     def _reset_rows(self, mask):
@@ -244,10 +270,10 @@ class AVRVecEnv:
         ids = [self.env_offset + int(i) for i in idx]
         if self.task == ABI.TASK_SCRATCH:
             from . import reset_scratch as RSS
-            Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, impairment=self.impairment, episodes=eps,
+            Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
                                            attempts=self.scratch_attempts, iters=self.scratch_iters)
         else:
-            Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, impairment=self.impairment, episodes=eps,
+            Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
                                                stream=self.reset_stream)
         S[idx] = Si
         self.sim.reset(mask.astype(np.uint8), S, frames, self._obs)
@@ -283,6 +309,12 @@ class AVRVecEnv:
             self._reset_rows(done)
             obs = self._obs.copy()
         return obs, rew, done, info
+
+    def observe(self):
+        """Observation of the current state without stepping (what _get_obs returns right after
+        p.restoreState, feeding.py:322-325)."""
+        self._obs[:] = self.sim.settle(0)
+        return self._obs.copy()
 
     def flags(self):
         """Per-env health flags (include/avr.h avr_get_flags; 0 = healthy), without copying the state."""

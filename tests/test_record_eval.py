@@ -1,0 +1,134 @@
+"""Record / replay (the .bullet + setup.pkl + actions.pkl flow, avr/record.py) and the policy
+evaluation harness (enjoy_vr.py's contract, avr/policy_eval.py)."""
+import json
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from avr import _abi as ABI
+from avr import policy_eval as PE
+from avr import record as R
+
+
+# ------------------------------------------------------------------ CPU
+class _FakeSim:
+    def __init__(self, task, n):
+        self.md = SimpleNamespace(task=task)
+        self.n = n
+        self.words = ABI.LAYOUTS[task].STATE_WORDS
+        self.S = np.arange(n * self.words, dtype=np.float32).reshape(n, self.words)
+
+    def get_state(self):
+        return self.S.copy()
+
+    def set_state(self, S):
+        self.S = np.array(S, np.float32)
+
+
+def test_state_snapshot_round_trip_and_layout_checks(tmp_path):
+    a = _FakeSim(ABI.TASK_FEEDING, 3)
+    p = str(tmp_path / 's.npz')
+    R.save_state(p, a)
+    b = _FakeSim(ABI.TASK_FEEDING, 3)
+    b.S[:] = 0
+    R.load_state(p, b)
+    np.testing.assert_array_equal(a.S, b.S)
+    with pytest.raises(ValueError):
+        R.load_state(p, _FakeSim(ABI.TASK_SCRATCH, 3))      # other task / layout
+    with pytest.raises(ValueError):
+        R.load_state(p, _FakeSim(ABI.TASK_FEEDING, 4))      # other env count
+
+
+def test_running_mean_std_matches_batch_statistics():
+    rng = np.random.default_rng(0)
+    x = rng.normal(2.0, 3.0, size=(500, 5))
+    r = PE.RunningMeanStd((5,), count=0.0 + 1e-12)
+    for k in range(0, 500, 37):
+        r.update(x[k:k + 37])
+    np.testing.assert_allclose(r.mean, x.mean(0), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(r.var, x.var(0), rtol=1e-6)
+
+
+def test_normalize_is_vecnormalize_eval():
+    rms = PE.RunningMeanStd((3,), mean=[1.0, 0.0, -1.0], var=[4.0, 1e-12, 1.0])
+    o = torch.tensor([[3.0, 1.0, -1.0]])
+    n = PE.normalize(o, rms)
+    np.testing.assert_allclose(n.numpy(), [[1.0, 10.0, 0.0]], rtol=1e-5)     # clipped at +-10
+
+
+def test_policy_checkpoint_round_trip(tmp_path):
+    torch.manual_seed(0)
+    pol = PE.ActorCritic(25, 7)
+    rms = PE.RunningMeanStd((25,), mean=np.linspace(0, 1, 25), var=np.linspace(1, 2, 25), count=7.0)
+    p = str(tmp_path / 'FeedingJaco-v0.pt')
+    PE.save_policy(p, pol, rms)
+    pol2, rms2 = PE.load_policy(p)
+    o = torch.randn(4, 25)
+    h, m = torch.zeros(4, 1), torch.zeros(4, 1)
+    v1, a1, _, _ = pol.act(o, h, m, deterministic=True)
+    v2, a2, _, _ = pol2.act(o, h, m, deterministic=True)
+    assert torch.equal(a1, a2) and torch.equal(v1, v2) and a1.shape == (4, 7) and v1.shape == (4, 1)
+    np.testing.assert_array_equal(rms2.mean, rms.mean)
+    assert rms2.count == 7.0
+
+
+def test_setup_rejects_uncompiled_heights():
+    from avr import env as E
+    v = object.__new__(E.AVRVecEnv)
+    v._prefetch = None
+    with pytest.raises(NotImplementedError):
+        E.AVRVecEnv.setup(v, 'female', 3, 'Static', 0.60)
+    E.AVRVecEnv.setup(v, 'female', 3, 'Static', 0.54)
+    assert v.genders == 'female' and v.participant == 3
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_record_then_replay_is_bit_identical(tmp_path):
+    from avr import env as E, _lib
+    n = 4
+    env = E.AVRVecEnv('FeedingJaco-v0', n, auto_reset=False, prefetch=False)
+    rec = R.Recorder(env, str(tmp_path / 'rec'))
+    o0 = rec.reset()
+    obs, rews = [o0], []
+    for t in range(15):
+        o, r, d, info = rec.step(_lib.random_actions(1001, np.arange(n), t))
+        obs.append(o); rews.append(r)
+    rec.close()
+    snap = str(tmp_path / 'frame_0.npz')
+    R.save_state(snap, env)
+    env.close()
+    setup = json.load(open(tmp_path / 'rec' / 'setup.json'))
+    assert setup['env_id'] == 'FeedingJaco-v0' and len(setup['gender']) == n
+    rp = R.ReplayEnv(str(tmp_path / 'rec'))
+    np.testing.assert_array_equal(rp.reset(), o0)
+    for t in range(15):
+        o, r, d, info = rp.step(None)
+        np.testing.assert_array_equal(o, obs[t + 1])
+        np.testing.assert_array_equal(r, rews[t])
+        assert d.all() == (t == 14)
+    assert rp.mismatch == []
+    R.load_state(snap, rp.env)               # a snapshot restores into a fresh handle
+    np.testing.assert_array_equal(rp.env.get_state(), np.load(tmp_path / 'rec' / 'states.npy')[-1])
+    rp.close()
+    res = R.savemeta(str(tmp_path / 'rec*'))
+    (d, v), = res.items()
+    assert v['rewards'].shape == (15, n) and v['replay_mismatch'] == []
+
+
+@pytest.mark.gpu
+def test_policy_evaluation_harness(tmp_path):
+    torch.manual_seed(1)
+    pol = PE.ActorCritic(25, 7)
+    rms = PE.RunningMeanStd((25,))
+    p = str(tmp_path / 'FeedingJaco-v0.pt')
+    PE.save_policy(p, pol, rms)
+    pol, rms = PE.load_policy(p)
+    a = PE.evaluate('FeedingJaco-v0', pol, rms, n_envs=16, steps=200, setup=dict(gender='female', participant=2, policy_name='Static'))
+    b = PE.evaluate('FeedingJaco-v0', pol, rms, n_envs=16, steps=200, setup=dict(gender='female', participant=2, policy_name='Static'))
+    assert np.all(np.isfinite(a['returns'])) and a['done'].all()
+    np.testing.assert_array_equal(a['returns'], b['returns'])          # deterministic policy, same reset streams
+    assert a['task_success'].shape == (16,)
