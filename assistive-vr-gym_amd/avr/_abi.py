@@ -11,8 +11,8 @@ import numpy as np
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # ---- capacities / offsets (must match include/avr_model.h) ----
-ABI_VERSION = 3
-TASK_FEEDING, TASK_SCRATCH = 0, 1
+ABI_VERSION = 4
+TASK_FEEDING, TASK_SCRATCH, TASK_BEDBATH = 0, 1, 2
 DESC_HC = 8                               # avr_model_desc hc_* capacity
 BODY_ROBOT, BODY_FREE, BODY_STATIC, BODY_HUMAN, BODY_RSTATIC = 0, 1, 2, 3, 4
 # FeedingJaco-v0 layout (module-level names; the ScratchItchPR2-v0 layout is `SI` below)
@@ -49,9 +49,9 @@ FEEDING = _Layout(TASK=TASK_FEEDING, MAX_LINKS=MAX_LINKS, MAX_DOF=MAX_DOF, MAX_F
                   STATE_WORDS=STATE_WORDS)
 
 
-def _scratch_layout():
-    L = dict(TASK=TASK_SCRATCH, MAX_LINKS=32, MAX_DOF=24, HC_N=8, MAX_FREE=1, MAX_HUMAN=20, MAX_CONTACTS=64,
-             ACT_DIM=7, OBS_DIM=30, INFO_DIM=2)
+def _scratch_layout(task=TASK_SCRATCH):
+    L = dict(TASK=task, MAX_LINKS=32, MAX_DOF=24, HC_N=8, MAX_FREE=1, MAX_HUMAN=20, MAX_CONTACTS=64,
+             ACT_DIM=7, OBS_DIM=30 if task == TASK_SCRATCH else 24, INFO_DIM=2)
     L['S_Q'] = 0
     L['S_QD'] = L['S_Q'] + L['MAX_DOF']
     L['S_QTGT'] = L['S_QD'] + L['MAX_DOF']
@@ -66,11 +66,14 @@ def _scratch_layout():
     L['S_HCH'] = L['S_HUMAN'] + L['MAX_HUMAN'] * 7      # [HC_N] targets, tremors, lower, upper limits
     L['S_CP'] = L['S_HCH'] + 4 * L['HC_N']
     L['STATE_WORDS'] = L['S_CP'] + L['MAX_CONTACTS'] * CP_WORDS
+    if task == TASK_BEDBATH:            # BedBathingPR2: the wipe-target bit set and the target count
+        L.update(T_WIPE=17, T_NTGT=23, MAX_TARGETS=160)
     return _Layout(**L)
 
 
 SI = _scratch_layout()
-LAYOUTS = {TASK_FEEDING: FEEDING, TASK_SCRATCH: SI}
+BB = _scratch_layout(TASK_BEDBATH)
+LAYOUTS = {TASK_FEEDING: FEEDING, TASK_SCRATCH: SI, TASK_BEDBATH: BB}
 
 PI32 = C.POINTER(C.c_int32)
 PF64 = C.POINTER(C.c_double)
@@ -136,6 +139,9 @@ class avr_model_desc(C.Structure):
         ('torso_com', C.c_double * 3), ('tool_handle_shapes', C.c_int32),
         ('w_tool_force', C.c_double), ('w_scratch', C.c_double),
         ('robot_gravity', C.c_double * 3),
+        # ABI 4
+        ('bb_targets', PF64), ('bb_ntgt', (C.c_int32 * 2) * 2), ('bb_limb_slots', C.c_int32 * 2),
+        ('bb_joint_slots', C.c_int32 * 3), ('w_wipe', C.c_double), ('closest_distance', C.c_double),
     ]
 
 
@@ -194,7 +200,25 @@ SCRATCH_PARAMS = dict(
     reactive_force=1.0,          # scratch_itch.py:263 human_reactive_force (x human_strength)
 )
 
-SCENES = {TASK_FEEDING: 'feeding_jaco', TASK_SCRATCH: 'scratch_itch_pr2'}
+# BedBathingPR2 physics / task constants
+BEDBATH_PARAMS = dict(SCRATCH_PARAMS)
+BEDBATH_PARAMS.update(
+    solver_iterations=50,        # bed_bathing.py:338 (numSubSteps=0, numSolverIterations=50)
+    robot_gain=0.05,             # config.ini:14 (bed_bathing robot_gains)
+    robot_force=1.0,             # config.ini:13
+    finger_target=0.2,           # bed_bathing.py:319 set_gripper_open_position(position=0.2)
+    w_distance=1.0, w_action=0.01,                                   # config.ini:15-16
+    w_tool_force=0.0, w_scratch=0.0,
+    w_wipe=5.0,                  # config.ini:17 wiping_reward_weight
+    task_success_threshold=0.3,  # config.ini:18 (x total_target_count, bed_bathing.py:70)
+    human_gain=0.05,             # bed_bathing.py:46 take_step(..., human_gains=0.05) (no tremor: impairment 'none')
+    closest_distance=4.0,        # bed_bathing.py:61 getClosestPoints(..., distance=4.0)
+    settle_motor_force=0.1,      # world_creation.py:164-166: bed_bathing human joints VELOCITY_CONTROL force 0.1 (reset settle)
+    settle_frames=100,           # bed_bathing.py:288-289
+)
+HOST_ONLY_PARAMS = ('reactive_gain', 'reactive_force', 'settle_motor_force', 'settle_frames')
+
+SCENES = {TASK_FEEDING: 'feeding_jaco', TASK_SCRATCH: 'scratch_itch_pr2', TASK_BEDBATH: 'bed_bathing_pr2'}
 
 
 def load_scene(name='feeding_jaco'):
@@ -204,6 +228,8 @@ def load_scene(name='feeding_jaco'):
 
 
 def scene_task(A):
+    if 'bb_targets' in A:
+        return TASK_BEDBATH
     return TASK_SCRATCH if 'n_rstatic' in A else TASK_FEEDING
 
 
@@ -212,7 +238,7 @@ class ModelDesc:
 
     def __init__(self, A, params=None):
         task = scene_task(A)
-        P = dict(SCRATCH_PARAMS if task == TASK_SCRATCH else FEEDING_PARAMS)
+        P = dict({TASK_SCRATCH: SCRATCH_PARAMS, TASK_BEDBATH: BEDBATH_PARAMS}.get(task, FEEDING_PARAMS))
         if params:
             P.update(params)
         self.task = task
@@ -273,12 +299,12 @@ class ModelDesc:
             d.torso_link = int(A['task_torso_link'])
             d.head_slot = int(A['task_head_slot'])
         d.task = task
-        if task == TASK_SCRATCH:
+        if task in (TASK_SCRATCH, TASK_BEDBATH):
             d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, -1, -1, 0
             d.table_body = d.bowl_body = d.food_body0 = -1
             d.spoon_body = int(A['task_tool_body'])
             d.n_rstatic = int(A['n_rstatic'])
-            d.human_gravity[2] = -1.0                    # scratch_itch.py:260
+            d.human_gravity[2] = -1.0                    # scratch_itch.py:260; bed_bathing.py:286 (the reset settle)
             for i in range(3):
                 d.fix_pivot_b[i] = float(A['task_tool_pivot'][i])
                 d.tool_tip[i] = float(A['task_tool_tip'][i])
@@ -286,6 +312,15 @@ class ModelDesc:
             d.tool_handle_shapes = int(A['task_tool_handle_shapes'])
             d.torso_link = -1
             d.head_slot = -1
+            if task == TASK_BEDBATH:
+                d.bb_targets = arr('bb_targets', np.float64)
+                for g in range(2):
+                    for l in range(2):
+                        d.bb_ntgt[g][l] = int(A['bb_ntgt'][g][l])
+                for i in range(2):
+                    d.bb_limb_slots[i] = int(A['bb_limb_slots'][i])
+                for i in range(3):
+                    d.bb_joint_slots[i] = int(A['bb_joint_slots'][i])
         else:
             d.spoon_free, d.bowl_free, d.food_free0, d.n_food = 0, 1, 2, 8
             d.table_body = int(A['task_table_body'])
@@ -328,7 +363,7 @@ class ModelDesc:
                         d.hc_jpos[g][k][i] = float(A['hc_jpos'][g][k][i])
                         d.hc_inertia[g][k][i] = float(A['hc_inertia'][g][k][i])
         for k, v in P.items():
-            if k in ('reactive_gain', 'reactive_force'):
+            if k in HOST_ONLY_PARAMS:
                 continue
             if k == 'robot_gravity':
                 for i in range(3):

@@ -31,7 +31,9 @@ from . import _lib
 from . import reset as RS
 
 MAX_EPISODE_STEPS = 200          # assistive_gym/__init__.py TimeLimit
-SETTLE_FRAMES = {ABI.TASK_FEEDING: 100, ABI.TASK_SCRATCH: 0}    # feeding.py:318-320; scratch_itch.py has none
+# settle frames after the reset state is in place: feeding.py:318-320; scratch_itch.py has none;
+# bed_bathing.py's 100-frame arm settle (:288-289) comes before the robot is placed (reset_bedbath)
+SETTLE_FRAMES = {ABI.TASK_FEEDING: 100, ABI.TASK_SCRATCH: 0, ABI.TASK_BEDBATH: 0}
 
 
 class Box:
@@ -56,8 +58,8 @@ class Box:
 
 
 # id -> (task, robot, implemented): every id the reference registers (assistive_gym/__init__.py);
-# this build implements FeedingJaco-v0 and ScratchItchPR2-v0, the rest raise
-# NotImplementedError.
+# this build implements FeedingJaco-v0, ScratchItchPR2-v0 and BedBathingPR2-v0, the
+# rest raise NotImplementedError.
 REGISTRY = {
     'HumanTesting-v0':           ('human_testing', '-', False),
     'ScratchItchPR2-v0':         ('scratch_itch', 'pr2', True),
@@ -72,7 +74,7 @@ REGISTRY = {
     'ScratchItchVRJacoHuman-v0': ('scratch_itch', 'jaco', False),
     'ScratchItchVRPR2New-v0':    ('scratch_itch', 'pr2', False),
     'ScratchItchVRJacoNew-v0':   ('scratch_itch', 'jaco', False),
-    'BedBathingPR2-v0':          ('bed_bathing', 'pr2', False),
+    'BedBathingPR2-v0':          ('bed_bathing', 'pr2', True),
     'BedBathingJaco-v0':         ('bed_bathing', 'jaco', False),
     'BedBathingPR2Human-v0':     ('bed_bathing', 'pr2', False),
     'BedBathingJacoHuman-v0':    ('bed_bathing', 'jaco', False),
@@ -111,7 +113,7 @@ REGISTRY = {
 }
 
 _SCENES = {}
-_TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH}
+_TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH, 'bed_bathing': ABI.TASK_BEDBATH}
 
 
 def _scene(task):
@@ -182,7 +184,7 @@ class AVRVecEnv:
             raise KeyError('unknown env id %r' % env_id)
         task, robot, ok = REGISTRY[env_id]
         if not ok:
-            raise NotImplementedError('%s: only FeedingJaco-v0 and ScratchItchPR2-v0 are built (SURVEY 8)' % env_id)
+            raise NotImplementedError('%s: only FeedingJaco-v0, ScratchItchPR2-v0 and BedBathingPR2-v0 are built (SURVEY 8)' % env_id)
         self.env_id = env_id
         self.n = int(n_envs)
         self.seed = int(seed)
@@ -195,6 +197,7 @@ class AVRVecEnv:
         self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'
         self.scratch_attempts, self.scratch_iters = scratch_attempts, scratch_iters
         self.reset_stream = reset_stream
+        self.device = device
         self.sim = _lib.Sim(self.md, self.n, device=device, seed=self.seed, env_offset=self.env_offset)
         self.observation_space = Box(-1e9, 1e9, (self.L.OBS_DIM,))
         self.action_space = Box(-1.0, 1.0, (self.L.ACT_DIM,))
@@ -268,7 +271,11 @@ class AVRVecEnv:
                 self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
             return
         ids = [self.env_offset + int(i) for i in idx]
-        if self.task == ABI.TASK_SCRATCH:
+        if self.task == ABI.TASK_BEDBATH:
+            from . import reset_bedbath as RBB
+            Si, _ = RBB.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=eps,
+                                           attempts=self.scratch_attempts, iters=self.scratch_iters, device=self.device)
+        elif self.task == ABI.TASK_SCRATCH:
             from . import reset_scratch as RSS
             Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
                                            attempts=self.scratch_attempts, iters=self.scratch_iters)

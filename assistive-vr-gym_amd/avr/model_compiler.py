@@ -780,15 +780,16 @@ def build_pr2():
     return rob, groups, torso_com, sub
 
 
-def build_scratcher():
-    """tool_scratch.urdf (world_creation.py:344): handle (base) + tool cylinder + tip sphere,
-    welded by fixed joints, loaded without URDF_USE_INERTIA_FROM_FILE (inertia per link from its
-    collision AABB).  A floating base with only fixed links moves as one rigid body: the three
-    links are composed into one free body at the composite COM, axes those of the handle (every
-    link's principal axes are the handle's).  Returns the body plus the offsets, in that body
-    frame, of the handle origin (the fixed constraint's child pivot, world_creation.py:363) and of
-    tool link 1's COM (getLinkState(tool, 1), scratch_itch.py:51,106)."""
-    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, 'scratcher', 'tool_scratch.urdf'))
+def build_composite_tool(rel, tip_link):
+    """A tool URDF loaded by init_tool (world_creation.py:330-365): a base link plus links welded
+    by fixed joints, loaded without URDF_USE_INERTIA_FROM_FILE (inertia per link from its
+    collision AABB).  A floating base with only fixed links moves as one rigid body: the links
+    are composed into one free body at the composite COM, axes those of the base (every link's
+    principal axes are the base's).  Returns the body plus the offsets, in that body frame, of
+    the base origin (the fixed constraint's child pivot, world_creation.py:363) and of `tip_link`'s
+    COM (the tool link getLinkState(tool, 1) reads), and the number of leading shapes that do not
+    belong to tip_link (handle_shapes: the shapes the tool-force-at-target rule skips)."""
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, rel))
     parts = [(links[root], np.zeros(3), np.array([0, 0, 0, 1.0]))]
     frames = {root: (np.zeros(3), np.array([0, 0, 0, 1.0]))}
     for J, parent in dfs:
@@ -800,20 +801,39 @@ def build_scratcher():
     c = sum(L.mass * cm for (L, _, _), cm in zip(parts, coms)) / mass
     I = np.zeros(3)
     shapes = []
+    lead = None
     for (L, p, q), cm in zip(parts, coms):
         sh = urdf_shapes(L)
+        if L.name == tip_link:
+            lead = len(shapes)
         lo, hi = compound_aabb(sh)
         Ii = box_inertia(L.mass, lo, hi)
         assert np.allclose(q, [0, 0, 0, 1]) and np.allclose(L.com_quat, [0, 0, 0, 1])
         d = cm - c
-        I += Ii + L.mass * (np.dot(d, d) - d * d)        # parallel axes (offsets along the handle axes)
+        I += Ii + L.mass * (np.dot(d, d) - d * d)        # parallel axes (offsets along the base axes)
         lp, lq = G.tf_mul(p, q, L.com_pos, L.com_quat)
         for s in sh:
             s.pos, s.quat = G.tf_mul(lp - c, lq, s.pos, s.quat)
             shapes.append(s)
-    tip = frames['tool_tip'][0] + links['tool_tip'].com_pos
+    tip = frames[tip_link][0] + links[tip_link].com_pos
     return dict(mass=mass, inertia=I, shapes=shapes, friction=links[root].friction,
-                pivot=-c, tip=tip - c, handle_shapes=len(urdf_shapes(links[root])))
+                pivot=-c, tip=tip - c, handle_shapes=lead)
+
+
+def build_scratcher():
+    """tool_scratch.urdf (world_creation.py:344): handle (base) + tool cylinder + tip sphere; the
+    tool-force-at-target rule counts tool links 0 and 1 (scratch_itch.py:95), i.e. every shape
+    after the handle's."""
+    t = build_composite_tool('scratcher/tool_scratch.urdf', 'tool_tip')
+    links, root, _ = parse_urdf(os.path.join(REF_ASSETS, 'scratcher', 'tool_scratch.urdf'))
+    t['handle_shapes'] = len(urdf_shapes(links[root]))
+    return t
+
+
+def build_wiper():
+    """bed_bathing/wiper.urdf (world_creation.py:346): handle (base) + 'tool' box + 'cloth' box;
+    bed_bathing.py counts and wipes with tool link 1 only (the cloth, :97)."""
+    return build_composite_tool('bed_bathing/wiper.urdf', 'cloth')
 
 
 def compile_scratch_pr2():
@@ -893,6 +913,131 @@ def compile_scratch_pr2():
         tool_pivot=tool['pivot'], tool_tip=tool['tip'], tool_handle_shapes=tool['handle_shapes'],
         # generate_target (scratch_itch.py:275-287): limb link, capsule length and radius per gender
         limbs={'male': [(9, 0.279, 0.043), (11, 0.257, 0.033)], 'female': [(9, 0.264, 0.0355), (11, 0.234, 0.027)]},
+    )
+    return S
+
+
+BED_Y_OFFSET = -0.53                                     # bed_bathing.py:203
+BED_FRICTION = 5.0                                       # bed_bathing.py:281-282 (lateralFriction)
+BED_JOINT_TARGETS = ((7, 50), (8, -50), (17, -30), (28, -60), (35, -60))   # bed_bathing.py:283 (degrees)
+BED_HUMAN_BASE = (np.array([0, 0, 0.7]), G.quat_from_euler([np.deg2rad(-30), 0, 0]))   # bed_bathing.py:194
+
+
+def capsule_points(p1, p2, radius, distance_between_points=0.05, position_scale=1.0):
+    """util.capsule_points (util.py:134-167): rings of points around a capsule's axis."""
+    p1, p2 = np.asarray(p1, float), np.asarray(p2, float)
+    axis = (p2 - p1) / np.linalg.norm(p2 - p1)
+    m = int(np.argmax(np.abs(axis)))                     # util.orthogonal_vector (util.py:168-176)
+    y = np.zeros(3)
+    y[(m + 1) % 3] = 1
+    ortho = np.cross(axis, y)
+    ortho = ortho / np.linalg.norm(ortho)
+    normal = np.cross(axis, ortho)
+    sections = int(np.linalg.norm(p2 - p1) / distance_between_points)
+    out = []
+    for i in range(sections):
+        sec = (p2 - p1) / (sections + 1) * (i + 1)
+        theta_dist = distance_between_points / radius
+        for j in range(int(2 * np.pi * radius / distance_between_points)):
+            th = theta_dist * j
+            out.append(p1 + sec * position_scale + radius * np.cos(th) * ortho + radius * np.sin(th) * normal)
+    return np.array(out)
+
+
+def bed_targets():
+    """generate_targets (bed_bathing.py:359-380) at the default hipbone_to_mouth_height (hmhs 1):
+    wipe targets on the upper arm (link 9) and forearm (link 11) capsules, 3 cm apart, in the
+    link frame, per gender."""
+    limbs = {'male': ((9, 0.279, 0.043), (11, 0.257, 0.033)), 'female': ((9, 0.264, 0.0355), (11, 0.234, 0.027))}
+    out = {}
+    for g, ((lu, Lu, ru), (lf, Lf, rf)) in limbs.items():
+        out[g] = (capsule_points([0, 0, 0], [0, 0, -Lu], ru, 0.03), capsule_points([0, 0, 0], [0, 0, -Lf], rf, 0.03))
+    return out
+
+
+def compile_bedbath_pr2():
+    """BedBathingPR2-v0 scene (bed_bathing.py:155-357 + world_creation.py:27-93,181-217,330-365):
+    plane, the two mattress boxes and the VHACD bed frame (bed_bathing.py:201-218; the bed loaded
+    by create_new_world is removed at :202), the human lying on the bed (base at [0, 0, 0.7]
+    pitched -30 deg, :194; right arm 7..13 articulated for the reset's 100-frame settle onto the
+    mattress under gravity -1, :283-289, static during the episode, :292-300), the PR2 and the
+    wiper."""
+    S = Scene()
+    rob, groups, torso_com, sub = build_pr2()
+    S.robot = rob
+    S.robot_base_pos = np.zeros(3)                 # per env (position_robot_toc): lives in the state
+    S.robot_base_quat = np.array([0, 0, 0, 1.0])
+    robot_body = {}
+    for i in range(len(rob['name'])):
+        if rob['shapes'][i]:
+            robot_body[i] = S.add_body(KIND_ROBOT, i, rob['shapes'][i], rob['friction'][i], rob['name'][i])
+    rstatic_body = [S.add_body(KIND_RSTATIC, k, shapes, 0.5, name) for k, (name, shapes) in enumerate(groups)]
+    tool = build_wiper()
+    S.free = [dict(name='wiper', mass=tool['mass'], inertia=tool['inertia'], gravity=np.zeros(3))]
+    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'wiper')
+    plane = build_static_urdf('plane/plane.urdf')
+    m1 = [Shape(BOX, (0, 0, 0.15 / 2.0), half_extents=(0.88 / 2.0, 1.25 / 2.0, 0.15 / 2.0))]
+    m2 = [Shape(BOX, (0, 0.7 / 2.0, 0), half_extents=(0.88 / 2.0, 0.7 / 2.0, 0.15 / 2.0))]
+    frame = [Shape(HULL, hull=Hull(g * np.array([1, 1.2, 1]))) for g in obj_groups(os.path.join(REF_ASSETS, 'bed', 'hospital_bed_frame_vhacd.obj'))]
+    S.static = [dict(name='plane', pos=np.zeros(3), quat=np.array([0, 0, 0, 1.0])),
+                dict(name='mattress', pos=np.array([0, BED_Y_OFFSET, 0.4]), quat=np.array([0, 0, 0, 1.0])),
+                dict(name='mattress_head', pos=np.array([0, 1.25 / 2.0 + BED_Y_OFFSET, 0.4 + 0.15 / 2.0]), quat=G.quat_from_euler([np.deg2rad(60), 0, 0])),
+                dict(name='bed_frame', pos=np.array([0, BED_Y_OFFSET + 0.45, 0.42]), quat=G.quat_from_euler([np.pi / 2.0, 0, -np.pi / 2.0]))]
+    static_body = [S.add_body(KIND_STATIC, 0, plane['shapes'], plane['friction'], 'plane'),
+                   S.add_body(KIND_STATIC, 1, m1, BED_FRICTION, 'mattress', single=False),
+                   S.add_body(KIND_STATIC, 2, m2, BED_FRICTION, 'mattress_head', single=False),
+                   S.add_body(KIND_STATIC, 3, frame, BED_FRICTION, 'bed_frame')]
+    S.human = {}
+    human_body = {}
+    for gender in ('male', 'female'):
+        S.human[gender] = build_human(gender)
+    slot_links = [-1] + [i for i, L in enumerate(S.human['male'][1]) if L['shapes']]
+    S.human_slots = slot_links
+    for si, li in enumerate(slot_links):
+        shapes = []
+        for gi, gender in enumerate(('male', 'female')):
+            base_shapes, hl = S.human[gender]
+            for s in (base_shapes if li < 0 else hl[li]['shapes']):
+                s.gender = gi
+                shapes.append(s)
+        human_body[li] = S.add_body(KIND_HUMAN, si, shapes, 0.5, 'human%d' % li)
+    chain = [human_body[li] for li in ARM_CHAIN if li in human_body]
+    arm_partners = [human_body[li] for li in slot_links if li < 4 or li >= 14]
+    pairs = []
+    for li, b in sorted(robot_body.items()):
+        if not (PR2_LEFT_ROOT + li in PR2_TOOL_FILTER):
+            pairs.append((b, tool_body))
+        for sb in static_body:
+            pairs.append((b, sb))
+        for h in slot_links:
+            pairs.append((b, human_body[h]))
+    for rb in rstatic_body:
+        pairs.append((rb, tool_body))
+        for hb in chain:
+            pairs.append((rb, hb))
+    for sb in static_body:
+        pairs.append((tool_body, sb))
+    for h in slot_links:
+        pairs.append((tool_body, human_body[h]))
+    for hb in chain:                               # the reset's settle: the arm onto the mattress / itself
+        for sb in static_body:
+            pairs.append((hb, sb))
+        for pb in arm_partners:
+            pairs.append((hb, pb))
+    S.n_pairs_base = len(pairs)
+    S.pairs = pairs
+    S.robot_body = robot_body
+    S.free_body = [tool_body]
+    S.static_body = static_body
+    S.human_body = human_body
+    S.rstatic = groups
+    S.task = dict(
+        arm_dofs=[rob['dof'][sub.index(j)] for j in PR2_LEFT_ARM],
+        finger_dofs=[rob['dof'][sub.index(j)] for j in PR2_LEFT_FINGERS],
+        tool_link=sub.index(PR2_TOOL_LINK), torso_com=torso_com,
+        tool_pos_offset=np.zeros(3), tool_orient_offset=np.array([0, 0, 0, 1.0]),   # bed_bathing.py:320
+        tool_pivot=tool['pivot'], tool_tip=tool['tip'], tool_handle_shapes=tool['handle_shapes'],
+        targets=bed_targets(),
     )
     return S
 
@@ -1047,15 +1192,55 @@ def compile_scratch(out_dir=DATA_DIR):
     return path, A
 
 
+def compile_bedbath(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    S = compile_bedbath_pr2()
+    A = to_arrays(S)
+    _human_tables(S, A)
+    A.update(head_chain(S, ARM_CHAIN, cap=HC_CAP))
+    t = S.task
+    A['task_arm_dofs'] = np.array(t['arm_dofs'], np.int32)
+    A['task_finger_dofs'] = np.array(t['finger_dofs'], np.int32)
+    A['task_tool_link'] = np.int32(t['tool_link'])
+    A['task_tool_offset'] = np.concatenate([t['tool_pos_offset'], t['tool_orient_offset']])
+    A['task_torso_com'] = np.asarray(t['torso_com'], float)
+    A['task_tool_pivot'] = np.asarray(t['tool_pivot'], float)
+    A['task_tool_tip'] = np.asarray(t['tool_tip'], float)
+    A['task_tool_handle_shapes'] = np.int32(t['tool_handle_shapes'])
+    A['task_tool_body'] = np.int32(S.free_body[0])
+    A['task_human_body0'] = np.int32(S.human_body[S.human_slots[0]])
+    A['n_rstatic'] = np.int32(len(S.rstatic))
+    A['rl_urdf'] = np.array(S.robot['urdf'], np.int32)
+    # wipe targets [gender][k] = (x, y, z in the limb frame, limb 0 upper arm / 1 forearm)
+    T = np.zeros((2, 160, 4))
+    NT = np.zeros((2, 2), np.int32)
+    for g, gender in enumerate(('male', 'female')):
+        up, fo = t['targets'][gender]
+        NT[g] = len(up), len(fo)
+        T[g, :len(up), :3] = up
+        T[g, len(up):len(up) + len(fo), :3] = fo
+        T[g, len(up):len(up) + len(fo), 3] = 1.0
+    A['bb_targets'] = T
+    A['bb_ntgt'] = NT
+    A['bb_limb_slots'] = np.array([S.human_slots.index(9), S.human_slots.index(11)], np.int32)
+    A['bb_joint_slots'] = np.array([S.human_slots.index(9), S.human_slots.index(11), S.human_slots.index(13)], np.int32)
+    A['bb_human_base'] = np.concatenate(BED_HUMAN_BASE)
+    A['bb_bed_bodies'] = np.array(S.static_body[1:], np.int32)
+    path = os.path.join(out_dir, 'bed_bathing_pr2.npz')
+    np.savez_compressed(path, **A)
+    return path, A
+
+
 def compile_all(out_dir=DATA_DIR):
-    """Both compiled scenes; returns the FeedingJaco one (path, arrays) first."""
+    """All compiled scenes; returns the FeedingJaco one (path, arrays) first."""
     out = compile_feeding(out_dir)
     compile_scratch(out_dir)
+    compile_bedbath(out_dir)
     return out
 
 
 if __name__ == '__main__':
-    for path, A in (compile_feeding(), compile_scratch()):
+    for path, A in (compile_feeding(), compile_scratch(), compile_bedbath()):
         print(path)
         for k, v in A.items():
             print('%-24s %s %s' % (k, getattr(v, 'shape', ()), getattr(v, 'dtype', type(v))))

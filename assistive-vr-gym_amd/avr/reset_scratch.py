@@ -168,13 +168,14 @@ def jlwki(J, q, lower, upper):
     return np.power(det, 1.0 / 6.0) / (np.trace(M, axis1=1, axis2=2) / 6.0)
 
 
-def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200):
-    """Batched position_robot_toc for the PR2 (env.py:489-585; scratch_itch.py:189-190): per env,
-    `attempts` random base poses; at each the start goal (link 76 to target_pos with identity
-    orientation, base offset pos_offset=[0.1, 0, 0]) must be reached (0.03 on position and
-    quaternion), then the shoulder / elbow / wrist positions count as further goals; the best
-    base maximises goals reached, then summed manipulability.  Returns (base_pos, base_quat,
-    arm q, start target, ok) per env."""
+def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart=None, pos_offset=(0.1, 0, 0)):
+    """Batched position_robot_toc for the PR2 (env.py:489-585; scratch_itch.py:189-190,
+    bed_bathing.py:317): per env, `attempts` random base poses; at each the start goal (link 76
+    to the start target with identity orientation, base offset pos_offset) must be reached (0.03
+    on position and quaternion), then the shoulder / elbow / wrist positions count as further
+    goals; the best base maximises goals reached, then summed manipulability.  tstart: the start
+    targets (N, 3), or None for ScratchItch's jittered target (drawn first from each stream).
+    Returns (base_pos, base_quat, arm q, start target, ok) per env."""
     N = len(rngs)
     nd = int(A['n_dof'])
     arm = np.array(md.arm_dofs)
@@ -182,13 +183,14 @@ def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200):
     lo = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
     hi = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
     # draws per env: the start goal, then per attempt the base pose and the IK rest pose
-    tstart = np.stack([np.array([-0.55, 0, 0.8]) + r.uniform(-0.05, 0.05, size=3) for r in rngs])
+    if tstart is None:
+        tstart = np.stack([np.array([-0.55, 0, 0.8]) + r.uniform(-0.05, 0.05, size=3) for r in rngs])
     M = N * attempts
     bp = np.zeros((M, 3)); yaw = np.zeros(M); rest = np.zeros((M, len(arm)))
     for e, r in enumerate(rngs):
         for a in range(attempts):
             k = e * attempts + a
-            bp[k] = np.array([-0.85, -0.4, 0]) + np.array([0.1, 0, 0]) + np.array([r.uniform(-0.5, 0), r.uniform(-0.5, 0.5), 0])
+            bp[k] = np.array([-0.85, -0.4, 0]) + np.asarray(pos_offset, float) + np.array([r.uniform(-0.5, 0), r.uniform(-0.5, 0.5), 0])
             yaw[k] = np.deg2rad(r.uniform(-30, 30))
             rest[k] = r.uniform(lo, hi)
     bq = np.stack([np.zeros(M), np.zeros(M), np.sin(0.5 * yaw), np.cos(0.5 * yaw)], 1)

@@ -1,6 +1,6 @@
 // avr_api.cpp -- the extern "C" entry points of libavr.so (include/avr.h).  A handle records its
 // task (avr_model_desc.task) and forwards every call to that task's instantiation of the C-ABI
-// body (avr_capi.hip inside namespace avr_feeding / avr_scratch, see avr_task_tu.h).
+// body (avr_capi.hip inside namespace avr_feeding / avr_scratch / avr_bedbath, see avr_task_tu.h).
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -46,22 +46,31 @@
 
 AVR_TASK_DECLS(avr_feeding)
 AVR_TASK_DECLS(avr_scratch)
+AVR_TASK_DECLS(avr_bedbath)
 
 struct avr_sim {
     int32_t task;
-    void *impl;          // avr_feeding::avr_sim or avr_scratch::avr_sim
+    void *impl;          // avr_feeding::avr_sim, avr_scratch::avr_sim or avr_bedbath::avr_sim
     char err[256];       // dispatch-level errors (no impl yet)
 };
 
-#define DISPATCH(s, call)                                                                     \
+#define DISPATCH_ANY(s, call)                                                                 \
     do {                                                                                      \
-        if (!(s) || !(s)->impl) return -1;                                                    \
         if ((s)->task == AVR_TASK_SCRATCH) {                                                  \
             avr_scratch::avr_sim *h = (avr_scratch::avr_sim *)(s)->impl;                      \
             return call;                                                                      \
         }                                                                                     \
+        if ((s)->task == AVR_TASK_BEDBATH) {                                                  \
+            avr_bedbath::avr_sim *h = (avr_bedbath::avr_sim *)(s)->impl;                      \
+            return call;                                                                      \
+        }                                                                                     \
         avr_feeding::avr_sim *h = (avr_feeding::avr_sim *)(s)->impl;                          \
         return call;                                                                          \
+    } while (0)
+#define DISPATCH(s, call)                                                                     \
+    do {                                                                                      \
+        if (!(s) || !(s)->impl) return -1;                                                    \
+        DISPATCH_ANY(s, call);                                                                \
     } while (0)
 
 extern "C" {
@@ -69,10 +78,14 @@ extern "C" {
 int32_t avr_abi_version(void) { return AVR_ABI_VERSION; }
 int32_t avr_state_words(void) { return AVR_STATE_WORDS; }
 int32_t avr_task_state_words(int32_t task) {
-    return task == AVR_TASK_FEEDING ? AVR_STATE_WORDS : task == AVR_TASK_SCRATCH ? AVR_SI_STATE_WORDS : -1;
+    return task == AVR_TASK_FEEDING ? AVR_STATE_WORDS : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH) ? AVR_SI_STATE_WORDS : -1;
 }
-int32_t avr_task_obs_dim(int32_t task) { return task == AVR_TASK_FEEDING ? AVR_OBS_DIM : task == AVR_TASK_SCRATCH ? AVR_SI_OBS_DIM : -1; }
-int32_t avr_task_act_dim(int32_t task) { return task == AVR_TASK_FEEDING ? AVR_ACT_DIM : task == AVR_TASK_SCRATCH ? AVR_SI_ACT_DIM : -1; }
+int32_t avr_task_obs_dim(int32_t task) {
+    return task == AVR_TASK_FEEDING ? AVR_OBS_DIM : task == AVR_TASK_SCRATCH ? AVR_SI_OBS_DIM : task == AVR_TASK_BEDBATH ? AVR_BB_OBS_DIM : -1;
+}
+int32_t avr_task_act_dim(int32_t task) {
+    return task == AVR_TASK_FEEDING ? AVR_ACT_DIM : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH) ? AVR_SI_ACT_DIM : -1;
+}
 int32_t avr_task(avr_sim *s) { return s ? s->task : -1; }
 
 int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
@@ -93,6 +106,10 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         avr_scratch::avr_sim *h = nullptr;
         r = avr_scratch::avr_create(cfg, d, &h);
         s->impl = h;
+    } else if (d->task == AVR_TASK_BEDBATH) {
+        avr_bedbath::avr_sim *h = nullptr;
+        r = avr_bedbath::avr_create(cfg, d, &h);
+        s->impl = h;
     } else {
         snprintf(s->err, sizeof(s->err), "unknown task %d in avr_model_desc.task", (int)d->task);
         return -2;
@@ -105,6 +122,7 @@ int avr_destroy(avr_sim *s) {
     int r = 0;
     if (s->impl) {
         if (s->task == AVR_TASK_SCRATCH) r = avr_scratch::avr_destroy((avr_scratch::avr_sim *)s->impl);
+        else if (s->task == AVR_TASK_BEDBATH) r = avr_bedbath::avr_destroy((avr_bedbath::avr_sim *)s->impl);
         else r = avr_feeding::avr_destroy((avr_feeding::avr_sim *)s->impl);
     }
     delete s;
@@ -114,18 +132,16 @@ int avr_destroy(avr_sim *s) {
 const char *avr_last_error(avr_sim *s) {
     if (!s) return "null handle";
     if (!s->impl) return s->err;
-    if (s->task == AVR_TASK_SCRATCH) return avr_scratch::avr_last_error((avr_scratch::avr_sim *)s->impl);
-    return avr_feeding::avr_last_error((avr_feeding::avr_sim *)s->impl);
+    DISPATCH_ANY(s, avr_last_error(h));
 }
 
 void *avr_stream(avr_sim *s) {
     if (!s || !s->impl) return nullptr;
-    return s->task == AVR_TASK_SCRATCH ? avr_scratch::avr_stream((avr_scratch::avr_sim *)s->impl) : avr_feeding::avr_stream((avr_feeding::avr_sim *)s->impl);
+    DISPATCH_ANY(s, avr_stream(h));
 }
 void *avr_state_device_ptr(avr_sim *s) {
     if (!s || !s->impl) return nullptr;
-    return s->task == AVR_TASK_SCRATCH ? avr_scratch::avr_state_device_ptr((avr_scratch::avr_sim *)s->impl)
-                                       : avr_feeding::avr_state_device_ptr((avr_feeding::avr_sim *)s->impl);
+    DISPATCH_ANY(s, avr_state_device_ptr(h));
 }
 
 int32_t avr_n_envs(avr_sim *s) { if (!s || !s->impl) return 0; DISPATCH(s, avr_n_envs(h)); }

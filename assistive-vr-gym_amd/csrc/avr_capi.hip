@@ -237,6 +237,26 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     k.tool_handle_shapes = d->tool_handle_shapes;
     k.w_tool_force = (float)d->w_tool_force; k.w_scratch = (float)d->w_scratch;
     int r;
+#if AVR_TASK == AVR_TASK_BEDBATH
+    {
+        bool okt = d->bb_targets != nullptr;
+        for (int g = 0; g < 2; g++)
+            okt = okt && d->bb_ntgt[g][0] >= 0 && d->bb_ntgt[g][1] >= 0 && d->bb_ntgt[g][0] + d->bb_ntgt[g][1] <= AVR_BB_MAX_TARGETS &&
+                  d->bb_ntgt[g][0] + d->bb_ntgt[g][1] <= 6 * 24;
+        for (int q = 0; q < 2; q++) okt = okt && d->bb_limb_slots[q] >= 0 && d->bb_limb_slots[q] < d->n_human;
+        for (int q = 0; q < 3; q++) okt = okt && d->bb_joint_slots[q] >= 0 && d->bb_joint_slots[q] < d->n_human;
+        if (!okt) return fail(s, -2, "BedBathing: wipe targets / limb slots out of range");
+        std::vector<float4> tg(2 * AVR_BB_MAX_TARGETS);
+        for (int i = 0; i < 2 * AVR_BB_MAX_TARGETS; i++)
+            tg[i] = make_float4((float)d->bb_targets[4 * i], (float)d->bb_targets[4 * i + 1], (float)d->bb_targets[4 * i + 2], (float)d->bb_targets[4 * i + 3]);
+        if ((r = upload(s, tg, &k.bb_tgt))) return r;
+        for (int g = 0; g < 2; g++) { k.bb_ntgt[g][0] = d->bb_ntgt[g][0]; k.bb_ntgt[g][1] = d->bb_ntgt[g][1]; }
+        for (int q = 0; q < 2; q++) k.bb_limb_slot[q] = d->bb_limb_slots[q];
+        for (int q = 0; q < 3; q++) k.bb_joint_slot[q] = d->bb_joint_slots[q];
+        k.w_wipe = (float)d->w_wipe;
+        k.closest_distance = (float)d->closest_distance;
+    }
+#endif
     if ((r = upload(s, par, &k.rl_parent))) return r;
     if ((r = upload(s, jt, &k.rl_jtype))) return r;
     if ((r = upload(s, dofv, &k.rl_dof))) return r;

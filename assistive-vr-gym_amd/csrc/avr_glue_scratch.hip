@@ -1,8 +1,9 @@
-// avr_glue_scratch.hip -- ScratchItchPR2-v0 task glue (included by avr_kernel.hip for
-// AVR_TASK_SCRATCH): take_step with the PR2's left arm and the human arm's tremor
-// (env.py:274-351), update_targets (scratch_itch.py:289-293), get_total_force
-// (scratch_itch.py:84-102), _get_obs (:104-128) and the reward with human_preferences
-// (:47-76, env.py:412-448).
+// avr_glue_scratch.hip -- task glue of the PR2 tasks (included by avr_kernel.hip for
+// AVR_TASK_SCRATCH and AVR_TASK_BEDBATH): take_step with the PR2's left arm and the human arm's
+// tremor (env.py:274-351; both tasks drive the left arm with gains 0.05 / forces 1.0,
+// config.ini:4-5,13-14), then ScratchItchPR2-v0's update_targets (scratch_itch.py:289-293),
+// get_total_force (scratch_itch.py:84-102), _get_obs (:104-128) and the reward with
+// human_preferences (:47-76, env.py:412-448); BedBathingPR2-v0's are in avr_glue_bedbath.hip.
 
 // take_step (env.py:274-337) for robot_arm='left', gains/forces from config.ini:4-5
 // (scratch_itch.py:45).  One thread per env.  The human arm keeps its reactive motors
@@ -46,6 +47,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     ws[WS_ASQ] = asq;
 }
 
+#if AVR_TASK == AVR_TASK_SCRATCH
 // target_pos = limb frame x target_on_arm (update_targets, scratch_itch.py:289-293); the limb is
 // a link of the articulated arm chain, whose frames robot_fk has just computed
 AVR_DI void scratch_target(const KModel &m, EnvLDS &L) {
@@ -194,3 +196,7 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     for (int i = lane; i < S_CP; i += 64) gst[i] = L.st[i];
     prof_flush(m, L, env);
 }
+
+#else
+#include "avr_glue_bedbath.hip"
+#endif  // AVR_TASK_SCRATCH

@@ -13,7 +13,7 @@
 #define MAXSH 320      // shapes (the pair kernel stages their packed info in LDS, 16 bits each)
 #define MAXSP 256
 #define MAXAP 256
-#if AVR_TASK == AVR_TASK_SCRATCH
+#if K_PR2
 #define MAXNC 48       // non-contact rows: 21 motors, the 6-row tool weld, violated limits
 #else
 #define MAXNC 32
@@ -109,6 +109,10 @@ struct KModel {
     float torso_com[4];        // ScratchItch: PR2 torso link COM in the base frame
     int tool_handle_shapes;    // ScratchItch: leading tool shapes that belong to the handle (link -1)
     float w_tool_force, w_scratch;
+    const float4 *bb_tgt;      // BedBathing: wipe targets [2][AVR_BB_MAX_TARGETS] (xyz in the limb frame, limb)
+    int bb_ntgt[2][2];         // [gender][limb]
+    int bb_limb_slot[2], bb_joint_slot[3];
+    float w_wipe, closest_distance;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
     int rowcap;                // rows per env = MAXNC + 3 * K_MAX_CONTACTS
     int rowstride;             // floats between consecutive envs' row buffers

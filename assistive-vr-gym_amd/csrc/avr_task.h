@@ -6,7 +6,7 @@
 #include "../../include/avr_model.h"
 
 #ifndef AVR_TASK
-#error "AVR_TASK must be defined (AVR_TASK_FEEDING or AVR_TASK_SCRATCH)"
+#error "AVR_TASK must be defined (AVR_TASK_FEEDING, AVR_TASK_SCRATCH or AVR_TASK_BEDBATH)"
 #endif
 
 #define T_TARGET 0      // task words common to both layouts
@@ -44,7 +44,10 @@
 #define K_CHAIN_LIMITS_IN_STATE 0
 #define K_HUMAN_GRAVITY 0       // robot, human and spoon gravity are 0 (feeding.py:285-287)
 #define K_TOOL_PIVOT 0          // the spoon's base COM is its body frame
-#elif AVR_TASK == AVR_TASK_SCRATCH
+#define K_PR2 0
+#elif AVR_TASK == AVR_TASK_SCRATCH || AVR_TASK == AVR_TASK_BEDBATH
+// the PR2 family: ScratchItchPR2 and BedBathingPR2 share the state layout (AVR_SI_*)
+#define K_PR2 1
 #define K_MAX_LINKS AVR_SI_MAX_LINKS
 #define K_MAX_DOF AVR_SI_MAX_DOF
 #define K_HC_N AVR_SI_HC_N
@@ -52,7 +55,13 @@
 #define K_MAX_HUMAN AVR_SI_MAX_HUMAN
 #define K_MAX_CONTACTS AVR_SI_MAX_CONTACTS
 #define K_ACT_DIM AVR_SI_ACT_DIM
+#if AVR_TASK == AVR_TASK_BEDBATH
+#define K_OBS_DIM AVR_BB_OBS_DIM
+#define T_WIPE AVR_BB_T_WIPE
+#define T_NTGT AVR_BB_T_NTGT
+#else
 #define K_OBS_DIM AVR_SI_OBS_DIM
+#endif
 #define S_Q AVR_SI_S_Q
 #define S_QD AVR_SI_S_QD
 #define S_QTGT AVR_SI_S_QTGT
@@ -73,8 +82,8 @@
 #define T_ONARM AVR_SI_T_ONARM
 #define K_RBASE_IN_STATE 1      // PR2 base pose per env (position_robot_toc, env.py:489-585)
 #define K_CHAIN_LIMITS_IN_STATE 1   // human arm limits x limit_scale per env (human_creation.py:226)
-#define K_HUMAN_GRAVITY 1       // human gravity -1 (scratch_itch.py:260)
-#define K_TOOL_PIVOT 1          // the scratcher is a composite body: its handle COM is off the body frame
+#define K_HUMAN_GRAVITY 1       // human gravity -1 (scratch_itch.py:260; BedBathing's reset settle, bed_bathing.py:286)
+#define K_TOOL_PIVOT 1          // the scratcher / wiper is a composite body: its handle COM is off the body frame
 #else
 #error "unknown AVR_TASK"
 #endif

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: env-steps/s on MI355X.  Default: FeedingJaco-v0 at 4096 envs (BASELINE.json
-configs[1]); --task ScratchItchPR2-v0 runs configs[2].
+configs[1]); --task ScratchItchPR2-v0 runs configs[2]; --task BedBathingPR2-v0 is the PR2 variant
+of configs[3] (BASELINE's BedBathingSawyer-v0 does not exist in the reference):
+32768 envs over 8 GPUs = torchrun --nproc-per-node 8 bench.py --task BedBathingPR2-v0 --gpus 8.
 
 One "step" = one gym step of every env (take_step + 5 x stepSimulation (FeedingJaco: 2 sub-steps
 each, ScratchItch: 1) + task glue) = one launch sequence of the gfx950 kernels.  Synthetic random
@@ -36,6 +38,10 @@ TASKS = {
                            workload='FeedingJaco-v0, %d envs/GPU, rigid-only, random actions'),
     'ScratchItchPR2-v0': dict(task=1, bytes=2252 * 2 + 120 + 28 + 136, settle=0, substeps=5, iters=50, pool=128,
                               workload='ScratchItchPR2-v0, %d envs/GPU, human-capsule contact + tool force reward, random actions'),
+    # BedBathingPR2 (SURVEY 8(d) recipe, ScratchItch's state minus the scratch target plus the wipe bit
+    # set: 2252 + 28 B each way) + obs 24 + reward + done + 2 info + action in
+    'BedBathingPR2-v0': dict(task=2, bytes=2280 * 2 + 120 + 28 + 112, settle=0, substeps=5, iters=50, pool=128,
+                             workload='BedBathingPR2-v0, %d envs/GPU, wiping targets + tool-human closest distance, random actions'),
 }
 VALU_CYC = 2.0          # v_fma_f32 wave64 issue throughput, cycles (MI355X_MICROARCH.md cycle table)
 SIMDS, CLOCK_HZ = 1024, 2.4e9
@@ -48,6 +54,9 @@ def layout_bytes_per_env_step(L):
 
 
 def reset_pool(task, A, md, ids, impairment):
+    if task == 2:
+        from avr import reset_bedbath as RBB
+        return RBB.batch_reset_states(A, md, 1001, ids, attempts=25, iters=100)
     if task == 1:
         from avr import reset_scratch as RSS
         return RSS.batch_reset_states(A, md, 1001, ids, impairment=impairment, attempts=25, iters=100)
@@ -85,7 +94,7 @@ def cpu_baseline(name, md, A, seconds, threads, impairment):
 def pmc_summary(name, kernels, ms_per_step, E):
     """HBM traffic and SQ issue figures from the committed rocprofv3 PMC summary of this task's
     bench (profiles/pmc_<task>.json, tools/rocpd_summary.py), if its kernel set and env count match."""
-    fname = {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json'}[name]
+    fname = {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json', 'BedBathingPR2-v0': 'pmc_bedbath.json'}[name]
     path = os.path.join(ROOT, 'profiles', fname)
     if not os.path.exists(path):
         return None

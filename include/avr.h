@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 3      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters */
+#define AVR_ABI_VERSION 4      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters;
+                                  4: BedBathingPR2 (avr_model_desc bb_* fields, task 2) */
 
 typedef struct avr_config {
     int32_t n_envs;        /* envs owned by this handle (one GPU)                          */

@@ -20,6 +20,7 @@ extern "C" {
 /* ---- tasks: one compiled scene and one state layout each ---- */
 #define AVR_TASK_FEEDING 0       /* FeedingJaco-v0   (feeding.py, feeding_robots.py:7-9)       */
 #define AVR_TASK_SCRATCH 1       /* ScratchItchPR2-v0 (scratch_itch.py, scratch_itch_robots.py) */
+#define AVR_TASK_BEDBATH 2       /* BedBathingPR2-v0  (bed_bathing.py, bed_bathing_robots.py)   */
 
 /* ==== FeedingJaco-v0 layout ==== */
 /* ---- capacities (compile-time; checked against the model at create time) ---- */
@@ -120,6 +121,17 @@ enum { AVR_J_FIXED = 0, AVR_J_REVOLUTE = 1, AVR_J_PRISMATIC = 2 };
 #define AVR_SI_S_CP       (AVR_SI_S_HCH + 4 * AVR_SI_HC_N)
 #define AVR_SI_STATE_WORDS (AVR_SI_S_CP + AVR_SI_MAX_CONTACTS * AVR_CP_WORDS)
 
+/* ==== BedBathingPR2-v0 layout ====
+ * The ScratchItchPR2 layout (AVR_SI_*): the same PR2 left-arm subtree, composite tool (the wiper)
+ * and human right-arm chain.  The chain is articulated only while the reset lets the arm settle
+ * onto the mattress (bed_bathing.py:283-289: T_HDYN 1, gravity -1); during the episode the human
+ * is static (:292-300: T_HDYN 0).  Task words 0-4 and 7-10 as in FeedingJaco; T_TREMOR (14) is 0
+ * (the task's impairment is 'none', :188); the wipe targets still on the arm are a bit set. */
+#define AVR_BB_MAX_TARGETS 160    /* wipe targets per env (male 81 + 48, female 56 + 35)        */
+#define AVR_BB_T_WIPE     17      /* [6] 24 targets per word (exact integers in a float)        */
+#define AVR_BB_T_NTGT     23      /* total_target_count (bed_bathing.py:379)                    */
+#define AVR_BB_OBS_DIM    24      /* bed_bathing.py:147                                         */
+
 /* ---- compiled scene (host arrays; row-major) ---- */
 #define AVR_DESC_HC 8             /* capacity of the hc_* arrays below                          */
 typedef struct avr_model_desc {
@@ -206,6 +218,14 @@ typedef struct avr_model_desc {
     double robot_gravity[3];               /* gravity on the robot's links: 0 in both tasks (feeding.py:285,
                                               scratch_itch.py:259); the kernels reject anything else,
                                               the oracle honours it (known-answer tests) */
+    /* ---- ABI 4 (BedBathingPR2) ---- */
+    const double *bb_targets;              /* [2][AVR_BB_MAX_TARGETS][4]: xyz in the limb frame, limb
+                                              (0 upper arm, 1 forearm) -- generate_targets, bed_bathing.py:359-380 */
+    int32_t bb_ntgt[2][2];                 /* [gender][limb] target counts                          */
+    int32_t bb_limb_slots[2];              /* human slots of links 9 (upper arm) and 11 (forearm)  */
+    int32_t bb_joint_slots[3];             /* human slots of links 9, 11, 13 (obs, bed_bathing.py:143-145) */
+    double w_wipe;                         /* config.ini:17 wiping_reward_weight                    */
+    double closest_distance;               /* getClosestPoints(tool, human, distance=4.0) (bed_bathing.py:61) */
 } avr_model_desc;
 
 #ifdef __cplusplus

@@ -68,7 +68,13 @@
 #define K_MAX_HUMAN AVR_SI_MAX_HUMAN
 #define K_MAX_CONTACTS AVR_SI_MAX_CONTACTS
 #define K_ACT_DIM AVR_SI_ACT_DIM
+#if AVR_TASK == AVR_TASK_BEDBATH
+#define K_OBS_DIM AVR_BB_OBS_DIM
+#define T_WIPE AVR_BB_T_WIPE
+#define T_NTGT AVR_BB_T_NTGT
+#else
 #define K_OBS_DIM AVR_SI_OBS_DIM
+#endif
 #define S_Q AVR_SI_S_Q
 #define S_QD AVR_SI_S_QD
 #define S_QTGT AVR_SI_S_QTGT
@@ -88,6 +94,8 @@
 #define T_ONARM AVR_SI_T_ONARM
 #endif
 #define SCRATCH (AVR_TASK == AVR_TASK_SCRATCH)
+#define BEDBATH (AVR_TASK == AVR_TASK_BEDBATH)
+#define PR2F (AVR_TASK != AVR_TASK_FEEDING)     /* the PR2 tasks: per-env base, composite tool, arm chain */
 
 #ifdef AVR_ORACLE_FLOAT
 typedef float real;
@@ -264,7 +272,7 @@ static tf slot_pose(const real *st, int slot) {
 static void robot_fk(const model *m, real *st, ws_t *w) {
     for (int i = 0; i < m->nl; i++) {
         int p = m->parent[i];
-#if SCRATCH
+#if PR2F
         tf base; base.p = ld3(st + S_RBASE); base.q = ldq(st + S_RBASE + 3);   /* position_robot_toc: per env */
 #else
         tf base = m->base;
@@ -819,7 +827,7 @@ static tf body_tf(const model *m, const real *st, const ws_t *w, int b) {
         return t;
     }
     if (kind == AVR_BODY_STATIC) return ldtf(m->d.st_pose + 7 * idx);
-#if SCRATCH
+#if PR2F
     if (kind == AVR_BODY_RSTATIC) { t.p = ld3(st + S_RBASE); t.q = ldq(st + S_RBASE + 3); return t; }
 #endif
     const real *h = st + S_HUMAN + 7 * idx;
@@ -1024,7 +1032,7 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
         int dof = m->dof[i];
         real q = st[S_Q + dof];
         real lo = m->lower[i], hi = m->upper[i];
-#if SCRATCH
+#if PR2F
         if (i >= m->nl_robot) {   /* human arm limits x the env's limit_scale (human_creation.py:226) */
             lo = st[S_HCH + 2 * K_HC_N + (i - m->nl_robot)];
             hi = st[S_HCH + 3 * K_HC_N + (i - m->nl_robot)];
@@ -1075,7 +1083,7 @@ static void build_noncontact_rows(const model *m, const real *st, ws_t *w, real 
         qt frA = qmul(ta.q, off.q);
         const real *f = st + S_FREE + AVR_FB_WORDS * fb;
         tf tb; tb.p = ld3(f); tb.q = ldq(f + 3);
-#if SCRATCH
+#if PR2F
         v3 pivB = tfpt(tb, ld3d(m->d.fix_pivot_b));   /* the composite tool's base (handle) COM */
 #else
         v3 pivB = tb.p;
@@ -1383,7 +1391,7 @@ static real contact_force(const model *m, real *st, int (*pred)(const model *, i
     return s;
 }
 
-#if !SCRATCH
+#if !PR2F
 static int is_robot(const model *m, int b) { return m->d.body_kind[b] == AVR_BODY_ROBOT; }
 static int is_human(const model *m, int b) { return m->d.body_kind[b] == AVR_BODY_HUMAN; }
 static int pred_robot_human(const model *m, int a, int b, void *c) { (void)c; return (is_robot(m, a) && is_human(m, b)) || (is_robot(m, b) && is_human(m, a)); }
@@ -1426,7 +1434,7 @@ static void observe(const model *m, real *st, ws_t *w, float spoon_force, float 
 static void hard_limits(const model *m, real *st) {
     for (int k = 0; k < m->d.hc_n; k++) {
         int d = m->nd_robot + k;
-#if SCRATCH
+#if PR2F
         real lo = st[S_HCH + 2 * K_HC_N + k], hi = st[S_HCH + 3 * K_HC_N + k];
 #else
         real lo = R(m->d.hc_lower[k]), hi = R(m->d.hc_upper[k]);
@@ -1436,7 +1444,7 @@ static void hard_limits(const model *m, real *st) {
     }
 }
 
-#if !SCRATCH
+#if !PR2F
 static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
     real *st = o->state + (size_t)e * K_STATE_WORDS;
     const model *m = oview(o, st);
@@ -1544,8 +1552,10 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
     return 0;
 }
 
-#else
+#elif SCRATCH
 #include "avr_oracle_scratch.c"
+#else
+#include "avr_oracle_bedbath.c"
 #endif
 
 /* ---------------------------------------------------------------- public API */
@@ -1580,6 +1590,10 @@ EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **o
     CP(shape_pose, 7 * S, double); CP(shape_param, 4 * S, double); CP(shape_margin, S, double); CP(shape_aabb, 6 * S, double);
     CP(hull_verts, 3 * d->n_hull_verts, double); CP(hull_planes, 4 * d->n_hull_planes, double);
     CP(pair_a, d->n_pairs, int32_t); CP(pair_b, d->n_pairs, int32_t);
+#if BEDBATH
+    if (!d->bb_targets) { free(o); return -2; }
+    CP(bb_targets, 2 * 4 * AVR_BB_MAX_TARGETS, double);
+#endif
 #undef CP
     m->nl = L; m->nd = d->n_dof; m->nf = d->n_free; m->nb = B; m->ns = S;
     m->np = d->hc_n > 0 ? d->n_pairs_base : d->n_pairs;
@@ -1678,6 +1692,8 @@ EXPORT int avr_oracle_settle(avr_oracle *o, int n_frames, float *obs) {
 #if SCRATCH
         scratch_target(m, st, w);
         if (obs) scratch_observe(m, st, w, 0.0f, obs + (size_t)e * K_OBS_DIM);   /* _get_obs([0], [0, 0]) */
+#elif BEDBATH
+        if (obs) bb_observe(m, st, 0.0f, obs + (size_t)e * K_OBS_DIM);           /* _get_obs([0], [0, 0]) (bed_bathing.py:351) */
 #else
         mouth_target(m, st, st + S_TASK + T_TARGET);
         if (obs) observe(m, st, w, 0.0f, obs + (size_t)e * K_OBS_DIM);

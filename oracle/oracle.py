@@ -19,7 +19,7 @@ def build():
 
 
 def _load(precision, task=0):
-    name = 'libavr_oracle%s%s.so' % ('_scratch' if task == 1 else '', '' if precision == 'f64' else '_f32')
+    name = 'libavr_oracle%s%s.so' % ({1: '_scratch', 2: '_bedbath'}.get(task, ''), '' if precision == 'f64' else '_f32')
     path = os.path.join(HERE, name)
     if not os.path.exists(path):
         build()
@@ -39,6 +39,8 @@ def _load(precision, task=0):
     lib.avr_oracle_last_error.argtypes = [vp]
     lib.avr_oracle_last_error.restype = C.c_char_p
     lib.avr_oracle_state_words.restype = C.c_int
+    if task == 2:
+        lib.avr_oracle_bb_closest.argtypes = [vp, C.c_int, vp]
     return lib
 
 
@@ -46,7 +48,7 @@ _LIBS = {}
 
 
 def lib(precision='f64', task=0):
-    """The oracle build for `task` (0 FeedingJaco, 1 ScratchItchPR2; avr_model.h AVR_TASK_*)."""
+    """The oracle build for `task` (0 FeedingJaco, 1 ScratchItchPR2, 2 BedBathingPR2; avr_model.h AVR_TASK_*)."""
     key = (precision, task)
     if key not in _LIBS:
         _LIBS[key] = _load(precision, task)
@@ -65,7 +67,7 @@ class Oracle:
             raise RuntimeError('avr_oracle_create failed: %d' % rc)
         self.h = h
         self.words = self.lib.avr_oracle_state_words()
-        self.obs_dim = 30 if self.task == 1 else 25
+        self.obs_dim = {1: 30, 2: 24}.get(self.task, 25)
 
     def set_threads(self, n):
         self.lib.avr_oracle_set_threads(self.h, int(n))
@@ -121,6 +123,12 @@ class Oracle:
         pb = np.ascontiguousarray(pb, np.float64)
         r = self.lib.avr_oracle_narrowphase(self.h, sa, pa.ctypes.data, sb, pb.ctypes.data, thr, out.ctypes.data)
         return bool(r), out
+
+    def bb_closest(self, env=0):
+        """BedBathing: min getClosestPoints(tool, human, 4.0) distance of env's current state."""
+        out = np.zeros(1)
+        self.lib.avr_oracle_bb_closest(self.h, int(env), out.ctypes.data)
+        return float(out[0])
 
     def robot_fk(self, env=0):
         out = np.zeros((self.md.desc.n_links, 7))

@@ -13,14 +13,15 @@ def test_registry_has_every_reference_id():
     assert len(E.REGISTRY) == 49
     assert E.REGISTRY['FeedingJaco-v0'] == ('feeding', 'jaco', True)
     assert E.REGISTRY['ScratchItchPR2-v0'] == ('scratch_itch', 'pr2', True)
-    assert sum(v[2] for v in E.REGISTRY.values()) == 2
+    assert E.REGISTRY['BedBathingPR2-v0'] == ('bed_bathing', 'pr2', True)
+    assert sum(v[2] for v in E.REGISTRY.values()) == 3
     for k in E.REGISTRY:
         assert re.match(r'^[A-Za-z0-9]+-v0$', k)
 
 
 def test_unbuilt_ids_raise_not_implemented():
     with pytest.raises(NotImplementedError):
-        E.AVRVecEnv('BedBathingPR2-v0', 4)
+        E.AVRVecEnv('BedBathingJaco-v0', 4)
     with pytest.raises(KeyError):
         E.AVRVecEnv('NoSuchEnv-v0', 4)
 
@@ -37,6 +38,7 @@ def test_constants_follow_reference():
     assert E.MAX_EPISODE_STEPS == 200      # TimeLimit in assistive_gym/__init__.py
     assert E.SETTLE_FRAMES[ABI.TASK_FEEDING] == 100    # feeding.py:318-320
     assert E.SETTLE_FRAMES[ABI.TASK_SCRATCH] == 0      # scratch_itch.py reset: no settle frames
+    assert E.SETTLE_FRAMES[ABI.TASK_BEDBATH] == 0      # the arm settle precedes the robot placement
     P = ABI.FEEDING_PARAMS
     assert P['num_sub_steps'] == 2 and P['solver_iterations'] == 10    # feeding.py:289
     assert P['time_step'] == 0.02                                      # world_creation.py:75

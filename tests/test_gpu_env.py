@@ -128,3 +128,14 @@ def test_torch_vec_env_rollover_follows_device_done():
     assert np.all(g.iteration == 0) and np.all(g.episode == 1)
     np.testing.assert_array_equal(o.cpu().numpy(), g._obs)
     g.close()
+
+
+def test_bed_bathing_facade():
+    from avr import env as E
+    e = E.make('BedBathingPR2-v0')
+    o = e.reset()
+    assert o.shape == (24,) and np.all(np.isfinite(o)) and o[23] == 0
+    o, r, d, info = e.step(e.action_space.sample(np.random.default_rng(0)))
+    assert o.shape == (24,) and info['obs_robot_len'] == 24 and info['action_robot_len'] == 7
+    assert np.isfinite(r) and r < 0 and not d
+    e.close()

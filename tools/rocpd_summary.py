@@ -22,7 +22,7 @@ import numpy as np
 
 # launches per env-step: one take_step, one task launch and, per sub-step, the five sub-step kernels
 # (FeedingJaco: 5 frames x 2 sub-steps; ScratchItchPR2: 5 frames x 1 sub-step)
-SUBSTEPS = {'FeedingJaco-v0': 10, 'ScratchItchPR2-v0': 5}
+SUBSTEPS = {'FeedingJaco-v0': 10, 'ScratchItchPR2-v0': 5, 'BedBathingPR2-v0': 5}
 
 
 def step_kernels(task):
@@ -113,7 +113,7 @@ def main(pdir, tag, envs=4096, groups=None, task='FeedingJaco-v0'):
         out['hbm_bytes_per_step'] = fb + wb
         out['hbm_bytes_per_env_step'] = (fb + wb) / envs
         out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x dispatches per step (launches x env groups)'
-        json.dump(out, open(os.path.join(prof, 'pmc_traffic.json' if task == 'FeedingJaco-v0' else 'pmc_scratch.json'), 'w'), indent=1)
+        json.dump(out, open(os.path.join(prof, {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json'}.get(task, 'pmc_bedbath.json')), 'w'), indent=1)
     json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
     print(json.dumps(out, indent=1))
 
