@@ -326,8 +326,10 @@ def robot_fk_batch(A, Q):
 def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, tol=0.01):
     """Vectorised DLS IK (same acceptance rule as `ik`), one random restart per round for every
     env that has not converged yet.  init (N, restarts, n_arm): the restarts' starting joints,
-    drawn up front from each env's reset stream (reset_inputs).  Restated on the device by
-    avr_reset_ik (csrc/avr_reset_ik.hip), which runs the same rules one env at a time."""
+    drawn up front from each env's reset stream (reset_inputs).  Every env runs on its own: it
+    stops updating at the first 10th iteration at which it has converged, so its result does not
+    depend on the other envs of the batch (or on how envs are sharded over GPUs).  Restated on the
+    device by avr_reset_ik (csrc/avr_reset_ik.hip), which runs the same rules one env at a time."""
     N = tpos.shape[0]
     restarts = init.shape[1]
     chain = _chain(A, link)
@@ -344,6 +346,7 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, t
         Q = np.repeat(q0[None], len(idx), 0)
         Q[:, arm_dofs] = init[idx, r]
         tp, tq = tpos[idx], tquat[idx]
+        live = np.ones(len(idx), bool)     # per env: stops at the first 10th iteration that has converged
         for it in range(iters):
             CP, CQ, AX, OR = robot_fk_batch(A, Q)
             ep = tp - CP[:, link]
@@ -353,8 +356,10 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, t
             ang = 2.0 * np.arctan2(s, dq[:, 3])
             er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
             err = np.concatenate([ep, er], 1)
-            if it % 10 == 9 and np.all(np.linalg.norm(ep, axis=1) < 1e-5) and np.all(np.linalg.norm(er, axis=1) < 1e-4):
-                break
+            if it % 10 == 9:
+                live &= ~((np.linalg.norm(ep, axis=1) < 1e-5) & (np.linalg.norm(er, axis=1) < 1e-4))
+                if not live.any():
+                    break
             J = np.zeros((len(idx), 6, len(arm_dofs)))
             for c, l in enumerate(cols):
                 if l < 0:
@@ -363,7 +368,8 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, t
                 J[:, 3:, c] = AX[:, l]
             JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
             step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, err[..., None])
-            Q[:, arm_dofs] = np.clip(Q[:, arm_dofs] + step[..., 0], lower, upper)
+            rows = np.nonzero(live)[0]
+            Q[np.ix_(rows, arm_dofs)] = np.clip(Q[:, arm_dofs] + step[..., 0], lower, upper)[rows]
         CP, CQ, _, _ = robot_fk_batch(A, Q)
         pe = np.linalg.norm(tp - CP[:, link], axis=1)
         qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))

@@ -1,5 +1,7 @@
 """Env sharding + rollout all-gather (the multi-GPU data path of bench.py) on CPU with gloo,
-world_size 2: the gathered rollout equals the single-process rollout of all global envs."""
+world_size 2: each rank simulates its shard of global env ids on the CPU oracle (reset states
+and actions keyed by global id, as on the GPUs) and the gathered rollout equals the
+single-process rollout of all global envs, bit for bit."""
 import os
 import socket
 
@@ -17,29 +19,40 @@ def _free_port():
     return p
 
 
-def _fake_step(env_ids, t):
-    """Deterministic per-global-env outputs standing in for a sim step (host Philox actions)."""
-    from avr import _lib
-    a = _lib.random_actions(1001, env_ids, t).astype(np.float32)
-    obs = np.concatenate([a, a, a, a[:, :4]], 1)            # 25
-    rew = a.sum(1)
-    info = a[:, :2] * 3
-    done = (a[:, 0] > 0.5).astype(np.uint8)
-    return obs, rew, info, done
+SETTLE, G = 20, 3
 
 
-def _worker(rank, world, port, E, G, q):
+def _rollout(ids, steps):
+    """FeedingJaco rollout of the global envs `ids` on the CPU oracle: reset states from the host
+    reset path keyed by global id, a settle, then `steps` gym steps of the Philox action stream --
+    what one rank of bench.py runs on its shard (the oracle stands in for the GPU)."""
+    from avr import _abi as ABI, _lib, reset as RS
+    from oracle.oracle import Oracle
+    A = ABI.load_scene()
+    md = ABI.ModelDesc(A)
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(ids), impairment='random')
+    o = Oracle(md, len(ids))
+    o.set_state(S)
+    o.settle(SETTLE)
+    out = []
+    for t in range(steps):
+        obs, rew, done, info = o.step(_lib.random_actions(1001, np.asarray(ids), t))
+        out.append((obs, rew, info, done.astype(np.uint8)))
+    return out
+
+
+def _worker(rank, world, port, E, q):
     import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'assistive-vr-gym_amd'))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, 'assistive-vr-gym_amd'))
+    sys.path.insert(0, root)
     from avr import dist as D
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     off, n = D.shard(E, rank)
-    ids = np.arange(off, off + n)
     roll = torch.zeros(G, E, D.ROLL_WIDTH)
-    for j in range(G):
-        obs, rew, info, done = _fake_step(ids, j)
+    for j, (obs, rew, info, done) in enumerate(_rollout(np.arange(off, off + n), G)):
         D.pack_rollout(roll, j, torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(info), torch.from_numpy(done))
     out = D.gather_rollouts(roll)
     if rank == 0:
@@ -49,22 +62,21 @@ def _worker(rank, world, port, E, G, q):
 
 
 def test_rollout_gather_world2_matches_single_process():
-    import sys
-    from avr import dist as D
-    world, E, G = 2, 6, 3
+    """Two gloo ranks, each simulating its shard (env_offset = rank x E) and packing its rollout as
+    bench.py does; the all-gathered rollout equals one process simulating all global envs."""
+    world, E = 2, 3
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, E, G, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, E, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got = q.get(timeout=300)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    ids = np.arange(world * E)
-    for j in range(G):
-        obs, rew, info, done = _fake_step(ids, j)
+    ref = _rollout(np.arange(world * E), G)
+    for j, (obs, rew, info, done) in enumerate(ref):
         assert np.array_equal(got[j, :, :25], obs)
         assert np.array_equal(got[j, :, 25], rew)
         assert np.array_equal(got[j, :, 26:28], info)

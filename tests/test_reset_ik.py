@@ -17,7 +17,8 @@ MD = ABI.ModelDesc(A)
 
 
 def _host_ik_per_env(S, t7, init, q0):
-    """ik_batch one env at a time: its early exit then depends on that env alone, the device's rule."""
+    """ik_batch one env at a time (ik_batch's per-env early exit makes this equal to one batched
+    call; test_ik_batch_is_batch_independent)."""
     lower, upper = RS.arm_limits(MD)
     tool = int(A['task_tool_link'])
     Q, ok = [], []
@@ -38,6 +39,14 @@ def test_reset_inputs_reproduce_host_reset():
     np.testing.assert_allclose(Si, S, rtol=0, atol=1e-12)
     assert [m['gender'] for m in mi] == [m['gender'] for m in meta]
     assert [m['impairment'] for m in mi] == [m['impairment'] for m in meta]
+
+
+def test_ik_batch_is_batch_independent():
+    """An env's reset state does not depend on the other envs of the batch (per-env early exit),
+    so sharded resets equal single-process ones (multi-GPU)."""
+    S1, _ = RS.batch_reset_states_fast(A, MD, 1001, list(range(6)), impairment='random')
+    S2, _ = RS.batch_reset_states_fast(A, MD, 1001, [3, 4, 5], impairment='random')
+    np.testing.assert_array_equal(S1[3:], S2)
 
 
 def test_restart_draws_follow_the_env_stream():
