@@ -142,6 +142,7 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     if (cfg->flags & AVR_CFG_RESERVED_MASK) { int r = fail(s, -1, "avr_config.flags 0x%x: no flag is defined", (unsigned)cfg->flags); *out = s; return r; }
     const int hc = d->hc_n > 0 ? d->hc_n : 0;
     if (d->task != AVR_TASK) { int r = fail(s, -2, "model task %d does not match this instantiation (%d)", (int)d->task, (int)AVR_TASK); *out = s; return r; }
+    if (d->n_dof != K_ND) { int r = fail(s, -2, "model has %d robot DoFs, this instantiation %d", (int)d->n_dof, (int)K_ND); *out = s; return r; }
     if (d->n_links + hc > K_MAX_LINKS || d->n_dof + hc > K_MAX_DOF || d->n_free > K_MAX_FREE || d->n_human > K_MAX_HUMAN ||
         d->n_bodies > MAXB || d->n_pairs > 65535 || d->n_shapes > MAXSH || d->n_arm > K_ACT_DIM || hc > K_HC_N || hc > AVR_DESC_HC ||
         d->n_free < 1 || d->robot_gravity[0] != 0.0 || d->robot_gravity[1] != 0.0 || d->robot_gravity[2] != 0.0) {

@@ -219,9 +219,32 @@ AVR_DI void dof_col(const KModel &m, const EnvLDS &L, int j, v3 p, v3 &lin, v3 &
     }
 }
 
-// Mass matrix: one lane per lower-triangle entry (a,b); Cholesky on lane 0 in LDS.  Rows and
+// Mass matrix: one lane per lower-triangle entry (a,b), then the Cholesky factor in LDS.  Rows and
 // columns beyond nd are padded with the identity so M^-1 solves run over MAXD unrolled.
-AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x);
+
+// x = M^-1 e_c for a column c of the block [B0, B1) of the block-diagonal factor (entries of x
+// outside the block are 0): forward / back substitution over the block only -- the full-size solve
+// on e_c adds nothing but products with exact zeros (the other block, the zero head of y)
+template <int B0, int B1>
+AVR_DI void chol_solve_block(const EnvLDS &L, int c, float *x) {
+    float y[MAXD];
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) { y[i] = 0.f; x[i] = 0.f; }
+#pragma unroll
+    for (int i = B0; i < B1; i++) {
+        float s = i == c ? 1.f : 0.f;
+#pragma unroll
+        for (int k = B0; k < i; k++) s -= L.Mi[i][k] * y[k];
+        y[i] = s / L.Mi[i][i];
+    }
+#pragma unroll
+    for (int i = B1 - 1; i >= B0; i--) {
+        float s = y[i];
+#pragma unroll
+        for (int k = i + 1; k < B1; k++) s -= L.Mi[k][i] * x[k];
+        x[i] = s / L.Mi[i][i];
+    }
+}
 
 AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
     PROF_START(pm);
@@ -268,31 +291,48 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
     }
     SYNC();
     PROF_STOP(24, pm);
-    // column Cholesky, rows of each column in parallel (one lane per row)
+    // column Cholesky, rows of each column in parallel (one lane per row).  M is block diagonal:
+    // the robot's K_ND DoFs, then the articulated human chain's (and identity padding), which share
+    // no link.  The two blocks factor side by side -- iteration j takes robot column j and chain
+    // column K_ND + j -- and skip the cross-block terms, which are exact zeros: the same values,
+    // bit for bit, as the full column loop.
+    static_assert(K_ND <= MAXD, "robot block");
+    constexpr int NH = MAXD - K_ND;
+    constexpr int NJ = K_ND > NH ? K_ND : NH;
     int ok = 1;
-    for (int j = 0; j < MAXD; j++) {
-        float s = L.Mi[j][j];
-        for (int k = 0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
-        if (s <= 0.f) ok = 0;
-        const float d = sqrtf(fmaxf(s, 1e-30f));
-        float t = 0.f;
+    {
         const int i = lane;
-        if (i > j && i < MAXD) {
-            t = L.Mi[i][j];
-            for (int k = 0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
+        const bool rob = i < K_ND;
+        const int k0 = rob ? 0 : K_ND;         // the first column of this lane's block
+        for (int jj = 0; jj < NJ; jj++) {
+            const int j = rob ? jj : K_ND + jj;    // this lane's block's column
+            const bool live = rob ? jj < K_ND : (jj < NH && i < MAXD);
+            float s = 0.f, t = 0.f;
+            if (live) {
+                s = L.Mi[j][j];
+                for (int k = k0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
+                if (i > j) {
+                    t = L.Mi[i][j];
+                    for (int k = k0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
+                }
+            }
+            // every column's diagonal is positive in exact arithmetic; a lane of either block reports
+            const int bad = __any(live && s <= 0.f);
+            if (bad) ok = 0;
+            const float d = sqrtf(fmaxf(s, 1e-30f));
+            SYNC();
+            if (live && i > j) L.Mi[i][j] = t / d;
+            if (live && i == j) L.Mi[j][j] = d;
+            SYNC();
         }
-        SYNC();
-        if (i > j && i < MAXD) L.Mi[i][j] = t / d;
-        if (i == j) L.Mi[j][j] = d;
-        SYNC();
     }
     PROF_STOP(25, pm);
-    // columns of M^-1 (one lane per DoF): every robot row gets M^-1 J^T from these
+    // columns of M^-1 (one lane per DoF), each within its block: every robot row gets M^-1 J^T
+    // from these
     if (lane < MAXD) {
-        float e[MAXD], x[MAXD];
-#pragma unroll
-        for (int k = 0; k < MAXD; k++) e[k] = k == lane ? 1.f : 0.f;
-        chol_solve(m, L, e, x);
+        float x[MAXD];
+        if (lane < K_ND) chol_solve_block<0, K_ND>(L, lane, x);
+        else chol_solve_block<K_ND, MAXD>(L, lane, x);
 #pragma unroll
         for (int k = 0; k < MAXD; k++) L.Minv[k][lane] = x[k];
     }
@@ -317,26 +357,6 @@ AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
 #pragma unroll
         for (int k = 0; k < MAXD; k++) s += Mv[i * MAXD + k] * x[k];
         y[i] = s;
-    }
-}
-
-// x = M^-1 b with the Cholesky factor in LDS; fixed-size, fully unrolled (register arrays)
-AVR_DI void chol_solve(const KModel &m, const EnvLDS &L, const float *b, float *x) {
-    (void)m;
-    float y[MAXD];
-#pragma unroll
-    for (int i = 0; i < MAXD; i++) {
-        float s = b[i];
-#pragma unroll
-        for (int k = 0; k < i; k++) s -= L.Mi[i][k] * y[k];
-        y[i] = s / L.Mi[i][i];
-    }
-#pragma unroll
-    for (int i = MAXD - 1; i >= 0; i--) {
-        float s = y[i];
-#pragma unroll
-        for (int k = i + 1; k < MAXD; k++) s -= L.Mi[k][i] * x[k];
-        x[i] = s / L.Mi[i][i];
     }
 }
 
@@ -1632,6 +1652,7 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     if (lane == 0) {
         cs[CS_NSP] = __int_as_float(nsp); cs[CS_FLAGS] = __int_as_float(L.flags);
         cs[CS_N0] = __int_as_float(n0); cs[CS_N1] = __int_as_float(n1);
+        cs[CS_COOP] = 0.f;
     }
     PROF_STOP(2, pt);
 }
@@ -2496,6 +2517,7 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
     float4 *o = (float4 *)(cs + CS_RES) + 2 * k;
     o[0] = make_float4(__int_as_float(rc), nB.x, nB.y, nB.z);
     o[1] = make_float4(pB.x, pB.y, pB.z, d);
+    if (rc == 2) cs[CS_COOP] = 1.f;      // (every writer stores the same value)
 }
 
 // the listed pairs (n of them) that the lane path left to the wave-cooperative narrowphase (rc 2:
@@ -2697,7 +2719,10 @@ __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__
 #ifdef AVR_WAVETIME   // [4][env] (start, end) in 100 MHz ticks
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    np_coop(m, cs, __float_as_int(gld(cs + CS_NSP)), E);
+    // most envs have no pair for the cooperative path: the narrowphase kernel's flag says so without
+    // a scan of the per-pair results (the flag is written only by np_store, rc 2, after the pair
+    // kernel cleared it in this sub-step)
+    if (gld(cs + CS_COOP) != 0.f) np_coop(m, cs, __float_as_int(gld(cs + CS_NSP)), E);
 #ifdef AVR_WAVETIME
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
     if (m.prof && lane_id() == 0) { m.prof[((size_t)4 * n_envs + env) * 2] = wt0; m.prof[((size_t)4 * n_envs + env) * 2 + 1] = wt1; }

@@ -52,7 +52,8 @@ static_assert(MAXD <= 16 * NDL && MAXL <= 32, "DoF slots per lane / 32-bit link 
 #define CS_ORG (CS_AX + 4 * MAXL)                   // [MAXL][4] joint origins (world)
 #define CS_L0 (CS_ORG + 4 * MAXL)                   // [MAXSP][2] the sphere-hull pairs, ascending: (k | ba << 16 | bb << 24, sa | sb << 16)
 #define CS_L1 (CS_L0 + 2 * MAXSP)                   // [MAXSP][2] the other pairs, ascending, the same entries
-#define CS_WORDS (CS_L1 + 2 * MAXSP)
+#define CS_COOP (CS_L1 + 2 * MAXSP)                 // nonzero: some pair of this sub-step was left to the coop kernel (rc 2)
+#define CS_WORDS (CS_COOP + 4)                      // (keeps every env's CS_RES 16-byte aligned)
 static_assert(MAXB <= 256 && MAXSP <= 65536, "narrowphase list entries pack k (16 bits) and two body indices (8 bits each)");
 
 // Articulated links: the robot's nl links, then (impairment 'tremor') the head/neck chain's

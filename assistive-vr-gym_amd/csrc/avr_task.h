@@ -45,9 +45,11 @@
 #define K_HUMAN_GRAVITY 0       // robot, human and spoon gravity are 0 (feeding.py:285-287)
 #define K_TOOL_PIVOT 0          // the spoon's base COM is its body frame
 #define K_PR2 0
+#define K_ND 10                 // robot DoFs (Jaco); the articulated human chain's DoFs follow
 #elif AVR_TASK == AVR_TASK_SCRATCH || AVR_TASK == AVR_TASK_BEDBATH
 // the PR2 family: ScratchItchPR2 and BedBathingPR2 share the state layout (AVR_SI_*)
 #define K_PR2 1
+#define K_ND 14                 // robot DoFs (PR2 left-arm subtree); the human arm chain's DoFs follow
 #define K_MAX_LINKS AVR_SI_MAX_LINKS
 #define K_MAX_DOF AVR_SI_MAX_DOF
 #define K_HC_N AVR_SI_HC_N

@@ -1,5 +1,6 @@
-"""Bit-identity fingerprint of the shipped FeedingJaco kernels: reset states (impairment 'random'),
-100 settle frames, then K gym steps of Philox random actions.  Writes every step's obs / reward /
+"""Bit-identity fingerprint of the shipped kernels: reset states (FeedingJaco: impairment 'random'
+and 100 settle frames; TASK=1/2: the PR2 tasks' bench reset pool), then K gym steps of Philox
+random actions.  Writes every step's obs / reward /
 info and the final state to an .npz, so that a refactor of the kernels can be checked bit for bit
 against a run of the previous build (python tools/fingerprint.py OUT.npz [REF.npz]).
 """
@@ -16,12 +17,18 @@ sys.path.insert(0, ROOT)
 
 def run(n=512, k=20, lib=None):
     from avr import _abi as ABI, reset as RS, _lib
-    A = ABI.load_scene()
+    task = int(os.environ.get('TASK', '0'))
+    A = ABI.load_scene(task)
     md = ABI.ModelDesc(A)
-    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)), impairment='random')
+    if task == 0:
+        S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)), impairment='random')
+    else:
+        import bench
+        S, _ = bench.reset_pool(task, A, md, list(range(32)), 'random')
+        S = np.tile(S, ((n + len(S) - 1) // len(S), 1))[:n]
     sim = _lib.Sim(md, n, seed=1001)
     sim.set_state(S.astype(np.float32))
-    sim.settle(100)
+    sim.settle(100 if task == 0 else 0)
     out = dict(settle=sim.get_state())
     obs, rew, info = [], [], []
     for t in range(k):

@@ -10,14 +10,20 @@ lib = _lib.load(so)
 lib.avr_set_profile_buffer.argtypes = [C.c_void_p, C.c_void_p]
 import torch
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-A = ABI.load_scene(); md = ABI.ModelDesc(A)
-S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
+TASK = int(os.environ.get('TASK', '0'))        # 0 FeedingJaco, 1 ScratchItchPR2, 2 BedBathingPR2
+A = ABI.load_scene(TASK); md = ABI.ModelDesc(A)
+L = md.layout
+if TASK == 0:
+    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(min(N, 256))), impairment=os.environ.get('IMPAIRMENT', 'random'))
+else:
+    import bench
+    S, _ = bench.reset_pool(TASK, A, md, list(range(min(N, 64))), os.environ.get('IMPAIRMENT', 'random'))
 S = np.tile(S, ((N + len(S) - 1) // len(S), 1))[:N]
 sim = _lib.Sim(md, N)
 SLOTS = 48
 prof = torch.zeros(N * SLOTS, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
-sim.set_state(S.astype(np.float32)); sim.settle(100)
+sim.set_state(S.astype(np.float32)); sim.settle(100 if TASK == 0 else 0)
 names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-',
          ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '-', '-', '-',
          '#np sph-hull', '#np other', '#np refill trips', '#np ph_steps', '#np GJK it', '#np GJK it max', '#np GJK pairs', '#np closed form',
@@ -36,4 +42,4 @@ for t in range(int(os.environ.get('PROF_STEPS', '3'))):
             continue
         print('  %-13s %6.2f%%  mean %.3g  max %.3g' % (nm, 100 * p[:, k].mean() / tot, p[:, k].mean(), p[:, k].max()))
 St = sim.get_state()
-print('ncp mean', St[:, ABI.S_TASK + ABI.T_NCP].mean(), 'flags', np.unique(St[:, ABI.S_TASK + ABI.T_FLAGS]))
+print('ncp mean', St[:, L.S_TASK + L.T_NCP].mean(), 'flags', np.unique(St[:, L.S_TASK + L.T_FLAGS]))
