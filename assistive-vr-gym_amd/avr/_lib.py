@@ -19,7 +19,7 @@ EXPORTS = [
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_env_groups', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
-    'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik',
+    'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik', 'avr_base_search',
 ]
 
 
@@ -88,6 +88,7 @@ def load(path=LIB_PATH):
     lib.avr_get_contact_summary.argtypes = [vp, vp]
     lib.avr_get_flags.argtypes = [vp, vp]
     lib.avr_reset_ik.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, C.c_int32, vp, vp]
+    lib.avr_base_search.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp, vp]
     if lib.avr_abi_version() != ABI.ABI_VERSION or any(
             lib.avr_task_state_words(t) != L.STATE_WORDS or lib.avr_task_obs_dim(t) != L.OBS_DIM or lib.avr_task_act_dim(t) != L.ACT_DIM
             for t, L in ABI.LAYOUTS.items()):
@@ -184,6 +185,26 @@ class Sim:
                                         int(init.shape[1]), int(iters), float(tol), None if box is None else box.ctypes.data, int(frames),
                                         obs.ctypes.data, ok.ctypes.data))
         return obs, ok.astype(bool)
+
+    def base_search(self, base7, rest, tstart, goals, iters=200, tol=0.03, per_attempt=False):
+        """PR2 base-pose search on the device (include/avr.h avr_base_search): base7 (n, attempts, 7),
+        rest (n, attempts, n_arm), tstart (n, 3), goals (n, 3, 3).  Returns (best (n,) attempt index,
+        ok (n,) bool, q_arm (n, n_arm)[, res (n, attempts, 4) when per_attempt])."""
+        b = np.ascontiguousarray(base7, np.float32)
+        assert b.ndim == 3 and b.shape[2] == 7
+        n, att = b.shape[:2]
+        r = np.ascontiguousarray(rest, np.float32)
+        na = r.shape[2]
+        assert r.shape[:2] == (n, att)
+        t = np.ascontiguousarray(tstart, np.float32).reshape(n, 3)
+        g = np.ascontiguousarray(goals, np.float32).reshape(n, 9)
+        best = np.zeros(n, np.int32)
+        ok = np.zeros(n, np.uint8)
+        q = np.zeros((n, na), np.float32)
+        res = np.zeros((n, att, 4), np.float32) if per_attempt else None
+        self._chk(self.lib.avr_base_search(self.h, int(n), int(att), b.ctypes.data, r.ctypes.data, t.ctypes.data, g.ctypes.data, int(iters),
+                                           float(tol), best.ctypes.data, ok.ctypes.data, q.ctypes.data, None if res is None else res.ctypes.data))
+        return (best, ok.astype(bool), q) + ((res,) if per_attempt else ())
 
     def substep(self, dt):
         self._chk(self.lib.avr_substep(self.h, dt))

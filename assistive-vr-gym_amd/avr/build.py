@@ -17,7 +17,7 @@ ARCH = os.environ.get('AVR_OFFLOAD_ARCH', 'gfx950')
 # one translation unit per task (the shared kernel / C-ABI sources instantiated in a namespace,
 # csrc/avr_task_tu.h), the extern "C" dispatcher, the hull support tables
 SOURCES = ['avr_task_feeding.hip', 'avr_task_scratch.hip', 'avr_task_bedbath.hip', 'avr_api.cpp', 'avr_hulltab.cpp']
-HEADERS = ['avr_math.h', 'avr_kmodel.h', 'avr_task.h', 'avr_task_tu.h', 'avr_kernel.hip', 'avr_capi.hip', 'avr_glue_scratch.hip', 'avr_glue_bedbath.hip', 'avr_reset_ik.hip']
+HEADERS = ['avr_math.h', 'avr_kmodel.h', 'avr_task.h', 'avr_task_tu.h', 'avr_kernel.hip', 'avr_capi.hip', 'avr_glue_scratch.hip', 'avr_glue_bedbath.hip', 'avr_reset_ik.hip', 'avr_base_search.hip']
 OBJDIR = os.path.join(PKG, 'build')
 
 

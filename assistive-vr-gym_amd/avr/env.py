@@ -172,7 +172,8 @@ class AVRVecEnv:
 
     impairment: 'random' (the tasks' own setting, feeding.py:175 / scratch_itch.py:178: none /
     limits / weakness / tremor, one draw per episode), a fixed one of those four, or 'no_tremor'.
-    reset_ik: 'device' (FeedingJaco default: avr_reset_ik) or 'host' (host IK, then avr_reset).
+    reset_ik: 'device' (default: FeedingJaco's IK through avr_reset_ik, the PR2 tasks' base-pose
+    search through avr_base_search) or 'host' (the fp64 host restatements, then avr_reset).
     reset_stream: FeedingJaco's reset draws, 'philox' (counter-based, vectorised; default) or
     'numpy' (the per-env Generator stream of the bench's reset pools and the golden fixtures).
     """
@@ -195,6 +196,7 @@ class AVRVecEnv:
         self.task = self.md.task
         self.L = self.md.layout
         self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'
+        self.device_search = self.task != ABI.TASK_FEEDING and reset_ik == 'device'
         self.scratch_attempts, self.scratch_iters = scratch_attempts, scratch_iters
         self.reset_stream = reset_stream
         self.device = device
@@ -274,11 +276,12 @@ class AVRVecEnv:
         if self.task == ABI.TASK_BEDBATH:
             from . import reset_bedbath as RBB
             Si, _ = RBB.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=eps,
-                                           attempts=self.scratch_attempts, iters=self.scratch_iters, device=self.device)
+                                           attempts=self.scratch_attempts, iters=self.scratch_iters, device=self.device,
+                                           sim=self.sim if self.device_search else None)
         elif self.task == ABI.TASK_SCRATCH:
             from . import reset_scratch as RSS
             Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
-                                           attempts=self.scratch_attempts, iters=self.scratch_iters)
+                                           attempts=self.scratch_attempts, iters=self.scratch_iters, sim=self.sim if self.device_search else None)
         else:
             Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
                                                stream=self.reset_stream)

@@ -145,9 +145,10 @@ def settled_arms(A, md, device=0, frames=None, runner=None):
     return out
 
 
-def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, attempts=100, iters=200, settled=None, device=0):
+def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, attempts=100, iters=200, settled=None, device=0, sim=None):
     """Initial BedBathing state blocks (float64 (N, BB.STATE_WORDS)) and per-env metadata.
-    settled: settled_arms() output (computed on the device when None)."""
+    settled: settled_arms() output (computed on the device when None).  sim: run the base-pose
+    search on the device (reset_scratch.position_robot_toc)."""
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
@@ -166,7 +167,7 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, attemp
         goals[k] = slots[js, :3]                                       # shoulder, elbow, wrist (:305-307)
         S[k, BB.S_Q + nd:BB.S_Q + nd + len(qc)] = qc
     tstart = np.repeat(START_GOAL[None], N, 0)
-    bp, bq, Qa, _, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, tstart=tstart, pos_offset=(0, 0, 0))
+    bp, bq, Qa, _, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, tstart=tstart, pos_offset=(0, 0, 0), sim=sim)
     from .reset_scratch import arm_fk
     for d in md.finger_dofs:                                           # set_gripper_open_position(0.2, set_instantly)
         Qa[:, d] = md.params['finger_target']

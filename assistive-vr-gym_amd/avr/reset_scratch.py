@@ -25,7 +25,7 @@ import numpy as np
 
 from . import _abi as ABI
 from . import geom as G
-from .reset import _cross, _impairment, _qaxis, _qmul, _qrot, _rng, human_link_poses
+from .reset import _cross, _impairment, _qaxis, _qmul, _qrot, _rng, arm_limits, human_link_poses
 
 SI = ABI.SI
 HUMAN_SCALED = set(range(7, 14)) | set(range(17, 24)) | set(range(24, 28))   # limit_scale joints (human_creation.py)
@@ -127,11 +127,13 @@ def arm_jacobian(A, link, cols, CP, AX, OR):
 
 def ik_dls(A, link, Q0, bp, bq, tp, tq, dofs, lower, upper, iters):
     """Damped least squares on the rows of Q0 (N, nd) towards positions tp (N, 3) and, when tq is
-    not None, orientations tq (N, 4) of link's COM frame (FK of link's chain only; rows that have
-    converged stop moving, and the loop ends once all have)."""
+    not None, orientations tq (N, 4) of link's COM frame (FK of link's chain only).  A row stops
+    at an iteration it % 10 == 9 where every component of its error is below 1e-6 (the rule of
+    the device search, avr_base_search); the loop ends once every row has."""
     Q = Q0.copy()
     chain = _chain(A, link)
     cols = _chain_cols(A, link, dofs)
+    live = np.ones(len(Q), bool)
     for it in range(iters):
         CP, CQ, AX, OR = arm_fk(A, Q, bp, bq, chain)
         ep = tp - CP[:, link]
@@ -147,12 +149,15 @@ def ik_dls(A, link, Q0, bp, bq, tp, tq, dofs, lower, upper, iters):
         else:
             err = ep
             Jr = J[:, :3]
-        if it % 10 == 9 and np.all(np.abs(err) < 1e-6):
-            break
+        if it % 10 == 9:
+            live &= ~np.all(np.abs(err) < 1e-6, axis=1)
+            if not live.any():
+                break
         k = Jr.shape[1]
         JJ = Jr @ np.transpose(Jr, (0, 2, 1)) + 1e-4 * np.eye(k)[None]
         step = np.transpose(Jr, (0, 2, 1)) @ np.linalg.solve(JJ, err[..., None])
-        Q[:, dofs] = np.clip(Q[:, dofs] + step[..., 0], lower, upper)
+        Qn = np.clip(Q[:, dofs] + step[..., 0], lower, upper)
+        Q[:, dofs] = np.where(live[:, None], Qn, Q[:, dofs])
     CP, CQ, AX, OR = arm_fk(A, Q, bp, bq, chain)
     return Q, CP, CQ, AX, OR
 
@@ -168,35 +173,80 @@ def jlwki(J, q, lower, upper):
     return np.power(det, 1.0 / 6.0) / (np.trace(M, axis1=1, axis2=2) / 6.0)
 
 
-def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart=None, pos_offset=(0.1, 0, 0)):
+def base_search_draws(rngs, attempts, lo, hi, pos_offset=(0.1, 0, 0), tstart=None):
+    """Per-env draws of position_robot_toc: the start goal (ScratchItch: jittered, drawn first;
+    tstart given: none), then one block of `attempts` rows (base x, base y, yaw, rest pose) per
+    env (env.py:509-511, util.py:99).  Returns tstart (N, 3), base7 (N, attempts, 7), rest
+    (N, attempts, n_arm)."""
+    N, na = len(rngs), len(lo)
+    if tstart is None:
+        tstart = np.stack([np.array([-0.55, 0, 0.8]) + r.uniform(-0.05, 0.05, size=3) for r in rngs])
+    U = np.stack([r.random((attempts, 3 + na)) for r in rngs]) if N else np.zeros((0, attempts, 3 + na))
+    base = np.zeros((N, attempts, 7))
+    base[..., :3] = np.array([-0.85, -0.4, 0]) + np.asarray(pos_offset, float)
+    base[..., 0] += -0.5 + 0.5 * U[..., 0]                     # uniform(-0.5, 0) (right side)
+    base[..., 1] += -0.5 + U[..., 1]                           # uniform(-0.5, 0.5)
+    yaw = np.deg2rad(-30 + 60 * U[..., 2])                     # uniform(-30, 30) degrees
+    base[..., 5] = np.sin(0.5 * yaw)
+    base[..., 6] = np.cos(0.5 * yaw)
+    rest = lo + (hi - lo) * U[..., 3:]
+    return np.asarray(tstart, float), base, rest
+
+
+def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart=None, pos_offset=(0.1, 0, 0), sim=None):
     """Batched position_robot_toc for the PR2 (env.py:489-585; scratch_itch.py:189-190,
     bed_bathing.py:317): per env, `attempts` random base poses; at each the start goal (link 76
     to the start target with identity orientation, base offset pos_offset) must be reached (0.03
     on position and quaternion), then the shoulder / elbow / wrist positions count as further
     goals; the best base maximises goals reached, then summed manipulability.  tstart: the start
     targets (N, 3), or None for ScratchItch's jittered target (drawn first from each stream).
+    sim: a _lib.Sim of the task -- the search runs on the device (avr_base_search, fp32), else
+    here in fp64 (the device search's checker).
     Returns (base_pos, base_quat, arm q, start target, ok) per env."""
     N = len(rngs)
     nd = int(A['n_dof'])
     arm = np.array(md.arm_dofs)
     link = int(A['task_tool_link'])
-    lo = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
-    hi = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
-    # draws per env: the start goal, then per attempt the base pose and the IK rest pose
-    if tstart is None:
-        tstart = np.stack([np.array([-0.55, 0, 0.8]) + r.uniform(-0.05, 0.05, size=3) for r in rngs])
-    M = N * attempts
-    bp = np.zeros((M, 3)); yaw = np.zeros(M); rest = np.zeros((M, len(arm)))
-    for e, r in enumerate(rngs):
+    lo, hi = arm_limits(md)
+    tstart, base, rest = base_search_draws(rngs, attempts, lo, hi, pos_offset, tstart)
+    if sim is not None:
+        best, ok, qa = sim.base_search(base, rest, tstart, human_goals, iters=iters, tol=0.03)
+        out_q = np.zeros((N, nd))
+        for d in md.finger_dofs:
+            out_q[:, d] = md.params['finger_target']
+        out_q[:, arm] = qa
+        b = base[np.arange(N), best]
+        return b[:, :3].copy(), b[:, 3:].copy(), out_q, tstart, ok
+    res = base_search_host(A, md, base, rest, tstart, human_goals, iters)
+    goals, manip, pe, Qs = res
+    out_bp, out_bq, out_q, ok = np.zeros((N, 3)), np.zeros((N, 4)), np.zeros((N, nd)), np.zeros(N, bool)
+    for e in range(N):
+        best = None
         for a in range(attempts):
-            k = e * attempts + a
-            bp[k] = np.array([-0.85, -0.4, 0]) + np.asarray(pos_offset, float) + np.array([r.uniform(-0.5, 0), r.uniform(-0.5, 0.5), 0])
-            yaw[k] = np.deg2rad(r.uniform(-30, 30))
-            rest[k] = r.uniform(lo, hi)
-    bq = np.stack([np.zeros(M), np.zeros(M), np.sin(0.5 * yaw), np.cos(0.5 * yaw)], 1)
+            g, mm = goals[e, a], manip[e, a]
+            if g > 0 and (best is None or g > goals[e, best] or (g == goals[e, best] and mm > manip[e, best])):
+                best = a
+        if best is None:                                  # no start goal reached: the closest attempt
+            best = int(np.argmin(pe[e]))
+        else:
+            ok[e] = True
+        out_bp[e], out_bq[e], out_q[e] = base[e, best, :3], base[e, best, 3:], Qs[e, best]
+    return out_bp, out_bq, out_q, tstart, ok
+
+
+def base_search_host(A, md, base, rest, tstart, human_goals, iters):
+    """Every attempt of the search in fp64: (goals reached or -1 (N, attempts), manipulability,
+    start-goal position error, start-goal joints (N, attempts, nd))."""
+    N, attempts = base.shape[:2]
+    M = N * attempts
+    nd = int(A['n_dof'])
+    arm = np.array(md.arm_dofs)
+    link = int(A['task_tool_link'])
+    lo, hi = arm_limits(md)
+    bp = base[..., :3].reshape(M, 3)
+    bq = base[..., 3:].reshape(M, 4)
     Q0 = np.zeros((M, nd))
-    for i, d in enumerate(arm):
-        Q0[:, d] = rest[:, i]
+    Q0[:, arm] = rest.reshape(M, len(arm))
     for d in md.finger_dofs:
         Q0[:, d] = md.params['finger_target']
     tp = np.repeat(tstart, attempts, 0)
@@ -210,31 +260,18 @@ def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart
     goals = ok0.astype(int)
     for g in range(3):                                   # shoulder, elbow, wrist (position only)
         hp = np.repeat(human_goals[:, g], attempts, 0)
-        Qg, CPg, _, AXg, ORg = ik_dls(A, link, np.where(ok0[:, None], Q0, Q0), bp, bq, hp, None, arm, lo, hi, iters)
+        Qg, CPg, _, AXg, ORg = ik_dls(A, link, Q0, bp, bq, hp, None, arm, lo, hi, iters)
         okg = ok0 & (np.linalg.norm(hp - CPg[:, link], axis=1) < 0.03)
         manip = manip + np.where(okg, jlwki(arm_jacobian(A, link, cols, CPg, AXg, ORg), Qg[:, arm], lo, hi), 0.0)
         goals = goals + okg.astype(int)
     goals = np.where(ok0, goals, -1).reshape(N, attempts)
-    manip = manip.reshape(N, attempts)
-    out_bp, out_bq, out_q, ok = np.zeros((N, 3)), np.zeros((N, 4)), np.zeros((N, nd)), np.zeros(N, bool)
-    for e in range(N):
-        best = None
-        for a in range(attempts):
-            g, mm = goals[e, a], manip[e, a]
-            if g > 0 and (best is None or g > goals[e, best] or (g == goals[e, best] and mm > manip[e, best])):
-                best = a
-        if best is None:                                  # no start goal reached: the closest attempt
-            best = int(np.argmin(pe.reshape(N, attempts)[e]))
-        else:
-            ok[e] = True
-        k = e * attempts + best
-        out_bp[e], out_bq[e], out_q[e] = bp[k], bq[k], Qs[k]
-    return out_bp, out_bq, out_q, tstart, ok
+    return goals, manip.reshape(N, attempts), pe.reshape(N, attempts), Qs.reshape(N, attempts, nd)
 
 
 # ----------------------------------------------------------------------------- full reset
-def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100, iters=200):
-    """Initial ScratchItch state blocks (float64 (N, SI.STATE_WORDS)) and per-env metadata."""
+def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100, iters=200, sim=None):
+    """Initial ScratchItch state blocks (float64 (N, SI.STATE_WORDS)) and per-env metadata.
+    sim: run the base-pose search on the device (position_robot_toc)."""
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
@@ -274,7 +311,7 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', 
         st[t + SI.T_TREMOR] = 1.0 if imp == 'tremor' else 0.0
         st[t + SI.T_STRENGTH] = strength
         meta.append(dict(gender=g, impairment=imp, limit_scale=ls, strength=strength))
-    bp, bq, Qa, tstart, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters)
+    bp, bq, Qa, tstart, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, sim=sim)
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
     link = int(A['task_tool_link'])
     piv = A['task_tool_pivot']

@@ -42,6 +42,9 @@
     int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init,      \
                      int32_t restarts, int32_t iters, float tol, const float *keepout8, int32_t n_frames,           \
                      float *host_obs, uint8_t *host_ok);                                                           \
+    int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest,            \
+                        const float *tstart3, const float *goals9, int32_t iters, float tol, int32_t *best,         \
+                        uint8_t *ok, float *q_arm, float *res4);                                                   \
     }
 
 AVR_TASK_DECLS(avr_feeding)
@@ -169,6 +172,10 @@ int avr_get_flags(avr_sim *s, int32_t *f) { DISPATCH(s, avr_get_flags(h, f)); }
 int avr_reset_ik(avr_sim *s, const uint8_t *m, const float *p, const float *t7, const float *init, int32_t r, int32_t it, float tol,
                  const float *box8, int32_t n, float *o, uint8_t *ok) {
     DISPATCH(s, avr_reset_ik(h, m, p, t7, init, r, it, tol, box8, n, o, ok));
+}
+int avr_base_search(avr_sim *s, int32_t n, int32_t a, const float *b7, const float *rest, const float *t3, const float *g9, int32_t it, float tol,
+                    int32_t *best, uint8_t *ok, float *q, float *res4) {
+    DISPATCH(s, avr_base_search(h, n, a, b7, rest, t3, g9, it, tol, best, ok, q, res4));
 }
 
 }  // extern "C"

@@ -44,6 +44,8 @@ struct avr_sim {
     size_t qcap;
     float *d_ik;                           // device scratch of avr_reset_ik (targets, restart draws, ok bytes)
     size_t ikcap;
+    float *d_bs;                           // device scratch of avr_base_search (draws, goals, per-attempt results)
+    size_t bscap;
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -493,6 +495,7 @@ int avr_destroy(avr_sim *s) {
     if (s->d_mask) (void)hipFree(s->d_mask);
     if (s->d_query) (void)hipFree(s->d_query);
     if (s->d_ik) (void)hipFree(s->d_ik);
+    if (s->d_bs) (void)hipFree(s->d_bs);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     for (int i = 0; i < s->ngroups; i++) {
         if (s->gstream[i]) (void)hipStreamDestroy(s->gstream[i]);
@@ -786,6 +789,52 @@ int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *t
         if (!mask[e]) continue;
         if (host_obs) memcpy(host_obs + e * K_OBS_DIM, o.data() + e * K_OBS_DIM, K_OBS_DIM * sizeof(float));
         if (host_ok) host_ok[e] = okh[e];
+    }
+    return 0;
+#endif
+}
+
+// ------------------------------------------------------------------ device base-pose search (PR2 tasks)
+int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest, const float *tstart3, const float *goals9,
+                    int32_t iters, float tol, int32_t *best, uint8_t *ok, float *q_arm, float *res4) {
+    CHECK_SIM(s);
+#if !K_PR2
+    (void)n; (void)attempts; (void)base7; (void)rest; (void)tstart3; (void)goals9; (void)iters; (void)tol; (void)best; (void)ok; (void)q_arm; (void)res4;
+    return fail(s, -1, "avr_base_search: the PR2 tasks' base-pose search (this task has a fixed robot base)");
+#else
+    const int na = s->km.n_arm;
+    if (n < 0 || attempts < 1 || iters < 1 || !(tol > 0.f)) return fail(s, -1, "avr_base_search: n >= 0, attempts, iters >= 1, tol > 0");
+    if (!base7 || !rest || !tstart3 || !goals9 || !best || !ok || !q_arm) return fail(s, -1, "avr_base_search: NULL buffer");
+    if (na < 1 || na > 8) return fail(s, -1, "avr_base_search: %d arm DoFs (1..8 supported)", na);
+    if (n == 0) return 0;
+    const size_t N = (size_t)n, M = N * (size_t)attempts;
+    // layout (floats): base7 [M][7], rest [M][na], tstart [N][3], goals [N][9], res [M][4], q [M][na], best [N] (int), ok [N] (bytes)
+    const size_t o_b = 0, o_r = o_b + 7 * M, o_t = o_r + M * na, o_g = o_t + 3 * N, o_res = (o_g + 9 * N + 3) & ~(size_t)3, o_q = o_res + 4 * M,
+                 o_best = o_q + M * na, o_ok = o_best + N, need = o_ok + (N + 3) / 4 + 1;
+    if (need > s->bscap) {
+        if (s->d_bs) HIPCHK(s, hipFree(s->d_bs));
+        s->d_bs = nullptr;
+        s->bscap = 0;
+        HIPCHK(s, hipMalloc(&s->d_bs, need * sizeof(float)));
+        s->bscap = need;
+    }
+    float *d = s->d_bs;
+    HIPCHK(s, hipMemcpyAsync(d + o_b, base7, 7 * M * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(d + o_r, rest, M * na * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(d + o_t, tstart3, 3 * N * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(d + o_g, goals9, 9 * N * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, avr_launch_base_search(&s->km, s->d_km, d + o_b, d + o_r, d + o_t, d + o_g, attempts, iters, tol, (float4 *)(d + o_res), d + o_q,
+                                     (int *)(d + o_best), (unsigned char *)(d + o_ok), n, s->stream));
+    std::vector<float> q(M * na);
+    HIPCHK(s, hipMemcpyAsync(best, d + o_best, N * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(ok, d + o_ok, N, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(q.data(), d + o_q, M * na * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (res4) HIPCHK(s, hipMemcpyAsync(res4, d + o_res, 4 * M * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    for (size_t e = 0; e < N; e++) {
+        const int b = best[e];
+        if (b < 0 || b >= attempts) return fail(s, -3, "avr_base_search: bad pick %d for env %d", b, (int)e);
+        memcpy(q_arm + e * na, q.data() + (e * attempts + b) * na, na * sizeof(float));
     }
     return 0;
 #endif

@@ -2540,12 +2540,24 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
             v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
             float d2 = 0.f;
             int nit, nk;
+#ifdef AVR_PROF
+            const unsigned long long c0t = __builtin_readcyclecounter();
+#endif
             const int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk);
 #ifdef AVR_PROF
             if (m.prof && lane == 0) {     // cooperative pairs, their GJK iterations, the time they took
+                const unsigned long long dc = __builtin_readcyclecounter() - c0t;
                 unsigned long long *pr = m.prof + (size_t)(cs - m.cscr) / CS_WORDS * AVR_PROF_SLOTS;
                 atomicAdd(pr + 11, 1ull);
                 atomicAdd(pr + 28, (unsigned long long)nit);
+                // by shape kinds: 19 sphere-hull, 20 hull-hull, 21 other; 22 big hull (no support
+                // table); 29 cycles, 30 the slowest pair's cycles
+                const bool ha = A.kind == AVR_HULL, hb = B.kind == AVR_HULL;
+                const bool sph = (A.kind == AVR_SPHERE && hb) || (B.kind == AVR_SPHERE && ha);
+                atomicAdd(pr + (sph ? 19 : (ha && hb) ? 20 : 21), 1ull);
+                if ((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0)) atomicAdd(pr + 22, 1ull);
+                atomicAdd(pr + 29, dc);
+                atomicMax(pr + 30, dc);
             }
 #endif
             SYNC();
@@ -3386,7 +3398,9 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
         mark(AVR_K_NARROW);
         hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 8 * NP_ENVS - 1) / (8 * NP_ENVS))), dim3(64), 0, stream, d_m, mask, env0, env1);
         mark(AVR_K_COOP);
+#ifndef AVR_EXP_NOCOOP    // (timing experiment only: results are wrong without it)
         hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
+#endif
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);

@@ -23,5 +23,6 @@ namespace AVR_NS {
 #include "avr_kmodel.h"
 #include "avr_kernel.hip"
 #include "avr_reset_ik.hip"
+#include "avr_base_search.hip"
 #include "avr_capi.hip"
 }  // namespace AVR_NS

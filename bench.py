@@ -54,12 +54,19 @@ def layout_bytes_per_env_step(L):
 
 
 def reset_pool(task, A, md, ids, impairment):
-    if task == 2:
-        from avr import reset_bedbath as RBB
-        return RBB.batch_reset_states(A, md, 1001, ids, attempts=25, iters=100)
-    if task == 1:
-        from avr import reset_scratch as RSS
-        return RSS.batch_reset_states(A, md, 1001, ids, impairment=impairment, attempts=25, iters=100)
+    """Reset states of the bench's env pool; the PR2 tasks' base-pose search runs on the device
+    (avr_base_search) with the reference's 100 attempts of 200 IK iterations."""
+    if task in (1, 2):
+        from avr import _lib
+        sim = _lib.Sim(md, 1)
+        try:
+            if task == 2:
+                from avr import reset_bedbath as RBB
+                return RBB.batch_reset_states(A, md, 1001, ids, sim=sim)
+            from avr import reset_scratch as RSS
+            return RSS.batch_reset_states(A, md, 1001, ids, impairment=impairment, sim=sim)
+        finally:
+            sim.close()
     from avr import reset as RS
     return RS.batch_reset_states_fast(A, md, 1001, ids, impairment=impairment)
 

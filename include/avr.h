@@ -157,6 +157,24 @@ const char *avr_last_error(avr_sim *sim);
 int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state, const float *target7, const float *init, int32_t restarts,
                  int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok);
 
+/* ---- device base-pose search (ScratchItchPR2, BedBathingPR2) ----
+ * avr_base_search: position_robot_toc (env.py:489-585; scratch_itch.py:189-190,
+ *   bed_bathing.py:317) for n envs on the device, one lane per (env, attempt).  Host buffers:
+ *   base7[n*attempts*7] each attempt's robot base pose (position, quaternion xyzw; the host draws
+ *   the random offset and yaw, env.py:509-511), rest[n*attempts*n_arm] its IK rest pose
+ *   (util.py:99), tstart3[n*3] the start goal of the tool link's COM (identity orientation),
+ *   goals9[n*9] the shoulder, elbow and wrist positions.  Per attempt: damped-least-squares IK
+ *   (`iters` updates, util.py:59-74 ik_jlwki with success threshold `tol`) to the start goal --
+ *   missed: the attempt is discarded -- then to each human goal; reached goals add their
+ *   joint-limit-weighted kinematic isotropy (env.py:536-553).  Per env the best attempt (most
+ *   goals, then manipulability, the first on ties; none reaching the start goal: the closest)
+ *   goes to best[n], ok[n] (1: start goal reached) and q_arm[n*n_arm] (its start-goal joints).
+ *   res4[n*attempts*4] (may be NULL) receives every attempt's {goals reached or -1,
+ *   manipulability, start position error, start quaternion distance}.  The state is not touched.
+ *   Returns -1 for FeedingJaco (fixed base). */
+int avr_base_search(avr_sim *sim, int32_t n, int32_t attempts, const float *base7, const float *rest, const float *tstart3,
+                    const float *goals9, int32_t iters, float tol, int32_t *best, uint8_t *ok, float *q_arm, float *res4);
+
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
  * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times
  * returns the accumulated milliseconds and launch counts per kernel kind

@@ -24,8 +24,8 @@ SLOTS = 48
 prof = torch.zeros(N * SLOTS, dtype=torch.int64, device='cuda')
 lib.avr_set_profile_buffer(sim.h, prof.data_ptr())
 sim.set_state(S.astype(np.float32)); sim.settle(100 if TASK == 0 else 0)
-names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop robot-robot', '#coop robot-free', '#coop robot-static', '#coop other', '-',
-         ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '-', '-', '-',
+names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop sph-hull', '#coop hull-hull', '#coop other', '#coop bighull', '-',
+         ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '#coop cycles', '#coop max cyc', '-',
          '#np sph-hull', '#np other', '#np refill trips', '#np ph_steps', '#np GJK it', '#np GJK it max', '#np GJK pairs', '#np closed form',
          '-', '-', '-', '-', '-', '-', '-', '-']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
@@ -38,7 +38,7 @@ for t in range(int(os.environ.get('PROF_STEPS', '3'))):
         if nm == '-':
             continue
         if nm.startswith('#'):
-            print('  %-13s per env-step mean %.1f (per substep %.1f)' % (nm, p[:, k].mean(), p[:, k].mean() / 10))
+            print('  %-13s per env-step mean %.1f (per substep %.1f), max %.0f' % (nm, p[:, k].mean(), p[:, k].mean() / 10, p[:, k].max()))
             continue
         print('  %-13s %6.2f%%  mean %.3g  max %.3g' % (nm, 100 * p[:, k].mean() / tot, p[:, k].mean(), p[:, k].max()))
 St = sim.get_state()
