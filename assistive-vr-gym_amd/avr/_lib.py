@@ -107,7 +107,7 @@ class Sim:
         self.md = md
         self.n = int(n_envs)
         self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel',
-                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel', 'avr_coop_kernel')
+                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel')
         cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))
@@ -280,10 +280,10 @@ class Sim:
         return out
 
     def kernel_info(self):
-        """{kernel: dict(vgprs, lds_bytes, scratch_bytes)} of the five sub-step kernels."""
+        """{kernel: dict(vgprs, lds_bytes, scratch_bytes)} of the step's kernels (include/avr.h)."""
         out = np.zeros(20, np.int32)
         self._chk(self.lib.avr_kernel_info(self.h, out.ctypes.data))
-        names = ('pairs', 'narrowphase', 'coop', 'a', 'b')
+        names = ('pairs', 'narrowphase', 'a', 'b', 'task')
         return {n: dict(vgprs=int(out[4 * i]), lds_bytes=int(out[4 * i + 2]), scratch_bytes=int(out[4 * i + 3])) for i, n in enumerate(names)}
 
 

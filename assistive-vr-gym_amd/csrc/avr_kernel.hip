@@ -2037,11 +2037,11 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
 }
 
 // --------------------------------------------------------------------------- one sub-step
-// A sub-step is five kernels: avr_substep_pairs_kernel (forward kinematics, body frames,
+// A sub-step is four kernels: avr_substep_pairs_kernel (forward kinematics, body frames,
 // broadphase, shape-pair list), avr_narrowphase_kernel (one lane per listed shape pair, across
-// all envs), avr_coop_kernel (the rare pairs that need the wave-cooperative narrowphase),
-// avr_substep_a_kernel (manifold update, unconstrained velocities, constraint rows) and
-// avr_substep_b4_kernel (PGS + integration).  What crosses the kernel boundaries goes
+// all envs), avr_substep_a_kernel (the rare pairs that need the wave-cooperative narrowphase,
+// then manifold update, unconstrained velocities, constraint rows) and avr_substep_b4_kernel
+// (PGS + integration).  What crosses the kernel boundaries goes
 // through the per-env collision scratch (m.cscr), the workspace (m.ws) and the row buffer
 // (m.rows).
 AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *ws, float *rows, const float *cs) {
@@ -2719,35 +2719,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
     }
 }
 
-// Sub-step part A2b: the pairs the narrowphase kernel left to the wave-cooperative path (rc 2),
-// one block per env (nearly all exit after a scan of their results; its own kernel, so that the
-// cooperative GJK/EPA does not inflate the register budget of the lane kernels).
-__global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0, int n_envs) {
-    const int env = env0 + blockIdx.x;
-    if (env >= n_envs || (mask && !mask[env])) return;
-    const KModel &m = *mp;
-    __shared__ EpaBuf E;        // the EPA polytope in LDS (9.5 KB; this kernel has no other LDS)
-    float *cs = env_cs(m, env);
-#ifdef AVR_WAVETIME   // [4][env] (start, end) in 100 MHz ticks
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    // most envs have no pair for the cooperative path: the narrowphase kernel's flag says so without
-    // a scan of the per-pair results (the flag is written only by np_store, rc 2, after the pair
-    // kernel cleared it in this sub-step)
-    if (gld(cs + CS_COOP) != 0.f) np_coop(m, cs, __float_as_int(gld(cs + CS_NSP)), E);
-#ifdef AVR_WAVETIME
-    const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
-    if (m.prof && lane_id() == 0) { m.prof[((size_t)4 * n_envs + env) * 2] = wt0; m.prof[((size_t)4 * n_envs + env) * 2 + 1] = wt1; }
-#endif
-}
-
-// Sub-step part A3: one 64-lane block per env, state staged in LDS -- manifold update,
-// unconstrained velocities, constraint rows.
+// Sub-step part A3: one 64-lane block per env, state staged in LDS -- the pairs the narrowphase
+// kernel left to the wave-cooperative path (rc 2: EPA, big hulls; 0.2-0.3 per env-step), then
+// manifold update, unconstrained velocities, constraint rows.  The cooperative pairs open this
+// kernel rather than a kernel of their own: the few envs that have one (an EPA can take ~40 us)
+// delay only their own wave, not a whole launch that every env's kernel a waits behind.
 __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                                      const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
     __shared__ EnvLDS L;
     AVR_ENV_GUARD();
     WT_START();
+    // the pairs left to the wave-cooperative narrowphase, before the prologue claims the LDS (the
+    // EPA polytope overlays it).  Most envs have none: the narrowphase kernel's flag says so
+    // without a scan of the per-pair results (written only by np_store, rc 2, after the pairs
+    // kernel cleared it in this sub-step)
+    static_assert(sizeof(EpaBuf) <= sizeof(EnvLDS), "EPA buffer overlay");
+    if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
+        np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L));
+        SYNC();
+    }
     float *gst = state + (size_t)env * K_STATE_WORDS;
     load_a(m, L, gst, env_cs(m, env));
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
@@ -3397,10 +3387,6 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
         hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
         mark(AVR_K_NARROW);
         hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 8 * NP_ENVS - 1) / (8 * NP_ENVS))), dim3(64), 0, stream, d_m, mask, env0, env1);
-        mark(AVR_K_COOP);
-#ifndef AVR_EXP_NOCOOP    // (timing experiment only: results are wrong without it)
-        hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
-#endif
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
@@ -3435,10 +3421,10 @@ hipError_t avr_launch_random_actions(unsigned long long seed, int env_offset, lo
     return hipGetLastError();
 }
 
-// [vgprs, 0, lds bytes, scratch bytes] of each sub-step kernel: pairs, narrowphase, coop, a, b4
+// [vgprs, 0, lds bytes, scratch bytes] of each kernel of a step: pairs, narrowphase, a, b4, task
 hipError_t avr_kernel_attrs(int *out20) {
-    const void *k[5] = {(const void *)avr_substep_pairs_kernel, (const void *)avr_narrowphase_kernel, (const void *)avr_coop_kernel,
-                        (const void *)avr_substep_a_kernel, (const void *)avr_substep_b4_kernel};
+    const void *k[5] = {(const void *)avr_substep_pairs_kernel, (const void *)avr_narrowphase_kernel, (const void *)avr_substep_a_kernel,
+                        (const void *)avr_substep_b4_kernel, (const void *)avr_task_kernel};
     for (int i = 0; i < 5; i++) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, k[i]);

@@ -337,7 +337,7 @@ def main():
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
                      'sq_by_kernel': pmc.get('sq') if pmc else None,
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': 'one env-step = 1 take_step + %d x (substep_pairs, narrowphase, coop, substep_a, substep_b4) + 1 task launch; '
+                     'scope': 'one env-step = 1 take_step + %d x (substep_pairs, narrowphase, substep_a, substep_b4) + 1 task launch; '
                               'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
                               'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
                               'sequences, so its stream time per step is below the summed durations; traffic = PMC HBM bytes of the '

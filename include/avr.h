@@ -106,10 +106,10 @@ int32_t avr_task_state_words(int32_t task);
 int32_t avr_task_obs_dim(int32_t task);
 int32_t avr_task_act_dim(int32_t task);
 int32_t avr_task(avr_sim *sim);
-/* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of each sub-step kernel, in
- * launch order: pairs (kinematics, broadphase, shape-pair list), narrowphase, coop (the
- * wave-cooperative GJK/EPA), a (manifolds, dynamics, constraint rows), b (PGS + integration):
- * out20 holds 5 x 4 ints. */
+/* Kernel resource usage: [vgprs, 0, lds_bytes, scratch_bytes] of each kernel of a step, in
+ * launch order: pairs (kinematics, broadphase, shape-pair list), narrowphase, a (the
+ * wave-cooperative GJK/EPA of the rare pairs that need it, manifolds, dynamics, constraint rows),
+ * b (PGS + integration), task (the task glue after the frames): out20 holds 5 x 4 ints. */
 int avr_kernel_info(avr_sim *sim, int32_t *out20);
 
 /* ---- state queries (device-side gathers; host buffers; block until done) ----
@@ -178,7 +178,7 @@ int avr_base_search(avr_sim *sim, int32_t n, int32_t attempts, const float *base
 /* Per-kernel timing on the handle's stream: while enabled, every launch of a step/settle is
  * bracketed by HIP events (adds a little launch overhead; off by default).  avr_kernel_times
  * returns the accumulated milliseconds and launch counts per kernel kind
- * [take_step, substep_a, substep_b, task, substep_pairs, narrowphase, coop, -] since enabling
+ * [take_step, substep_a, substep_b, task, substep_pairs, narrowphase, -, -] since enabling
  * (synchronises the stream). */
 int avr_profile_kernels(avr_sim *sim, int32_t enable);
 int avr_kernel_times(avr_sim *sim, double *ms8, int64_t *count8);

@@ -20,12 +20,17 @@ def run(n=512, k=20, lib=None):
     task = int(os.environ.get('TASK', '0'))
     A = ABI.load_scene(task)
     md = ABI.ModelDesc(A)
-    if task == 0:
+    states = os.environ.get('FP_STATES')      # initial states shared by an A/B pair of runs
+    if states and os.path.exists(states):
+        S = np.load(states)['S']
+    elif task == 0:
         S, _ = RS.batch_reset_states_fast(A, md, 1001, list(range(n)), impairment='random')
     else:
         import bench
         S, _ = bench.reset_pool(task, A, md, list(range(32)), 'random')
         S = np.tile(S, ((n + len(S) - 1) // len(S), 1))[:n]
+    if states and not os.path.exists(states):
+        np.savez_compressed(states, S=S)
     sim = _lib.Sim(md, n, seed=1001)
     sim.set_state(S.astype(np.float32))
     sim.settle(100 if task == 0 else 0)

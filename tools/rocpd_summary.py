@@ -27,7 +27,7 @@ SUBSTEPS = {'FeedingJaco-v0': 10, 'ScratchItchPR2-v0': 5, 'BedBathingPR2-v0': 5}
 
 def step_kernels(task):
     n = SUBSTEPS[task]
-    return {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n, 'avr_coop_kernel': n,
+    return {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n,
             'avr_substep_a_kernel': n, 'avr_substep_b4_kernel': n, 'avr_task_kernel': 1}
 
 
