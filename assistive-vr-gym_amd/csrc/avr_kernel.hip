@@ -1769,12 +1769,20 @@ AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.
 // R D R^T the world inverse inertia.  Part B then keeps the body's velocity increment in the
 // same coordinates (dv = v~ / sqrt(m) ... ) so that J.dv = g.v~ and M^-1 J^T delta = g delta:
 // one 6-vector per endpoint serves both halves of a row resolve.
+#ifndef B4_PK
+#define B4_PK 1     // free parts stored as (linear, angular) pairs per axis: packed-f32 row resolves (0: scalar layout)
+#endif
 AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
     const float *g = L.gsc[f];
     const qt q = ldq(L.st + S_FREE + AVR_FB_WORDS * f + 3);
     const v3 b = qrot(qconj(q), ja);
+#if B4_PK
+    w[0] = jl.x * g[0]; w[1] = b.x * g[1]; w[2] = jl.y * g[0];
+    w[3] = b.y * g[2]; w[4] = jl.z * g[0]; w[5] = b.z * g[3];
+#else
     w[0] = jl.x * g[0]; w[1] = jl.y * g[0]; w[2] = jl.z * g[0];
     w[3] = b.x * g[1]; w[4] = b.y * g[2]; w[5] = b.z * g[3];
+#endif
 }
 AVR_DI void put_free_zero(float *w) {
 #pragma unroll
@@ -2775,7 +2783,11 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
 // select: the waits the compiler places for a row then count only that row's loads, and the
 // software pipeline's read-ahead (headers 2D rows ahead, the header-dependent parts D ahead)
 // stays in flight.
+#if B4_PK
+struct DV { float rq, rq2; f2v v1, v2, v3; };             // v1 = (vx, wx), v2 = (vy, wy), v3 = (vz, wz)
+#else
 struct DV { float rq, rq2, vx, vy, vz, wx, wy, wz; };   // rq2: DoF sl + 16 (NDL 2)
+#endif
 
 AVR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -2941,6 +2953,32 @@ AVR_DI float row16_sum(float x) {
 template <bool RP, class R>
 AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi) {
 #pragma clang fp contract(off)
+#if B4_PK
+    // the same products and roundings as below, two per packed instruction: parts are stored as
+    // (linear, angular) pairs per axis and the velocity increments likewise, so the lo half of
+    // the chain is the linear dot product p and the hi half the angular one q
+    f2v s = X.j0 * d.v1;
+    if (RP) {
+        s.y = fmaf(X.r.x, d.rq, s.y);
+#if NDL == 2
+        s.y = fmaf(X.r.z, d.rq2, s.y);
+#endif
+    }
+    s = __builtin_elementwise_fma(X.j1, d.v2, s);
+    s = __builtin_elementwise_fma(X.j2, d.v3, s);
+    const float dv = row16_sum(s.x + s.y);
+    const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
+    const float delta = ni - imp;
+    const f2v dd = {delta, delta};
+    d.v1 = __builtin_elementwise_fma(X.j0, dd, d.v1);
+    d.v2 = __builtin_elementwise_fma(X.j1, dd, d.v2);
+    d.v3 = __builtin_elementwise_fma(X.j2, dd, d.v3);
+    if (RP) d.rq = fmaf(X.r.y, delta, d.rq);
+#if NDL == 2
+    if (RP) d.rq2 = fmaf(X.r.w, delta, d.rq2);
+#endif
+    return ni;
+#else
     const float p = fmaf(X.j1.x, d.vz, fmaf(X.j0.y, d.vy, X.j0.x * d.vx));
 #if NDL == 2
     const float q = RP ? fmaf(X.j2.y, d.wz, fmaf(X.j2.x, d.wy, fmaf(X.r.z, d.rq2, fmaf(X.r.x, d.rq, X.j1.y * d.wx))))
@@ -2959,6 +2997,7 @@ AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, f
     if (RP) d.rq2 = fmaf(X.r.w, delta, d.rq2);
 #endif
     return ni;
+#endif
 }
 
 // sweep over n (wave-uniform) steps; at(R, j) sets R's addresses for step j (a null row for
@@ -3002,7 +3041,11 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
     typedef typename NS::Row NR;
     typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
+#if B4_PK
+    d.rq = d.rq2 = 0.f; d.v1 = d.v2 = d.v3 = f2v{0.f, 0.f};
+#else
     d.rq = d.rq2 = 0.f; d.vx = d.vy = d.vz = d.wx = d.wy = d.wz = 0.f;
+#endif
     // normal rows in contact order: record j at cn + 64 j, impulse slot ipn + j
     auto at_n = [&](CR &R, int j) { cs.set(R, j < n_c, cs.cn + CRW * 4 * j, cs.ipn + j); };
     // warm start (normal rows, contact order): delta = cached impulse x warm-start factor, which
@@ -3198,14 +3241,19 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     if (!live) return;
     const float *ws = env_ws(m, ev);
     // owner lane f: mass-normalised increments back to (dv, dw) (see put_free)
+#if B4_PK
+    struct { float vx, vy, vz, wx, wy, wz; } dl = {d.v1.x, d.v2.x, d.v3.x, d.v1.y, d.v2.y, d.v3.y};
+#else
+    DV &dl = d;
+#endif
     if (sl < m.nf) {
         const qt q = ldq(st + S_FREE + AVR_FB_WORDS * sl + 3);
         const v3 I = gld3(m.fb_inertia + 4 * sl);
         const float rs = 1.f / sqrtf(gld(m.fb_mass + (sl)));
         const v3 sd = V(sqrtf(I.x > 0.f ? 1.f / I.x : 0.f), sqrtf(I.y > 0.f ? 1.f / I.y : 0.f), sqrtf(I.z > 0.f ? 1.f / I.z : 0.f));
-        const v3 w = qrot(q, V(d.wx * sd.x, d.wy * sd.y, d.wz * sd.z));
-        d.vx *= rs; d.vy *= rs; d.vz *= rs;
-        d.wx = w.x; d.wy = w.y; d.wz = w.z;
+        const v3 w = qrot(q, V(dl.wx * sd.x, dl.wy * sd.y, dl.wz * sd.z));
+        dl.vx *= rs; dl.vy *= rs; dl.vz *= rs;
+        dl.wx = w.x; dl.wy = w.y; dl.wz = w.z;
     }
     const float vmax = m.max_vel;
     const int nda = env_hdyn(m, st) ? m.nd + m.hc_n : m.nd;
@@ -3231,8 +3279,8 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     }
     if (sl < m.nf) {
         float *fb = st + S_FREE + AVR_FB_WORDS * sl;
-        v3 v = clamp3(add(ld3(ws + WS_FV + 4 * sl), V(d.vx, d.vy, d.vz)), vmax);
-        v3 om = clamp3(add(ld3(ws + WS_FW + 4 * sl), V(d.wx, d.wy, d.wz)), vmax);
+        v3 v = clamp3(add(ld3(ws + WS_FV + 4 * sl), V(dl.vx, dl.vy, dl.vz)), vmax);
+        v3 om = clamp3(add(ld3(ws + WS_FW + 4 * sl), V(dl.wx, dl.wy, dl.wz)), vmax);
         st3(fb + 7, v);
         st3(fb + 10, om);
         st3(fb, add(ld3(fb), scl(v, dt)));

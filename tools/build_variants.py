@@ -22,6 +22,8 @@ VARIANTS = {
     'dn2': ('-DB4_DN=2',), 'dn3': ('-DB4_DN=3',), 'dn4': ('-DB4_DN=4',), 'dc2': ('-DB4_DC=2',),
     'np4': ('-DNP_WAVES=4',), 'ne1': ('-DNP_ENVS=1',), 'ne2': ('-DNP_ENVS=2',), 'ne8': ('-DNP_ENVS=8',),
     'l11k': ('-DB4_LDSW=11264',), 'l12k': ('-DB4_LDSW=12288',), 'aw4': ('-DAVR_WAVES_PER_EU=4',), 'aw3': ('-DAVR_WAVES_PER_EU=3',),
+    # round 3
+    'nopk': ('-DB4_PK=0',), 'slp3': ('-fslp-vectorize',),
     'l8k': ('-DB4_LDSW=8192',), 'l7k': ('-DB4_LDSW=7168',), 'l6k': ('-DB4_LDSW=6144',), 'np4nb4': ('-DNP_WAVES=4', '-DGJK_NB=4'),
 }
 
