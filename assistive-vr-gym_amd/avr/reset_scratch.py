@@ -269,80 +269,127 @@ def base_search_host(A, md, base, rest, tstart, human_goals, iters):
 
 
 # ----------------------------------------------------------------------------- full reset
+def human_joint_angles_batch(A, gender, limit_scale):
+    """human_joint_angles for many envs of one gender: limit_scale (N,) -> q (N, n), lo, hi (N, n)."""
+    n = len(A['human_%s_parent' % gender])
+    lo0 = A['human_%s_lower' % gender].astype(float)
+    hi0 = A['human_%s_upper' % gender].astype(float)
+    sc = np.zeros(n, bool)
+    sc[[j for j in HUMAN_SCALED if j < n]] = True
+    ls = np.asarray(limit_scale, float)[:, None]
+    lo = np.where(sc[None], lo0[None] * ls, lo0[None])
+    hi = np.where(sc[None], hi0[None] * ls, hi0[None])
+    q = np.zeros(n)
+    for j, ang in JOINT_TARGETS:
+        q[j] = np.deg2rad(ang)
+    q = np.broadcast_to(q, lo.shape)
+    c = (A['human_%s_jtype' % gender] == 1)[None] & ~((lo == 0) & (hi == -1))
+    return np.where(c, np.minimum(np.maximum(q, lo), hi), q), lo, hi
+
+
+def human_link_poses_batch(A, gender, QH):
+    """reset.human_link_poses for many envs of one gender: QH (N, n) -> base_p (3,), base_q (4,),
+    P (N, n, 3), Q (N, n, 4)."""
+    base_p = np.array([0, 0.03, 0.89 - 0.23725 if gender == 'male' else 0.86 - 0.225])
+    base_q = np.array([0, 0, 0, 1.0])
+    par, jt, ax, pos = (A['human_%s_%s' % (gender, k)] for k in ('parent', 'jtype', 'axis', 'pos'))
+    N, n = QH.shape
+    P = np.zeros((N, n, 3)); Q = np.zeros((N, n, 4))
+    bp, bq = np.broadcast_to(base_p, (N, 3)), np.broadcast_to(base_q, (N, 4))
+    for i in range(n):
+        pp, pq = (bp, bq) if par[i] < 0 else (P[:, par[i]], Q[:, par[i]])
+        P[:, i] = pp + _qrot(pq, np.broadcast_to(pos[i], (N, 3)))
+        Q[:, i] = _qmul(pq, _qaxis(np.broadcast_to(ax[i], (N, 3)), QH[:, i])) if jt[i] == 1 else pq
+    return base_p, base_q, P, Q
+
+
 def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100, iters=200, sim=None):
     """Initial ScratchItch state blocks (float64 (N, SI.STATE_WORDS)) and per-env metadata.
-    sim: run the base-pose search on the device (position_robot_toc)."""
+    sim: run the base-pose search on the device (position_robot_toc).  The per-env draws run
+    in each env's stream order (human, base search, target); the rest is vectorised over envs."""
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
     rngs = [_rng(seed, e, ep) for e, ep in zip(env_ids, eps)]
     S = np.zeros((N, SI.STATE_WORDS))
     nd = int(A['n_dof'])
-    hc = int(A['hc_n'])
-    meta = []
-    goals = np.zeros((N, 3, 3))
-    slot_link = A['human_slot_link']
-    for k in range(N):
+    nc = len(ARM_CHAIN)
+    slot_link = np.asarray(A['human_slot_link'])
+    gl, il, ls, strength = [], [], np.ones(N), np.ones(N)
+    tremors = np.zeros((N, len(CONTROLLABLE)))
+    for k in range(N):                      # the human's draws (scratch_itch.py:163, world_creation.py:66-72)
         rng = rngs[k]
-        g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')   # scratch_itch.py:163
+        gl.append(genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female'))
         imp = _impairment(rng, impairment)
-        ls = rng.uniform(0.5, 1.0) if imp == 'limits' else 1.0          # world_creation.py:71
-        strength = rng.uniform(0.25, 1.0) if imp == 'weakness' else 1.0  # world_creation.py:72
-        tremors = rng.uniform(np.deg2rad(-10), np.deg2rad(10), size=len(CONTROLLABLE)) if imp == 'tremor' else np.zeros(len(CONTROLLABLE))
-        qh, lo, hi = human_joint_angles(A, g, ls)
-        base_p, base_q, P, Q = human_link_poses(A, g, qh)
-        st = S[k]
-        for s, l in enumerate(slot_link):
-            st[SI.S_HUMAN + 7 * s:SI.S_HUMAN + 7 * s + 7] = np.concatenate([base_p, base_q]) if l < 0 else np.concatenate([P[l], Q[l]])
-        goals[k] = P[[9, 11, 13]]                                       # shoulder, elbow, wrist (scratch_itch.py:187-190)
-        for c, j in enumerate(ARM_CHAIN):
-            st[SI.S_Q + nd + c] = qh[j]
-            st[SI.S_HCH + c] = qh[j]                                    # target_human_joint_positions
-            st[SI.S_HCH + SI.HC_N + c] = tremors[CONTROLLABLE.index(j)]
-            st[SI.S_HCH + 2 * SI.HC_N + c] = lo[j]
-            st[SI.S_HCH + 3 * SI.HC_N + c] = hi[j]
-            # reactive motors (world_creation.py:171-179), replaced by take_step's under 'tremor'
-            st[SI.S_QTGT + nd + c] = qh[j]
-            st[SI.S_KP + nd + c] = md.params['reactive_gain']
-            st[SI.S_MAXIMP + nd + c] = md.params['reactive_force'] * strength * md.params['time_step']
-        t = SI.S_TASK
-        st[t + SI.T_GENDER] = 0 if g == 'male' else 1
-        st[t + SI.T_HDYN] = 1.0
-        st[t + SI.T_TREMOR] = 1.0 if imp == 'tremor' else 0.0
-        st[t + SI.T_STRENGTH] = strength
-        meta.append(dict(gender=g, impairment=imp, limit_scale=ls, strength=strength))
+        il.append(imp)
+        if imp == 'limits':
+            ls[k] = rng.uniform(0.5, 1.0)
+        if imp == 'weakness':
+            strength[k] = rng.uniform(0.25, 1.0)
+        if imp == 'tremor':
+            tremors[k] = rng.uniform(np.deg2rad(-10), np.deg2rad(10), size=len(CONTROLLABLE))
+    nj = len(A['human_male_parent'])
+    QH, LO, HI = np.zeros((N, nj)), np.zeros((N, nj)), np.zeros((N, nj))
+    P = np.zeros((N, nj, 3)); Q = np.zeros((N, nj, 4))
+    BP, BQ = np.zeros((N, 3)), np.zeros((N, 4))
+    for g in ('male', 'female'):
+        idx = np.array([k for k in range(N) if gl[k] == g], int)
+        if not len(idx):
+            continue
+        qh, lo, hi = human_joint_angles_batch(A, g, ls[idx])
+        bp, bq, Pg, Qg = human_link_poses_batch(A, g, qh)
+        QH[idx], LO[idx], HI[idx], P[idx], Q[idx], BP[idx], BQ[idx] = qh, lo, hi, Pg, Qg, bp, bq
+    for s_, l in enumerate(slot_link):
+        o = SI.S_HUMAN + 7 * s_
+        S[:, o:o + 3] = BP if l < 0 else P[:, l]
+        S[:, o + 3:o + 7] = BQ if l < 0 else Q[:, l]
+    goals = P[:, [9, 11, 13]]                                   # shoulder, elbow, wrist (scratch_itch.py:187-190)
+    chain = list(ARM_CHAIN)
+    S[:, SI.S_Q + nd:SI.S_Q + nd + nc] = QH[:, chain]
+    S[:, SI.S_HCH:SI.S_HCH + nc] = QH[:, chain]                 # target_human_joint_positions
+    S[:, SI.S_HCH + SI.HC_N:SI.S_HCH + SI.HC_N + nc] = tremors[:, [CONTROLLABLE.index(j) for j in chain]]
+    S[:, SI.S_HCH + 2 * SI.HC_N:SI.S_HCH + 2 * SI.HC_N + nc] = LO[:, chain]
+    S[:, SI.S_HCH + 3 * SI.HC_N:SI.S_HCH + 3 * SI.HC_N + nc] = HI[:, chain]
+    # reactive motors (world_creation.py:171-179), replaced by take_step's under 'tremor'
+    S[:, SI.S_QTGT + nd:SI.S_QTGT + nd + nc] = QH[:, chain]
+    S[:, SI.S_KP + nd:SI.S_KP + nd + nc] = md.params['reactive_gain']
+    S[:, SI.S_MAXIMP + nd:SI.S_MAXIMP + nd + nc] = md.params['reactive_force'] * strength[:, None] * md.params['time_step']
+    t = SI.S_TASK
+    S[:, t + SI.T_GENDER] = [0 if g == 'male' else 1 for g in gl]
+    S[:, t + SI.T_HDYN] = 1.0
+    S[:, t + SI.T_TREMOR] = [1.0 if i == 'tremor' else 0.0 for i in il]
+    S[:, t + SI.T_STRENGTH] = strength
+    meta = [dict(gender=gl[k], impairment=il[k], limit_scale=float(ls[k]), strength=float(strength[k])) for k in range(N)]
     bp, bq, Qa, tstart, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, sim=sim)
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
     link = int(A['task_tool_link'])
-    piv = A['task_tool_pivot']
+    S[:, SI.S_RBASE:SI.S_RBASE + 3] = bp
+    S[:, SI.S_RBASE + 3:SI.S_RBASE + 7] = bq
+    S[:, SI.S_Q:SI.S_Q + nd] = Qa
+    S[:, SI.S_KP:SI.S_KP + nd] = 0.0                 # default velocity motors (PyBullet createJointMotors)
+    S[:, SI.S_QTGT:SI.S_QTGT + nd] = 0.0
+    S[:, SI.S_MAXIMP:SI.S_MAXIMP + nd] = md.params['default_motor_impulse']
+    for d in md.finger_dofs:                         # set_gripper_open_position(0.25) (world_creation.py:323-328)
+        S[:, SI.S_KP + d] = md.params['finger_gain']
+        S[:, SI.S_QTGT + d] = md.params['finger_target']
+        S[:, SI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+    # scratcher: its base (handle) COM on link 76's COM frame; the body frame is the composite COM
+    hq = CQ[:, link]
+    S[:, SI.S_FREE:SI.S_FREE + 3] = CP[:, link] - _qrot(hq, np.broadcast_to(A['task_tool_pivot'], (N, 3)))
+    S[:, SI.S_FREE + 3:SI.S_FREE + 7] = hq
+    # generate_target (scratch_itch.py:275-287): each env's limb and point, drawn after the search
     gidx = {'male': 0, 'female': 1}
+    limbs = np.zeros(N, int)
+    on_arm = np.zeros((N, 3))
     for k in range(N):
-        st = S[k]
-        rng = rngs[k]
-        st[SI.S_RBASE:SI.S_RBASE + 3] = bp[k]
-        st[SI.S_RBASE + 3:SI.S_RBASE + 7] = bq[k]
-        st[SI.S_Q:SI.S_Q + nd] = Qa[k]
-        for d in range(nd):                          # default velocity motors (PyBullet createJointMotors)
-            st[SI.S_KP + d] = 0.0
-            st[SI.S_QTGT + d] = 0.0
-            st[SI.S_MAXIMP + d] = md.params['default_motor_impulse']
-        for d in md.finger_dofs:                     # set_gripper_open_position(0.25) (world_creation.py:323-328)
-            st[SI.S_KP + d] = md.params['finger_gain']
-            st[SI.S_QTGT + d] = md.params['finger_target']
-            st[SI.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
-        # scratcher: its base (handle) COM on link 76's COM frame; the body frame is the composite COM
-        hq = CQ[k, link]
-        st[SI.S_FREE:SI.S_FREE + 3] = CP[k, link] - G.quat_rotate(hq, piv)
-        st[SI.S_FREE + 3:SI.S_FREE + 7] = hq
-        # generate_target (scratch_itch.py:275-287)
-        g = meta[k]['gender']
-        li, ln, rad = A['task_limbs'][gidx[g]][int(rng.integers(2))]
-        on_arm = point_on_capsule(rng, ln, rad)
-        t = SI.S_TASK
-        ck = ARM_CHAIN.index(int(li))
-        st[t + SI.T_LIMB] = ck
-        st[t + SI.T_ONARM:t + SI.T_ONARM + 3] = on_arm
-        lp = st[SI.S_HUMAN + 7 * list(slot_link).index(int(li)):][:7]
-        st[t + SI.T_TARGET:t + SI.T_TARGET + 3] = G.tf_mul(lp[:3], lp[3:], on_arm, [0, 0, 0, 1])[0]
-        meta[k].update(base_ok=bool(ok[k]), limb=int(li), start_goal=tstart[k])
+        li, ln, rad = A['task_limbs'][gidx[gl[k]]][int(rngs[k].integers(2))]
+        limbs[k] = int(li)
+        on_arm[k] = point_on_capsule(rngs[k], ln, rad)
+    si = np.array([list(slot_link).index(l) for l in limbs])
+    lp = S[np.arange(N)[:, None], SI.S_HUMAN + 7 * si[:, None] + np.arange(7)[None]]
+    S[:, t + SI.T_LIMB] = [chain.index(l) for l in limbs]
+    S[:, t + SI.T_ONARM:t + SI.T_ONARM + 3] = on_arm
+    S[:, t + SI.T_TARGET:t + SI.T_TARGET + 3] = lp[:, :3] + _qrot(lp[:, 3:], on_arm)
+    for k in range(N):
+        meta[k].update(base_ok=bool(ok[k]), limb=int(limbs[k]), start_goal=tstart[k])
     return S, meta
