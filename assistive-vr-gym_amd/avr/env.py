@@ -214,7 +214,10 @@ class AVRVecEnv:
         self.max_steps = int(self.md.params['max_episode_steps'])
         self._obs = np.zeros((self.n, self.L.OBS_DIM), np.float32)
         self._keepout = RS.keepout_box(self.A) if self.task == ABI.TASK_FEEDING else None
-        self._prefetch = _Prefetch(self._inputs) if (prefetch and self.device_ik) else None
+        if self.task == ABI.TASK_BEDBATH:          # the reset's arm settle, once per gender (device)
+            from . import reset_bedbath as RBB
+            RBB.settled_arms(self.A, self.md, device)
+        self._prefetch = _Prefetch(self._inputs) if (prefetch and (self.device_ik or self.device_search)) else None
         self.last_ik_ok = None
         self.reset_timing = None
 
@@ -242,7 +245,17 @@ class AVRVecEnv:
 
     # ------------------------------------------------------------------ reset
     def _inputs(self, idx, episodes):
-        return RS.reset_inputs(self.A, self.md, self.seed, [self.env_offset + int(i) for i in idx], genders=self._genders(idx),
+        """The host part of the masked envs' resets (everything before the device's part)."""
+        ids = [self.env_offset + int(i) for i in idx]
+        if self.task == ABI.TASK_BEDBATH:
+            from . import reset_bedbath as RBB
+            return RBB.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes),
+                                     attempts=self.scratch_attempts, device=self.device)
+        if self.task == ABI.TASK_SCRATCH:
+            from . import reset_scratch as RSS
+            return RSS.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment,
+                                     episodes=list(episodes), attempts=self.scratch_attempts)
+        return RS.reset_inputs(self.A, self.md, self.seed, ids, genders=self._genders(idx),
                                impairment=self.impairment, episodes=list(episodes), stream=self.reset_stream)
 
     def _reset_rows(self, mask):
@@ -273,15 +286,24 @@ class AVRVecEnv:
                 self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
             return
         ids = [self.env_offset + int(i) for i in idx]
-        if self.task == ABI.TASK_BEDBATH:
-            from . import reset_bedbath as RBB
-            Si, _ = RBB.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=eps,
-                                           attempts=self.scratch_attempts, iters=self.scratch_iters, device=self.device,
-                                           sim=self.sim if self.device_search else None)
-        elif self.task == ABI.TASK_SCRATCH:
-            from . import reset_scratch as RSS
-            Si, _ = RSS.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
-                                           attempts=self.scratch_attempts, iters=self.scratch_iters, sim=self.sim if self.device_search else None)
+        if self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH):
+            # host part (prefetched on a background thread during the previous episode when the
+            # same envs finish together), then the base-pose search on the device
+            from . import reset_bedbath as RBB, reset_scratch as RSS
+            t0 = time.perf_counter()
+            key = (tuple(idx.tolist()), tuple(eps.tolist()))
+            got = self._prefetch.take(key) if self._prefetch else None
+            P = got if got is not None else self._inputs(idx, eps)
+            t1 = time.perf_counter()
+            fin = RBB.finish_reset if self.task == ABI.TASK_BEDBATH else RSS.finish_reset
+            Si, _ = fin(self.A, self.md, P, self.scratch_iters, self.sim if self.device_search else None)
+            t2 = time.perf_counter()
+            if self._prefetch:
+                self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
+            S[idx] = Si
+            self.sim.reset(mask.astype(np.uint8), S, frames, self._obs)
+            self.reset_timing = dict(inputs_s=t1 - t0, prefetched=got is not None, search_s=t2 - t1, device_s=time.perf_counter() - t2)
+            return
         else:
             Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
                                                stream=self.reset_stream)

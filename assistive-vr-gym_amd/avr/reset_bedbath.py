@@ -149,6 +149,16 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, attemp
     """Initial BedBathing state blocks (float64 (N, BB.STATE_WORDS)) and per-env metadata.
     settled: settled_arms() output (computed on the device when None).  sim: run the base-pose
     search on the device (reset_scratch.position_robot_toc)."""
+    P = prepare_reset(A, md, seed, env_ids, genders, episodes, attempts, settled, device)
+    return finish_reset(A, md, P, iters, sim)
+
+
+def prepare_reset(A, md, seed, env_ids, genders=None, episodes=None, attempts=100, settled=None, device=0):
+    """The reset's draws (gender, the base search's attempts) and the settled human, vectorised
+    over envs; no search result is needed (AVRVecEnv prepares the next episode's resets on a
+    background thread)."""
+    from .reset_scratch import base_search_draws
+    from .reset import arm_limits
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
@@ -156,47 +166,54 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, attemp
     settled = settled_arms(A, md, device) if settled is None else settled
     nd = int(A['n_dof'])
     S = np.zeros((N, BB.STATE_WORDS))
-    gl = []
-    goals = np.zeros((N, 3, 3))
+    gl = [genders[k] if genders is not None else ('male' if rngs[k].integers(2) == 0 else 'female') for k in range(N)]   # bed_bathing.py:182
     js = A['bb_joint_slots']
-    for k in range(N):
-        g = genders[k] if genders is not None else ('male' if rngs[k].integers(2) == 0 else 'female')   # bed_bathing.py:182
-        gl.append(g)
+    goals = np.zeros((N, 3, 3))
+    for g in ('male', 'female'):
+        idx = np.array([k for k in range(N) if gl[k] == g], int)
+        if not len(idx):
+            continue
         qc, slots = settled[g]
-        S[k, BB.S_HUMAN:BB.S_HUMAN + 7 * BB.MAX_HUMAN] = slots.ravel()
-        goals[k] = slots[js, :3]                                       # shoulder, elbow, wrist (:305-307)
-        S[k, BB.S_Q + nd:BB.S_Q + nd + len(qc)] = qc
-    tstart = np.repeat(START_GOAL[None], N, 0)
-    bp, bq, Qa, _, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, tstart=tstart, pos_offset=(0, 0, 0), sim=sim)
-    from .reset_scratch import arm_fk
+        S[idx, BB.S_HUMAN:BB.S_HUMAN + 7 * BB.MAX_HUMAN] = slots.ravel()
+        goals[idx] = slots[js, :3]                                     # shoulder, elbow, wrist (:305-307)
+        S[idx, BB.S_Q + nd:BB.S_Q + nd + len(qc)] = qc
+    lo, hi = arm_limits(md)
+    tstart, base, rest = base_search_draws(rngs, attempts, lo, hi, (0, 0, 0), np.repeat(START_GOAL[None], N, 0))
+    return dict(S=S, genders=gl, goals=goals, tstart=tstart, base=base, rest=rest)
+
+
+def finish_reset(A, md, P, iters=200, sim=None):
+    """The base-pose search (on the device when sim is given) and the robot, gripper, wiper and
+    wipe targets it places, on a prepare_reset result.  Returns (S, meta)."""
+    from .reset_scratch import arm_fk, base_search
+    S = P['S'].copy()
+    gl = P['genders']
+    N = len(S)
+    nd = int(A['n_dof'])
+    bp, bq, Qa, _, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim)
     for d in md.finger_dofs:                                           # set_gripper_open_position(0.2, set_instantly)
         Qa[:, d] = md.params['finger_target']
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
     link = int(A['task_tool_link'])
-    meta = []
-    for k in range(N):
-        st = S[k]
-        g = gl[k]
-        st[BB.S_RBASE:BB.S_RBASE + 3] = bp[k]
-        st[BB.S_RBASE + 3:BB.S_RBASE + 7] = bq[k]
-        st[BB.S_Q:BB.S_Q + nd] = Qa[k]
-        for d in range(nd):                          # default velocity motors (PyBullet createJointMotors)
-            st[BB.S_MAXIMP + d] = md.params['default_motor_impulse']
-        for d in md.finger_dofs:                     # gripper position motors (world_creation.py:323-328)
-            st[BB.S_KP + d] = md.params['finger_gain']
-            st[BB.S_QTGT + d] = md.params['finger_target']
-            st[BB.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
-        tp, tq = _tool_pose(A, CP[k, link], CQ[k, link])
-        st[BB.S_FREE:BB.S_FREE + 3] = tp
-        st[BB.S_FREE + 3:BB.S_FREE + 7] = tq
-        t = BB.S_TASK
-        gi = 0 if g == 'male' else 1
-        st[t + BB.T_GENDER] = gi
-        st[t + BB.T_HDYN] = 0.0                       # the human is static from here on (:292-300)
-        nt = int(A['bb_ntgt'][gi].sum())
-        for w in range(6):                            # every target alive
-            nb = min(24, max(0, nt - 24 * w))
-            st[t + BB.T_WIPE + w] = float((1 << nb) - 1)
-        st[t + BB.T_NTGT] = nt
-        meta.append(dict(gender=g, impairment='none', base_ok=bool(ok[k]), n_targets=nt))   # (bed_bathing.py:188)
+    S[:, BB.S_RBASE:BB.S_RBASE + 3] = bp
+    S[:, BB.S_RBASE + 3:BB.S_RBASE + 7] = bq
+    S[:, BB.S_Q:BB.S_Q + nd] = Qa
+    S[:, BB.S_MAXIMP:BB.S_MAXIMP + nd] = md.params['default_motor_impulse']   # default velocity motors (createJointMotors)
+    for d in md.finger_dofs:                                           # gripper position motors (world_creation.py:323-328)
+        S[:, BB.S_KP + d] = md.params['finger_gain']
+        S[:, BB.S_QTGT + d] = md.params['finger_target']
+        S[:, BB.S_MAXIMP + d] = md.params['finger_force'] * md.params['time_step']
+    cq = CQ[:, link]                                                   # the wiper: base COM on link 76's COM frame
+    S[:, BB.S_FREE:BB.S_FREE + 3] = CP[:, link] - _qrot(cq, np.broadcast_to(A['task_tool_pivot'], (N, 3)))
+    S[:, BB.S_FREE + 3:BB.S_FREE + 7] = cq
+    t = BB.S_TASK
+    gi = np.array([0 if g == 'male' else 1 for g in gl])
+    S[:, t + BB.T_GENDER] = gi
+    S[:, t + BB.T_HDYN] = 0.0                                          # the human is static from here on (:292-300)
+    nt = A['bb_ntgt'].sum(1)[gi].astype(int)
+    for w in range(6):                                                 # every target alive
+        nb = np.clip(nt - 24 * w, 0, 24)
+        S[:, t + BB.T_WIPE + w] = (1 << nb) - 1
+    S[:, t + BB.T_NTGT] = nt
+    meta = [dict(gender=gl[k], impairment='none', base_ok=bool(ok[k]), n_targets=int(nt[k])) for k in range(N)]   # (bed_bathing.py:188)
     return S, meta

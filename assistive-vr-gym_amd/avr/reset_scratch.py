@@ -203,12 +203,17 @@ def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart
     sim: a _lib.Sim of the task -- the search runs on the device (avr_base_search, fp32), else
     here in fp64 (the device search's checker).
     Returns (base_pos, base_quat, arm q, start target, ok) per env."""
-    N = len(rngs)
-    nd = int(A['n_dof'])
-    arm = np.array(md.arm_dofs)
-    link = int(A['task_tool_link'])
     lo, hi = arm_limits(md)
     tstart, base, rest = base_search_draws(rngs, attempts, lo, hi, pos_offset, tstart)
+    return base_search(A, md, tstart, base, rest, human_goals, iters, sim)
+
+
+def base_search(A, md, tstart, base, rest, human_goals, iters=200, sim=None):
+    """The search of position_robot_toc on drawn attempts (base_search_draws): on the device when
+    sim is given, else here in fp64.  Returns (base_pos, base_quat, arm q, start target, ok)."""
+    N, attempts = base.shape[:2]
+    nd = int(A['n_dof'])
+    arm = np.array(md.arm_dofs)
     if sim is not None:
         best, ok, qa = sim.base_search(base, rest, tstart, human_goals, iters=iters, tol=0.03)
         out_q = np.zeros((N, nd))
@@ -305,8 +310,14 @@ def human_link_poses_batch(A, gender, QH):
 
 def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100, iters=200, sim=None):
     """Initial ScratchItch state blocks (float64 (N, SI.STATE_WORDS)) and per-env metadata.
-    sim: run the base-pose search on the device (position_robot_toc).  The per-env draws run
-    in each env's stream order (human, base search, target); the rest is vectorised over envs."""
+    sim: run the base-pose search on the device (position_robot_toc)."""
+    return finish_reset(A, md, prepare_reset(A, md, seed, env_ids, genders, impairment, episodes, attempts), iters, sim)
+
+
+def prepare_reset(A, md, seed, env_ids, genders=None, impairment='random', episodes=None, attempts=100):
+    """Everything of the reset that needs no search result -- every draw, in each env's stream
+    order (human, base search, target), the human pose, motors and target -- vectorised over envs
+    (AVRVecEnv prepares the next episode's resets on a background thread)."""
     env_ids = list(env_ids)
     N = len(env_ids)
     eps = [0] * N if episodes is None else list(episodes)
@@ -360,7 +371,33 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', 
     S[:, t + SI.T_TREMOR] = [1.0 if i == 'tremor' else 0.0 for i in il]
     S[:, t + SI.T_STRENGTH] = strength
     meta = [dict(gender=gl[k], impairment=il[k], limit_scale=float(ls[k]), strength=float(strength[k])) for k in range(N)]
-    bp, bq, Qa, tstart, ok = position_robot_toc(A, md, rngs, goals, attempts=attempts, iters=iters, sim=sim)
+    lo_a, hi_a = arm_limits(md)
+    tstart, base, rest = base_search_draws(rngs, attempts, lo_a, hi_a)
+    # generate_target (scratch_itch.py:275-287): each env's limb and point, drawn after the search's
+    gidx = {'male': 0, 'female': 1}
+    limbs = np.zeros(N, int)
+    on_arm = np.zeros((N, 3))
+    for k in range(N):
+        li, ln, rad = A['task_limbs'][gidx[gl[k]]][int(rngs[k].integers(2))]
+        limbs[k] = int(li)
+        on_arm[k] = point_on_capsule(rngs[k], ln, rad)
+    si = np.array([list(slot_link).index(l) for l in limbs])
+    lp = S[np.arange(N)[:, None], SI.S_HUMAN + 7 * si[:, None] + np.arange(7)[None]]
+    S[:, t + SI.T_LIMB] = [chain.index(l) for l in limbs]
+    S[:, t + SI.T_ONARM:t + SI.T_ONARM + 3] = on_arm
+    S[:, t + SI.T_TARGET:t + SI.T_TARGET + 3] = lp[:, :3] + _qrot(lp[:, 3:], on_arm)
+    for k in range(N):
+        meta[k].update(limb=int(limbs[k]), start_goal=tstart[k])
+    return dict(S=S, meta=meta, goals=goals, tstart=tstart, base=base, rest=rest)
+
+
+def finish_reset(A, md, P, iters=200, sim=None):
+    """The base-pose search (on the device when sim is given) and the robot and tool placement
+    it decides, on a prepare_reset result.  Returns (S, meta)."""
+    S, meta = P['S'].copy(), [dict(m) for m in P['meta']]
+    N = len(S)
+    nd = int(A['n_dof'])
+    bp, bq, Qa, tstart, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim)
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
     link = int(A['task_tool_link'])
     S[:, SI.S_RBASE:SI.S_RBASE + 3] = bp
@@ -377,19 +414,6 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='random', 
     hq = CQ[:, link]
     S[:, SI.S_FREE:SI.S_FREE + 3] = CP[:, link] - _qrot(hq, np.broadcast_to(A['task_tool_pivot'], (N, 3)))
     S[:, SI.S_FREE + 3:SI.S_FREE + 7] = hq
-    # generate_target (scratch_itch.py:275-287): each env's limb and point, drawn after the search
-    gidx = {'male': 0, 'female': 1}
-    limbs = np.zeros(N, int)
-    on_arm = np.zeros((N, 3))
     for k in range(N):
-        li, ln, rad = A['task_limbs'][gidx[gl[k]]][int(rngs[k].integers(2))]
-        limbs[k] = int(li)
-        on_arm[k] = point_on_capsule(rngs[k], ln, rad)
-    si = np.array([list(slot_link).index(l) for l in limbs])
-    lp = S[np.arange(N)[:, None], SI.S_HUMAN + 7 * si[:, None] + np.arange(7)[None]]
-    S[:, t + SI.T_LIMB] = [chain.index(l) for l in limbs]
-    S[:, t + SI.T_ONARM:t + SI.T_ONARM + 3] = on_arm
-    S[:, t + SI.T_TARGET:t + SI.T_TARGET + 3] = lp[:, :3] + _qrot(lp[:, 3:], on_arm)
-    for k in range(N):
-        meta[k].update(base_ok=bool(ok[k]), limb=int(limbs[k]), start_goal=tstart[k])
+        meta[k].update(base_ok=bool(ok[k]))
     return S, meta
