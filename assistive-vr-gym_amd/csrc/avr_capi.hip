@@ -46,6 +46,17 @@ struct avr_sim {
     size_t ikcap;
     float *d_bs;                           // device scratch of avr_base_search (draws, goals, per-attempt results)
     size_t bscap;
+    // the step's launch sequence (every group's 52 launches and the fork / join events) captured
+    // once as a HIP graph and replayed; keyed by the step's buffers and mode, the step counter t
+    // is patched into the take-step nodes before each replay
+    int use_graph;
+    hipGraph_t graph;
+    hipGraphExec_t gexec;
+    const void *gkey[6];
+    struct TakeArgs { const KModel *m; float *state; const float *act; const unsigned char *mask; int mode; long long t; int env0, env1; };
+    std::vector<hipGraphNode_t> gtake;     // take-step kernel nodes (one per group)
+    std::vector<hipKernelNodeParams> gtp;  // their launch parameters
+    std::vector<TakeArgs> gargs;           // and argument values
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -177,6 +188,8 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         if (ng > AVR_MAX_GROUPS) ng = AVR_MAX_GROUPS;
         if (ng > cfg->n_envs) ng = cfg->n_envs;
         s->ngroups = ng;
+        const char *gr = getenv("AVR_GRAPH");
+        s->use_graph = gr ? atoi(gr) : 0;
         HIPCHK(s, hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         for (int i = 1; i < ng; i++) {      // (group 0 runs on the handle's stream)
             HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));
@@ -458,8 +471,8 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
 // block's share) whose sequences run concurrently: group 0 on the handle's stream itself, the
 // others forked from it and joined back (ngroups streams in all, within the device's hardware
 // queues)
-static hipError_t run_step(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
-                           const unsigned char *mask, int mode, long long t) {
+static hipError_t run_step_direct(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
+                                  const unsigned char *mask, int mode, long long t) {
     const int E = s->cfg.n_envs;
     if (s->ngroups <= 1 || s->evlog.cap)
         return avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, 0, E, s->stream,
@@ -480,9 +493,64 @@ static hipError_t run_step(avr_sim *s, float *state, const float *act, float *ob
     return hipSuccess;
 }
 
+static void drop_graph(avr_sim *s) {
+    if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+    if (s->graph) (void)hipGraphDestroy(s->graph);
+    s->gexec = nullptr; s->graph = nullptr;
+    s->gtake.clear(); s->gtp.clear(); s->gargs.clear();
+}
+
+// a gym step (modes 0 / 1, no mask, no per-kernel timing) replays the captured launch sequence;
+// everything else launches directly
+static hipError_t run_step(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
+                           const unsigned char *mask, int mode, long long t) {
+    if (!s->use_graph || mask || s->evlog.cap || (mode != 0 && mode != 1) || state != s->d_state)
+        return run_step_direct(s, state, act, obs, rew, done, info, mask, mode, t);
+    const void *key[6] = {act, obs, rew, done, info, (const void *)(size_t)mode};
+    hipError_t e;
+    if (!s->gexec || memcmp(key, s->gkey, sizeof(key)) != 0) {
+        drop_graph(s);
+        if ((e = hipStreamBeginCapture(s->stream, hipStreamCaptureModeRelaxed)) != hipSuccess) return e;
+        hipError_t el = run_step_direct(s, state, act, obs, rew, done, info, nullptr, mode, t);
+        if ((e = hipStreamEndCapture(s->stream, &s->graph)) != hipSuccess) return e;
+        if (el != hipSuccess) { drop_graph(s); return el; }
+        size_t n = 0;
+        if ((e = hipGraphGetNodes(s->graph, nullptr, &n)) != hipSuccess) return e;
+        std::vector<hipGraphNode_t> nodes(n);
+        if ((e = hipGraphGetNodes(s->graph, nodes.data(), &n)) != hipSuccess) return e;
+        for (hipGraphNode_t nd : nodes) {
+            hipGraphNodeType ty;
+            if (hipGraphNodeGetType(nd, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+            hipKernelNodeParams p;
+            if ((e = hipGraphKernelNodeGetParams(nd, &p)) != hipSuccess) return e;
+            if (p.func != (void *)avr_take_step_kernel) continue;
+            avr_sim::TakeArgs a;
+            a.m = *(const KModel **)p.kernelParams[0]; a.state = *(float **)p.kernelParams[1];
+            a.act = *(const float **)p.kernelParams[2]; a.mask = *(const unsigned char **)p.kernelParams[3];
+            a.mode = *(int *)p.kernelParams[4]; a.t = *(long long *)p.kernelParams[5];
+            a.env0 = *(int *)p.kernelParams[6]; a.env1 = *(int *)p.kernelParams[7];
+            p.kernelParams = nullptr;
+            s->gtake.push_back(nd); s->gtp.push_back(p); s->gargs.push_back(a);
+        }
+        if (s->gtake.empty()) { drop_graph(s); return hipErrorInvalidValue; }
+        if ((e = hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0)) != hipSuccess) { drop_graph(s); return e; }
+        memcpy(s->gkey, key, sizeof(key));
+    }
+    for (size_t i = 0; i < s->gtake.size(); i++) {
+        avr_sim::TakeArgs &a = s->gargs[i];
+        a.t = t;
+        void *args[8] = {&a.m, &a.state, &a.act, &a.mask, &a.mode, &a.t, &a.env0, &a.env1};
+        hipKernelNodeParams p = s->gtp[i];
+        p.kernelParams = args;
+        if ((e = hipGraphExecKernelNodeSetParams(s->gexec, s->gtake[i], &p)) != hipSuccess) return e;
+    }
+    return hipGraphLaunch(s->gexec, s->stream);
+}
+
 int avr_destroy(avr_sim *s) {
     if (!s) return -1;
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    drop_graph(s);
     for (void *p : s->allocs) (void)hipFree(p);
     if (s->d_state) (void)hipFree(s->d_state);
     if (s->d_km) (void)hipFree(s->d_km);

@@ -359,12 +359,12 @@ def test_tremor_targets_and_hard_limits_match_oracle(lib_and_scene):
     sim.close()
 
 
-def _b_path_run(md, S, force_global, steps=5, frames=30, env=None):
+def _b_path_run(md, S, force_global, steps=5, frames=30, env=None, random_steps=0):
     from avr import _lib
     env = dict(env or {})
     if force_global:
         env['AVR_B4_GLOBAL'] = '1'
-    keys = ('AVR_B4_GLOBAL', 'AVR_ENV_GROUPS')
+    keys = ('AVR_B4_GLOBAL', 'AVR_ENV_GROUPS', 'AVR_GRAPH')
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(env)
     try:
@@ -377,6 +377,8 @@ def _b_path_run(md, S, force_global, steps=5, frames=30, env=None):
     sim.set_state(S)
     sim.settle(frames)
     outs = [sim.step(_lib.random_actions(1001, np.arange(len(S)), k)) for k in range(steps)]
+    for k in range(random_steps):     # device-drawn actions: t differs per step
+        sim.step_random_device(100 + k, 0, 0, 0, 0)
     G = sim.get_state()
     sim.close()
     return G, outs
@@ -411,6 +413,21 @@ def test_env_groups_bit_identical(lib_and_scene):
         for a, b in zip(o1, og):
             for x, y in zip(a, b):
                 assert np.array_equal(x, y)
+
+
+def test_graph_replay_bit_identical(lib_and_scene):
+    """AVR_GRAPH=1 captures a gym step's launch sequence (every env group's launches and the
+    fork / join events) once per output-buffer set and replays it, patching the step counter into
+    the take-step nodes: the same kernels on the same data, so the same bits as direct launches,
+    for host-action steps and for device-drawn actions whose Philox counter changes every step."""
+    A, md = lib_and_scene
+    S = np.concatenate([reset_states(A, md, range(0, 150), 'random'), reset_states(A, md, range(150, 200), 'tremor')])
+    G0, o0 = _b_path_run(md, S, False, steps=3, frames=10, env={'AVR_ENV_GROUPS': '3', 'AVR_GRAPH': '0'}, random_steps=3)
+    G1, o1 = _b_path_run(md, S, False, steps=3, frames=10, env={'AVR_ENV_GROUPS': '3', 'AVR_GRAPH': '1'}, random_steps=3)
+    assert np.array_equal(G0, G1)
+    for a, b in zip(o0, o1):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
 
 
 _POISON_RUN = r'''
