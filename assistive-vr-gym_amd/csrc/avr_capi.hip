@@ -189,7 +189,7 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         if (ng > cfg->n_envs) ng = cfg->n_envs;
         s->ngroups = ng;
         const char *gr = getenv("AVR_GRAPH");
-        s->use_graph = gr ? atoi(gr) : 0;
+        s->use_graph = gr ? atoi(gr) : 1;
         HIPCHK(s, hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         for (int i = 1; i < ng; i++) {      // (group 0 runs on the handle's stream)
             HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));

@@ -342,9 +342,14 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
 }
 
 // y = M^-1 x (padding DoFs have identity rows)
+#ifndef AVR_MINV_LAUNDER
+#define AVR_MINV_LAUNDER 1
+#endif
 AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
-#ifdef AVR_MINV_LAUNDER
-    // keep the 196 M^-1 loads inside the caller's loops (hoisted, they pin ~200 VGPRs)
+#if AVR_MINV_LAUNDER
+    // keep the MAXD^2 M^-1 loads inside the caller's loops: hoisted, they pin ~200 VGPRs (the PR2
+    // tasks' kernel a 281 -> 190 VGPRs, two waves per SIMD instead of one: ScratchItch 1.16M ->
+    // 1.31M env-steps/s, BedBathing 1.35M -> 1.55M; FeedingJaco unchanged)
     int z = 0;
     asm volatile("" : "+v"(z));
     const float *Mv = &L.Minv[0][0] + z;
@@ -1804,6 +1809,25 @@ AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 #endif
 }
 
+// the second robot endpoint of a contact row: adds its (J, M^-1 J^T) to the part the first one
+// wrote (this lane's own stores, read back)
+AVR_DI void add_robot(float *w, const float *J, const float *MJ) {
+#if NDL == 2
+#pragma unroll
+    for (int d = 0; d < 16; d++) {
+        w[4 * d] += J[d]; w[4 * d + 1] += MJ[d];
+        if (d + 16 < MAXD) { w[4 * d + 2] += J[d + 16]; w[4 * d + 3] += MJ[d + 16]; }
+        if ((d & 3) == 3) asm volatile("" ::: "memory");    // (keeps the read-backs from being hoisted together)
+    }
+#else
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+        w[2 * d] += J[d]; w[2 * d + 1] += MJ[d];
+        if ((d & 3) == 3) asm volatile("" ::: "memory");
+    }
+#endif
+}
+
 // Non-contact rows (limits, motors, fixed constraint), one lane per row.
 // Row order restates btMultiBodyConstraintSolver's setup order: joint-limit rows
 // of violated limits (link order, lower then upper), motor rows (link order), fixed rows.
@@ -1992,20 +2016,22 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         float fric = fminf(gld(m.body_friction + (ba)) * gld(m.body_friction + (bb)), 10.f);
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
+#pragma unroll 1
         for (int k = 0; k < 3; k++) {
             v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
             const int slot = rob ? slot0 + k : -1;
             float *w = row_crec(rows, k == 0 ? i : ncp + 2 * i + (k - 1));
             float den = 0.f, rel = 0.f;
-            float J[MAXD], MJ[MAXD];
-#pragma unroll
-            for (int d = 0; d < MAXD; d++) { J[d] = 0.f; MJ[d] = 0.f; }
+            // the robot part (J, M^-1 J^T) goes to the row buffer endpoint by endpoint (the second
+            // robot endpoint, if any, adds to the first's): one pair of MAXD arrays live at a time
+            float *wr = rob ? row_rob(m, rows, slot) : nullptr;
             if (kA == 1) {
                 float Ja[MAXD], Ma[MAXD];
                 robot_jac(m, L, iA, pa, dir, V(0, 0, 0), Ja);
                 minv_mul(L, Ja, Ma);
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; J[d] += Ja[d]; MJ[d] += Ma[d]; }
+                for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; }
+                put_robot(wr, Ja, Ma);
                 put_free_zero(w + 4);
             } else if (kA == 2) {
                 v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
@@ -2019,7 +2045,9 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 robot_jac(m, L, iB, pb, nd, V(0, 0, 0), Jb);
                 minv_mul(L, Jb, Mb);
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; J[d] += Jb[d]; MJ[d] += Mb[d]; }
+                for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
+                if (kA == 1) add_robot(wr, Jb, Mb);
+                else put_robot(wr, Jb, Mb);
                 put_free_zero(w + 10);
             } else if (kB == 2) {
                 v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
@@ -2027,7 +2055,6 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 rel += free_dot(L, iB, nd, jb);
                 put_free(L, iB, w + 10, nd, jb);
             } else put_free_zero(w + 10);
-            if (rob) put_robot(row_rob(m, rows, slot), J, MJ);
             float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
             float rhs = -rel * inv;
             if (k == 0) {
@@ -2727,6 +2754,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
     }
 }
 
+// AVR_COOP_KERNEL 1: the wave-cooperative pairs run in a kernel of their own between the
+// narrowphase and kernel a (one 64-lane block per env, EPA polytope in LDS), so kernel a's
+// register budget is its own (the cooperative path needs ~190 VGPRs, kernel a alone ~130: four
+// waves per SIMD instead of two).  0: they open kernel a (an env with an EPA delays only itself).
+#ifndef AVR_COOP_KERNEL
+#define AVR_COOP_KERNEL 0
+#endif
+#if AVR_COOP_KERNEL
+__global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0, int n_envs) {
+    __shared__ EpaBuf E;
+    AVR_ENV_GUARD();
+    if (gld(env_cs(m, env) + CS_COOP) != 0.f) np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), E);
+}
+#endif
+
 // Sub-step part A3: one 64-lane block per env, state staged in LDS -- the pairs the narrowphase
 // kernel left to the wave-cooperative path (rc 2: EPA, big hulls; 0.2-0.3 per env-step), then
 // manifold update, unconstrained velocities, constraint rows.  The cooperative pairs open this
@@ -2742,10 +2784,12 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     // without a scan of the per-pair results (written only by np_store, rc 2, after the pairs
     // kernel cleared it in this sub-step)
     static_assert(sizeof(EpaBuf) <= sizeof(EnvLDS), "EPA buffer overlay");
+#if !AVR_COOP_KERNEL
     if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
         np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L));
         SYNC();
     }
+#endif
     float *gst = state + (size_t)env * K_STATE_WORDS;
     load_a(m, L, gst, env_cs(m, env));
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
@@ -2864,15 +2908,43 @@ struct NcSrc {
     }
 };
 
+// non-contact rows staged in LDS (B4_NC_LDS: the PR2 tasks, whose rows are nearly all non-contact
+// rows with 24-DoF robot parts), by byte address: a row's o is its record's address + 8, so its
+// header is read at o - 8 and o + 8 and its endpoint part w (1 A, 2 B) at o + 24 w; a null row
+// reads its header from the zero head (o = LNB_NCNULL); robot part of the row with slot + 1 = s
+// at rob + ROBW 4 s (this lane's DoFs), or the zero block
+#define LN_HEAD (NDL == 2 ? 80 : 48)   // NDL 2: zero robot parts at words 12-15 and 76-79
+#define LNB_NULL 24                // null contact record - 8 (bytes)
+#define LNB_ZERO 48                // zero block (bytes)
+#define LNB_NCNULL 16              // null non-contact row: header words 2-7 of the zero head
+typedef __attribute__((address_space(3))) char lds_c;
+struct NcLds {
+    typedef NcRow Row;
+    static constexpr bool robot_parts = true;
+    lds_c *blk;
+    int eo;                    // row 0's record address + 8 (bytes)
+    unsigned rob;              // robot part of the row with slot + 1 = s: rob + ROBW 4 s (bytes, this lane's DoFs)
+    lds_f *ip0, *nullip;       // impulse slots: row 0, null rows
+    AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : LNB_NCNULL; R.ip = v ? ip : nullip; }
+    AVR_DI void hdr(Row &R) const {
+        R.h0 = *(const lds_f4 *)(blk + R.o - 8);
+        R.h1 = *(const lds_f2 *)(blk + R.o + 8);
+        R.imp = *R.ip;
+    }
+    AVR_DI void parts(Row &R) const {
+        const int w = own_of(__float_as_int(R.h0.x));
+        const lds_f2 *q = (const lds_f2 *)(blk + (w ? R.o + 24 * w : LNB_ZERO));
+        R.j0 = q[0]; R.j1 = q[1]; R.j2 = q[2];
+        const unsigned sp = (unsigned)__float_as_int(R.h0.y);
+        R.r = *(const lds_rv *)(blk + (sp ? rob + ROBW * 4 * sp : LNB_ZERO));
+    }
+};
+
 // contact rows staged in LDS, by byte address: a row's wb is its record's address - 8, so its
 // header is read at wb + 8 and its endpoint part o (1 A, 2 B) at wb + 24 o.  Null rows and zero
 // parts come from the block's zero-filled head (LN_HEAD words): the null record's headers at
 // words 8-11 and 24-27 (a null friction unit), zero parts at words 12-17 and 28-33, zero robot
 // parts at words 12-13 and 44-45.
-#define LN_HEAD (NDL == 2 ? 80 : 48)   // NDL 2: zero robot parts at words 12-15 and 76-79
-#define LNB_NULL 24                // null record - 8 (bytes)
-#define LNB_ZERO 48                // zero block (bytes)
-typedef __attribute__((address_space(3))) char lds_c;
 struct CRowL { unsigned wb; lds_f *ip; f4v h; float imp; f2v j0, j1, j2; rv_t r; };
 template <bool RC>             // RC: the block has robot contacts (otherwise no contact row has a robot part)
 struct CLds {
@@ -3122,6 +3194,12 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
 #ifndef B4_DG
 #define B4_DG 3          // pipeline depth, contact rows from global memory (blocks that do not fit)
 #endif
+#ifndef B4_NC_LDS
+#define B4_NC_LDS K_PR2  // stage the non-contact rows and every robot part in LDS too (when the four envs fit)
+#endif
+#ifndef B4_DNL
+#define B4_DNL 1         // pipeline depth, non-contact rows staged in LDS
+#endif
 
 __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
                                                             const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
@@ -3154,12 +3232,21 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     for (int i = lane; i < B4_LDSW; i += 64) blk[i] = __int_as_float(-1);
     __syncthreads();
 #endif
-    // pack the groups' regions; stage the contact rows when all four fit
+    // pack the groups' regions; stage every row (B4_NC_LDS) or the contact rows when all four fit
     const int szA = al4(n_rows + 2) + al4(n_c), szB = 3 * n_c * CRW + n_rc * ROBW;
+#if B4_NC_LDS
+    const int szF = szB + n_nc * (RWC + ROBW);
+    const int f0 = __shfl(szA + szF, 0), f1 = __shfl(szA + szF, 16), f2 = __shfl(szA + szF, 32), f3 = __shfl(szA + szF, 48);
+    const bool full = uni(f0 + f1 + f2 + f3) <= B4_LDSW - LN_HEAD && !m.b4_global;
+#else
+    const int f0 = 0, f1 = 0, f2 = 0;
+    constexpr bool full = false;
+#endif
     const int t0 = __shfl(szA + szB, 0), t1 = __shfl(szA + szB, 16), t2 = __shfl(szA + szB, 32), t3 = __shfl(szA + szB, 48);
-    const bool in_lds = uni(t0 + t1 + t2 + t3) <= B4_LDSW - LN_HEAD && !m.b4_global;
+    const bool in_lds = full || (uni(t0 + t1 + t2 + t3) <= B4_LDSW - LN_HEAD && !m.b4_global);
     int base;
-    if (in_lds) base = g == 0 ? 0 : g == 1 ? t0 : g == 2 ? t0 + t1 : t0 + t1 + t2;
+    if (full) base = g == 0 ? 0 : g == 1 ? f0 : g == 2 ? f0 + f1 : f0 + f1 + f2;
+    else if (in_lds) base = g == 0 ? 0 : g == 1 ? t0 : g == 2 ? t0 + t1 : t0 + t1 + t2;
     else {
         const int a0 = __shfl(szA, 0), a1 = __shfl(szA, 16), a2 = __shfl(szA, 32);
         base = g == 0 ? 0 : g == 1 ? a0 : g == 2 ? a0 + a1 : a0 + a1 + a2;
@@ -3167,7 +3254,9 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     base += LN_HEAD;
     lds_f *imp = blk + base;
     lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
-    const int cw = base + szA, rw = cw + 3 * n_c * CRW;
+    // LDS regions: contact records at cw, then (full) the non-contact records at nw, then the
+    // robot parts at rw (full: every slot's; otherwise the robot-contact slots')
+    const int cw = base + szA, nw = cw + 3 * n_c * CRW, rw = full ? nw + n_nc * RWC : nw;
     // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
     // warm-start factor; null slots 0.  The cached impulses are loaded here and stored after the
     // staging loads below have been issued (one memory round trip for both).
@@ -3180,21 +3269,22 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         if (!(c >= 0 && c < n_c)) imp[r] = 0.f;
     }
     for (int i = lane; i < LN_HEAD; i += 64) blk[i] = 0.f;        // null rows, zero parts
-    if (in_lds) {   // contact records and robot-contact parts, 8 loads in flight per lane
-        const int n4r = 3 * n_c * (CRW / 4), n4s = n_rc * (ROBW / 4);
-        const int m4 = wmax(n4r + n4s);
+    if (in_lds) {   // contact records, (full) non-contact records, robot parts: 8 loads in flight per lane
+        const int n4r = 3 * n_c * (CRW / 4), n4n = full ? n_nc * (RWC / 4) : 0, n4s = (full ? n_rob : n_rc) * (ROBW / 4);
+        const int n4a = n4r + n4n, n4 = n4a + n4s, so = full ? ro : ro + n_nc * ROBW * 4;
+        const int m4 = wmax(n4);
         lds_f4 *l0 = (lds_f4 *)(blk + cw);
         for (int b = 0; b < m4; b += 8 * 16) {
             f4v t[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int i = b + 16 * q + sl;
-                t[q] = bld4(rs, i < n4r ? eo + CR_BASE * 4 + 16 * i : (i < n4r + n4s ? ro + n_nc * ROBW * 4 + 16 * (i - n4r) : B4_OOB));
+                t[q] = bld4(rs, i < n4r ? eo + CR_BASE * 4 + 16 * i : i < n4a ? eo + 16 * (i - n4r) : (i < n4 ? so + 16 * (i - n4a) : B4_OOB));
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int i = b + 16 * q + sl;
-                if (i < n4r + n4s) l0[i] = t[q];
+                if (i < n4) l0[i] = t[q];
             }
         }
     }
@@ -3207,6 +3297,21 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     NcSrc ns{rs, eo, ro, imp, nullip};
     DV d;
     int units, rcb = 0;
+#if B4_NC_LDS
+    if (full) {
+        // every row from LDS: robot part of the row with slot + 1 = s at rw + (s - 1) ROBW words
+        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - ROBW) + RVB * sl;
+        const NcLds nl{(lds_c *)blk, 4 * nw + 8, rob, imp, nullip};
+        if (wmax(n_rc) > 0) {
+            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+            rcb = 1;
+        } else {
+            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+        }
+    } else
+#endif
     if (in_lds) {
         // byte addresses: records - 8; robot part of slot s at rw + (s - n_nc) ROBW + 2 sl words
         const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW) + RVB * sl;
@@ -3435,6 +3540,10 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
         hipLaunchKernelGGL(avr_substep_pairs_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, env0, env1);
         mark(AVR_K_NARROW);
         hipLaunchKernelGGL(avr_narrowphase_kernel, dim3(16 * ((n_envs + 8 * NP_ENVS - 1) / (8 * NP_ENVS))), dim3(64), 0, stream, d_m, mask, env0, env1);
+#if AVR_COOP_KERNEL
+        mark(AVR_K_COOP);
+        hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
+#endif
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);

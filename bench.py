@@ -300,7 +300,7 @@ def main():
     bpe = T['bytes']
     achieved = bpe * E / (step_kernel_ms * 1e-3) / 1e9
     ms_per_step = el / args.steps * 1e3
-    pmc = pmc_summary(args.task, sim.kernel_kinds, ms_per_step, E)
+    pmc = pmc_summary(args.task, [k for k, v in kt.items() if v[1] > 0], ms_per_step, E)
     traffic = pmc['traffic'] if pmc else None
     # the bound: the larger of the two roofline fractions the path could sit on (HBM bytes vs the
     # dense matrix-core peak; the path issues no MFMA, so its MFMA fraction is 0)
@@ -337,13 +337,14 @@ def main():
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
                      'sq_by_kernel': pmc.get('sq') if pmc else None,
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': 'one env-step = 1 take_step + %d x (substep_pairs, narrowphase, substep_a, substep_b4) + 1 task launch; '
+                     'scope': 'one env-step = 1 take_step + %d x (%s) + 1 task launch; '
                               'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
                               'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
                               'sequences, so its stream time per step is below the summed durations; traffic = PMC HBM bytes of the '
                               'step and valu_busy = PMC VALU instructions x %.0f cycles / (%d SIMDs x %.1f GHz x ms_per_step), both from '
                               'the task\'s committed rocprofv3 summary (%s)' % (
-                                  T['substeps'], VALU_CYC, SIMDS, CLOCK_HZ / 1e9, pmc['source'] if pmc else 'none matching'),
+                                  T['substeps'], ', '.join(k[4:-7] for k in kernels if k not in ('avr_take_step_kernel', 'avr_task_kernel')),
+                                  VALU_CYC, SIMDS, CLOCK_HZ / 1e9, pmc['source'] if pmc else 'none matching'),
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(L),
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
                      'dominant_kernel': dominant, 'kernels': kernels},

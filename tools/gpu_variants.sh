@@ -11,6 +11,6 @@ for r in 1 2; do
     L=""
     if [ $v != default ]; then L=/root/repo/exp/libavr_$v.so; fi
     AVR_LIB=$L timeout -k 10 200 python3 bench.py --task $T --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/var/b_${v}_$r.json 2> gpurun_out/var/b_${v}_$r.err || exit $?
-    echo $v $r $(python3 -c "import json;d=json.loads(open('gpurun_out/var/b_${v}_$r.json').read().strip().splitlines()[-1]);k=d['roofline']['kernels'];print(round(d['value']), d['nan_or_overflow_envs'], {n[4:16]:round(x['avg_ms'],4) for n,x in k.items()})")
+    echo $T $v $r $(python3 -c "import json;d=json.loads(open('gpurun_out/var/b_${v}_$r.json').read().strip().splitlines()[-1]);k=d['roofline']['kernels'];print(round(d['value']), d['nan_or_overflow_envs'], {n[4:16]:round(x['avg_ms'],4) for n,x in k.items()})")
   done
 done
