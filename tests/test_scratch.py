@@ -325,3 +325,37 @@ def test_scratch_state_getters(sc, states):
     with pytest.raises(RuntimeError):
         sim.get_link_pose(99)
     sim.close()
+
+
+@pytest.mark.gpu
+def test_scratch_part_b_row_paths_bit_identical(sc, states):
+    """Part B of the PR2 tasks stages every row -- the non-contact rows with their 21-DoF robot
+    parts as well as the contact rows -- in LDS when a block's four envs fit, and reads them from
+    global memory otherwise (AVR_B4_GLOBAL=1 forces that for every block): the same rows in the
+    same order with the same arithmetic, so both agree bit for bit, with and without contacts."""
+    import scratch_util as U
+    from avr import _lib
+    A, md = sc
+    S, meta = states
+    C32 = U.contact_states(A, md, S, meta).astype(np.float32)
+    X = np.concatenate([S.astype(np.float32), C32])
+    outs = []
+    for g in ('0', '1'):
+        old = os.environ.pop('AVR_B4_GLOBAL', None)
+        os.environ['AVR_B4_GLOBAL'] = g
+        try:
+            sim = _sim(md, len(X))
+        finally:
+            os.environ.pop('AVR_B4_GLOBAL')
+            if old is not None:
+                os.environ['AVR_B4_GLOBAL'] = old
+        sim.set_state(X)
+        steps = [sim.step(_lib.random_actions(1001, np.arange(len(X)), t) * 0.5) for t in range(5)]
+        outs.append((sim.get_state(), steps))
+        sim.close()
+    (G0, s0), (G1, s1) = outs
+    assert np.array_equal(G0, G1)
+    for a, b in zip(s0, s1):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    assert np.count_nonzero(G0[:, SI.S_TASK + SI.T_NCP]) > 0

@@ -1,4 +1,5 @@
-# Round profile: rocprofv3 kernel-trace stats of the default bench workload, then separate PMC
+# Round profile (PMC passes with direct launches, AVR_GRAPH=0: the counters are per dispatch and the
+# kernels are the same; the kernel traces and the bench line use the default graph replay): rocprofv3 kernel-trace stats of the default bench workload, then separate PMC
 # passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix), then the full bench line (with the CPU
 # baseline).  Summaries: python tools/rocpd_summary.py gpurun_out/prof <tag>.
 set -o pipefail
@@ -9,9 +10,9 @@ B5="bench.py --task $TASK --steps 5 --warmup 1 --no-cpu-baseline"
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_before.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt -- python3 $B > gpurun_out/prof/kt_bench.log 2>&1 && \
 AVR_ENV_GROUPS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt1 -o kt1 -- python3 $B > gpurun_out/prof/kt1_bench.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 $B5 > gpurun_out/prof/fetch.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 $B5 > gpurun_out/prof/write.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/prof/sq -o sq -- python3 $B5 > gpurun_out/prof/sq.log 2>&1 && \
+AVR_GRAPH=0 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 $B5 > gpurun_out/prof/fetch.log 2>&1 && \
+AVR_GRAPH=0 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 $B5 > gpurun_out/prof/write.log 2>&1 && \
+AVR_GRAPH=0 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/prof/sq -o sq -- python3 $B5 > gpurun_out/prof/sq.log 2>&1 && \
 timeout -k 10 600 python3 bench.py --task $TASK > gpurun_out/prof/bench_full.log 2>&1
 rc=$?
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_after.txt

@@ -1,7 +1,12 @@
+# Round-end evidence: GPU suite, smoke, full bench lines (with the CPU baseline) and facade benches
+# (AVRTorchVecEnv with rollovers) for the three tasks.  Output: gpurun_out/g1/
 set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/g1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/g1/pytest.log 2>&1 || exit 11
-timeout -k 10 300 python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/g1/b0.json 2> gpurun_out/g1/b0.err || exit 12
-timeout -k 10 300 python3 bench.py --task ScratchItchPR2-v0 --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/g1/b1.json 2> gpurun_out/g1/b1.err || exit 13
-timeout -k 10 300 python3 bench.py --task BedBathingPR2-v0 --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/g1/b2.json 2> gpurun_out/g1/b2.err || exit 14
-bash tools/gpu_timeline.sh || exit 15
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/g1/smoke.log 2>&1 || exit 12
+timeout -k 10 300 python3 bench.py > gpurun_out/g1/bench_feeding.json 2> gpurun_out/g1/b0.err || exit 13
+timeout -k 10 300 python3 bench.py --task ScratchItchPR2-v0 > gpurun_out/g1/bench_scratch.json 2> gpurun_out/g1/b1.err || exit 14
+timeout -k 10 300 python3 bench.py --task BedBathingPR2-v0 > gpurun_out/g1/bench_bedbath.json 2> gpurun_out/g1/b2.err || exit 15
+for T in FeedingJaco-v0 ScratchItchPR2-v0 BedBathingPR2-v0; do
+  timeout -k 10 300 python3 bench.py --task $T --facade --steps 600 > gpurun_out/g1/facade_$T.json 2> gpurun_out/g1/facade_$T.err || exit 16
+done
