@@ -166,9 +166,12 @@ def facade_bench(args):
     K = max(1, min(100, v.max_steps - int(v.iteration.max()) - 1))
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    host_ms = []
     for k in range(K):
         act.uniform_(-1, 1, generator=gen)
+        th = time.perf_counter()
         v.step(act)
+        host_ms.append((time.perf_counter() - th) * 1e3)
     torch.cuda.synchronize(dev)
     no_roll = (time.perf_counter() - t1) / K
     out = {'metric': 'facade env-steps/sec (AVRTorchVecEnv, auto-reset at the 200-step TimeLimit)', 'value': E * args.steps / el,
@@ -177,7 +180,8 @@ def facade_bench(args):
            'data': 'synthetic: torch uniform(-1, 1) actions on the device; resets drawn per env and episode',
            'config': {'workload': args.task + ', %d envs, gym facade with rollover' % E, 'task': args.task, 'envs_per_gpu': E,
                       'impairment': args.impairment, 'reset_ik': 'device' if v.device_ik else 'host'},
-           'rollovers_timed': roll, 'env_steps_per_s_between_rollovers': E / no_roll,
+           'rollovers_timed': roll, 'env_steps_per_s_between_rollovers': E / no_roll, 'between_rollovers_steps': K,
+           'between_rollovers_host_ms_per_step': [round(float(np.median(host_ms)), 3), round(float(np.max(host_ms)), 3)],
            'rollover_ms': float(np.mean(t_roll) * 1e3) if roll else None, 'first_reset_s': t_reset,
            'ik_accept_rate': float(v.last_ik_ok.mean()) if v.last_ik_ok is not None else None,
            'last_rollover_breakdown_s': v.reset_timing,
