@@ -107,7 +107,7 @@ class Sim:
         self.md = md
         self.n = int(n_envs)
         self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel',
-                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel', 'avr_coop_kernel')
+                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel', 'avr_coop_kernel', 'avr_substep_ab_kernel')
         cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))
@@ -247,7 +247,7 @@ class Sim:
         ms = np.zeros(8, np.float64)
         n = np.zeros(8, np.int64)
         self._chk(self.lib.avr_kernel_times(self.h, ms.ctypes.data, n.ctypes.data))
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.kernel_kinds) if n[i] or i < 6}
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.kernel_kinds) if n[i]}
 
     # ---- state queries (include/avr.h avr_get_*)
     def n_dof(self):

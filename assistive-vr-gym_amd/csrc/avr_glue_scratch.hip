@@ -18,6 +18,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const KModel &m = *mp;
     float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
+    ws[WS_COOPROT] = 0.f;                       // the capped cooperative-pair window restarts every gym step (np_coop)
     float asq = 0.f;
     for (int i = 0; i < m.n_arm; i++) {
         float a_raw = mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * K_ACT_DIM + i];

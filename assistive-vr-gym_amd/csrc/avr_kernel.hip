@@ -114,7 +114,15 @@ static_assert(sizeof(PairsLDS) <= 10240, "pair kernel: 16 blocks per CU");
 static_assert(MAXSH % 64 == 0, "shape info staged 64 per pass");
 #endif
 
-#define SYNC() __syncthreads()
+// Intra-env synchronisation.  An env is one wavefront (a 64-lane block, or one wave of the fused
+// a + b kernel's block), so a workgroup fence -- this wave's memory operations complete and are
+// visible -- plus a compiler barrier is enough; no s_barrier, which in the fused kernel would
+// wait for the other envs' waves.
+#define SYNC()                                          \
+    do {                                                \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); \
+        __builtin_amdgcn_wave_barrier();                \
+    } while (0)
 
 // Diagnostic phase timers (separate AVR_PROF build only; the shipped kernel has none).
 #ifdef AVR_PROF
@@ -1758,6 +1766,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_ASQ 2     // sum of squared caller actions (take_step -> task glue)
 #define WS_XCC 3     // diagnostic builds: XCD that ran part A
 #define WS_NROB 4    // int bits: robot parts (slots) of the row set
+#define WS_COOPROT 5 // int bits: rotation of the capped cooperative-pair window (np_coop)
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV (WS_VQ + 16 * NDL)     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW (WS_FV + 4 * MAXF)     // [MAXF][4] angular
@@ -2360,6 +2369,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const KModel &m = *mp;
     float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
+    ws[WS_COOPROT] = 0.f;                       // the capped cooperative-pair window restarts every gym step (np_coop)
     float asq = 0.f;
     for (int i = 0; i < m.n_arm; i++) {
         float a_raw = mode == MODE_STEP_RANDOM ? philox_action(m.seed, m.env_offset + env, t, i) : act[(size_t)env * K_ACT_DIM + i];
@@ -2558,8 +2568,25 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
 // the listed pairs (n of them) that the lane path left to the wave-cooperative narrowphase (rc 2:
 // a big hull without a support table, penetrating cores that need EPA, the lane iteration cap):
 // the whole wave runs narrowphase<true> on each, E = the env's EPA buffer
-AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
+//
+// At most AVR_COOP_CAP of them per env and sub-step (an arm driven into the wheelchair's hulls
+// produced 21 EPAs per sub-step, ~1.3 ms of one wave that every env of the launch waited for):
+// beyond the cap, a rotating window of AVR_COOP_CAP pairs (rot: the env's sub-step counter) is
+// solved and the others report no new point this sub-step -- their manifolds keep and refresh the
+// points they hold.  Returns true when the cap applied (T_FLAGS bit 5).
+#ifndef AVR_COOP_CAP
+#define AVR_COOP_CAP 4
+#endif
+AVR_DI bool np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot) {
     const int lane = lane_id();
+    int nco = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int k = c0 + lane < n ? c0 + lane : -1;
+        nco += __popcll(__ballot(k >= 0 && __float_as_int(gld(cs + CS_RES + 8 * (k >= 0 ? k : 0))) == 2));
+    }
+    const bool capped = nco > AVR_COOP_CAP;
+    const int r0 = capped ? rot % nco : 0;
+    int jn = 0;            // order of the pair among the env's cooperative pairs
     for (int c0 = 0; c0 < n; c0 += 64) {
         const int k = c0 + lane < n ? c0 + lane : -1;
         unsigned long long cm = __ballot(k >= 0 && __float_as_int(gld(cs + CS_RES + 8 * (k >= 0 ? k : 0))) == 2);
@@ -2567,6 +2594,11 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
             const int j = __ffsll((long long)cm) - 1;
             cm &= cm - 1;
             const int kj = __shfl(k, j, 64);
+            const int jj = jn++;
+            if (capped && (jj - r0 + nco) % nco >= AVR_COOP_CAP) {
+                if (lane == 0) np_store(cs, kj, 0, V(0, 0, 0), V(0, 0, 0), 0.f);
+                continue;
+            }
             const int key = __float_as_int(gld(cs + CS_PAIRS + 2 * kj)), w = __float_as_int(gld(cs + CS_PAIRS + 2 * kj + 1));
             const int sa = key & 0xffff, sb = key >> 16;
             const int ba = (w >> 16) & 0xff, bb = (w >> 24) & 0xff;
@@ -2600,6 +2632,7 @@ AVR_DI void np_coop(const KModel &m, float *cs, int n, EpaBuf &E) {
             SYNC();
         }
     }
+    return capped;
 }
 
 // Sub-step part A2: the narrowphase of every listed shape pair across all envs.  A block takes one
@@ -2765,7 +2798,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
 __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0, int n_envs) {
     __shared__ EpaBuf E;
     AVR_ENV_GUARD();
-    if (gld(env_cs(m, env) + CS_COOP) != 0.f) np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), E);
+    if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
+        float *ws = env_ws(m, env);
+        const int rot = __float_as_int(gld(ws + WS_COOPROT));
+        (void)np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), E, rot);
+        if (lane_id() == 0) ws[WS_COOPROT] = __int_as_float(rot + AVR_COOP_CAP);
+    }
 }
 #endif
 
@@ -2774,10 +2812,8 @@ __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__
 // manifold update, unconstrained velocities, constraint rows.  The cooperative pairs open this
 // kernel rather than a kernel of their own: the few envs that have one (an EPA can take ~40 us)
 // delay only their own wave, not a whole launch that every env's kernel a waits behind.
-__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                                     const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
-    __shared__ EnvLDS L;
-    AVR_ENV_GUARD();
+AVR_DI void substep_a_env(const KModel &m, EnvLDS &L, float *__restrict__ state, float dt, int env, int n_envs) {
+    (void)n_envs;
     WT_START();
     // the pairs left to the wave-cooperative narrowphase, before the prologue claims the LDS (the
     // EPA polytope overlays it).  Most envs have none: the narrowphase kernel's flag says so
@@ -2785,13 +2821,20 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     // kernel cleared it in this sub-step)
     static_assert(sizeof(EpaBuf) <= sizeof(EnvLDS), "EPA buffer overlay");
 #if !AVR_COOP_KERNEL
+    bool capped = false;
     if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
-        np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L));
+        float *ws = env_ws(m, env);
+        const int rot = __float_as_int(gld(ws + WS_COOPROT));
+        capped = np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L), rot);
+        if (lane_id() == 0) ws[WS_COOPROT] = __int_as_float(rot + AVR_COOP_CAP);
         SYNC();
     }
 #endif
     float *gst = state + (size_t)env * K_STATE_WORDS;
     load_a(m, L, gst, env_cs(m, env));
+#if !AVR_COOP_KERNEL
+    if (capped && lane_id() == 0) L.flags |= 32;
+#endif
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
 #ifdef AVR_PROF
     if (lane_id() == 0) env_ws(m, env)[WS_XCC] = __int_as_float(xcc_id());
@@ -2805,6 +2848,13 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KMode
     if (lane_id() < 16) gst[S_TASK + lane_id()] = L.st[S_TASK + lane_id()];
     prof_flush(m, L, env);
     WT_END(0);
+}
+
+__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_a_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                                     const unsigned char *__restrict__ mask, float dt, int env0, int n_envs) {
+    __shared__ EnvLDS L;
+    AVR_ENV_GUARD();
+    substep_a_env(m, L, state, dt, env, n_envs);
 }
 
 // ---------------------------------------------------------------------------- part B: PGS solve
@@ -3201,21 +3251,17 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
 #define B4_DNL 1         // pipeline depth, non-contact rows staged in LDS
 #endif
 
-__global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                            const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
-                                                            int n_envs) {
-    const KModel &m = *mp;
+AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const unsigned char *__restrict__ mask, float dt, int frame_end,
+                             int env0, int n_envs, int bidx, lds_f *blk) {
 #ifdef AVR_WAVETIME
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    __shared__ f4v b4l[B4_LDSW / 4];
-    lds_f *blk = (lds_f *)(lds_f4 *)b4l;
     const int lane = lane_id(), sl = lane & 15, g = lane >> 4;
     // XCD-consistent mapping: blocks are dealt round-robin over the 8 XCDs, and part A runs env
     // e as block e - env0, so block b takes the envs e - env0 = 32 (b / 8) + (b % 8) + 8 g, which
     // part A ran on the same XCD: the rows, workspace and state it wrote are read through the
     // same L2 (per-XCD L2s are not coherent with each other)
-    const int env = env0 + 32 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * g;
+    const int env = env0 + 32 * (bidx >> 3) + (bidx & 7) + 8 * g;
     const bool live = env < n_envs && (!mask || mask[env]);
     const int ev = live ? env : env0;
     const gfp wsg = (gfp)env_ws(m, ev);
@@ -3230,7 +3276,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     const int eo = ev * m.rowstride * 4, ro = eo + m.rowcap * RWC * 4;
 #ifdef AVR_LDS_POISON   // diagnostic: NaN-fill the block's LDS (see load_state)
     for (int i = lane; i < B4_LDSW; i += 64) blk[i] = __int_as_float(-1);
-    __syncthreads();
+    SYNC();
 #endif
     // pack the groups' regions; stage every row (B4_NC_LDS) or the contact rows when all four fit
     const int szA = al4(n_rows + 2) + al4(n_c), szB = 3 * n_c * CRW + n_rc * ROBW;
@@ -3291,7 +3337,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
 #pragma unroll
     for (int q = 0; q < K_MAX_CONTACTS / 16; q++)
         if (sl + 16 * q < n_c) imp[n_nc + sl + 16 * q] = wimp[q] * m.warmstart;
-    __syncthreads();
+    SYNC();
     // impulse slots: rows 0 .. n_rows - 1 (non-contact, normal, friction pairs), then 2 null slots
     lds_f *const ipn = imp + n_nc, *const ipf = ipn + n_c, *const nullip = imp + n_rows;
     NcSrc ns{rs, eo, ro, imp, nullip};
@@ -3334,7 +3380,7 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
 #ifdef AVR_WAVETIME   // block timeline at its group-0 env: [1][env] (start, end); [2][env] (sweep lengths, LDS path, friction units)
     {
         const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
-        const int e0 = env0 + 32 * (blockIdx.x >> 3) + (blockIdx.x & 7);
+        const int e0 = env0 + 32 * (bidx >> 3) + (bidx & 7);
         if (m.prof && lane == 0 && e0 < n_envs) {
             m.prof[((size_t)1 * n_envs + e0) * 2] = wt0;
             m.prof[((size_t)1 * n_envs + e0) * 2 + 1] = wt1;
@@ -3398,6 +3444,35 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
         stq(fb + 3, qnorm(qmul(dq, ldq(fb + 3))));
     }
 }
+
+__global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                            const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
+                                                            int n_envs) {
+    __shared__ f4v b4l[B4_LDSW / 4];
+    substep_b4_block(*mp, state, mask, dt, frame_end, env0, n_envs, blockIdx.x, (lds_f *)(lds_f4 *)b4l);
+}
+
+// AVR_FUSE_AB: kernel a and part B in one launch.  A block of four waves takes part B's four envs
+// (block b: envs env0 + 32 (b / 8) + b % 8 + 8 w, the XCD that ran their pair and narrowphase
+// kernels); wave w runs kernel a for env w, then wave 0 runs part B on the four.  An env whose
+// kernel a is slow (a cooperative EPA) delays only its own block's part B, not every env's.
+#ifndef AVR_FUSE_AB
+#define AVR_FUSE_AB 0
+#endif
+#if AVR_FUSE_AB
+__global__ __launch_bounds__(256) void avr_substep_ab_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                             const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
+                                                             int n_envs) {
+    __shared__ union ABLds { EnvLDS a[4]; f4v b[B4_LDSW / 4]; } U;
+    const KModel &m = *mp;
+    const int w = threadIdx.x >> 6, b = blockIdx.x;
+    const int env = env0 + 32 * (b >> 3) + (b & 7) + 8 * w;
+    if (env < n_envs && (!mask || mask[env])) substep_a_env(m, U.a[w], state, dt, env, n_envs);
+    __syncthreads();
+    if (w == 0) substep_b4_block(m, state, mask, dt, frame_end, env0, n_envs, b, (lds_f *)(lds_f4 *)U.b);
+}
+#endif
+
 
 #if AVR_TASK == AVR_TASK_FEEDING
 // Task glue after the frames: update_targets (feeding.py:345-349), iteration count,
@@ -3544,10 +3619,15 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
         mark(AVR_K_COOP);
         hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
 #endif
+#if AVR_FUSE_AB
+        mark(AVR_K_AB);
+        hipLaunchKernelGGL(avr_substep_ab_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(256), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
+#else
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
         hipLaunchKernelGGL(avr_substep_b4_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
+#endif
     };
     if (mode == MODE_SUBSTEP) {
         float h;

@@ -68,7 +68,7 @@ AVR_DI m3 qmat(qt q) {
 }
 
 // ---- wave-level helpers (wave64) ----
-AVR_DI int lane_id() { return (int)threadIdx.x; }
+AVR_DI int lane_id() { return (int)(threadIdx.x & 63u); }   // lane within the wavefront
 // exclusive prefix count of `pred` over lanes < lane, and total
 AVR_DI int ballot_prefix(bool pred, int *total) {
     unsigned long long b = __ballot(pred);

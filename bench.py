@@ -295,7 +295,7 @@ def main():
         one_step(args.warmup + args.steps + k, k)
     kt = sim.kernel_times()
     sim.profile_kernels(False)
-    kernels = {k: {'avg_ms': v[0] / max(v[1], 1), 'launches_per_step': v[1] / P, 'ms_per_step': v[0] / P} for k, v in kt.items()}
+    kernels = {k: {'avg_ms': v[0] / max(v[1], 1), 'launches_per_step': v[1] / P, 'ms_per_step': v[0] / P} for k, v in kt.items() if v[1] > 0}
     step_kernel_ms = sum(v['ms_per_step'] for v in kernels.values())
     dominant = max(kernels, key=lambda k: kernels[k]['ms_per_step'])
     St = sim.get_state()
@@ -354,7 +354,7 @@ def main():
                      'dominant_kernel': dominant, 'kernels': kernels},
         'nan_or_overflow_envs': int(np.count_nonzero(flags)),
         'flagged_envs_by_bit': {name: int(np.count_nonzero(flags & (1 << b))) for b, name in enumerate(
-            ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full'))},
+            ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full', 'coop_capped'))},
         'reset_pool_sha1': pool_sha,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -135,7 +135,9 @@ int avr_get_link_pose(avr_sim *sim, int32_t link, float *out7);
 int avr_get_contact_summary(avr_sim *sim, float *out4);
 /* avr_get_flags: per-env health flags, flags[n_envs] (bit0 NaN / failed mass-matrix
  *   factorisation, bit1 contact pool full, bit2 AABB pair list full, bit3 shape pair list full,
- *   bit4 non-contact row buffer full); 0 = healthy.  No reference counterpart (PyBullet has no
+ *   bit4 non-contact row buffer full, bit5 more than AVR_COOP_CAP = 4 penetrating hull pairs in
+ *   one sub-step: the EPA ran on a rotating window of 4 of them, the others kept their manifold
+ *   points); 0 = healthy.  No reference counterpart (PyBullet has no
  *   such report); a vectorised trainer polls it instead of the whole state block. */
 int avr_get_flags(avr_sim *sim, int32_t *flags);
 const char *avr_last_error(avr_sim *sim);

@@ -465,3 +465,33 @@ def test_lds_poison_build_is_bit_identical(lib_and_scene, tmp_path, b4_global):
         subprocess.run([sys.executable, '-c', _POISON_RUN, root, f], env=env, check=True, timeout=150)
         outs.append(np.load(f))
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
+    """An env whose arm was driven into the wheelchair's VHACD hulls (captured from a facade run
+    after three rollovers, tests/golden/feeding_arm_in_wheelchair.npy) has ~21 penetrating hull
+    pairs per sub-step, each an EPA on the wave-cooperative path.  At most AVR_COOP_CAP = 4 are
+    solved per sub-step (a rotating window; the others keep their manifold points) and the env is
+    flagged (bit 5); it stays finite, and every other env of its launch is bit-identical to a run
+    without it."""
+    from avr import _lib
+    A, md = lib_and_scene
+    bad = np.load(os.path.join(HERE, 'feeding_arm_in_wheelchair.npy')).astype(np.float32)
+    S = reset_states(A, md, range(63), 'random')
+    X = np.concatenate([S[:20], bad, S[20:]])
+    keep = np.r_[0:20, 21:64]
+    runs = []
+    for states in (X, S):
+        sim = make_sim(md, len(states))
+        sim.set_state(states)
+        for t in range(3):
+            a = _lib.random_actions(1001, np.arange(63), t)
+            if len(states) == 64:
+                a = np.concatenate([a[:20], np.zeros((1, a.shape[1]), a.dtype), a[20:]])
+            sim.step(a)
+        runs.append((sim.get_state(), sim.get_flags()))
+        sim.close()
+    (G, f), (G0, f0) = runs
+    assert f[20] & 32, f[20]
+    assert np.all(np.isfinite(G[20]))
+    assert np.array_equal(G[keep], G0) and not np.any(f0 & 32)

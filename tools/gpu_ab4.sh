@@ -8,5 +8,6 @@ for t in 0 1 2; do
 done
 rm -f gpurun_out/ab/*.npz
 for T in ${TASKS:-ScratchItchPR2-v0}; do
+  [ "$T" = none ] && continue
   TASK=$T VARIANTS="${VARIANTS:-default}" bash tools/gpu_variants.sh > gpurun_out/ab/var_$T.txt 2>&1 || exit 12
 done

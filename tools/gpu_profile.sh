@@ -6,7 +6,7 @@ set -o pipefail
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/prof
 TASK=${TASK:-FeedingJaco-v0}
 B="bench.py --task $TASK --steps 20 --warmup 3 --no-cpu-baseline"
-B5="bench.py --task $TASK --steps 5 --warmup 1 --no-cpu-baseline"
+B5="bench.py --task $TASK --steps 20 --warmup 5 --no-cpu-baseline"
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_before.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt -- python3 $B > gpurun_out/prof/kt_bench.log 2>&1 && \
 AVR_ENV_GROUPS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt1 -o kt1 -- python3 $B > gpurun_out/prof/kt1_bench.log 2>&1 && \
