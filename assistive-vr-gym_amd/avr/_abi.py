@@ -27,6 +27,7 @@ S_MAXIMP = S_KP + MAX_DOF
 S_FREE = S_MAXIMP + MAX_DOF
 S_TASK = S_FREE + MAX_FREE * FB_WORDS
 T_TARGET, T_ITER, T_SUCCESS, T_ALIVE, T_HIT, T_GENDER, T_FLAGS, T_NCP, T_HDYN, T_WORDS = 0, 3, 4, 5, 6, 7, 8, 9, 10, 16
+T_COOPN = 15        # consecutive sub-steps with more than 4 EPAs (the kernels' EPA cap; all tasks)
 S_HUMAN = S_TASK + T_WORDS
 S_HCH = S_HUMAN + MAX_HUMAN * 7          # [HC_N] target_human_joint_positions, [HC_N] human_tremors
 S_CP = S_HCH + 2 * HC_N
@@ -45,7 +46,7 @@ FEEDING = _Layout(TASK=TASK_FEEDING, MAX_LINKS=MAX_LINKS, MAX_DOF=MAX_DOF, MAX_F
                   MAX_CONTACTS=MAX_CONTACTS, HC_N=HC_N, ACT_DIM=ACT_DIM, OBS_DIM=OBS_DIM, INFO_DIM=INFO_DIM,
                   S_Q=S_Q, S_QD=S_QD, S_QTGT=S_QTGT, S_KP=S_KP, S_MAXIMP=S_MAXIMP, S_FREE=S_FREE, S_TASK=S_TASK,
                   T_TARGET=T_TARGET, T_ITER=T_ITER, T_SUCCESS=T_SUCCESS, T_ALIVE=T_ALIVE, T_HIT=T_HIT, T_GENDER=T_GENDER,
-                  T_FLAGS=T_FLAGS, T_NCP=T_NCP, T_HDYN=T_HDYN, T_WORDS=T_WORDS, S_HUMAN=S_HUMAN, S_HCH=S_HCH, S_CP=S_CP,
+                  T_FLAGS=T_FLAGS, T_NCP=T_NCP, T_HDYN=T_HDYN, T_COOPN=T_COOPN, T_WORDS=T_WORDS, S_HUMAN=S_HUMAN, S_HCH=S_HCH, S_CP=S_CP,
                   STATE_WORDS=STATE_WORDS)
 
 
@@ -61,7 +62,7 @@ def _scratch_layout(task=TASK_SCRATCH):
     L['S_RBASE'] = L['S_FREE'] + L['MAX_FREE'] * FB_WORDS
     L['S_TASK'] = L['S_RBASE'] + 8
     L.update(T_TARGET=0, T_ITER=3, T_SUCCESS=4, T_LIMB=5, T_STRENGTH=6, T_GENDER=7, T_FLAGS=8, T_NCP=9, T_HDYN=10,
-             T_PREV=11, T_TREMOR=14, T_ONARM=16, T_WORDS=24)
+             T_PREV=11, T_TREMOR=14, T_COOPN=15, T_ONARM=16, T_WORDS=24)
     L['S_HUMAN'] = L['S_TASK'] + L['T_WORDS']
     L['S_HCH'] = L['S_HUMAN'] + L['MAX_HUMAN'] * 7      # [HC_N] targets, tremors, lower, upper limits
     L['S_CP'] = L['S_HCH'] + 4 * L['HC_N']

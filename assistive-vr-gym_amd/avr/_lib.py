@@ -107,7 +107,7 @@ class Sim:
         self.md = md
         self.n = int(n_envs)
         self.kernel_kinds = ('avr_take_step_kernel', 'avr_substep_a_kernel', 'avr_substep_b4_kernel', 'avr_task_kernel',
-                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel', 'avr_coop_kernel', 'avr_substep_ab_kernel')
+                             'avr_substep_pairs_kernel', 'avr_narrowphase_kernel', 'avr_coop_kernel')
         cfg = avr_config(n_envs=self.n, device=device, env_offset=env_offset, flags=int(flags), seed=seed)
         h = C.c_void_p()
         rc = self.lib.avr_create(C.byref(cfg), C.cast(md.ptr(), C.c_void_p), C.byref(h))

@@ -114,10 +114,9 @@ static_assert(sizeof(PairsLDS) <= 10240, "pair kernel: 16 blocks per CU");
 static_assert(MAXSH % 64 == 0, "shape info staged 64 per pass");
 #endif
 
-// Intra-env synchronisation.  An env is one wavefront (a 64-lane block, or one wave of the fused
-// a + b kernel's block), so a workgroup fence -- this wave's memory operations complete and are
-// visible -- plus a compiler barrier is enough; no s_barrier, which in the fused kernel would
-// wait for the other envs' waves.
+// Intra-env synchronisation.  An env is one wavefront, so a workgroup fence -- this wave's memory
+// operations complete and are visible -- plus a compiler barrier is enough; no s_barrier (the
+// kernels' bodies are device functions that a multi-env block could run one wave per env).
 #define SYNC()                                          \
     do {                                                \
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); \
@@ -1057,7 +1056,8 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
 // (nit, kind: diagnostic out-parameters -- GJK iterations, and 0 sphere-sphere, 1 sphere-box,
 // 2 sphere-capsule, 3 GJK; unused outside the AVR_PROF build)
 template <bool COOP>
-AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist, int &nit, int &kind) {
+AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist, int &nit, int &kind,
+                       int *epa_budget = nullptr) {
     int ka = A.kind, kb = B.kind;
     nit = 0;
     kind = 3;
@@ -1140,6 +1140,10 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
         d = cd - ma - mb;
     } else {
         if (!COOP) return 2;
+        if (epa_budget) {           // (np_coop's per-sub-step EPA cap: 3 = penetrating, not solved)
+            if (*epa_budget <= 0) return 3;
+            --*epa_budget;
+        }
         float depth;
         v3 en;
         if (epa(m, E, A, B, S, en, depth, pa, pb)) return 0;
@@ -2569,70 +2573,84 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
 // a big hull without a support table, penetrating cores that need EPA, the lane iteration cap):
 // the whole wave runs narrowphase<true> on each, E = the env's EPA buffer
 //
-// At most AVR_COOP_CAP of them per env and sub-step (an arm driven into the wheelchair's hulls
-// produced 21 EPAs per sub-step, ~1.3 ms of one wave that every env of the launch waited for):
-// beyond the cap, a rotating window of AVR_COOP_CAP pairs (rot: the env's sub-step counter) is
-// solved and the others report no new point this sub-step -- their manifolds keep and refresh the
-// points they hold.  Returns true when the cap applied (T_FLAGS bit 5).
+// EPA budget (cap): an env whose penetrating hull pairs needed more than AVR_COOP_CAP EPAs in
+// each of its last AVR_COOP_PERSIST sub-steps (T_COOPN counts them) gets at most AVR_COOP_CAP per
+// sub-step from then on -- an arm driven into the wheelchair's hulls produced 21 per sub-step,
+// ~1.3 ms of one wave that every env of the launch waited for.  The pairs are visited from a
+// rotating start (rot: the env's counter, restarted every gym step); once the budget is spent a
+// penetrating pair reports no new point this sub-step and its manifold keeps and refreshes the
+// points it holds.  Transient penetrations (food dropped into the spoon at reset) never persist
+// that long, so normal envs are never capped; GJK-only pairs are always solved, and with the
+// budget unspent the visiting order changes nothing.  Returns the sub-step's EPA demand (solved +
+// skipped).
 #ifndef AVR_COOP_CAP
 #define AVR_COOP_CAP 4
 #endif
-AVR_DI bool np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot) {
+#ifndef AVR_COOP_PERSIST
+#define AVR_COOP_PERSIST 20
+#endif
+AVR_DI int np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot, int budget) {
     const int lane = lane_id();
+    // the cooperative pairs of each 64-pair chunk, read once (the stores below rewrite CS_RES)
+    unsigned long long bm[MAXSP / 64];
     int nco = 0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int k = c0 + lane < n ? c0 + lane : -1;
-        nco += __popcll(__ballot(k >= 0 && __float_as_int(gld(cs + CS_RES + 8 * (k >= 0 ? k : 0))) == 2));
+#pragma unroll
+    for (int q = 0; q < MAXSP / 64; q++) {
+        const int k = 64 * q + lane;
+        bm[q] = __ballot(k < n && __float_as_int(gld(cs + CS_RES + 8 * (k < n ? k : 0))) == 2);
+        nco += __popcll(bm[q]);
     }
-    const bool capped = nco > AVR_COOP_CAP;
-    const int r0 = capped ? rot % nco : 0;
-    int jn = 0;            // order of the pair among the env's cooperative pairs
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int k = c0 + lane < n ? c0 + lane : -1;
-        unsigned long long cm = __ballot(k >= 0 && __float_as_int(gld(cs + CS_RES + 8 * (k >= 0 ? k : 0))) == 2);
-        while (cm) {
-            const int j = __ffsll((long long)cm) - 1;
-            cm &= cm - 1;
-            const int kj = __shfl(k, j, 64);
-            const int jj = jn++;
-            if (capped && (jj - r0 + nco) % nco >= AVR_COOP_CAP) {
-                if (lane == 0) np_store(cs, kj, 0, V(0, 0, 0), V(0, 0, 0), 0.f);
-                continue;
-            }
-            const int key = __float_as_int(gld(cs + CS_PAIRS + 2 * kj)), w = __float_as_int(gld(cs + CS_PAIRS + 2 * kj + 1));
-            const int sa = key & 0xffff, sb = key >> 16;
-            const int ba = (w >> 16) & 0xff, bb = (w >> 24) & 0xff;
-            const float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
-            const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
-            v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
-            float d2 = 0.f;
-            int nit, nk;
+    const int r0 = nco > 0 ? rot % nco : 0;
+    const int budget0 = budget;
+    int skipped = 0;
+    for (int pass = 0; pass < 2; pass++) {       // cooperative pairs r0 .. nco - 1, then 0 .. r0 - 1
+        int jn = 0;
+#pragma unroll
+        for (int q = 0; q < MAXSP / 64; q++) {
+            const int k = 64 * q + lane;
+            unsigned long long cm = bm[q];
+            while (cm) {
+                const int j = __ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const int jj = jn++;
+                if ((jj >= r0) != (pass == 0)) continue;
+                const int kj = __shfl(k, j, 64);
+                const int key = __float_as_int(gld(cs + CS_PAIRS + 2 * kj)), w = __float_as_int(gld(cs + CS_PAIRS + 2 * kj + 1));
+                const int sa = key & 0xffff, sb = key >> 16;
+                const int ba = (w >> 16) & 0xff, bb = (w >> 24) & 0xff;
+                const float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
+                const WShape A = make_wshape(m, sa, ldtf(cs + CS_BTF + 8 * ba)), B = make_wshape(m, sb, ldtf(cs + CS_BTF + 8 * bb));
+                v3 n2 = V(0, 0, 0), p2 = V(0, 0, 0);
+                float d2 = 0.f;
+                int nit, nk;
 #ifdef AVR_PROF
-            const unsigned long long c0t = __builtin_readcyclecounter();
+                const unsigned long long c0t = __builtin_readcyclecounter();
 #endif
-            const int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk);
+                int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk, &budget);
+                if (r2 == 3) { r2 = 0; skipped++; }
 #ifdef AVR_PROF
-            if (m.prof && lane == 0) {     // cooperative pairs, their GJK iterations, the time they took
-                const unsigned long long dc = __builtin_readcyclecounter() - c0t;
-                unsigned long long *pr = m.prof + (size_t)(cs - m.cscr) / CS_WORDS * AVR_PROF_SLOTS;
-                atomicAdd(pr + 11, 1ull);
-                atomicAdd(pr + 28, (unsigned long long)nit);
-                // by shape kinds: 19 sphere-hull, 20 hull-hull, 21 other; 22 big hull (no support
-                // table); 29 cycles, 30 the slowest pair's cycles
-                const bool ha = A.kind == AVR_HULL, hb = B.kind == AVR_HULL;
-                const bool sph = (A.kind == AVR_SPHERE && hb) || (B.kind == AVR_SPHERE && ha);
-                atomicAdd(pr + (sph ? 19 : (ha && hb) ? 20 : 21), 1ull);
-                if ((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0)) atomicAdd(pr + 22, 1ull);
-                atomicAdd(pr + 29, dc);
-                atomicMax(pr + 30, dc);
-            }
+                if (m.prof && lane == 0) {     // cooperative pairs, their GJK iterations, the time they took
+                    const unsigned long long dc = __builtin_readcyclecounter() - c0t;
+                    unsigned long long *pr = m.prof + (size_t)(cs - m.cscr) / CS_WORDS * AVR_PROF_SLOTS;
+                    atomicAdd(pr + 11, 1ull);
+                    atomicAdd(pr + 28, (unsigned long long)nit);
+                    // by shape kinds: 19 sphere-hull, 20 hull-hull, 21 other; 22 big hull (no support
+                    // table); 29 cycles, 30 the slowest pair's cycles
+                    const bool ha = A.kind == AVR_HULL, hb = B.kind == AVR_HULL;
+                    const bool sph = (A.kind == AVR_SPHERE && hb) || (B.kind == AVR_SPHERE && ha);
+                    atomicAdd(pr + (sph ? 19 : (ha && hb) ? 20 : 21), 1ull);
+                    if ((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0)) atomicAdd(pr + 22, 1ull);
+                    atomicAdd(pr + 29, dc);
+                    atomicMax(pr + 30, dc);
+                }
 #endif
-            SYNC();
-            if (lane == 0) np_store(cs, kj, r2, n2, p2, d2);
-            SYNC();
+                SYNC();
+                if (lane == 0) np_store(cs, kj, r2, n2, p2, d2);
+                SYNC();
+            }
         }
     }
-    return capped;
+    return budget0 - budget + skipped;
 }
 
 // Sub-step part A2: the narrowphase of every listed shape pair across all envs.  A block takes one
@@ -2801,7 +2819,7 @@ __global__ __launch_bounds__(64) void avr_coop_kernel(const KModel *__restrict__
     if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
         float *ws = env_ws(m, env);
         const int rot = __float_as_int(gld(ws + WS_COOPROT));
-        (void)np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), E, rot);
+        (void)np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), E, rot, 1 << 30);
         if (lane_id() == 0) ws[WS_COOPROT] = __int_as_float(rot + AVR_COOP_CAP);
     }
 }
@@ -2821,19 +2839,28 @@ AVR_DI void substep_a_env(const KModel &m, EnvLDS &L, float *__restrict__ state,
     // kernel cleared it in this sub-step)
     static_assert(sizeof(EpaBuf) <= sizeof(EnvLDS), "EPA buffer overlay");
 #if !AVR_COOP_KERNEL
-    bool capped = false;
+    float *gst = state + (size_t)env * K_STATE_WORDS;
+    const bool persist = gld(gst + S_TASK + T_COOPN) >= (float)AVR_COOP_PERSIST;
+    int demand = 0;
     if (gld(env_cs(m, env) + CS_COOP) != 0.f) {
         float *ws = env_ws(m, env);
         const int rot = __float_as_int(gld(ws + WS_COOPROT));
-        capped = np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L), rot);
+        demand = np_coop(m, env_cs(m, env), __float_as_int(gld(env_cs(m, env) + CS_NSP)), *reinterpret_cast<EpaBuf *>(&L), rot,
+                         persist ? AVR_COOP_CAP : 1 << 30);
         if (lane_id() == 0) ws[WS_COOPROT] = __int_as_float(rot + AVR_COOP_CAP);
         SYNC();
     }
 #endif
+#if AVR_COOP_KERNEL
     float *gst = state + (size_t)env * K_STATE_WORDS;
+#endif
     load_a(m, L, gst, env_cs(m, env));
 #if !AVR_COOP_KERNEL
-    if (capped && lane_id() == 0) L.flags |= 32;
+    if (lane_id() == 0) {
+        L.st[S_TASK + T_COOPN] = demand > AVR_COOP_CAP ? L.st[S_TASK + T_COOPN] + 1.f : 0.f;
+        if (persist && demand > AVR_COOP_CAP) L.flags |= 32;
+    }
+    SYNC();
 #endif
     bool ok = substep_a(m, L, dt, gst, env_ws(m, env), env_rows(m, env), env_cs(m, env));
 #ifdef AVR_PROF
@@ -3452,26 +3479,6 @@ __global__ __launch_bounds__(64) void avr_substep_b4_kernel(const KModel *__rest
     substep_b4_block(*mp, state, mask, dt, frame_end, env0, n_envs, blockIdx.x, (lds_f *)(lds_f4 *)b4l);
 }
 
-// AVR_FUSE_AB: kernel a and part B in one launch.  A block of four waves takes part B's four envs
-// (block b: envs env0 + 32 (b / 8) + b % 8 + 8 w, the XCD that ran their pair and narrowphase
-// kernels); wave w runs kernel a for env w, then wave 0 runs part B on the four.  An env whose
-// kernel a is slow (a cooperative EPA) delays only its own block's part B, not every env's.
-#ifndef AVR_FUSE_AB
-#define AVR_FUSE_AB 0
-#endif
-#if AVR_FUSE_AB
-__global__ __launch_bounds__(256) void avr_substep_ab_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                             const unsigned char *__restrict__ mask, float dt, int frame_end, int env0,
-                                                             int n_envs) {
-    __shared__ union ABLds { EnvLDS a[4]; f4v b[B4_LDSW / 4]; } U;
-    const KModel &m = *mp;
-    const int w = threadIdx.x >> 6, b = blockIdx.x;
-    const int env = env0 + 32 * (b >> 3) + (b & 7) + 8 * w;
-    if (env < n_envs && (!mask || mask[env])) substep_a_env(m, U.a[w], state, dt, env, n_envs);
-    __syncthreads();
-    if (w == 0) substep_b4_block(m, state, mask, dt, frame_end, env0, n_envs, b, (lds_f *)(lds_f4 *)U.b);
-}
-#endif
 
 
 #if AVR_TASK == AVR_TASK_FEEDING
@@ -3619,15 +3626,10 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
         mark(AVR_K_COOP);
         hipLaunchKernelGGL(avr_coop_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, mask, env0, env1);
 #endif
-#if AVR_FUSE_AB
-        mark(AVR_K_AB);
-        hipLaunchKernelGGL(avr_substep_ab_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(256), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
-#else
         mark(AVR_K_A);
         hipLaunchKernelGGL(avr_substep_a_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, mask, h, env0, env1);
         mark(AVR_K_B);
         hipLaunchKernelGGL(avr_substep_b4_kernel, dim3(8 * ((n_envs + 31) / 32)), dim3(64), 0, stream, d_m, state, mask, h, frame_end, env0, env1);
-#endif
     };
     if (mode == MODE_SUBSTEP) {
         float h;

@@ -126,7 +126,7 @@ struct KModel {
 
 // Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):
 // an event is recorded before every launch (kind = AVR_K_*) and after the last one (kind -1).
-enum { AVR_K_TAKE = 0, AVR_K_A = 1, AVR_K_B = 2, AVR_K_TASK = 3, AVR_K_PAIRS = 4, AVR_K_NARROW = 5, AVR_K_COOP = 6, AVR_K_AB = 7, AVR_K_KINDS = 8 };
+enum { AVR_K_TAKE = 0, AVR_K_A = 1, AVR_K_B = 2, AVR_K_TASK = 3, AVR_K_PAIRS = 4, AVR_K_NARROW = 5, AVR_K_COOP = 6, AVR_K_KINDS = 8 };
 struct avr_evlog {
     hipEvent_t *ev;
     int *kind;

@@ -16,6 +16,7 @@
 #define T_FLAGS 8
 #define T_NCP 9
 #define T_HDYN 10
+#define T_COOPN 15      // consecutive sub-steps with more than AVR_COOP_CAP EPAs (avr_kernel.hip np_coop)
 
 #if AVR_TASK == AVR_TASK_FEEDING
 #define K_MAX_LINKS AVR_MAX_LINKS

@@ -67,6 +67,7 @@ enum { AVR_J_FIXED = 0, AVR_J_REVOLUTE = 1, AVR_J_PRISMATIC = 2 };
 #define AVR_T_FLAGS    8      /* bit0: NaN guard tripped                             */
 #define AVR_T_NCP      9      /* number of live contact points                       */
 #define AVR_T_HDYN     10     /* 1: impairment 'tremor', the head/neck chain is articulated */
+#define AVR_T_COOPN    15     /* consecutive sub-steps with more than 4 EPAs (all tasks; np_coop's cap) */
 #define AVR_T_WORDS    16
 #define AVR_S_HUMAN    (AVR_S_TASK + AVR_T_WORDS)          /* [AVR_MAX_HUMAN*7] slot poses */
 #define AVR_S_HCH      (AVR_S_HUMAN + AVR_MAX_HUMAN * 7)    /* head chain: [AVR_HC_N] target_human_joint_positions, [AVR_HC_N] human_tremors */

@@ -470,10 +470,11 @@ def test_lds_poison_build_is_bit_identical(lib_and_scene, tmp_path, b4_global):
 def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
     """An env whose arm was driven into the wheelchair's VHACD hulls (captured from a facade run
     after three rollovers, tests/golden/feeding_arm_in_wheelchair.npy) has ~21 penetrating hull
-    pairs per sub-step, each an EPA on the wave-cooperative path.  At most AVR_COOP_CAP = 4 are
-    solved per sub-step (a rotating window; the others keep their manifold points) and the env is
-    flagged (bit 5); it stays finite, and every other env of its launch is bit-identical to a run
-    without it."""
+    pairs per sub-step, each an EPA on the wave-cooperative path.  Once the overload has lasted
+    AVR_COOP_PERSIST = 20 sub-steps (T_COOPN), at most AVR_COOP_CAP = 4 are solved per sub-step (a
+    rotating window; the others keep their manifold points) and the env is flagged (bit 5); it
+    stays finite, every other env of its launch is bit-identical to a run without it, and none of
+    those -- fresh resets with food dropped into the spoon, transient penetrations -- is capped."""
     from avr import _lib
     A, md = lib_and_scene
     bad = np.load(os.path.join(HERE, 'feeding_arm_in_wheelchair.npy')).astype(np.float32)
@@ -484,7 +485,7 @@ def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
     for states in (X, S):
         sim = make_sim(md, len(states))
         sim.set_state(states)
-        for t in range(3):
+        for t in range(4):
             a = _lib.random_actions(1001, np.arange(63), t)
             if len(states) == 64:
                 a = np.concatenate([a[:20], np.zeros((1, a.shape[1]), a.dtype), a[20:]])
@@ -492,6 +493,8 @@ def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
         runs.append((sim.get_state(), sim.get_flags()))
         sim.close()
     (G, f), (G0, f0) = runs
+    from avr import _abi as ABI
     assert f[20] & 32, f[20]
+    assert G[20, ABI.S_TASK + ABI.T_COOPN] >= 20
     assert np.all(np.isfinite(G[20]))
     assert np.array_equal(G[keep], G0) and not np.any(f0 & 32)
