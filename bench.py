@@ -206,6 +206,9 @@ def main():
     ap.add_argument('--facade', action='store_true',
                     help='time the gym facade (avr.env.AVRTorchVecEnv: device tensors, TimeLimit 200 with auto-reset) '
                          'instead of the bare step; --steps should span rollovers (e.g. 600)')
+    ap.add_argument('--dist-backend', default='nccl', choices=('nccl', 'gloo'),
+                    help="torch.distributed backend for --gpus > 1: nccl (RCCL over xGMI, the product path); gloo only "
+                         "rehearses the multi-rank flow where ranks share a GPU (rollouts gathered through host memory)")
     ap.add_argument('--impairment', default='random',
                     help="human impairment per env: 'random' is the tasks' own setting (feeding.py:175, scratch_itch.py:178)")
     args = ap.parse_args()
@@ -223,10 +226,16 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
+    gloo = args.dist_backend == 'gloo'
+    if gloo:        # rehearsal: ranks may share the GPUs there are
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if gloo:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
     A = ABI.load_scene(T['task'])
@@ -253,7 +262,7 @@ def main():
     G = args.gather_every
     W = D.roll_width(L.OBS_DIM)
     roll = torch.zeros(G, E, W, device=dev)
-    gathered = torch.zeros(world * G * E * W, device=dev) if world > 1 else None
+    gathered = torch.zeros(world * G * E * W, device='cpu' if gloo else dev) if world > 1 else None
 
     def one_step(t, k):
         sim.step_random_device(t, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr())
@@ -262,7 +271,7 @@ def main():
                 j = k % G
                 D.pack_rollout(roll, j, obs, rew, info, done)
                 if j == G - 1:
-                    D.gather_rollouts(roll, out=gathered)
+                    D.gather_rollouts(roll.cpu() if gloo else roll, out=gathered)
 
     for w in range(args.warmup):
         one_step(w, w)
@@ -284,7 +293,7 @@ def main():
     el = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64, device='cpu' if gloo else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     # per-kernel launch durations (HIP events between the launches of a step, on the sim
@@ -334,6 +343,7 @@ def main():
                    'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
                    'global_envs': world * E, 'substeps_per_env_step': T['substeps'], 'solver_iterations': T['iters'],
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None,
+                   'dist_backend': args.dist_backend if world > 1 else None,
                    'env_groups': sim.env_groups()},
         'roofline': {'bound': bound, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
