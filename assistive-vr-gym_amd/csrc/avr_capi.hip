@@ -46,17 +46,13 @@ struct avr_sim {
     size_t ikcap;
     float *d_bs;                           // device scratch of avr_base_search (draws, goals, per-attempt results)
     size_t bscap;
-    // the step's launch sequence (every group's 52 launches and the fork / join events) captured
-    // once as a HIP graph and replayed; keyed by the step's buffers and mode, the step counter t
-    // is patched into the take-step nodes before each replay
+    // the step's launch sequence (every group's launches and the fork / join events) captured
+    // once as a HIP graph and replayed; keyed by the step's buffers and mode.  The take-step
+    // nodes read the step counter from km.step_t, written before each replay
     int use_graph;
     hipGraph_t graph;
     hipGraphExec_t gexec;
     const void *gkey[6];
-    struct TakeArgs { const KModel *m; float *state; const float *act; const unsigned char *mask; int mode; long long t; int env0, env1; };
-    std::vector<hipGraphNode_t> gtake;     // take-step kernel nodes (one per group)
-    std::vector<hipKernelNodeParams> gtp;  // their launch parameters
-    std::vector<TakeArgs> gargs;           // and argument values
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -451,6 +447,13 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         s->allocs.push_back(cscr);
         k.cscr = cscr;
     }
+    {
+        long long *st = nullptr;
+        HIPCHK(s, hipMalloc(&st, sizeof(long long)));
+        HIPCHK(s, hipMemset(st, 0, sizeof(long long)));
+        s->allocs.push_back(st);
+        k.step_t = st;
+    }
     HIPCHK(s, hipMalloc(&s->d_km, sizeof(KModel)));
     HIPCHK(s, hipMemcpy(s->d_km, &s->km, sizeof(KModel), hipMemcpyHostToDevice));
     HIPCHK(s, hipMalloc(&s->d_state, E * K_STATE_WORDS * sizeof(float)));
@@ -497,7 +500,6 @@ static void drop_graph(avr_sim *s) {
     if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
     if (s->graph) (void)hipGraphDestroy(s->graph);
     s->gexec = nullptr; s->graph = nullptr;
-    s->gtake.clear(); s->gtp.clear(); s->gargs.clear();
 }
 
 // a gym step (modes 0 / 1, no mask, no per-kernel timing) replays the captured launch sequence;
@@ -509,41 +511,18 @@ static hipError_t run_step(avr_sim *s, float *state, const float *act, float *ob
     const void *key[6] = {act, obs, rew, done, info, (const void *)(size_t)mode};
     hipError_t e;
     if (!s->gexec || memcmp(key, s->gkey, sizeof(key)) != 0) {
+        if (s->gexec && (e = hipStreamSynchronize(s->stream)) != hipSuccess) return e;   // (no replay of the old graph in flight)
         drop_graph(s);
         if ((e = hipStreamBeginCapture(s->stream, hipStreamCaptureModeRelaxed)) != hipSuccess) return e;
-        hipError_t el = run_step_direct(s, state, act, obs, rew, done, info, nullptr, mode, t);
+        hipError_t el = run_step_direct(s, state, act, obs, rew, done, info, nullptr, mode, -1);
         if ((e = hipStreamEndCapture(s->stream, &s->graph)) != hipSuccess) return e;
         if (el != hipSuccess) { drop_graph(s); return el; }
-        size_t n = 0;
-        if ((e = hipGraphGetNodes(s->graph, nullptr, &n)) != hipSuccess) return e;
-        std::vector<hipGraphNode_t> nodes(n);
-        if ((e = hipGraphGetNodes(s->graph, nodes.data(), &n)) != hipSuccess) return e;
-        for (hipGraphNode_t nd : nodes) {
-            hipGraphNodeType ty;
-            if (hipGraphNodeGetType(nd, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
-            hipKernelNodeParams p;
-            if ((e = hipGraphKernelNodeGetParams(nd, &p)) != hipSuccess) return e;
-            if (p.func != (void *)avr_take_step_kernel) continue;
-            avr_sim::TakeArgs a;
-            a.m = *(const KModel **)p.kernelParams[0]; a.state = *(float **)p.kernelParams[1];
-            a.act = *(const float **)p.kernelParams[2]; a.mask = *(const unsigned char **)p.kernelParams[3];
-            a.mode = *(int *)p.kernelParams[4]; a.t = *(long long *)p.kernelParams[5];
-            a.env0 = *(int *)p.kernelParams[6]; a.env1 = *(int *)p.kernelParams[7];
-            p.kernelParams = nullptr;
-            s->gtake.push_back(nd); s->gtp.push_back(p); s->gargs.push_back(a);
-        }
-        if (s->gtake.empty()) { drop_graph(s); return hipErrorInvalidValue; }
         if ((e = hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0)) != hipSuccess) { drop_graph(s); return e; }
         memcpy(s->gkey, key, sizeof(key));
     }
-    for (size_t i = 0; i < s->gtake.size(); i++) {
-        avr_sim::TakeArgs &a = s->gargs[i];
-        a.t = t;
-        void *args[8] = {&a.m, &a.state, &a.act, &a.mask, &a.mode, &a.t, &a.env0, &a.env1};
-        hipKernelNodeParams p = s->gtp[i];
-        p.kernelParams = args;
-        if ((e = hipGraphExecKernelNodeSetParams(s->gexec, s->gtake[i], &p)) != hipSuccess) return e;
-    }
+    // the step counter goes to device memory in stream order (an executable graph is never edited
+    // while an earlier replay of it may still run)
+    if ((e = avr_launch_set_step(s->km.step_t, t, s->stream)) != hipSuccess) return e;
     return hipGraphLaunch(s->gexec, s->stream);
 }
 

@@ -1790,6 +1790,9 @@ AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.
 #ifndef B4_PK
 #define B4_PK 1     // free parts stored as (linear, angular) pairs per axis: packed-f32 row resolves (0: scalar layout)
 #endif
+#ifndef B4_FPAIR
+#define B4_FPAIR B4_PK   // friction units resolved as a pair through their coupling (go4_pair)
+#endif
 AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
     const float *g = L.gsc[f];
     const qt q = ldq(L.st + S_FREE + AVR_FB_WORDS * f + 3);
@@ -2078,6 +2081,25 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 rhs = (poserr + velerr) * inv;
             }
             w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs; w[3] = fric;
+#if B4_FPAIR
+            if (k == 2) {
+                // the friction unit's coupling c = J_2 M^-1 J_1^T (its second row's 4th header word,
+                // where the first row keeps the friction coefficient): part B resolves the second
+                // row with J_2.dv + delta_1 c instead of re-reading the velocities row 1 changed.
+                // In part B's mass-normalised coordinates: the two rows' free parts dotted, plus the
+                // second row's J against the first's M^-1 J^T (this lane's own stores, read back)
+                const float *w1 = row_crec(rows, ncp + 2 * i);
+                float cc = 0.f;
+#pragma unroll
+                for (int q = 4; q < CRW; q++) cc = fmaf(w1[q], w[q], cc);
+                if (rob) {
+                    const float *r1 = row_rob(m, rows, slot0 + 1), *r2 = row_rob(m, rows, slot0 + 2);
+#pragma unroll
+                    for (int q = 0; q < 16 * NDL; q++) cc = fmaf(r2[2 * q], r1[2 * q + 1], cc);
+                }
+                w[3] = cc;
+            }
+#endif
         }
     }
     if (lane == 0) L.n_c = ncp;
@@ -2371,6 +2393,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const int env = env0 + 512 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
+    if (t < 0) t = *m.step_t;                  // graph replay: the counter written before the launch (run_step)
     float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
     ws[WS_COOPROT] = 0.f;                       // the capped cooperative-pair window restarts every gym step (np_coop)
@@ -3039,9 +3062,12 @@ struct CLds {
         R.h.x = a.x; R.h.y = a.y; R.h.z = q[2];
         R.imp = *R.ip;
     }
-    AVR_DI void hdr2(Row &B, const Row &A) const {   // a unit's second row: inv, rhs (the rest is the first row's)
+    AVR_DI void hdr2(Row &B, const Row &A) const {   // a unit's second row: inv, rhs, coupling (the rest is the first row's)
         const lds_f *q = (const lds_f *)(blk + A.wb + 8 + CRW * 4);
         B.h.y = q[1]; B.h.z = q[2];
+#if B4_FPAIR
+        B.h.w = q[3];
+#endif
         B.imp = A.ip[1];
     }
     AVR_DI unsigned own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.wb + 24 * o : LNB_ZERO; }
@@ -3072,7 +3098,11 @@ struct CGlb {
     AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
+#if B4_FPAIR
+    AVR_DI void hdr2(Row &B, const Row &A) const { const f4v a = bld3(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.h.w = a.z; B.imp = A.ip[1]; }
+#else
     AVR_DI void hdr2(Row &B, const Row &A) const { const f2v a = bld2(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.imp = A.ip[1]; }
+#endif
     AVR_DI int own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.o - 8 + 24 * o : B4_OOB; }
     AVR_DI void own_at(Row &R, int b) const { R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16); }
     AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + ROBW * 4 * s : B4_OOB; }
@@ -3148,6 +3178,42 @@ AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, f
     return ni;
 #endif
 }
+
+// A friction unit: its two rows share their bodies, so the second row's J.dv after the first
+// row's update is J_2.dv + delta_1 c with c = J_2 M^-1 J_1^T (kernel a stores it in the second
+// row's header).  Both dot products are formed from the same velocities side by side, so only the
+// scalar correction stays on the dependency chain between the two resolves; the velocities then
+// take both rows' increments.  The same Gauss-Seidel step as two go4 calls, rounded differently.
+#if B4_FPAIR
+template <bool RP, class R>
+AVR_DI void go4_pair(const R &A, const R &B, DV &d, float &ia, float &ib, float lim) {
+#pragma clang fp contract(off)
+    f2v sa = A.j0 * d.v1, sb = B.j0 * d.v1;
+    if (RP) {
+        sa.y = fmaf(A.r.x, d.rq, sa.y); sb.y = fmaf(B.r.x, d.rq, sb.y);
+#if NDL == 2
+        sa.y = fmaf(A.r.z, d.rq2, sa.y); sb.y = fmaf(B.r.z, d.rq2, sb.y);
+#endif
+    }
+    sa = __builtin_elementwise_fma(A.j1, d.v2, sa); sb = __builtin_elementwise_fma(B.j1, d.v2, sb);
+    sa = __builtin_elementwise_fma(A.j2, d.v3, sa); sb = __builtin_elementwise_fma(B.j2, d.v3, sb);
+    const float dva = row16_sum(sa.x + sa.y), dvb0 = row16_sum(sb.x + sb.y);
+    const float na = __builtin_amdgcn_fmed3f(ia + fmaf(-dva, A.h.y, A.h.z), -lim, lim);
+    const float da = na - ia;
+    const float dvb = fmaf(da, B.h.w, dvb0);
+    const float nb = __builtin_amdgcn_fmed3f(ib + fmaf(-dvb, B.h.y, B.h.z), -lim, lim);
+    const float db = nb - ib;
+    const f2v dda = {da, da}, ddb = {db, db};
+    d.v1 = __builtin_elementwise_fma(B.j0, ddb, __builtin_elementwise_fma(A.j0, dda, d.v1));
+    d.v2 = __builtin_elementwise_fma(B.j1, ddb, __builtin_elementwise_fma(A.j1, dda, d.v2));
+    d.v3 = __builtin_elementwise_fma(B.j2, ddb, __builtin_elementwise_fma(A.j2, dda, d.v3));
+    if (RP) d.rq = fmaf(B.r.y, db, fmaf(A.r.y, da, d.rq));
+#if NDL == 2
+    if (RP) d.rq2 = fmaf(B.r.w, db, fmaf(A.r.w, da, d.rq2));
+#endif
+    ia = na; ib = nb;
+}
+#endif
 
 // sweep over n (wave-uniform) steps; at(R, j) sets R's addresses for step j (a null row for
 // every j past this lane's group's rows).  Software pipeline of depth D: headers 2D steps ahead,
@@ -3240,8 +3306,14 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
         };
         auto go = [&](const Pair4<CS> &Y) {
             const float lim = Y.a.h.w * Y.in;
+#if B4_FPAIR
+            float ia = Y.a.imp, ib = Y.b.imp;
+            go4_pair<CS::robot_parts>(Y.a, Y.b, d, ia, ib, lim);
+            Y.a.ip[0] = ia; Y.a.ip[1] = ib;
+#else
             Y.a.ip[0] = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
             Y.a.ip[1] = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
+#endif
         };
         // (whole rounds of K units, null units past the end, unconditional read-ahead: sweep4)
         int cn = lst(0);
@@ -3650,6 +3722,12 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
     mark(AVR_K_TASK);
     hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, env0, env1);
     mark(-1);
+    return hipGetLastError();
+}
+
+__global__ void avr_set_step_kernel(long long *dst, long long t) { *dst = t; }
+hipError_t avr_launch_set_step(long long *dst, long long t, hipStream_t stream) {
+    hipLaunchKernelGGL(avr_set_step_kernel, dim3(1), dim3(1), 0, stream, dst, t);
     return hipGetLastError();
 }
 

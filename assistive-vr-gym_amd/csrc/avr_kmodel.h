@@ -122,6 +122,7 @@ struct KModel {
     float *ws;                 // per-env workspace between sub-step kernels: [n_envs][128]
     float *cscr;               // per-env collision scratch between the part-A kernels: [n_envs][CS_WORDS]
     unsigned long long *prof;  // diagnostic builds only (AVR_PROF): [n_envs][16] cycle counters
+    long long *step_t;         // the step counter of a replayed step graph (take_step reads it when passed t < 0)
 };
 
 // Optional event log filled by avr_launch_step (per-kernel timing, see avr_kernel_times):

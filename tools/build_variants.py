@@ -27,6 +27,7 @@ VARIANTS = {
     'l8k': ('-DB4_LDSW=8192',), 'l7k': ('-DB4_LDSW=7168',), 'l6k': ('-DB4_LDSW=6144',), 'np4nb4': ('-DNP_WAVES=4', '-DGJK_NB=4'),
     'coopk': ('-DAVR_COOP_KERNEL=1',), 'ml': ('-DAVR_MINV_LAUNDER=1',), 'mlc': ('-DAVR_MINV_LAUNDER=1', '-DAVR_COOP_KERNEL=1'),
     'mlc2': ('-DAVR_MINV_LAUNDER=1', '-DAVR_COOP_KERNEL=1', '-DAVR_WAVES_PER_EU=2'),
+    'nofp': ('-DB4_FPAIR=0',),
     'nonl': ('-DB4_NC_LDS=0',), 'fnl': ('-DB4_NC_LDS=1',), 'fnl12': ('-DB4_NC_LDS=1', '-DB4_LDSW=12288'), 'fnl11': ('-DB4_NC_LDS=1', '-DB4_LDSW=11264'), 'dnl2': ('-DB4_DNL=2',), 'noml': ('-DAVR_MINV_LAUNDER=0',),
 }
 
