@@ -20,7 +20,9 @@ EXPORTS = [
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
     'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik', 'avr_base_search',
+    'avr_graph_captures',
 ]
+FLAGS_FAULT_MASK = 0x1f      # include/avr.h AVR_FLAGS_FAULT_MASK: bits 0-4; bit 5 (EPA budget) is informational
 
 
 # avr_config.flags: no bit is defined (include/avr.h); avr_create rejects any set bit
@@ -69,6 +71,8 @@ def load(path=LIB_PATH):
     lib.avr_n_envs.argtypes = [vp]
     lib.avr_env_groups.argtypes = [vp]
     lib.avr_env_groups.restype = C.c_int32
+    lib.avr_graph_captures.argtypes = [vp]
+    lib.avr_graph_captures.restype = C.c_int64
     lib.avr_state_words.restype = C.c_int32
     lib.avr_abi_version.restype = C.c_int32
     lib.avr_kernel_info.argtypes = [vp, vp]
@@ -237,7 +241,9 @@ class Sim:
     def env_groups(self):
         return int(self.lib.avr_env_groups(self.h))
 
-
+    def graph_captures(self):
+        """HIP-graph captures this handle has made (one per distinct output-buffer key)."""
+        return int(self.lib.avr_graph_captures(self.h))
 
     def profile_kernels(self, enable=True):
         self._chk(self.lib.avr_profile_kernels(self.h, int(bool(enable))))

@@ -349,7 +349,9 @@ class AVRVecEnv:
         return self._obs.copy()
 
     def flags(self):
-        """Per-env health flags (include/avr.h avr_get_flags; 0 = healthy), without copying the state."""
+        """Per-env health flags (include/avr.h avr_get_flags), without copying the state.  Bits 0-4
+        (_lib.FLAGS_FAULT_MASK) are faults, 0 there = healthy; bit 5 is informational (the env ran
+        under the EPA budget, its state is finite)."""
         return self.sim.get_flags().astype(np.int64)
 
     def get_state(self):
@@ -376,7 +378,7 @@ class AVRTorchVecEnv(AVRVecEnv):
         super().__init__(*args, **kw)
         import torch
         self.torch = torch
-        self.dev = torch.device('cuda', kw.get('device', 0))
+        self.dev = torch.device('cuda', int(self.device))
         self.ext = torch.cuda.ExternalStream(self.sim.stream(), device=self.dev)
         n, L = self.n, self.L
         self.t_obs = torch.zeros(n, L.OBS_DIM, device=self.dev)

@@ -14,6 +14,8 @@ checkpoint format that loads with torch.load(weights_only=True) -- and evaluates
 AVRTorchVecEnv, n_envs episodes at once.  Policies are synthetic (random init) unless a
 checkpoint saved by save_policy is given.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -87,7 +89,8 @@ def load_policy(path, device='cpu'):
 
 def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=True, setup=None, device=0, seed=1001):
     """Run one 200-step trial in each of n_envs envs (enjoy_vr.py:92-116 per env) and return
-    per-env episode return, mean total_force_on_human and final task_success.
+    per-env episode return, mean total_force_on_human and final task_success, plus the stepping
+    loop's wall time (policy forward + env.step, synchronised at both ends) as loop_s.
     setup: dict(gender, participant, policy_name[, hipbone_to_mouth_height]) for env.setup."""
     from .env import AVRTorchVecEnv
     env = AVRTorchVecEnv(env_id, n_envs, device=device, seed=seed, auto_reset=False)
@@ -102,6 +105,8 @@ def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=T
         ret = torch.zeros(n_envs, device=dev)
         force = torch.zeros(n_envs, device=dev)
         info = None
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
         for _ in range(steps):
             with torch.no_grad():
                 _, action, _, hxs = actor_critic.act(normalize(obs, ob_rms), hxs, masks, deterministic=deterministic)
@@ -110,7 +115,10 @@ def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=T
             masks = (~done).float()[:, None]
             ret += rew
             force += info['total_force_on_human']
+        torch.cuda.synchronize(dev)
+        loop_s = time.perf_counter() - t0
         return dict(returns=ret.cpu().numpy(), mean_force=(force / steps).cpu().numpy(),
-                    task_success=info['task_success'].cpu().numpy() if info is not None else None, done=done.cpu().numpy())
+                    task_success=info['task_success'].cpu().numpy() if info is not None else None, done=done.cpu().numpy(),
+                    loop_s=loop_s, graph_captures=env.sim.graph_captures())
     finally:
         env.close()

@@ -19,6 +19,7 @@
     void *avr_state_device_ptr(avr_sim *s);                                                                        \
     int32_t avr_n_envs(avr_sim *s);                                                                                \
     int32_t avr_env_groups(avr_sim *s);                                                                            \
+    int64_t avr_graph_captures(avr_sim *s);                                                                        \
     int32_t avr_n_dof(avr_sim *s);                                                                                 \
     int avr_set_state(avr_sim *s, const float *h);                                                                 \
     int avr_set_state_masked(avr_sim *s, const uint8_t *mask, const float *h);                                     \
@@ -150,6 +151,7 @@ void *avr_state_device_ptr(avr_sim *s) {
 int32_t avr_n_envs(avr_sim *s) { if (!s || !s->impl) return 0; DISPATCH(s, avr_n_envs(h)); }
 int32_t avr_env_groups(avr_sim *s) { if (!s || !s->impl) return 0; DISPATCH(s, avr_env_groups(h)); }
 int32_t avr_n_dof(avr_sim *s) { if (!s || !s->impl) return 0; DISPATCH(s, avr_n_dof(h)); }
+int64_t avr_graph_captures(avr_sim *s) { if (!s || !s->impl) return -1; DISPATCH(s, avr_graph_captures(h)); }
 int avr_set_state(avr_sim *s, const float *p) { DISPATCH(s, avr_set_state(h, p)); }
 int avr_get_state(avr_sim *s, float *p) { DISPATCH(s, avr_get_state(h, p)); }
 int avr_set_state_masked(avr_sim *s, const uint8_t *m, const float *p) { DISPATCH(s, avr_set_state_masked(h, m, p)); }

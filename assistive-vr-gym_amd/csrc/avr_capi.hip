@@ -15,6 +15,7 @@
 #include "../../include/avr.h"
 
 #define AVR_MAX_GROUPS 8
+#define AVR_GRAPH_SLOTS 4
 
 struct avr_sim {
     avr_config cfg;
@@ -47,12 +48,30 @@ struct avr_sim {
     float *d_bs;                           // device scratch of avr_base_search (draws, goals, per-attempt results)
     size_t bscap;
     // the step's launch sequence (every group's launches and the fork / join events) captured
-    // once as a HIP graph and replayed; keyed by the step's buffers and mode.  The take-step
-    // nodes read the step counter from km.step_t, written before each replay
+    // once as a HIP graph and replayed.  A graph reads its actions from the handle's own d_act
+    // (a caller's action buffer is copied there in stream order first), so it is keyed only by
+    // the output buffers and the mode: one executable graph per key, a few keys cached (least
+    // recently used evicted).  The take-step nodes read the step counter from km.step_t, written
+    // in stream order before each replay; an executable graph is never edited.
     int use_graph;
-    hipGraph_t graph;
-    hipGraphExec_t gexec;
-    const void *gkey[6];
+    struct GraphSlot { hipGraph_t graph; hipGraphExec_t gexec; const void *key[5]; unsigned long long used; };
+    GraphSlot gslot[AVR_GRAPH_SLOTS];
+    unsigned long long gclock;
+    long long n_captures;                  // diagnostics (avr_graph_captures)
+};
+
+// Every entry point runs on the handle's device and restores the caller's current device on
+// return: scratch buffers allocated lazily (hipMalloc) land on the handle's GPU whatever device
+// the caller (or another handle, or torch) made current.
+struct DevGuard {
+    int prev = -1, dev;
+    explicit DevGuard(int d) : dev(d) {
+        if (hipGetDevice(&prev) != hipSuccess || prev == d) prev = -1;
+        else (void)hipSetDevice(d);
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
 };
 
 static int fail(avr_sim *s, int code, const char *fmt, ...) {
@@ -171,7 +190,12 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     if (e != hipSuccess || ndev == 0) { int r = fail(s, -4, "no HIP device available (%s)", hipGetErrorString(e)); *out = s; return r; }
     if (cfg->device < 0 || cfg->device >= ndev) { int r = fail(s, -4, "device %d out of range (%d devices)", cfg->device, ndev); *out = s; return r; }
     *out = s;
-    HIPCHK(s, hipSetDevice(cfg->device));
+    DevGuard dg(cfg->device);
+    {
+        int cur = -1;
+        HIPCHK(s, hipGetDevice(&cur));
+        if (cur != cfg->device) return fail(s, -4, "hipSetDevice(%d) failed", cfg->device);
+    }
     HIPCHK(s, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     {
         // default: one group per 1024 envs, at most 4 (4096 envs: 600k -> 680k env-steps/s, the
@@ -496,40 +520,64 @@ static hipError_t run_step_direct(avr_sim *s, float *state, const float *act, fl
     return hipSuccess;
 }
 
-static void drop_graph(avr_sim *s) {
-    if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-    if (s->graph) (void)hipGraphDestroy(s->graph);
-    s->gexec = nullptr; s->graph = nullptr;
+static void drop_graph(avr_sim::GraphSlot &g) {
+    if (g.gexec) (void)hipGraphExecDestroy(g.gexec);
+    if (g.graph) (void)hipGraphDestroy(g.graph);
+    g.gexec = nullptr; g.graph = nullptr;
+    memset(g.key, 0, sizeof(g.key));
+    g.used = 0;
 }
 
-// a gym step (modes 0 / 1, no mask, no per-kernel timing) replays the captured launch sequence;
-// everything else launches directly
+// a gym step (modes 0 / 1, no mask, no per-kernel timing) replays a captured launch sequence;
+// everything else launches directly.  Mode 0's actions are first copied (stream-ordered,
+// device to device) into the handle's d_act, which every graph reads: a caller that hands a new
+// action buffer each step (a policy's output tensor) replays the same graph.
 static hipError_t run_step(avr_sim *s, float *state, const float *act, float *obs, float *rew, unsigned char *done, float *info,
                            const unsigned char *mask, int mode, long long t) {
     if (!s->use_graph || mask || s->evlog.cap || (mode != 0 && mode != 1) || state != s->d_state)
         return run_step_direct(s, state, act, obs, rew, done, info, mask, mode, t);
-    const void *key[6] = {act, obs, rew, done, info, (const void *)(size_t)mode};
     hipError_t e;
-    if (!s->gexec || memcmp(key, s->gkey, sizeof(key)) != 0) {
-        if (s->gexec && (e = hipStreamSynchronize(s->stream)) != hipSuccess) return e;   // (no replay of the old graph in flight)
-        drop_graph(s);
-        if ((e = hipStreamBeginCapture(s->stream, hipStreamCaptureModeRelaxed)) != hipSuccess) return e;
-        hipError_t el = run_step_direct(s, state, act, obs, rew, done, info, nullptr, mode, -1);
-        if ((e = hipStreamEndCapture(s->stream, &s->graph)) != hipSuccess) return e;
-        if (el != hipSuccess) { drop_graph(s); return el; }
-        if ((e = hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0)) != hipSuccess) { drop_graph(s); return e; }
-        memcpy(s->gkey, key, sizeof(key));
+    if (mode == 0 && act != s->d_act) {
+        if (!act) return hipErrorInvalidValue;
+        if ((e = hipMemcpyAsync(s->d_act, act, (size_t)s->cfg.n_envs * K_ACT_DIM * sizeof(float), hipMemcpyDeviceToDevice, s->stream)) != hipSuccess)
+            return e;
     }
+    const void *key[5] = {obs, rew, done, info, (const void *)(size_t)(mode + 1)};
+    avr_sim::GraphSlot *g = nullptr;
+    for (auto &x : s->gslot)
+        if (x.gexec && memcmp(key, x.key, sizeof(key)) == 0) g = &x;
+    if (!g) {
+        // a free slot, else the least recently used one (after the stream has drained: no replay
+        // of the graph being destroyed may still be in flight)
+        for (auto &x : s->gslot)
+            if (!x.gexec && !g) g = &x;
+        if (!g) {
+            g = &s->gslot[0];
+            for (auto &x : s->gslot)
+                if (x.used < g->used) g = &x;
+            if ((e = hipStreamSynchronize(s->stream)) != hipSuccess) return e;
+            drop_graph(*g);
+        }
+        if ((e = hipStreamBeginCapture(s->stream, hipStreamCaptureModeRelaxed)) != hipSuccess) return e;
+        hipError_t el = run_step_direct(s, state, mode == 0 ? s->d_act : nullptr, obs, rew, done, info, nullptr, mode, -1);
+        if ((e = hipStreamEndCapture(s->stream, &g->graph)) != hipSuccess) return e;
+        if (el != hipSuccess) { drop_graph(*g); return el; }
+        if ((e = hipGraphInstantiate(&g->gexec, g->graph, nullptr, nullptr, 0)) != hipSuccess) { drop_graph(*g); return e; }
+        memcpy(g->key, key, sizeof(key));
+        s->n_captures++;
+    }
+    g->used = ++s->gclock;
     // the step counter goes to device memory in stream order (an executable graph is never edited
     // while an earlier replay of it may still run)
     if ((e = avr_launch_set_step(s->km.step_t, t, s->stream)) != hipSuccess) return e;
-    return hipGraphLaunch(s->gexec, s->stream);
+    return hipGraphLaunch(g->gexec, s->stream);
 }
 
 int avr_destroy(avr_sim *s) {
     if (!s) return -1;
+    DevGuard dg(s->cfg.device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    drop_graph(s);
+    for (auto &x : s->gslot) drop_graph(x);
     for (void *p : s->allocs) (void)hipFree(p);
     if (s->d_state) (void)hipFree(s->d_state);
     if (s->d_km) (void)hipFree(s->d_km);
@@ -560,8 +608,11 @@ void *avr_state_device_ptr(avr_sim *s) { return s ? (void *)s->d_state : nullptr
 int32_t avr_n_envs(avr_sim *s) { return s ? s->cfg.n_envs : 0; }
 int32_t avr_env_groups(avr_sim *s) { return s ? s->ngroups : 0; }
 
-#define CHECK_SIM(s) \
-    if (!(s) || !(s)->d_state) return -1
+#define CHECK_SIM(s)                         \
+    if (!(s) || !(s)->d_state) return -1;    \
+    DevGuard dev_guard_((s)->cfg.device)
+
+int64_t avr_graph_captures(avr_sim *s) { return s ? s->n_captures : -1; }
 
 int avr_set_state(avr_sim *s, const float *h) {
     CHECK_SIM(s);
@@ -640,6 +691,9 @@ int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, 
 
 int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info) {
     CHECK_SIM(s);
+    // (negative step indices are reserved: the graph-captured take-step reads the counter from
+    // device memory when its argument is negative)
+    if (t < 0) return fail(s, -1, "avr_step_random_device: step index %lld < 0", (long long)t);
     HIPCHK(s, run_step(s, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
                               d_info ? d_info : s->d_info, nullptr, 1, t));
     return 0;
@@ -647,6 +701,7 @@ int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, ui
 
 int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {
     CHECK_SIM(s);
+    if (t < 0) return fail(s, -1, "avr_random_actions_device: step index %lld < 0", (long long)t);
     HIPCHK(s, avr_launch_random_actions(s->cfg.seed, s->cfg.env_offset, t, d_act, s->cfg.n_envs, s->km.n_arm, s->stream));
     return 0;
 }

@@ -53,16 +53,16 @@ def layout_bytes_per_env_step(L):
     return 2 * L.STATE_WORDS * 4 + (L.OBS_DIM + 1 + L.INFO_DIM) * 4 + 1
 
 
-def reset_pool(task, A, md, ids, impairment):
+def reset_pool(task, A, md, ids, impairment, device=0):
     """Reset states of the bench's env pool; the PR2 tasks' base-pose search runs on the device
-    (avr_base_search) with the reference's 100 attempts of 200 IK iterations."""
+    (avr_base_search) with the reference's 100 attempts of 200 IK iterations, on this rank's GPU."""
     if task in (1, 2):
         from avr import _lib
-        sim = _lib.Sim(md, 1)
+        sim = _lib.Sim(md, 1, device=device)
         try:
             if task == 2:
                 from avr import reset_bedbath as RBB
-                return RBB.batch_reset_states(A, md, 1001, ids, sim=sim)
+                return RBB.batch_reset_states(A, md, 1001, ids, sim=sim, device=device)
             from avr import reset_scratch as RSS
             return RSS.batch_reset_states(A, md, 1001, ids, impairment=impairment, sim=sim)
         finally:
@@ -148,17 +148,29 @@ def facade_bench(args):
         act.uniform_(-1, 1, generator=gen)
         v.step(act)
     torch.cuda.synchronize(dev)
-    roll, t_roll = 0, []
+    roll, t_roll, t_drain = 0, [], []
+    c0 = v.sim.graph_captures()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        act.uniform_(-1, 1, generator=gen)
+        if args.fresh_actions:      # a new action tensor every step, as a policy's output is
+            act = torch.rand(E, v.L.ACT_DIM, device=dev, generator=gen) * 2 - 1
+        else:
+            act.uniform_(-1, 1, generator=gen)
+        due = bool((v.iteration + 1 >= v.max_steps).any())
+        if due:
+            # a rollover step synchronises inside step(): drain the steps queued ahead of it first,
+            # so that rollover_ms is the rollover step itself (its launches + the masked reset)
+            td = time.perf_counter()
+            torch.cuda.synchronize(dev)
+            t_drain.append(time.perf_counter() - td)
         ts = time.perf_counter()
         _, _, _, info = v.step(act)
-        if 'terminal_observation' in info:     # (a rollover step synchronises inside step)
+        if 'terminal_observation' in info:
             roll += 1
             t_roll.append(time.perf_counter() - ts)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    captures = v.sim.graph_captures() - c0
     # the same loop over steps that end no episode (synchronised at both ends, after the next
     # episode's reset draws are ready so that no prefetch runs beside it)
     if v._prefetch:
@@ -179,10 +191,16 @@ def facade_bench(args):
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
            'data': 'synthetic: torch uniform(-1, 1) actions on the device; resets drawn per env and episode',
            'config': {'workload': args.task + ', %d envs, gym facade with rollover' % E, 'task': args.task, 'envs_per_gpu': E,
-                      'impairment': args.impairment, 'reset_ik': 'device' if v.device_ik else 'host'},
+                      'impairment': args.impairment,
+                      'reset_ik': ('device IK' if v.device_ik else 'device base-pose search' if v.device_search else 'host')},
            'rollovers_timed': roll, 'env_steps_per_s_between_rollovers': E / no_roll, 'between_rollovers_steps': K,
            'between_rollovers_host_ms_per_step': [round(float(np.median(host_ms)), 3), round(float(np.max(host_ms)), 3)],
-           'rollover_ms': float(np.mean(t_roll) * 1e3) if roll else None, 'first_reset_s': t_reset,
+           'rollover_ms': float(np.mean(t_roll) * 1e3) if roll else None,
+           'rollover_scope': 'one rollover step: its launches, the synchronisation and the masked device reset, after the steps '
+                             'queued ahead of it were drained (drain_ms_before_rollover, not part of rollover_ms)',
+           'drain_ms_before_rollover': float(np.mean(t_drain) * 1e3) if t_drain else None,
+           'fresh_action_tensor_per_step': bool(args.fresh_actions), 'graph_captures_in_timed_loop': captures,
+           'first_reset_s': t_reset,
            'ik_accept_rate': float(v.last_ik_ok.mean()) if v.last_ik_ok is not None else None,
            'last_rollover_breakdown_s': v.reset_timing,
            'flagged_envs': int(np.count_nonzero(v.flags()))}
@@ -190,54 +208,15 @@ def facade_bench(args):
     v.close()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--task', default='FeedingJaco-v0', choices=sorted(TASKS))
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
-    ap.add_argument('--settle', type=int, default=None, help='reset settle frames (FeedingJaco 100, ScratchItch 0)')
-    ap.add_argument('--gather-every', type=int, default=16)
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--reset-pool', type=int, default=None,
-                    help='distinct host reset states, tiled over the envs (IK is host-side; FeedingJaco 1024, ScratchItch 128)')
-    ap.add_argument('--facade', action='store_true',
-                    help='time the gym facade (avr.env.AVRTorchVecEnv: device tensors, TimeLimit 200 with auto-reset) '
-                         'instead of the bare step; --steps should span rollovers (e.g. 600)')
-    ap.add_argument('--dist-backend', default='nccl', choices=('nccl', 'gloo'),
-                    help="torch.distributed backend for --gpus > 1: nccl (RCCL over xGMI, the product path); gloo only "
-                         "rehearses the multi-rank flow where ranks share a GPU (rollouts gathered through host memory)")
-    ap.add_argument('--impairment', default='random',
-                    help="human impairment per env: 'random' is the tasks' own setting (feeding.py:175, scratch_itch.py:178)")
-    args = ap.parse_args()
-    if args.facade:
-        return facade_bench(args)
-    T = TASKS[args.task]
-    settle = T['settle'] if args.settle is None else args.settle
-
+def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu_seconds):
+    """Time `steps` gym steps of task `name` (E = args.envs per GPU) after `warmup` untimed ones;
+    returns the JSON object of its bench line (cpu_baseline when cpu_seconds > 0)."""
     import numpy as np
     import torch
     from avr import _abi as ABI, _lib
     from avr import dist as D
-
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    dist = None
-    gloo = args.dist_backend == 'gloo'
-    if gloo:        # rehearsal: ranks may share the GPUs there are
-        local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if gloo:
-            dist.init_process_group('gloo')
-        else:
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
-
+    T = TASKS[name]
+    settle = T['settle'] if args.settle is None else args.settle
     A = ABI.load_scene(T['task'])
     md = ABI.ModelDesc(A)
     L = md.layout
@@ -245,7 +224,7 @@ def main():
     # reset pool: distinct initial states for global env ids; tiled if pool < E
     pool = min(args.reset_pool or T['pool'], E)
     base_id, _ = D.shard(E, rank)
-    S_pool, meta = reset_pool(T['task'], A, md, [base_id + i for i in range(pool)], args.impairment)
+    S_pool, meta = reset_pool(T['task'], A, md, [base_id + i for i in range(pool)], args.impairment, device=local)
     n_tremor = sum(m['impairment'] == 'tremor' for m in meta)
     import hashlib
     pool_sha = hashlib.sha1(S_pool.astype(np.float32).tobytes()).hexdigest()[:12]
@@ -273,7 +252,7 @@ def main():
                 if j == G - 1:
                     D.gather_rollouts(roll.cpu() if gloo else roll, out=gathered)
 
-    for w in range(args.warmup):
+    for w in range(warmup):
         one_step(w, w)
     sim.sync()
     torch.cuda.synchronize(dev)
@@ -283,25 +262,25 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(ext)
-    for k in range(args.steps):
-        one_step(args.warmup + k, k)
+    for k in range(steps):
+        one_step(warmup + k, k)
     ev1.record(ext)
     sim.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / steps
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device='cpu' if gloo else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     # per-kernel launch durations (HIP events between the launches of a step, on the sim
     # stream), from a separate short pass so the timed loop above carries no event overhead
-    P = min(10, args.steps)
+    P = min(10, steps)
     sim.profile_kernels(True)
     for k in range(P):
-        one_step(args.warmup + args.steps + k, k)
+        one_step(warmup + steps + k, k)
     kt = sim.kernel_times()
     sim.profile_kernels(False)
     kernels = {k: {'avg_ms': v[0] / max(v[1], 1), 'launches_per_step': v[1] / P, 'ms_per_step': v[0] / P} for k, v in kt.items() if v[1] > 0}
@@ -309,11 +288,11 @@ def main():
     dominant = max(kernels, key=lambda k: kernels[k]['ms_per_step'])
     St = sim.get_state()
     flags = St[:, L.S_TASK + L.T_FLAGS].astype(np.int64)
-    value = world * E * args.steps / el
+    value = world * E * steps / el
     bpe = T['bytes']
     achieved = bpe * E / (step_kernel_ms * 1e-3) / 1e9
-    ms_per_step = el / args.steps * 1e3
-    pmc = pmc_summary(args.task, [k for k, v in kt.items() if v[1] > 0], ms_per_step, E)
+    ms_per_step = el / steps * 1e3
+    pmc = pmc_summary(name, [k for k, v in kt.items() if v[1] > 0], ms_per_step, E)
     traffic = pmc['traffic'] if pmc else None
     # the bound: the larger of the two roofline fractions the path could sit on (HBM bytes vs the
     # dense matrix-core peak; the path issues no MFMA, so its MFMA fraction is 0)
@@ -331,15 +310,15 @@ def main():
         'value': value,
         'unit': 'env-steps/s',
         'n_gpus': world,
-        'steps': args.steps,
-        'warmup': args.warmup,
+        'steps': steps,
+        'warmup': warmup,
         'ms_per_step': ms_per_step,
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the host IK path (%d distinct per GPU, tiled)' % pool,
-        'config': {'workload': T['workload'] % E, 'task': args.task, 'envs_per_gpu': E,
+        'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the reset path (%d distinct per GPU, tiled)' % pool,
+        'config': {'workload': T['workload'] % E, 'task': name, 'envs_per_gpu': E,
                    'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
                    'global_envs': world * E, 'substeps_per_env_step': T['substeps'], 'solver_iterations': T['iters'],
                    'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None,
@@ -362,21 +341,116 @@ def main():
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(L),
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
                      'dominant_kernel': dominant, 'kernels': kernels},
-        'nan_or_overflow_envs': int(np.count_nonzero(flags)),
-        'flagged_envs_by_bit': {name: int(np.count_nonzero(flags & (1 << b))) for b, name in enumerate(
+        # fault bits only (bits 0-4); bit 5 (an env under the EPA budget) is informational
+        'nan_or_overflow_envs': int(np.count_nonzero(flags & _lib.FLAGS_FAULT_MASK)),
+        'flagged_envs_by_bit': {fname: int(np.count_nonzero(flags & (1 << b))) for b, fname in enumerate(
             ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full', 'coop_capped'))},
         'reset_pool_sha1': pool_sha,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    sim.close()
+    if rank == 0 and world == 1 and cpu_seconds > 0:
         # the host threads this process may use: OMP_NUM_THREADS (the GPU box's CPU share, 16 per
         # GPU; os.cpu_count() reports the whole machine there), else every CPU of this host
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-        out['cpu_baseline'] = cpu_baseline(args.task, md, A, args.cpu_seconds, max(1, threads), args.impairment)
+        out['cpu_baseline'] = cpu_baseline(name, md, A, cpu_seconds, max(1, threads), args.impairment)
     elif rank == 0:
         out['cpu_baseline'] = None
+    return out
+
+
+# the other single-GPU configs BASELINE.json names (configs[2], the PR2 variant of configs[3]),
+# timed after the headline in the same default run: extra keys of the one JSON line
+OTHER_TASKS = ('ScratchItchPR2-v0', 'BedBathingPR2-v0')
+OTHER_KEYS = ('value', 'unit', 'steps', 'warmup', 'ms_per_step', 'config', 'roofline', 'nan_or_overflow_envs', 'flagged_envs_by_bit',
+              'cpu_baseline')
+
+
+def policy_eval_bench(args):
+    """enjoy_vr.py's evaluation loop (avr.policy_eval.evaluate: policy forward on the normalised
+    obs, then AVRTorchVecEnv.step with the policy's fresh action tensor) for one 200-step trial in
+    each of --envs envs; env-steps/s of the stepping loop (env creation and reset excluded)."""
+    import numpy as np
+    import torch
+    from avr import policy_eval as PE, _abi as ABI
+    name = args.task
+    L = ABI.LAYOUTS[TASKS[name]['task']]
+    torch.manual_seed(0)
+    pol = PE.ActorCritic(L.OBS_DIM, L.ACT_DIM)
+    rms = PE.RunningMeanStd((L.OBS_DIM,))
+    t0 = time.perf_counter()
+    r = PE.evaluate(name, pol, rms, n_envs=args.envs, steps=200, deterministic=False, device=0)
+    total = time.perf_counter() - t0
+    out = {'metric': 'policy-eval env-steps/sec (avr.policy_eval.evaluate: enjoy_vr.py loop, fresh action tensor per step)',
+           'value': args.envs * 200 / r['loop_s'], 'unit': 'env-steps/s', 'n_gpus': 1, 'steps': 200, 'warmup': 0,
+           'ms_per_step': r['loop_s'] / 200 * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'data': 'synthetic policy (random-init MLP actor-critic), stochastic actions',
+           'config': {'workload': '%s, %d envs, policy evaluation harness' % (name, args.envs), 'task': name, 'envs_per_gpu': args.envs},
+           'graph_captures': r['graph_captures'], 'total_s_with_env_creation_and_reset': total,
+           'mean_return': float(np.mean(r['returns']))}
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--task', default='FeedingJaco-v0', choices=sorted(TASKS))
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    ap.add_argument('--settle', type=int, default=None, help='reset settle frames (FeedingJaco 100, ScratchItch 0)')
+    ap.add_argument('--gather-every', type=int, default=16)
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--other-steps', type=int, default=20,
+                    help='steps of each other single-GPU task (ScratchItchPR2, BedBathingPR2) timed after the FeedingJaco '
+                         'headline at N=1 (extra keys of the JSON line; 0 = skip)')
+    ap.add_argument('--reset-pool', type=int, default=None,
+                    help='distinct host reset states, tiled over the envs (IK is host-side; FeedingJaco 1024, ScratchItch 128)')
+    ap.add_argument('--facade', action='store_true',
+                    help='time the gym facade (avr.env.AVRTorchVecEnv: device tensors, TimeLimit 200 with auto-reset) '
+                         'instead of the bare step; --steps should span rollovers (e.g. 600)')
+    ap.add_argument('--fresh-actions', action='store_true',
+                    help='--facade: a new action tensor every step (as a policy returns), not one refilled tensor')
+    ap.add_argument('--policy-eval', action='store_true',
+                    help='time avr.policy_eval.evaluate (enjoy_vr.py harness: synthetic MLP policy, VecNormalize eval) at --envs '
+                         'envs for 200 steps')
+    ap.add_argument('--dist-backend', default='nccl', choices=('nccl', 'gloo'),
+                    help="torch.distributed backend for --gpus > 1: nccl (RCCL over xGMI, the product path); gloo only "
+                         "rehearses the multi-rank flow where ranks share a GPU (rollouts gathered through host memory)")
+    ap.add_argument('--impairment', default='random',
+                    help="human impairment per env: 'random' is the tasks' own setting (feeding.py:175, scratch_itch.py:178)")
+    args = ap.parse_args()
+    if args.facade:
+        return facade_bench(args)
+    if args.policy_eval:
+        return policy_eval_bench(args)
+
+    import torch
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    gloo = args.dist_backend == 'gloo'
+    if gloo:        # rehearsal: ranks may share the GPUs there are
+        local = local % max(1, torch.cuda.device_count())
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        if gloo:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_seconds
+    out = run_task(args.task, args, args.steps, args.warmup, world, rank, local, dist, gloo, dev, cpu_s)
+    if rank == 0 and world == 1 and args.task == 'FeedingJaco-v0' and args.other_steps > 0:
+        out['other_tasks'] = {}
+        for name in OTHER_TASKS:
+            o = run_task(name, args, args.other_steps, args.warmup, world, rank, local, dist, gloo, dev, min(cpu_s, 5.0))
+            out['other_tasks'][name] = {k: o[k] for k in OTHER_KEYS}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    sim.close()
     if world > 1:
         dist.destroy_process_group()
 

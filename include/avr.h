@@ -33,8 +33,10 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 4      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters;
-                                  4: BedBathingPR2 (avr_model_desc bb_* fields, task 2) */
+#define AVR_ABI_VERSION 5      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters;
+                                  4: BedBathingPR2 (avr_model_desc bb_* fields, task 2);
+                                  5: avr_graph_captures, per-handle device guard, t >= 0 */
+#define AVR_FLAGS_FAULT_MASK 0x1f  /* avr_get_flags bits 0-4; bit 5 (EPA budget) is informational */
 
 typedef struct avr_config {
     int32_t n_envs;        /* envs owned by this handle (one GPU)                          */
@@ -81,9 +83,14 @@ int avr_reset(avr_sim *sim, const uint8_t *env_mask, const float *host_state, in
  * (FeedingJaco: act 7, obs 25, feeding.py:30-81; ScratchItchPR2: act 7, obs 30,
  * scratch_itch.py:30-82). */
 int avr_step(avr_sim *sim, const float *act, float *obs, float *rew, uint8_t *done, float *info);
+/* avr_step_device: the same with device buffers, asynchronous on avr_stream(sim).  The step's
+ * launch sequence is replayed from a captured HIP graph keyed by (d_obs, d_rew, d_done, d_info,
+ * mode); d_act is first copied (stream-ordered) into the handle's own action buffer, so a caller
+ * may pass a fresh action buffer every step without a re-capture. */
 int avr_step_device(avr_sim *sim, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
 /* Same, with synthetic actions a[e,t] ~ U(-1,1)^7 drawn on the device from Philox4x32-10
- * keyed by (seed, env_offset + e, t) -- examples/random_actions.py semantics. */
+ * keyed by (seed, env_offset + e, t) -- examples/random_actions.py semantics.  t >= 0 (a
+ * negative t is rejected). */
 int avr_step_random_device(avr_sim *sim, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
 /* Device actions for inspection: d_act[n_envs*7] for step t (same Philox stream). */
 int avr_random_actions_device(avr_sim *sim, int64_t t, float *d_act);
@@ -99,6 +106,9 @@ int32_t avr_n_envs(avr_sim *sim);
  * (one per 1024 envs, at most 4; AVR_ENV_GROUPS=1..8 in the environment at avr_create overrides).
  * Results do not depend on it.  No reference counterpart (diagnostic). */
 int32_t avr_env_groups(avr_sim *sim);
+/* Graph captures made by this handle so far (each distinct step key captures once; a few keys
+ * are cached).  No reference counterpart (diagnostic). */
+int64_t avr_graph_captures(avr_sim *sim);
 int32_t avr_state_words(void);          /* FeedingJaco's: avr_task_state_words(AVR_TASK_FEEDING) */
 int32_t avr_abi_version(void);
 /* Per-task sizes (-1 for an unknown task) and the handle's task. */
@@ -137,7 +147,8 @@ int avr_get_contact_summary(avr_sim *sim, float *out4);
  *   factorisation, bit1 contact pool full, bit2 AABB pair list full, bit3 shape pair list full,
  *   bit4 non-contact row buffer full, bit5 more than AVR_COOP_CAP = 4 penetrating hull pairs in
  *   one sub-step: the EPA ran on a rotating window of 4 of them, the others kept their manifold
- *   points); 0 = healthy.  No reference counterpart (PyBullet has no
+ *   points -- informational, the env's state is finite); 0 = healthy.  AVR_FLAGS_FAULT_MASK
+ *   selects the fault bits (0-4).  No reference counterpart (PyBullet has no
  *   such report); a vectorised trainer polls it instead of the whole state block. */
 int avr_get_flags(avr_sim *sim, int32_t *flags);
 const char *avr_last_error(avr_sim *sim);

@@ -1,7 +1,10 @@
 """Env sharding + rollout all-gather (the multi-GPU data path of bench.py) on CPU with gloo,
 world_size 2: each rank simulates its shard of global env ids on the CPU oracle (reset states
 and actions keyed by global id, as on the GPUs) and the gathered rollout equals the
-single-process rollout of all global envs, bit for bit."""
+single-process rollout of all global envs, bit for bit.  FeedingJaco (25-dim obs) and
+BedBathingPR2 (24-dim obs: BASELINE's multi-GPU config, configs[3], in its PR2 variant), so the
+rollout packing is pinned for both row widths."""
+import pytest
 import os
 import socket
 
@@ -22,18 +25,31 @@ def _free_port():
 SETTLE, G = 20, 3
 
 
-def _rollout(ids, steps):
-    """FeedingJaco rollout of the global envs `ids` on the CPU oracle: reset states from the host
-    reset path keyed by global id, a settle, then `steps` gym steps of the Philox action stream --
-    what one rank of bench.py runs on its shard (the oracle stands in for the GPU)."""
+def _rollout(task, ids, steps):
+    """Rollout of the global envs `ids` on the CPU oracle: reset states from the host reset path
+    keyed by global id (FeedingJaco: then a settle), then `steps` gym steps of the Philox action
+    stream -- what one rank of bench.py runs on its shard (the oracle stands in for the GPU)."""
     from avr import _abi as ABI, _lib, reset as RS
     from oracle.oracle import Oracle
-    A = ABI.load_scene()
+    A = ABI.load_scene(task)
     md = ABI.ModelDesc(A)
-    S, _ = RS.batch_reset_states_fast(A, md, 1001, list(ids), impairment='random')
+    if task == ABI.TASK_BEDBATH:
+        from avr import reset_bedbath as RBB
+
+        def run(S, frames):         # the reset's arm settle on the oracle (no GPU here)
+            o = Oracle(md, len(S))
+            o.set_state(S)
+            o.settle(frames)
+            return o.get_state()
+        settled = RBB.settled_arms(A, md, runner=run)
+        S, _ = RBB.batch_reset_states(A, md, 1001, list(ids), attempts=6, iters=60, settled=settled)
+        settle = 0
+    else:
+        S, _ = RS.batch_reset_states_fast(A, md, 1001, list(ids), impairment='random')
+        settle = SETTLE
     o = Oracle(md, len(ids))
     o.set_state(S)
-    o.settle(SETTLE)
+    o.settle(settle)
     out = []
     for t in range(steps):
         obs, rew, done, info = o.step(_lib.random_actions(1001, np.asarray(ids), t))
@@ -41,7 +57,7 @@ def _rollout(ids, steps):
     return out
 
 
-def _worker(rank, world, port, E, q):
+def _worker(rank, world, port, E, task, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, 'assistive-vr-gym_amd'))
@@ -50,9 +66,10 @@ def _worker(rank, world, port, E, q):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
+    from avr import _abi as ABI
     off, n = D.shard(E, rank)
-    roll = torch.zeros(G, E, D.ROLL_WIDTH)
-    for j, (obs, rew, info, done) in enumerate(_rollout(np.arange(off, off + n), G)):
+    roll = torch.zeros(G, E, D.roll_width(ABI.LAYOUTS[task].OBS_DIM))
+    for j, (obs, rew, info, done) in enumerate(_rollout(task, np.arange(off, off + n), G)):
         D.pack_rollout(roll, j, torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(info), torch.from_numpy(done))
     out = D.gather_rollouts(roll)
     if rank == 0:
@@ -61,26 +78,30 @@ def _worker(rank, world, port, E, q):
     dist.destroy_process_group()
 
 
-def test_rollout_gather_world2_matches_single_process():
+@pytest.mark.parametrize('task', [0, 2], ids=['FeedingJaco', 'BedBathingPR2'])
+def test_rollout_gather_world2_matches_single_process(task):
     """Two gloo ranks, each simulating its shard (env_offset = rank x E) and packing its rollout as
     bench.py does; the all-gathered rollout equals one process simulating all global envs."""
+    from avr import _abi as ABI
+    od = ABI.LAYOUTS[task].OBS_DIM
     world, E = 2, 3
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, E, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, E, task, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    ref = _rollout(np.arange(world * E), G)
+    ref = _rollout(task, np.arange(world * E), G)
+    assert got.shape == (G, world * E, od + 4)
     for j, (obs, rew, info, done) in enumerate(ref):
-        assert np.array_equal(got[j, :, :25], obs)
-        assert np.array_equal(got[j, :, 25], rew)
-        assert np.array_equal(got[j, :, 26:28], info)
-        assert np.array_equal(got[j, :, 28], done.astype(np.float32))
+        assert np.array_equal(got[j, :, :od], obs)
+        assert np.array_equal(got[j, :, od], rew)
+        assert np.array_equal(got[j, :, od + 1:od + 3], info)
+        assert np.array_equal(got[j, :, od + 3], done.astype(np.float32))
 
 
 def test_shard_blocks_cover_global_ids():

@@ -139,3 +139,83 @@ def test_bed_bathing_facade():
     assert o.shape == (24,) and info['obs_robot_len'] == 24 and info['action_robot_len'] == 7
     assert np.isfinite(r) and r < 0 and not d
     e.close()
+
+
+def test_fresh_action_tensor_each_step_replays_one_graph():
+    """A caller that hands a new action tensor every step (policy_eval.evaluate: the policy's
+    output) replays one captured graph: the actions are copied into the handle's own buffer in
+    stream order, so the graph key holds no caller action pointer (avr_capi.hip run_step).  The
+    results are bit-identical to stepping with one persistent action tensor."""
+    import torch
+    from avr import env as E, _lib
+    n = 8
+    g1 = E.AVRTorchVecEnv('FeedingJaco-v0', n, auto_reset=False)
+    g2 = E.AVRTorchVecEnv('FeedingJaco-v0', n, auto_reset=False)
+    g1.reset(); g2.reset()
+    keep = torch.empty(n, 7, device='cuda')
+    c0 = g1.sim.graph_captures()
+    for t in range(6):
+        a = _lib.random_actions(1001, np.arange(n), t)
+        fresh = torch.from_numpy(a).cuda() * 1.0          # a new device buffer every step
+        keep.copy_(torch.from_numpy(a))
+        x1 = g1.step(fresh)
+        del fresh                                          # (its memory may be reused at once)
+        x2 = g2.step(keep)
+        np.testing.assert_array_equal(x1[0].cpu().numpy(), x2[0].cpu().numpy())
+        np.testing.assert_array_equal(x1[1].cpu().numpy(), x2[1].cpu().numpy())
+    assert g1.sim.graph_captures() - c0 <= 1, 'the step re-captured its graph for new action buffers'
+    np.testing.assert_array_equal(g1.get_state(), g2.get_state())
+    g1.close(); g2.close()
+
+
+def test_graph_cache_keeps_several_output_keys():
+    """Steps alternating between two output-buffer sets capture two graphs once each (a few keys
+    are cached) and match direct launches bit for bit."""
+    import torch
+    from avr import env as E, _lib
+    n = 8
+    v = E.AVRVecEnv('FeedingJaco-v0', n, auto_reset=False)
+    v.reset()
+    S0 = v.get_state()
+    sim = v.sim
+    outs = [(torch.zeros(n, 25, device='cuda'), torch.zeros(n, device='cuda'), torch.zeros(n, dtype=torch.uint8, device='cuda'),
+             torch.zeros(n, 2, device='cuda')) for _ in range(2)]
+    c0 = sim.graph_captures()
+    for t in range(6):
+        o = outs[t % 2]
+        sim.step_random_device(t, *(x.data_ptr() for x in o))
+    sim.sync()
+    assert sim.graph_captures() - c0 == 2
+    S_graph = sim.get_state()
+    sim.set_state(S0)
+    for t in range(6):
+        sim.step(_lib.random_actions(1001, np.arange(n), t))
+    np.testing.assert_array_equal(S_graph, sim.get_state())
+    v.close()
+
+
+def test_negative_step_index_rejected():
+    from avr import env as E
+    v = E.AVRVecEnv('FeedingJaco-v0', 2, auto_reset=False)
+    with pytest.raises(RuntimeError, match='step index'):
+        v.sim.step_random_device(-1)
+    v.close()
+
+
+def test_calls_keep_the_callers_current_device():
+    """Every C-API entry point runs on its handle's device and restores the caller's current
+    device (lazily allocated scratch lands on the handle's GPU).  With two GPUs: a handle on
+    device 1 used while device 0 is current."""
+    import torch
+    from avr import env as E
+    ndev = torch.cuda.device_count()
+    dev = 1 if ndev > 1 else 0
+    torch.cuda.set_device(0)
+    v = E.AVRVecEnv('FeedingJaco-v0', 4, device=dev, auto_reset=False)
+    assert torch.cuda.current_device() == 0
+    v.reset()                                # device IK: lazily allocated scratch
+    assert torch.cuda.current_device() == 0
+    assert np.all(v.flags() & 1 == 0)
+    q, _ = v.sim.get_q()
+    assert np.all(np.isfinite(q)) and torch.cuda.current_device() == 0
+    v.close()

@@ -417,9 +417,11 @@ def test_env_groups_bit_identical(lib_and_scene):
 
 def test_graph_replay_bit_identical(lib_and_scene):
     """AVR_GRAPH=1 captures a gym step's launch sequence (every env group's launches and the
-    fork / join events) once per output-buffer set and replays it, patching the step counter into
-    the take-step nodes: the same kernels on the same data, so the same bits as direct launches,
-    for host-action steps and for device-drawn actions whose Philox counter changes every step."""
+    fork / join events) once per output-buffer set and replays it; the step counter is written to
+    device memory by a stream-ordered one-thread kernel before each replay, and the take-step
+    nodes read it there (the executable graph is never edited): the same kernels on the same data,
+    so the same bits as direct launches, for host-action steps and for device-drawn actions whose
+    Philox counter changes every step."""
     A, md = lib_and_scene
     S = np.concatenate([reset_states(A, md, range(0, 150), 'random'), reset_states(A, md, range(150, 200), 'tremor')])
     G0, o0 = _b_path_run(md, S, False, steps=3, frames=10, env={'AVR_ENV_GROUPS': '3', 'AVR_GRAPH': '0'}, random_steps=3)
@@ -498,3 +500,34 @@ def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
     assert G[20, ABI.S_TASK + ABI.T_COOPN] >= 20
     assert np.all(np.isfinite(G[20]))
     assert np.array_equal(G[keep], G0) and not np.any(f0 & 32)
+
+
+def test_coop_capped_env_drift_vs_oracle(lib_and_scene):
+    """How far the EPA budget moves the capped env: the arm-in-wheelchair state
+    (tests/golden/feeding_arm_in_wheelchair.npy) for 20 gym steps on the GPU (capped: 4 EPAs per
+    sub-step once the overload has lasted 20 sub-steps, the other penetrating pairs keep their
+    manifold points) and on the fp64 and fp32 oracles (every pair solved each sub-step).  The
+    capped env's arm stays within the stated bound of the uncapped oracle,
+    and the budget's deviation is of the size of the fp32-vs-fp64 chaos of the same contact state."""
+    from avr import _lib
+    from oracle.oracle import Oracle
+    A, md = lib_and_scene
+    bad = np.load(os.path.join(HERE, 'feeding_arm_in_wheelchair.npy')).astype(np.float32)
+    sim = make_sim(md, 1)
+    sim.set_state(bad)
+    o64, o32 = Oracle(md, 1, 'f64'), Oracle(md, 1, 'f32')
+    o64.set_state(bad.astype(np.float64)); o32.set_state(bad.astype(np.float64))
+    dq_cap = dq_32 = 0.0
+    capped = False
+    for t in range(20):
+        a = _lib.random_actions(1001, np.arange(1), t)
+        sim.step(a); o64.step(a); o32.step(a)
+        G, C, C32 = sim.get_state(), o64.get_state(), o32.get_state()
+        dq_cap = max(dq_cap, float(np.abs(G[0, :7] - C[0, :7]).max()))
+        dq_32 = max(dq_32, float(np.abs(C32[0, :7] - C[0, :7]).max()))
+        capped = capped or bool(sim.get_flags()[0] & 32)
+    sim.close()
+    print('capped env: max |dq| GPU(capped) vs fp64 oracle %.3g rad, fp32 vs fp64 oracle %.3g rad' % (dq_cap, dq_32))
+    assert capped
+    assert np.all(np.isfinite(G))
+    assert dq_cap < 0.05, dq_cap
