@@ -143,6 +143,7 @@ class avr_model_desc(C.Structure):
         # ABI 4
         ('bb_targets', PF64), ('bb_ntgt', (C.c_int32 * 2) * 2), ('bb_limb_slots', C.c_int32 * 2),
         ('bb_joint_slots', C.c_int32 * 3), ('w_wipe', C.c_double), ('closest_distance', C.c_double),
+        ('body_rolling', PF64), ('body_spinning', PF64),
     ]
 
 
@@ -273,6 +274,12 @@ class ModelDesc:
             setattr(d, k, arr(k, np.int32))
         for k in ('body_friction', 'body_threshold', 'body_aabb'):
             setattr(d, k, arr(k, np.float64))
+        for k in ('body_rolling', 'body_spinning'):          # (scenes compiled before ABI 5: none)
+            if k in A:
+                setattr(d, k, arr(k, np.float64))
+            else:
+                self.A[k] = np.zeros(d.n_bodies)
+                setattr(d, k, self.A[k].ctypes.data_as(PF64))
         d.n_shapes = len(A['shape_kind'])
         for k in ('shape_kind', 'shape_body', 'shape_gender', 'shape_hull'):
             setattr(d, k, arr(k, np.int32))

@@ -219,6 +219,9 @@ def parse_urdf(path):
         if ct is not None and ct.find('lateral_friction') is not None:
             friction = float(ct.find('lateral_friction').get('value'))
         L.friction = friction
+        # <contact> rolling / spinning friction (PyBullet's URDF importer; default 0)
+        L.rolling = float(ct.find('rolling_friction').get('value')) if ct is not None and ct.find('rolling_friction') is not None else 0.0
+        L.spinning = float(ct.find('spinning_friction').get('value')) if ct is not None and ct.find('spinning_friction') is not None else 0.0
         links[L.name] = L
         order.append(L.name)
     joints = []
@@ -484,10 +487,13 @@ class Scene:
         self.pairs = []
         self.task = {}
 
-    def add_body(self, kind, index, shapes, friction, name, single=False):
+    def add_body(self, kind, index, shapes, friction, name, single=False, rolling=0.0, spinning=0.0):
         # single=True: a bare (non-compound) collision shape (createMultiBody without a frame
         # offset) -- Bullet runs convex-convex on it directly, no child AABB culling.
-        self.bodies.append(dict(kind=kind, index=index, shapes=shapes, friction=friction, name=name, single=single))
+        # rolling / spinning: the body's rolling and spinning friction (URDF <contact>,
+        # p.changeDynamics); a contact's torsional rows use the combined coefficients
+        self.bodies.append(dict(kind=kind, index=index, shapes=shapes, friction=friction, name=name, single=single,
+                                rolling=rolling, spinning=spinning))
         return len(self.bodies) - 1
 
 
@@ -816,7 +822,10 @@ def build_composite_tool(rel, tip_link):
             s.pos, s.quat = G.tf_mul(lp - c, lq, s.pos, s.quat)
             shapes.append(s)
     tip = frames[tip_link][0] + links[tip_link].com_pos
-    return dict(mass=mass, inertia=I, shapes=shapes, friction=links[root].friction,
+    # every link of both composite tools carries the same <contact> block (tool_scratch.urdf:22-25,
+    # wiper.urdf:21-24): the composite body takes it
+    assert all(links[L.name].rolling == links[root].rolling and links[L.name].spinning == links[root].spinning for L, _, _ in parts)
+    return dict(mass=mass, inertia=I, shapes=shapes, friction=links[root].friction, rolling=links[root].rolling, spinning=links[root].spinning,
                 pivot=-c, tip=tip - c, handle_shapes=lead)
 
 
@@ -852,7 +861,7 @@ def compile_scratch_pr2():
     rstatic_body = [S.add_body(KIND_RSTATIC, k, shapes, 0.5, name) for k, (name, shapes) in enumerate(groups)]
     tool = build_scratcher()
     S.free = [dict(name='scratcher', mass=tool['mass'], inertia=tool['inertia'], gravity=np.zeros(3))]
-    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'scratcher')
+    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'scratcher', rolling=tool['rolling'], spinning=tool['spinning'])
     plane = build_static_urdf('plane/plane.urdf')
     chair = build_static_urdf('wheelchair/wheelchair.urdf')
     S.static = [dict(name='plane', pos=np.zeros(3), quat=np.array([0, 0, 0, 1.0])),
@@ -919,6 +928,7 @@ def compile_scratch_pr2():
 
 BED_Y_OFFSET = -0.53                                     # bed_bathing.py:203
 BED_FRICTION = 5.0                                       # bed_bathing.py:281-282 (lateralFriction)
+BED_ROLLING = BED_SPINNING = 5.0                         # bed_bathing.py:282 (rollingFriction, spinningFriction)
 BED_JOINT_TARGETS = ((7, 50), (8, -50), (17, -30), (28, -60), (35, -60))   # bed_bathing.py:283 (degrees)
 BED_HUMAN_BASE = (np.array([0, 0, 0.7]), G.quat_from_euler([np.deg2rad(-30), 0, 0]))   # bed_bathing.py:194
 
@@ -974,7 +984,7 @@ def compile_bedbath_pr2():
     rstatic_body = [S.add_body(KIND_RSTATIC, k, shapes, 0.5, name) for k, (name, shapes) in enumerate(groups)]
     tool = build_wiper()
     S.free = [dict(name='wiper', mass=tool['mass'], inertia=tool['inertia'], gravity=np.zeros(3))]
-    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'wiper')
+    tool_body = S.add_body(KIND_FREE, 0, tool['shapes'], tool['friction'], 'wiper', rolling=tool['rolling'], spinning=tool['spinning'])
     plane = build_static_urdf('plane/plane.urdf')
     m1 = [Shape(BOX, (0, 0, 0.15 / 2.0), half_extents=(0.88 / 2.0, 1.25 / 2.0, 0.15 / 2.0))]
     m2 = [Shape(BOX, (0, 0.7 / 2.0, 0), half_extents=(0.88 / 2.0, 0.7 / 2.0, 0.15 / 2.0))]
@@ -984,9 +994,9 @@ def compile_bedbath_pr2():
                 dict(name='mattress_head', pos=np.array([0, 1.25 / 2.0 + BED_Y_OFFSET, 0.4 + 0.15 / 2.0]), quat=G.quat_from_euler([np.deg2rad(60), 0, 0])),
                 dict(name='bed_frame', pos=np.array([0, BED_Y_OFFSET + 0.45, 0.42]), quat=G.quat_from_euler([np.pi / 2.0, 0, -np.pi / 2.0]))]
     static_body = [S.add_body(KIND_STATIC, 0, plane['shapes'], plane['friction'], 'plane'),
-                   S.add_body(KIND_STATIC, 1, m1, BED_FRICTION, 'mattress', single=False),
-                   S.add_body(KIND_STATIC, 2, m2, BED_FRICTION, 'mattress_head', single=False),
-                   S.add_body(KIND_STATIC, 3, frame, BED_FRICTION, 'bed_frame')]
+                   S.add_body(KIND_STATIC, 1, m1, BED_FRICTION, 'mattress', single=False, rolling=BED_ROLLING, spinning=BED_SPINNING),
+                   S.add_body(KIND_STATIC, 2, m2, BED_FRICTION, 'mattress_head', single=False, rolling=BED_ROLLING, spinning=BED_SPINNING),
+                   S.add_body(KIND_STATIC, 3, frame, BED_FRICTION, 'bed_frame', rolling=BED_ROLLING, spinning=BED_SPINNING)]
     S.human = {}
     human_body = {}
     for gender in ('male', 'female'):
@@ -1108,6 +1118,8 @@ def to_arrays(S):
     A['body_shape_start'] = np.array(b_start, np.int32)
     A['body_shape_count'] = np.array(b_count, np.int32)
     A['body_friction'] = np.array(b_fric)
+    A['body_rolling'] = np.array([b['rolling'] for b in S.bodies], np.float64)
+    A['body_spinning'] = np.array([b['spinning'] for b in S.bodies], np.float64)
     A['body_threshold'] = np.array(b_thr)
     A['body_aabb'] = np.array(b_aabb)
     A['body_flags'] = np.array(b_flags, np.int32)

@@ -316,6 +316,17 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     if ((r = upload(s, ivec(d->body_flags, nb), &k.body_flags))) return r;
     if ((r = upload(s, cvt(d->body_friction, nb), &k.body_friction))) return r;
     if ((r = upload(s, cvt(d->body_threshold, nb), &k.body_threshold))) return r;
+    {
+        // rolling / spinning friction per body (ABI 5; NULL: none)
+        std::vector<float> zr(nb, 0.f);
+        if ((r = upload(s, d->body_rolling ? cvt(d->body_rolling, nb) : zr, &k.body_rolling))) return r;
+        if ((r = upload(s, d->body_spinning ? cvt(d->body_spinning, nb) : zr, &k.body_spinning))) return r;
+#if !K_TORSION
+        for (int b = 0; b < nb; b++)
+            if ((d->body_rolling && d->body_rolling[b] != 0.0) || (d->body_spinning && d->body_spinning[b] != 0.0))
+                return fail(s, -2, "body %d has rolling / spinning friction: this instantiation has no torsional rows", b);
+#endif
+    }
     if ((r = upload(s, cvt(d->body_aabb, (size_t)nb * 12), &k.body_aabb))) return r;
     if ((r = upload(s, ivec(d->shape_kind, ns), &k.shape_kind))) return r;
     if ((r = upload(s, ivec(d->shape_body, ns), &k.shape_body))) return r;
@@ -443,7 +454,7 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     }
     size_t E = (size_t)cfg->n_envs;
     // per-env constraint-row scratch (written and read inside each sub-step)
-    k.rowcap = MAXNC + 3 * K_MAX_CONTACTS;
+    k.rowcap = MAXNC + K_CROWS * K_MAX_CONTACTS;
     // records [rowcap][20] then robot parts [rowcap][32]; part B reads the whole row buffer
     // through one buffer resource with 32-bit byte offsets below B4_OOB (avr_kernel.hip)
     k.rowstride = (RWC + ROBW) * k.rowcap;

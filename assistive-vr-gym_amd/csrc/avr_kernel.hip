@@ -1766,7 +1766,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 // per-env workspace between the sub-step kernels: [n_envs][WS_WORDS] floats
 #define WS_WORDS 128
 #define WS_NNC 0     // int bits: non-contact rows
-#define WS_NC 1      // int bits: contact points (rows n_nc .. n_nc + 3 n_c)
+#define WS_NC 1      // int bits: contact points (rows n_nc .. n_nc + K_CROWS n_c)
 #define WS_ASQ 2     // sum of squared caller actions (take_step -> task glue)
 #define WS_XCC 3     // diagnostic builds: XCD that ran part A
 #define WS_NROB 4    // int bits: robot parts (slots) of the row set
@@ -1777,7 +1777,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 static_assert(MAXD <= 16 * NDL && WS_FW + 4 * MAXF <= WS_WORDS, "workspace layout");
 // A row's ownership mask: 2 bits per free body f (= part-B lane f): 1 endpoint A, 2 endpoint B
 AVR_DI int own_mask(int fa, int fb) { return (fa >= 0 ? 1 << (2 * fa) : 0) | (fb >= 0 ? 2 << (2 * fb) : 0); }
-static_assert(CR_BASE + 3 * K_MAX_CONTACTS * CRW <= (MAXNC + 3 * K_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
+static_assert(CR_BASE + K_CROWS * K_MAX_CONTACTS * CRW <= (MAXNC + K_CROWS * K_MAX_CONTACTS) * RWC, "contact records fit below the robot parts");
 
 AVR_DI float *row_rec(const KModel &m, float *base, int r) { (void)m; return base + r * RWC; }
 AVR_DI float *row_crec(float *base, int k) { return base + CR_BASE + k * CRW; }
@@ -2001,8 +2001,19 @@ AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, in
     }
 }
 
-// Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal) and
-// n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions).
+// Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal),
+// n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions) and (K_TORSION)
+// n_nc + 3 n_c + 3c + {0,1,2}: the torsional rows -- spinning about the normal, rolling about the
+// two friction directions; angular-only Jacobians, limits +-coefficient x normal impulse, no
+// positional term (btMultiBodyConstraintSolver::addMultiBodyTorsionalFrictionConstraint [ext]).
+// Their coefficients combine the bodies' as btManifoldResult does (roll_A fric_B + roll_B fric_A,
+// clamped to 10); a row whose coefficient is 0 is a null record.
+
+// btManifoldResult::calculateCombinedRollingFriction / SpinningFriction [ext]
+AVR_DI float torsion_coeff(const float *c, const KModel &m, int ba, int bb) {
+    const float x = gld(c + ba) * gld(m.body_friction + bb) + gld(c + bb) * gld(m.body_friction + ba);
+    return fminf(fmaxf(x, -10.f), 10.f);
+}
 AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
     const int ncp = (int)L.st[S_TASK + T_NCP];
@@ -2020,8 +2031,8 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         const bool rob = kA == 1 || kB == 1;
         int tot;
         const int pre = ballot_prefix(act && rob, &tot);
-        const int slot0 = nrob + 3 * pre;
-        nrob += 3 * tot;
+        const int slot0 = nrob + K_CROWS * pre;
+        nrob += K_CROWS * tot;
         if (!act) continue;
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
@@ -2032,33 +2043,52 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         float fric = fminf(gld(m.body_friction + (ba)) * gld(m.body_friction + (bb)), 10.f);
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
+#if K_TORSION
+        const float spin = torsion_coeff(m.body_spinning, m, ba, bb), roll = torsion_coeff(m.body_rolling, m, ba, bb);
+#endif
 #pragma unroll 1
-        for (int k = 0; k < 3; k++) {
-            v3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
+        for (int k = 0; k < K_CROWS; k++) {
+            const int kd = k < 3 ? k : k - 3;
+            v3 dir = kd == 0 ? n : (kd == 1 ? t1 : t2);
             const int slot = rob ? slot0 + k : -1;
-            float *w = row_crec(rows, k == 0 ? i : ncp + 2 * i + (k - 1));
+            float *w = row_crec(rows, k == 0 ? i : k < 3 ? ncp + 2 * i + (k - 1) : 3 * ncp + 3 * i + (k - 3));
             float den = 0.f, rel = 0.f;
+#if K_TORSION
+            // torsional rows (k >= 3): angular axis dir, no linear part
+            const bool tor = k >= 3;
+            const float tcoef = k == 3 ? spin : roll;
+            if (tor && !(tcoef > 0.f)) {          // null record: no endpoint, inv = rhs = coefficient = 0
+#pragma unroll
+                for (int q = 0; q < CRW; q++) w[q] = 0.f;
+                continue;
+            }
+            const v3 lin = tor ? V(0, 0, 0) : dir, angA = tor ? dir : V(0, 0, 0);
+#else
+            constexpr bool tor = false;
+            const float tcoef = 0.f;
+            const v3 lin = dir, angA = V(0, 0, 0);
+#endif
             // the robot part (J, M^-1 J^T) goes to the row buffer endpoint by endpoint (the second
             // robot endpoint, if any, adds to the first's): one pair of MAXD arrays live at a time
             float *wr = rob ? row_rob(m, rows, slot) : nullptr;
             if (kA == 1) {
                 float Ja[MAXD], Ma[MAXD];
-                robot_jac(m, L, iA, pa, dir, V(0, 0, 0), Ja);
+                robot_jac(m, L, iA, pa, lin, angA, Ja);
                 minv_mul(L, Ja, Ma);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; }
                 put_robot(wr, Ja, Ma);
                 put_free_zero(w + 4);
             } else if (kA == 2) {
-                v3 ja = crs(rA, dir), ma = iinv_mul(L, iA, ja), ml = scl(dir, imA);
-                den += dot(dir, ml) + dot(ja, ma);
-                rel += free_dot(L, iA, dir, ja);
-                put_free(L, iA, w + 4, dir, ja);
+                v3 ja = add(crs(rA, lin), angA), ma = iinv_mul(L, iA, ja), ml = scl(lin, imA);
+                den += dot(lin, ml) + dot(ja, ma);
+                rel += free_dot(L, iA, lin, ja);
+                put_free(L, iA, w + 4, lin, ja);
             } else put_free_zero(w + 4);
-            v3 nd = scl(dir, -1.f);
+            const v3 nd = scl(lin, -1.f), angB = scl(angA, -1.f);
             if (kB == 1) {
                 float Jb[MAXD], Mb[MAXD];
-                robot_jac(m, L, iB, pb, nd, V(0, 0, 0), Jb);
+                robot_jac(m, L, iB, pb, nd, angB, Jb);
                 minv_mul(L, Jb, Mb);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
@@ -2066,7 +2096,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 else put_robot(wr, Jb, Mb);
                 put_free_zero(w + 10);
             } else if (kB == 2) {
-                v3 jb = crs(rB, nd), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
+                v3 jb = add(crs(rB, nd), angB), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
                 den += dot(nd, ml) + dot(jb, mb);
                 rel += free_dot(L, iB, nd, jb);
                 put_free(L, iB, w + 10, nd, jb);
@@ -2080,7 +2110,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 else poserr = -pen * erp / dt;
                 rhs = (poserr + velerr) * inv;
             }
-            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs; w[3] = fric;
+            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs; w[3] = tor ? tcoef : fric;
 #if B4_FPAIR
             if (k == 2) {
                 // the friction unit's coupling c = J_2 M^-1 J_1^T (its second row's 4th header word,
@@ -2981,7 +3011,7 @@ AVR_DI int own_of(int mask) {
     const int sl = lane_id() & 15;
     return (int)__builtin_amdgcn_ubfe((unsigned)mask, sl < MAXF ? 2 * sl : 30, 2);
 }
-static_assert(2 * MAXF <= CI_SLOT && MAXNC + 3 * K_MAX_CONTACTS < (1 << (30 - CI_SLOT)), "own mask and slot bit fields");
+static_assert(2 * MAXF <= CI_SLOT && MAXNC + K_CROWS * K_MAX_CONTACTS < (1 << (30 - CI_SLOT)), "own mask and slot bit fields");
 
 // Row sources.  A sweep step sets a row's addresses with set(R, valid, address, impulse slot)
 // from per-lane bases plus a wave-uniform step offset (an invalid step is a null row), reads its
@@ -3054,6 +3084,8 @@ struct CLds {
     unsigned cn, cf;           // normal record 0 / friction unit 0 of this group, - 8 (bytes)
     unsigned rob;              // robot part of the row with slot + 1 = s: rob + 128 s (bytes, this lane's DoF)
     lds_f *ipn, *ipf, *nullip; // impulse slots: normal row 0, friction unit 0, null rows
+    unsigned ct;               // (K_TORSION) torsional unit 0 of this group, - 8 (bytes)
+    lds_f *ipt;                // (K_TORSION) impulse slot of torsional row 0
     AVR_DI void set(Row &R, bool v, unsigned wb, lds_f *ip) const { R.wb = v ? wb : LNB_NULL; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h = *(const lds_f4 *)(blk + R.wb + 8); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const {   // normal rows: the friction coefficient is not read
@@ -3095,6 +3127,8 @@ struct CGlb {
     int cn, cf;                // normal record 0 / friction unit 0 of this env (byte offsets)
     int rob;                   // robot part of the row with slot + 1 = s: rob + 128 s (this lane's DoF)
     lds_f *ipn, *ipf, *nullip;
+    int ct;                    // (K_TORSION) torsional unit 0 of this env (byte offset)
+    lds_f *ipt;
     AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
@@ -3251,6 +3285,22 @@ AVR_DI void sweep4(const S &s, int n, const AT &at, const GO &go) {
 template <class S>
 struct Pair4 { typename S::Row a, b; float in; };
 
+#if K_TORSION
+// torsional rows (spinning about the normal, rolling about the two friction directions) of the
+// active contacts: one flat sweep, step j = row j mod 3 of the j / 3-th active contact; a row
+// carries its contact's normal impulse (its limits are +-coefficient x that impulse)
+template <class CS>
+struct TorRow : CS::Row { float in; };
+template <class CS>
+struct TorSrc {
+    typedef TorRow<CS> Row;
+    static constexpr bool robot_parts = CS::robot_parts;
+    const CS &cs;
+    AVR_DI void hdr(Row &R) const { cs.hdr(R); }
+    AVR_DI void parts(Row &R) const { cs.parts(R); }
+};
+#endif
+
 template <int DN, int DC, class NS, class CS>
 AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename NS::Row NR;
@@ -3330,6 +3380,24 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
                 go(X[q]);
             }
         }
+#if K_TORSION
+        // torsional rows after the frictions (btMultiBodyConstraintSolver::solveSingleIteration
+        // [ext]), for the same active contacts; null records (coefficient 0) resolve to delta 0
+        {
+            const TorSrc<CS> ts{cs};
+            sweep4<DC, false>(ts, 3 * tmax, [&](TorRow<CS> &R, int j) {
+                const int u = j / 3, k = j - 3 * u;
+                const bool v = u < t;
+                const int c = list[v ? u : 0];
+                cs.set(R, v, cs.ct + 3 * CRW * 4 * c + CRW * 4 * k, cs.ipt + 3 * c + k);
+                const float x = cs.ipn[v ? c : 0];      // (read unconditionally)
+                R.in = v ? x : 0.f;
+            }, [&](const TorRow<CS> &R) {
+                const float lim = R.h.w * R.in;
+                *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, -lim, lim);
+            });
+        }
+#endif
     }
     return units;
 }
@@ -3367,7 +3435,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     float *st = state + (size_t)ev * K_STATE_WORDS;
     const int n_nc = live ? __float_as_int(wsg[WS_NNC]) : 0, n_c = live ? __float_as_int(wsg[WS_NC]) : 0;
     const int n_rob = live ? __float_as_int(wsg[WS_NROB]) : 0;
-    const int n_rows = n_nc + 3 * n_c, n_rc = max(n_rob - n_nc, 0);
+    const int n_rows = n_nc + K_CROWS * n_c, n_rc = max(n_rob - n_nc, 0);
     auto wmax = [&](int x) { x = max(x, __shfl_xor(x, 16)); x = max(x, __shfl_xor(x, 32)); return uni(x); };
     const int nnc_max = wmax(n_nc), nc_max = wmax(n_c);
     // the row buffer of every env as one buffer resource; this env's records at byte eo
@@ -3378,7 +3446,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     SYNC();
 #endif
     // pack the groups' regions; stage every row (B4_NC_LDS) or the contact rows when all four fit
-    const int szA = al4(n_rows + 2) + al4(n_c), szB = 3 * n_c * CRW + n_rc * ROBW;
+    const int szA = al4(n_rows + 2) + al4(n_c), szB = K_CROWS * n_c * CRW + n_rc * ROBW;
 #if B4_NC_LDS
     const int szF = szB + n_nc * (RWC + ROBW);
     const int f0 = __shfl(szA + szF, 0), f1 = __shfl(szA + szF, 16), f2 = __shfl(szA + szF, 32), f3 = __shfl(szA + szF, 48);
@@ -3401,7 +3469,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
     // LDS regions: contact records at cw, then (full) the non-contact records at nw, then the
     // robot parts at rw (full: every slot's; otherwise the robot-contact slots')
-    const int cw = base + szA, nw = cw + 3 * n_c * CRW, rw = full ? nw + n_nc * RWC : nw;
+    const int cw = base + szA, nw = cw + K_CROWS * n_c * CRW, rw = full ? nw + n_nc * RWC : nw;
     // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
     // warm-start factor; null slots 0.  The cached impulses are loaded here and stored after the
     // staging loads below have been issued (one memory round trip for both).
@@ -3415,7 +3483,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     }
     for (int i = lane; i < LN_HEAD; i += 64) blk[i] = 0.f;        // null rows, zero parts
     if (in_lds) {   // contact records, (full) non-contact records, robot parts: 8 loads in flight per lane
-        const int n4r = 3 * n_c * (CRW / 4), n4n = full ? n_nc * (RWC / 4) : 0, n4s = (full ? n_rob : n_rc) * (ROBW / 4);
+        const int n4r = K_CROWS * n_c * (CRW / 4), n4n = full ? n_nc * (RWC / 4) : 0, n4s = (full ? n_rob : n_rc) * (ROBW / 4);
         const int n4a = n4r + n4n, n4 = n4a + n4s, so = full ? ro : ro + n_nc * ROBW * 4;
         const int m4 = wmax(n4);
         lds_f4 *l0 = (lds_f4 *)(blk + cw);
@@ -3438,39 +3506,39 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
         if (sl + 16 * q < n_c) imp[n_nc + sl + 16 * q] = wimp[q] * m.warmstart;
     SYNC();
     // impulse slots: rows 0 .. n_rows - 1 (non-contact, normal, friction pairs), then 2 null slots
-    lds_f *const ipn = imp + n_nc, *const ipf = ipn + n_c, *const nullip = imp + n_rows;
+    lds_f *const ipn = imp + n_nc, *const ipf = ipn + n_c, *const ipt = ipf + 2 * n_c, *const nullip = imp + n_rows;
     NcSrc ns{rs, eo, ro, imp, nullip};
     DV d;
     int units, rcb = 0;
 #if B4_NC_LDS
     if (full) {
         // every row from LDS: robot part of the row with slot + 1 = s at rw + (s - 1) ROBW words
-        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - ROBW) + RVB * sl;
+        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, ct = cf + 8 * CRW * n_c, rob = 4 * (rw - ROBW) + RVB * sl;
         const NcLds nl{(lds_c *)blk, 4 * nw + 8, rob, imp, nullip};
         if (wmax(n_rc) > 0) {
-            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
             units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
             rcb = 1;
         } else {
-            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
             units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else
 #endif
     if (in_lds) {
         // byte addresses: records - 8; robot part of slot s at rw + (s - n_nc) ROBW + 2 sl words
-        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW) + RVB * sl;
+        const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, ct = cf + 8 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW) + RVB * sl;
         if (wmax(n_rc) > 0) {
-            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
             units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
             rcb = 1;
         } else {
-            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip};
+            CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
             units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else {
-        const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, rob = ro - ROBW * 4 + RVB * sl;
-        CGlb cs{rs, cn, cf, rob, ipn, ipf, nullip};
+        const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, ct = cf + 8 * CRW * n_c, rob = ro - ROBW * 4 + RVB * sl;
+        CGlb cs{rs, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
         units = pgs4<B4_DN, B4_DG>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
     }
     (void)units; (void)rcb;

@@ -75,6 +75,7 @@ struct KModel {
     const float *st_pose;                             // [nst][8]
     const int *body_kind, *body_index, *body_shape_start, *body_shape_count, *body_flags;
     const float *body_friction, *body_threshold, *body_aabb;   // [nb][12]
+    const float *body_rolling, *body_spinning;                 // [nb] (K_TORSION)
     const int *shape_kind, *shape_body, *shape_gender, *shape_hull;   // hull [ns][4]
     const float *shape_pose, *shape_param, *shape_margin, *shape_aabb; // [ns][8] [ns][4] [ns] [ns][8]
     const float4 *hull_verts;
@@ -115,7 +116,7 @@ struct KModel {
     int bb_limb_slot[2], bb_joint_slot[3];
     float w_wipe, closest_distance;
     float *rows;               // constraint-row scratch: [n_envs][2][rowcap][32] (see solve())
-    int rowcap;                // rows per env = MAXNC + 3 * K_MAX_CONTACTS
+    int rowcap;                // rows per env = MAXNC + K_CROWS * K_MAX_CONTACTS
     int rowstride;             // floats between consecutive envs' row buffers
     int rows_envs;             // envs covered by the row buffer (the handle's n_envs)
     int b4_global;             // diagnostic (AVR_B4_GLOBAL=1): part B reads every row from global memory

@@ -47,6 +47,7 @@
 #define K_TOOL_PIVOT 0          // the spoon's base COM is its body frame
 #define K_PR2 0
 #define K_ND 10                 // robot DoFs (Jaco); the articulated human chain's DoFs follow
+#define K_TORSION 0             // no rolling / spinning friction in the FeedingJaco scene
 #elif AVR_TASK == AVR_TASK_SCRATCH || AVR_TASK == AVR_TASK_BEDBATH
 // the PR2 family: ScratchItchPR2 and BedBathingPR2 share the state layout (AVR_SI_*)
 #define K_PR2 1
@@ -87,6 +88,12 @@
 #define K_CHAIN_LIMITS_IN_STATE 1   // human arm limits x limit_scale per env (human_creation.py:226)
 #define K_HUMAN_GRAVITY 1       // human gravity -1 (scratch_itch.py:260; BedBathing's reset settle, bed_bathing.py:286)
 #define K_TOOL_PIVOT 1          // the scratcher / wiper is a composite body: its handle COM is off the body frame
+#define K_TORSION 1             // torsional friction rows: the tools' rolling / spinning friction 0.001
+                                // (tool_scratch.urdf:22-25, wiper.urdf:21-24), the bed parts' 5 / 5
+                                // (bed_bathing.py:282)
 #else
 #error "unknown AVR_TASK"
 #endif
+// constraint rows per contact point: the normal and two lateral frictions, then (K_TORSION) the
+// spinning row about the normal and two rolling rows about the friction directions
+#define K_CROWS (K_TORSION ? 6 : 3)

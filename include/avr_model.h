@@ -227,6 +227,10 @@ typedef struct avr_model_desc {
     int32_t bb_joint_slots[3];             /* human slots of links 9, 11, 13 (obs, bed_bathing.py:143-145) */
     double w_wipe;                         /* config.ini:17 wiping_reward_weight                    */
     double closest_distance;               /* getClosestPoints(tool, human, distance=4.0) (bed_bathing.py:61) */
+    /* ---- ABI 5 ---- */
+    const double *body_rolling, *body_spinning;   /* [n_bodies] rolling / spinning friction: URDF <contact>
+                                              (tool_scratch.urdf:22-25, wiper.urdf:21-24), p.changeDynamics
+                                              (bed parts 5 / 5, bed_bathing.py:282); 0 elsewhere */
 } avr_model_desc;
 
 #ifdef __cplusplus

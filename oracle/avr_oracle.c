@@ -234,8 +234,8 @@ typedef struct {
     real dq[K_MAX_DOF];                 /* solver delta velocities */
     v3 dfv[K_MAX_FREE], dfw[K_MAX_FREE];
     row_t rows[MAX_ROWS];
-    int nrows, n_nc, n_nrm, n_fr;
-    int nc_idx[64], nrm_idx[MAX_ROWS / 3 + 8], fr_idx[MAX_ROWS];
+    int nrows, n_nc, n_nrm, n_fr, n_tor;
+    int nc_idx[64], nrm_idx[MAX_ROWS / 3 + 8], fr_idx[MAX_ROWS], tor_idx[MAX_ROWS];
     int sp_a[MAX_SPAIRS], sp_b[MAX_SPAIRS], sp_pair[MAX_SPAIRS];
     int nsp;
     int gender;
@@ -1157,6 +1157,15 @@ static void plane_space(v3 n, v3 *p, v3 *q) {
     }
 }
 
+/* btManifoldResult::calculateCombinedRollingFriction / ...SpinningFriction [ext]: the coefficient of
+ * one body times the other's lateral friction, summed both ways, clamped to +-10 (Bullet's
+ * MAX_FRICTION) */
+static real torsion_coeff(const model *m, int ba, int bb, const double *c) {
+    if (!c) return 0;
+    real x = R(c[ba] * m->d.body_friction[bb] + c[bb] * m->d.body_friction[ba]);
+    return x > 10 ? 10 : x < -10 ? -10 : x;
+}
+
 static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
     int ncp = (int)st[S_TASK + T_NCP];
     real erp = R(m->d.erp), ws = R(m->d.warmstart);
@@ -1204,6 +1213,25 @@ static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
             f->normal_row = nidx;
             w->fr_idx[w->n_fr++] = w->nrows - 1;
         }
+        /* torsional friction (btMultiBodyConstraintSolver::convertMultiBodyContact [ext]): with a
+         * combined spinning friction a row about the normal, with a combined rolling friction two
+         * rows about plane_space(n) -- angular-only Jacobians, no positional term, no warm start,
+         * in that order; Bullet adds them for the first 4 points of a manifold (rollingFriction
+         * counter), i.e. every point here (manifolds hold <= 4) */
+        real spin = torsion_coeff(m, ba, bb, m->d.body_spinning), roll = torsion_coeff(m, ba, bb, m->d.body_rolling);
+        for (int k = 0; k < 3; k++) {
+            if (k == 0 ? !(spin > 0) : !(roll > 0)) continue;
+            v3 ax = k == 0 ? n : k == 1 ? t1 : t2;
+            row_t *f = new_row(w);
+            row_endpoint(m, st, w, f, 0, ba, pa, V(0, 0, 0), ax);
+            row_endpoint(m, st, w, f, 1, bb, pb, V(0, 0, 0), scl(ax, -1));
+            row_finish(m, w, f);
+            real rv = row_relvel(m, w, f);
+            f->rhs = -rv * f->inv;
+            f->fric = k == 0 ? spin : roll;
+            f->normal_row = nidx;
+            w->tor_idx[w->n_tor++] = w->nrows - 1;
+        }
     }
 }
 
@@ -1228,6 +1256,17 @@ static void solve(const model *m, ws_t *w) {
         for (int j = 0; j < w->n_nrm; j++) resolve(m, w, &w->rows[w->nrm_idx[j]]);
         for (int j = 0; j < w->n_fr; j++) {
             row_t *f = &w->rows[w->fr_idx[j]];
+            real nimp = w->rows[w->nrm_idx[f->normal_row]].imp;
+            if (nimp > 0) {
+                f->lo = -f->fric * nimp;
+                f->hi = f->fric * nimp;
+                resolve(m, w, f);
+            }
+        }
+        /* torsional friction rows after the lateral ones (solveSingleIteration [ext]), limits
+         * +-coefficient x the contact's current normal impulse */
+        for (int j = 0; j < w->n_tor; j++) {
+            row_t *f = &w->rows[w->tor_idx[j]];
             real nimp = w->rows[w->nrm_idx[f->normal_row]].imp;
             if (nimp > 0) {
                 f->lo = -f->fric * nimp;
@@ -1341,7 +1380,7 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
         w->dfw[f] = V(0, 0, 0);
     }
     /* constraint rows + PGS */
-    w->nrows = w->n_nc = w->n_nrm = w->n_fr = 0;
+    w->nrows = w->n_nc = w->n_nrm = w->n_fr = w->n_tor = 0;
     build_noncontact_rows(m, st, w, dt);
     build_contact_rows(m, st, w, dt);
     w->stats_rows += w->nrows;
@@ -1586,6 +1625,8 @@ EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **o
     CP(st_pose, 7 * d->n_static, double);
     CP(body_kind, B, int32_t); CP(body_flags, B, int32_t); CP(body_index, B, int32_t); CP(body_shape_start, B, int32_t); CP(body_shape_count, B, int32_t);
     CP(body_friction, B, double); CP(body_threshold, B, double); CP(body_aabb, 12 * B, double);
+    if (d->body_rolling) CP(body_rolling, B, double);       /* (NULL: no rolling / spinning friction) */
+    if (d->body_spinning) CP(body_spinning, B, double);
     CP(shape_kind, S, int32_t); CP(shape_body, S, int32_t); CP(shape_gender, S, int32_t); CP(shape_hull, 4 * S, int32_t);
     CP(shape_pose, 7 * S, double); CP(shape_param, 4 * S, double); CP(shape_margin, S, double); CP(shape_aabb, 6 * S, double);
     CP(hull_verts, 3 * d->n_hull_verts, double); CP(hull_planes, 4 * d->n_hull_planes, double);
@@ -1654,6 +1695,7 @@ EXPORT int avr_oracle_destroy(avr_oracle *o) {
     free((void *)m->d.shape_gender); free((void *)m->d.shape_hull); free((void *)m->d.shape_pose); free((void *)m->d.shape_param);
     free((void *)m->d.shape_margin); free((void *)m->d.shape_aabb); free((void *)m->d.hull_verts); free((void *)m->d.hull_planes);
     free((void *)m->d.pair_a); free((void *)m->d.pair_b);
+    free((void *)m->d.body_rolling); free((void *)m->d.body_spinning);
     free(m->hv);
     free(o->state);
     free(o->ws);

@@ -5,9 +5,13 @@ on the GPU.
 
 Pins beyond self-consistency:
   * the wipe-target counts follow util.capsule_points' closed form (sections x points per ring);
-  * the arm settle lands within 0.06 rad of the right-arm pose the reference itself hard-codes
-    for its VR/replay bed bathing (bed_bathing.py:232, joint_angles of joints 7..13) -- the one
-    PyBullet-produced number the reference holds for this path.
+  * the male arm settle lands within 0.02 rad of the right-arm pose the reference itself
+    hard-codes for its VR/replay bed bathing (bed_bathing.py:232, joint_angles; the VR env's
+    default participant is male, bed_bathing.py:12) -- the one PyBullet-produced number the
+    reference holds for this path.  With the bed's rolling / spinning friction 5 (bed_bathing.py:282,
+    torsional rows, btMultiBodyConstraintSolver [ext]) the male settle is 0.012 rad from it;
+    without it 0.046 rad.  The female body's proportions differ (human_creation.py:116-161), so
+    its settle is held to 0.1 rad only.
 Tolerances (fp32 kernel vs fp64 oracle) as in test_scratch.py: one sub-step 1e-5 rad; 200
 contact-free steps 1e-3 rad; wipe bookkeeping bit-identical; rewards 2e-3.
 """
@@ -103,12 +107,16 @@ def test_committed_bedbath_scene_matches_compiler(tmp_path):
 
 
 # ------------------------------------------------------------------ reset
+VR_TOL = {'male': 0.02, 'female': 0.1}
+
+
 def test_arm_settle_matches_reference_vr_pose(bb, settled):
     """The 100-frame drop of the right arm onto the mattress (bed_bathing.py:283-289), fp64 oracle,
-    against the arm pose the reference hard-codes for its VR/replay bed bathing."""
+    against the arm pose the reference hard-codes for its VR/replay bed bathing (male: 0.012 rad
+    with the bed's rolling / spinning friction, 0.046 without)."""
     for g in ('male', 'female'):
         q, slots = settled[g]
-        assert np.abs(q - VR_ARM).max() < 0.06, (g, q)
+        assert np.abs(q - VR_ARM).max() < VR_TOL[g], (g, q)
     A, md = bb
     js = A['bb_joint_slots']
     q, slots = settled['male']
@@ -195,7 +203,7 @@ def test_bedbath_device_settle_matches_oracle(bb):
     c = RBB.settled_arms(A, md, runner=_oracle_runner(md, 'f32'))
     for gender in ('male', 'female'):
         assert np.abs(g[gender][0] - c[gender][0]).max() < 2e-3, (g[gender][0], c[gender][0])
-        assert np.abs(g[gender][0] - VR_ARM).max() < 0.06
+        assert np.abs(g[gender][0] - VR_ARM).max() < VR_TOL[gender]
 
 
 @pytest.mark.gpu

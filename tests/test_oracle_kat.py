@@ -462,3 +462,81 @@ def test_resting_sphere_normal_force_is_weight(scene, oracle_built):
         if food_body in (A['shape_body'][int(c[ABI.CP_SA])], A['shape_body'][int(c[ABI.CP_SB])]):
             imp += c[ABI.CP_IMP]
     assert imp / dt == pytest.approx(0.001 * 9.81, rel=2e-2)
+
+
+# ----------------------------------------------------------------------------- torsional friction KATs
+def _rolling_scene(scene, rolling=0.0, spinning=0.0):
+    """FeedingJaco's scene with rolling / spinning friction on the table (the combined coefficient
+    of a food sphere on it is table_coeff x food friction 0.5 + food_coeff 0 x table friction,
+    btManifoldResult [ext]); no damping, 50 solver iterations (a converged solve of the
+    one-point contact)."""
+    A, md = scene
+    A = dict(A)
+    tb = int(A['task_table_body'])
+    A['body_rolling'] = np.zeros(len(A['body_kind'])); A['body_rolling'][tb] = rolling
+    A['body_spinning'] = np.zeros(len(A['body_kind'])); A['body_spinning'][tb] = spinning
+    return A, ABI.ModelDesc(A, dict(linear_damping=0.0, angular_damping=0.0, solver_iterations=50))
+
+
+def _sphere_on_table(scene, A, md, v, w):
+    """Food sphere 1 resting on the table's far side (settled for 100 sub-steps), then given
+    linear velocity v and angular velocity w."""
+    from oracle.oracle import Oracle
+    _, _, S = _one_env_state(scene)
+    sb = shape_of(A, int(A['task_table_body']), 2)
+    top = A['st_pose'][2][2] + A['shape_pose'][sb][2] + A['shape_param'][sb][2]
+    f = ABI.S_FREE + ABI.FB_WORDS * 3
+    S[0, f:f + 3] = [0.35 + 0.5, -0.9 - 0.4, top + 0.005 + 0.001]
+    S[0, f + 3:f + 7] = [0, 0, 0, 1]
+    S[0, f + 7:f + 13] = 0
+    o = Oracle(md, 1)
+    o.set_state(S)
+    for _ in range(100):
+        o.substep(0.01)
+    S = o.get_state()
+    S[0, f + 7:f + 10] = v
+    S[0, f + 10:f + 13] = w
+    o.set_state(S)
+    return o, f
+
+
+def test_rolling_friction_decelerates_a_rolling_sphere(scene, oracle_built):
+    """A sphere rolling without slipping on a plane with rolling friction mu_r (btMultiBody torsional
+    rows about the contact's tangent axes, limit mu_r x normal impulse [ext]): the rolling
+    resistance torque mu_r m g against no-slip gives a = -mu_r g / (r (1 + I / (m r^2))) =
+    -mu_r g / (1.4 r).  Without rolling friction the sphere keeps rolling (no damping here)."""
+    r, g, dt = 0.005, 9.81, 0.01
+    mu_r = 1e-4                                  # table 2e-4 x food friction 0.5
+    v0 = 0.2
+    for rolling, want in ((0.0, 0.0), (2e-4, -mu_r * g / (1.4 * r))):
+        A, md = _rolling_scene(scene, rolling=rolling)
+        o, f = _sphere_on_table(scene, A, md, [v0, 0, 0], [0, v0 / r, 0])
+        vs = []
+        for _ in range(40):
+            o.substep(dt)
+            vs.append(o.get_state()[0, f + 7])
+        vs = np.array(vs)
+        a = np.polyfit(np.arange(1, 41) * dt, vs, 1)[0]
+        assert a == pytest.approx(want, abs=0.02 * abs(-mu_r * g / (1.4 * r))), (rolling, a, want)
+        St = o.get_state()[0]
+        assert abs(St[f + 7] - St[f + 11] * r) < 1e-3 * v0         # still rolling without slipping
+
+
+def test_spinning_friction_torque_is_bounded_by_mu_n(scene, oracle_built):
+    """A sphere spinning about the contact normal with spinning friction mu_s: the torsional row
+    about the normal saturates at mu_s x the normal impulse, so the spin decays linearly at
+    mu_s m g / I_zz (torque bounded by mu_spin N); without spinning friction it keeps spinning."""
+    m, r, g, dt = 0.001, 0.005, 9.81, 0.01
+    I = 0.4 * m * r * r
+    mu_s = 1e-5                                   # table 2e-5 x food friction 0.5
+    w0 = 5.0
+    for spinning, want in ((0.0, 0.0), (2e-5, -mu_s * m * g / I)):
+        A, md = _rolling_scene(scene, spinning=spinning)
+        o, f = _sphere_on_table(scene, A, md, [0, 0, 0], [0, 0, w0])
+        ws = []
+        for _ in range(20):
+            o.substep(dt)
+            ws.append(o.get_state()[0, f + 12])
+        alpha = np.polyfit(np.arange(1, 21) * dt, np.array(ws), 1)[0]
+        assert alpha == pytest.approx(want, abs=0.02 * mu_s * m * g / I), (spinning, alpha, want)
+        assert np.all(np.array(ws) > 0)
