@@ -12,7 +12,7 @@ DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # ---- capacities / offsets (must match include/avr_model.h) ----
 ABI_VERSION = 5
-TASK_FEEDING, TASK_SCRATCH, TASK_BEDBATH = 0, 1, 2
+TASK_FEEDING, TASK_SCRATCH, TASK_BEDBATH, TASK_DRESSING = 0, 1, 2, 3
 DESC_HC = 8                               # avr_model_desc hc_* capacity
 BODY_ROBOT, BODY_FREE, BODY_STATIC, BODY_HUMAN, BODY_RSTATIC = 0, 1, 2, 3, 4
 # FeedingJaco-v0 layout (module-level names; the ScratchItchPR2-v0 layout is `SI` below)
@@ -74,7 +74,33 @@ def _scratch_layout(task=TASK_SCRATCH):
 
 SI = _scratch_layout()
 BB = _scratch_layout(TASK_BEDBATH)
-LAYOUTS = {TASK_FEEDING: FEEDING, TASK_SCRATCH: SI, TASK_BEDBATH: BB}
+
+
+def _header_defines(path, prefix):
+    """Numeric #defines NAME -> value of a C header (the constants shared with the kernels)."""
+    import re
+    env = {}
+    for line in open(path):
+        m = re.match(r'#define\s+(%s\w+)\s+(.+?)\s*(/\*.*)?$' % prefix, line)
+        if not m:
+            continue
+        expr = m.group(2)
+        for k in sorted(env, key=len, reverse=True):
+            expr = expr.replace(k, repr(env[k]))
+        try:
+            env[m.group(1)] = eval(expr, {'__builtins__': {}})
+        except Exception:
+            pass
+    return env
+
+
+# DressingJaco-v0 (build-defined, include/avr_dressing.h): its constants and state layout
+_DRH = _header_defines(os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), 'include', 'avr_dressing.h'), 'AVR_DR_')
+DR = _Layout(TASK=TASK_DRESSING, ACT_DIM=7, INFO_DIM=2, **{k[len('AVR_DR_'):]: v for k, v in _DRH.items()})
+DR.STATE_WORDS = _DRH['AVR_DR_STATE_WORDS']
+DR.OBS_DIM = _DRH['AVR_DR_OBS_DIM']
+DR.S_TASK, DR.T_ITER, DR.T_FLAGS, DR.T_SUCCESS = _DRH['AVR_DR_S_TASK'], _DRH['AVR_DR_T_ITER'], _DRH['AVR_DR_T_FLAGS'], _DRH['AVR_DR_T_SUCCESS']
+LAYOUTS = {TASK_FEEDING: FEEDING, TASK_SCRATCH: SI, TASK_BEDBATH: BB, TASK_DRESSING: DR}
 
 PI32 = C.POINTER(C.c_int32)
 PF64 = C.POINTER(C.c_double)
@@ -230,6 +256,8 @@ def load_scene(name='feeding_jaco'):
 
 
 def scene_task(A):
+    if 'task_dressing' in A:
+        return TASK_DRESSING
     if 'bb_targets' in A:
         return TASK_BEDBATH
     return TASK_SCRATCH if 'n_rstatic' in A else TASK_FEEDING

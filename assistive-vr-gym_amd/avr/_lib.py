@@ -124,6 +124,8 @@ class Sim:
             raise RuntimeError('avr_create failed (%d): %s' % (rc, msg))
         self.task = int(self.lib.avr_task(h))
         self.L = ABI.LAYOUTS[self.task]
+        if self.task == ABI.TASK_DRESSING:      # one kernel per step, timed in kind slot 2 (avr_dressing.hip)
+            self.kernel_kinds = ('-', '-', 'avr_dress_step_kernel', '-', '-', '-', '-')
         self.words = self.lib.avr_task_state_words(self.task)
         self.obs_dim, self.act_dim = self.L.OBS_DIM, self.L.ACT_DIM
 

@@ -16,7 +16,7 @@ LIB = os.path.join(HERE, 'libavr.so')
 ARCH = os.environ.get('AVR_OFFLOAD_ARCH', 'gfx950')
 # one translation unit per task (the shared kernel / C-ABI sources instantiated in a namespace,
 # csrc/avr_task_tu.h), the extern "C" dispatcher, the hull support tables
-SOURCES = ['avr_task_feeding.hip', 'avr_task_scratch.hip', 'avr_task_bedbath.hip', 'avr_api.cpp', 'avr_hulltab.cpp']
+SOURCES = ['avr_task_feeding.hip', 'avr_task_scratch.hip', 'avr_task_bedbath.hip', 'avr_dressing.hip', 'avr_api.cpp', 'avr_hulltab.cpp']
 HEADERS = ['avr_math.h', 'avr_kmodel.h', 'avr_task.h', 'avr_task_tu.h', 'avr_kernel.hip', 'avr_capi.hip', 'avr_glue_scratch.hip', 'avr_glue_bedbath.hip', 'avr_reset_ik.hip', 'avr_base_search.hip']
 OBJDIR = os.path.join(PKG, 'build')
 
@@ -90,7 +90,7 @@ def lib_cmd(extra=(), out=LIB):
 
 def build_lib(force=False, extra=(), out=LIB):
     """Compile the translation units in parallel (one hipcc per TU), then link libavr*.so."""
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h')] + [os.path.abspath(__file__)]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', h) for h in ('avr.h', 'avr_model.h', 'avr_dressing.h')] + [os.path.abspath(__file__)]
     cmd = lib_cmd(extra, out)
     if not force and not _stale(out, deps, cmd):
         return out

@@ -33,7 +33,7 @@ from . import reset as RS
 MAX_EPISODE_STEPS = 200          # assistive_gym/__init__.py TimeLimit
 # settle frames after the reset state is in place: feeding.py:318-320; scratch_itch.py has none;
 # bed_bathing.py's 100-frame arm settle (:288-289) comes before the robot is placed (reset_bedbath)
-SETTLE_FRAMES = {ABI.TASK_FEEDING: 100, ABI.TASK_SCRATCH: 0, ABI.TASK_BEDBATH: 0}
+SETTLE_FRAMES = {ABI.TASK_FEEDING: 100, ABI.TASK_SCRATCH: 0, ABI.TASK_BEDBATH: 0, ABI.TASK_DRESSING: 0}
 
 
 class Box:
@@ -110,15 +110,22 @@ REGISTRY = {
     'FeedingVRJacoHuman-v0':     ('feeding', 'jaco', False),
     'FeedingVRPR2New-v0':        ('feeding', 'pr2', False),
     'FeedingVRJacoNew-v0':       ('feeding', 'jaco', False),
+    # BASELINE.json configs[4]; not registered by the reference (it has no dressing task, SURVEY
+    # 0.5): a build-defined task on the reference's dressing hooks (include/avr_dressing.h)
+    'DressingJaco-v0':           ('dressing', 'jaco', True),
 }
 
 _SCENES = {}
-_TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH, 'bed_bathing': ABI.TASK_BEDBATH}
+_TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH, 'bed_bathing': ABI.TASK_BEDBATH, 'dressing': ABI.TASK_DRESSING}
 
 
 def _scene(task):
     if task not in _SCENES:
-        A = ABI.load_scene(_TASK_OF[task])
+        if task == 'dressing':
+            from . import reset_dressing as RD
+            A = RD.dressing_scene()
+        else:
+            A = ABI.load_scene(_TASK_OF[task])
         _SCENES[task] = (A, ABI.ModelDesc(A))
     return _SCENES[task]
 
@@ -185,7 +192,7 @@ class AVRVecEnv:
             raise KeyError('unknown env id %r' % env_id)
         task, robot, ok = REGISTRY[env_id]
         if not ok:
-            raise NotImplementedError('%s: only FeedingJaco-v0, ScratchItchPR2-v0 and BedBathingPR2-v0 are built (SURVEY 8)' % env_id)
+            raise NotImplementedError('%s: only FeedingJaco-v0, ScratchItchPR2-v0, BedBathingPR2-v0 and DressingJaco-v0 are built (SURVEY 8)' % env_id)
         self.env_id = env_id
         self.n = int(n_envs)
         self.seed = int(seed)
@@ -196,7 +203,7 @@ class AVRVecEnv:
         self.task = self.md.task
         self.L = self.md.layout
         self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'
-        self.device_search = self.task != ABI.TASK_FEEDING and reset_ik == 'device'
+        self.device_search = self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH) and reset_ik == 'device'
         self.scratch_attempts, self.scratch_iters = scratch_attempts, scratch_iters
         self.reset_stream = reset_stream
         self.device = device
@@ -247,6 +254,9 @@ class AVRVecEnv:
     def _inputs(self, idx, episodes):
         """The host part of the masked envs' resets (everything before the device's part)."""
         ids = [self.env_offset + int(i) for i in idx]
+        if self.task == ABI.TASK_DRESSING:
+            from . import reset_dressing as RD
+            return RD.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes))
         if self.task == ABI.TASK_BEDBATH:
             from . import reset_bedbath as RBB
             return RBB.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes),
@@ -286,6 +296,13 @@ class AVRVecEnv:
                 self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
             return
         ids = [self.env_offset + int(i) for i in idx]
+        if self.task == ABI.TASK_DRESSING:
+            t0 = time.perf_counter()
+            Si, _ = self._inputs(idx, eps)
+            S[idx] = Si
+            self.sim.reset(mask.astype(np.uint8), S, 0, self._obs)
+            self.reset_timing = dict(host_s=time.perf_counter() - t0)
+            return
         if self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH):
             # host part (prefetched on a background thread during the previous episode when the
             # same envs finish together), then the base-pose search on the device

@@ -1,0 +1,174 @@
+"""Host reset path of DressingJaco-v0 (BASELINE configs[4]; a build-defined task, see
+include/avr_dressing.h and DESIGN.md section 10).
+
+Per env (numpy Generator keyed by (seed, env id, episode), like the other tasks' resets):
+  * gender, and the seated human of FeedingJaco's scene (human_joint_angles: feeding.py:242-245
+    arm and leg targets, random head) -> the left arm's collision geometry in the world: the
+    upper-arm and forearm capsules and the hand sphere (links 19, 21, 23 of human_creation.py's
+    left arm) and the cloth spheres at the shoulder, elbow and wrist (human_creation.py:90-95,
+    136-141: links 18, 20, 22);
+  * the sleeve's start: its held cuff (ring 0) just beyond the hand along the forearm axis
+    (jittered), the tool frame's z axis pointing back along the forearm towards the elbow; the
+    Jaco's arm joints by damped least squares to that tool pose (random restarts, as the other
+    resets' IK, util.py:34-105 semantics) -- the robot is kinematic in this task, so no collision
+    screening applies;
+  * the sleeve in its rest shape: ring k centred k * spacing beyond the cuff, away from the arm.
+"""
+import numpy as np
+
+from . import _abi as ABI
+from . import geom as G
+from . import reset as RS
+
+DR = ABI.DR
+# the Jaco's base for dressing the left arm (build-defined: the FeedingJaco base mirrored to the
+# person's left side and moved forward so that the hand, the elbow and the shoulder are in reach)
+DR_BASE = np.array([0.65, -0.3, 0.36, 0.0, 0.0, 0.0, 1.0])
+CLOTH_SPHERE_R = {'male': (0.043, 0.043, 0.033), 'female': (0.0355, 0.0355, 0.027)}   # human_creation.py:93-95, 139-141
+SH_LINK, EL_LINK, WR_LINK = 18, 20, 22          # cloth-sphere links of the left arm (DFS order)
+UA_LINK, FA_LINK, HAND_LINK = 19, 21, 23
+
+
+def dressing_scene():
+    """FeedingJaco's compiled scene with the dressing task's robot base."""
+    A = dict(ABI.load_scene(ABI.TASK_FEEDING))
+    A['robot_base'] = DR_BASE.copy()
+    A['task_dressing'] = np.int32(1)
+    return A
+
+
+def _slot_shape(A, link, gender):
+    """(shape index) of the compiled human shape on `link` for `gender`."""
+    sl = list(A['human_slot_link'])
+    slot = sl.index(link)
+    g = 0 if gender == 'male' else 1
+    for b in range(len(A['body_kind'])):
+        if A['body_kind'][b] == ABI.BODY_HUMAN and A['body_index'][b] == slot:
+            for s in range(A['body_shape_start'][b], A['body_shape_start'][b] + A['body_shape_count'][b]):
+                if A['shape_gender'][s] in (-1, g):
+                    return s
+    raise KeyError(link)
+
+
+def arm_geometry(A, gender, qh):
+    """The left arm's world geometry: the GEO words of the state block (avr_dressing.h)."""
+    _, _, P, Q = RS.human_link_poses(A, gender, qh)
+    geo = np.zeros(32)
+    geo[0:3], geo[3:6], geo[6:9] = P[SH_LINK], P[EL_LINK], P[WR_LINK]
+    s = _slot_shape(A, HAND_LINK, gender)
+    geo[9:12] = G.tf_mul(P[HAND_LINK], Q[HAND_LINK], A['shape_pose'][s][:3], A['shape_pose'][s][3:])[0]
+    for off, link in ((12, UA_LINK), (19, FA_LINK)):
+        s = _slot_shape(A, link, gender)
+        c, q = G.tf_mul(P[link], Q[link], A['shape_pose'][s][:3], A['shape_pose'][s][3:])
+        ax = G.quat_rotate(q, [0, 0, 1.0]) * A['shape_param'][s][1]          # GEOM_CAPSULE: z-aligned, half height
+        geo[off:off + 3], geo[off + 3:off + 6], geo[off + 6] = c + ax, c - ax, A['shape_param'][s][0]
+    geo[26] = A['shape_param'][_slot_shape(A, HAND_LINK, gender)][0]
+    geo[27:30] = CLOTH_SPHERE_R[gender]
+    return geo
+
+
+def _frame_z(z, x_hint):
+    z = z / np.linalg.norm(z)
+    x = x_hint - np.dot(x_hint, z) * z
+    x /= np.linalg.norm(x)
+    from scipy.spatial.transform import Rotation
+    return Rotation.from_matrix(np.stack([x, np.cross(z, x), z], 1)).as_quat()
+
+
+def arm_limits(md):
+    arm = md.arm_dofs
+    lo = np.array([md.desc.arm_lower[i] if md.desc.arm_lower[i] > -1e9 else -2 * np.pi for i in range(len(arm))])
+    hi = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
+    return arm, lo, hi
+
+
+def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01):
+    """Vectorised damped-least-squares IK of the tool link's COM frame (RS.ik_batch's update rule)
+    with per-env restarts init (N, R, 7); no collision screening (the robot is kinematic here).
+    Returns (Q (N, ndof), ok (N,))."""
+    N, R, _ = init.shape
+    nd = int(A['n_dof'])
+    chain = RS._chain(A, link)
+    cols = [[k for k in chain if A['rl_dof'][k] == d][0] for d in arm]
+    Qout = np.zeros((N, nd))
+    done = np.zeros(N, bool)
+    for r in range(R):
+        idx = np.nonzero(~done)[0]
+        if not len(idx):
+            break
+        Q = np.zeros((len(idx), nd))
+        Q[:, arm] = init[idx, r]
+        tp, tq = tpos[idx], tquat[idx]
+        for it in range(iters):
+            CP, CQ, AX, OR = RS.robot_fk_batch(A, Q)
+            ep = tp - CP[:, link]
+            dq = RS._qmul(tq, CQ[:, link] * np.array([-1, -1, -1, 1.0]))
+            dq = np.where(dq[:, 3:4] < 0, -dq, dq)
+            s = np.linalg.norm(dq[:, :3], axis=1)
+            ang = 2.0 * np.arctan2(s, dq[:, 3])
+            er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
+            J = np.zeros((len(idx), 6, len(arm)))
+            for c, l in enumerate(cols):
+                J[:, :3, c] = RS._cross(AX[:, l], CP[:, link] - OR[:, l])
+                J[:, 3:, c] = AX[:, l]
+            JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
+            step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, np.concatenate([ep, er], 1)[..., None])
+            Q[:, arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
+        CP, CQ, _, _ = RS.robot_fk_batch(A, Q)
+        pe = np.linalg.norm(tp - CP[:, link], axis=1)
+        qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))
+        good = (pe < tol) & (qe < tol)
+        for k, e in enumerate(idx):
+            if good[k] or r == R - 1:
+                Qout[e] = Q[k]
+                done[e] = good[k]
+    return Qout, done
+
+
+def cloth_rest(p_tool, q_tool):
+    """Particle positions [NP][3] of the sleeve at rest: ring k centred k * spacing along -z of
+    the tool frame, particle j at angle 2 pi j / segs in the frame's x-y plane."""
+    R = G.quat_to_mat(q_tool)
+    th = 2 * np.pi * np.arange(DR.SEGS) / DR.SEGS
+    ring = np.stack([DR.RADIUS * np.cos(th), DR.RADIUS * np.sin(th), np.zeros(DR.SEGS)], 1)
+    X = np.zeros((DR.RINGS, DR.SEGS, 3))
+    for k in range(DR.RINGS):
+        X[k] = p_tool + (ring - np.array([0, 0, k * DR.SPACING])) @ R.T
+    return X.reshape(-1, 3)
+
+
+def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restarts=8):
+    """(S (N, STATE_WORDS) float64, meta) for the global env ids."""
+    n = len(env_ids)
+    episodes = [0] * n if episodes is None else list(episodes)
+    arm, lo, hi = arm_limits(md)
+    tool = int(A['task_tool_link'])
+    S = np.zeros((n, DR.STATE_WORDS))
+    tpos = np.zeros((n, 3)); tquat = np.zeros((n, 4))
+    init = np.zeros((n, restarts, len(arm)))
+    meta = []
+    for k, e in enumerate(env_ids):
+        rng = RS._rng(seed, e, episodes[k])
+        g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
+        qh = RS.human_joint_angles(A, g, rng)
+        geo = arm_geometry(A, g, qh)
+        el, wr = geo[3:6], geo[6:9]
+        u = (wr - el) / np.linalg.norm(wr - el)
+        hand_end = wr + u * geo[26] * 2                        # util.py:191
+        tpos[k] = hand_end + u * 0.06 + rng.uniform(-0.02, 0.02, 3)
+        tquat[k] = _frame_z(-u, np.array([0, 0, 1.0]))
+        init[k] = rng.uniform(lo, hi, size=(restarts, len(arm)))
+        S[k, DR.S_GEO:DR.S_GEO + 32] = geo
+        S[k, DR.S_TASK + DR.T_GENDER] = 0 if g == 'male' else 1
+        meta.append(dict(gender=g, impairment='none'))
+    Q, ok = ik_batch(A, tool, tpos, tquat, arm, lo, hi, init)
+    CP, CQ, _, _ = RS.robot_fk_batch(A, Q)
+    for k in range(n):
+        S[k, DR.S_Q:DR.S_Q + 7] = Q[k, arm]
+        S[k, DR.S_QT:DR.S_QT + 7] = Q[k, arm]
+        S[k, DR.S_TOOL:DR.S_TOOL + 3] = CP[k, tool]
+        S[k, DR.S_TOOL + 3:DR.S_TOOL + 7] = CQ[k, tool]
+        X = cloth_rest(CP[k, tool], CQ[k, tool])
+        S[k, DR.S_X:DR.S_X + 4 * DR.NP].reshape(DR.NP, 4)[:, :3] = X
+        meta[k]['ik_ok'] = bool(ok[k])
+    return S, meta

@@ -8,6 +8,7 @@
 #include <new>
 
 #include "../../include/avr.h"
+#include "../../include/avr_dressing.h"
 
 #define AVR_TASK_DECLS(NS)                                                                                         \
     namespace NS {                                                                                                 \
@@ -51,6 +52,7 @@
 AVR_TASK_DECLS(avr_feeding)
 AVR_TASK_DECLS(avr_scratch)
 AVR_TASK_DECLS(avr_bedbath)
+AVR_TASK_DECLS(avr_dressing)
 
 struct avr_sim {
     int32_t task;
@@ -68,6 +70,10 @@ struct avr_sim {
             avr_bedbath::avr_sim *h = (avr_bedbath::avr_sim *)(s)->impl;                      \
             return call;                                                                      \
         }                                                                                     \
+        if ((s)->task == AVR_TASK_DRESSING) {                                                 \
+            avr_dressing::avr_sim *h = (avr_dressing::avr_sim *)(s)->impl;                    \
+            return call;                                                                      \
+        }                                                                                     \
         avr_feeding::avr_sim *h = (avr_feeding::avr_sim *)(s)->impl;                          \
         return call;                                                                          \
     } while (0)
@@ -82,13 +88,15 @@ extern "C" {
 int32_t avr_abi_version(void) { return AVR_ABI_VERSION; }
 int32_t avr_state_words(void) { return AVR_STATE_WORDS; }
 int32_t avr_task_state_words(int32_t task) {
-    return task == AVR_TASK_FEEDING ? AVR_STATE_WORDS : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH) ? AVR_SI_STATE_WORDS : -1;
+    return task == AVR_TASK_FEEDING ? AVR_STATE_WORDS : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH) ? AVR_SI_STATE_WORDS
+         : task == AVR_TASK_DRESSING ? AVR_DR_STATE_WORDS : -1;
 }
 int32_t avr_task_obs_dim(int32_t task) {
-    return task == AVR_TASK_FEEDING ? AVR_OBS_DIM : task == AVR_TASK_SCRATCH ? AVR_SI_OBS_DIM : task == AVR_TASK_BEDBATH ? AVR_BB_OBS_DIM : -1;
+    return task == AVR_TASK_FEEDING ? AVR_OBS_DIM : task == AVR_TASK_SCRATCH ? AVR_SI_OBS_DIM : task == AVR_TASK_BEDBATH ? AVR_BB_OBS_DIM
+         : task == AVR_TASK_DRESSING ? AVR_DR_OBS_DIM : -1;
 }
 int32_t avr_task_act_dim(int32_t task) {
-    return task == AVR_TASK_FEEDING ? AVR_ACT_DIM : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH) ? AVR_SI_ACT_DIM : -1;
+    return task == AVR_TASK_FEEDING ? AVR_ACT_DIM : (task == AVR_TASK_SCRATCH || task == AVR_TASK_BEDBATH || task == AVR_TASK_DRESSING) ? AVR_SI_ACT_DIM : -1;
 }
 int32_t avr_task(avr_sim *s) { return s ? s->task : -1; }
 
@@ -114,6 +122,10 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         avr_bedbath::avr_sim *h = nullptr;
         r = avr_bedbath::avr_create(cfg, d, &h);
         s->impl = h;
+    } else if (d->task == AVR_TASK_DRESSING) {
+        avr_dressing::avr_sim *h = nullptr;
+        r = avr_dressing::avr_create(cfg, d, &h);
+        s->impl = h;
     } else {
         snprintf(s->err, sizeof(s->err), "unknown task %d in avr_model_desc.task", (int)d->task);
         return -2;
@@ -127,6 +139,7 @@ int avr_destroy(avr_sim *s) {
     if (s->impl) {
         if (s->task == AVR_TASK_SCRATCH) r = avr_scratch::avr_destroy((avr_scratch::avr_sim *)s->impl);
         else if (s->task == AVR_TASK_BEDBATH) r = avr_bedbath::avr_destroy((avr_bedbath::avr_sim *)s->impl);
+        else if (s->task == AVR_TASK_DRESSING) r = avr_dressing::avr_destroy((avr_dressing::avr_sim *)s->impl);
         else r = avr_feeding::avr_destroy((avr_feeding::avr_sim *)s->impl);
     }
     delete s;

@@ -1496,6 +1496,17 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
     }
     if (nap > MAXAP) { if (lane == 0) L.flags |= 4; nap = MAXAP; }
     SYNC();
+    // the active pairs' records, loaded once (every round trip in flight together): lane l of
+    // slot q holds active pair 64 q + l's; the rounds below read them across lanes rather than
+    // from global memory each time
+    static_assert(MAXAP == 256, "four record slots");
+    auto rec_load = [&](int q) {
+        const int a = 64 * q + lane;
+        const int ap = L.u.c.apair[min(a, max(nap - 1, 0))];
+        const int4 r = m.pair_rec[ap];
+        return a < nap ? r : make_int4(0, 0, 0, 0);
+    };
+    const int4 rq0 = rec_load(0), rq1 = rec_load(1), rq2 = rec_load(2), rq3 = rec_load(3);
     PROF_STOP(1, pt);
     // Child shape pairs, in pair order (i-major, j-minor within a body pair), appended to the
     // list.  A child's world AABB lies inside its body's fattened AABB, so children of A that
@@ -1546,8 +1557,18 @@ AVR_DI void collide_pairs(const KModel &m, LT &L, float *cs) {
         } else if (k < nap) {
             if (gcull) { SYNC(); gcull = false; }   // candA / candB are rewritten below
             const int kk = k + lane;
-            int4 rec = make_int4(0, 0, 0, 0);
-            if (kk < nap) rec = m.pair_rec[L.u.c.apair[kk]];
+            int4 rec;
+            {
+                // record of active pair kk: slot kk / 64 (k / 64 or the next) of lane kk % 64
+                const int s0 = k >> 6;
+                const int4 lo = s0 == 0 ? rq0 : s0 == 1 ? rq1 : s0 == 2 ? rq2 : rq3;
+                const int4 hi = s0 == 0 ? rq1 : s0 == 1 ? rq2 : rq3;
+                const int src = kk & 63;
+                const bool up = (kk >> 6) != s0;
+                const int4 a = make_int4(__shfl(lo.x, src), __shfl(lo.y, src), __shfl(lo.z, src), __shfl(lo.w, src));
+                const int4 b = make_int4(__shfl(hi.x, src), __shfl(hi.y, src), __shfl(hi.z, src), __shfl(hi.w, src));
+                rec = kk < nap ? (up ? b : a) : make_int4(0, 0, 0, 0);
+            }
             const unsigned long long bm = __ballot(kk < nap && (rec.w & 2));
             const int run = bm == ~0ull ? 64 : __ffsll((long long)~bm) - 1;
             if (run > 0) {                          // a run of 1 x 1 pairs
@@ -2273,25 +2294,7 @@ AVR_DI void observe(const KModel &m, EnvLDS &L, float spoon_force, float *obs_ou
 #endif  // AVR_TASK_FEEDING
 
 // Philox4x32-10 (Salmon et al. 2011): counter (env, step, j, 0), key (seed lo, seed hi)
-AVR_DI void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1) {
-    for (int r = 0; r < 10; r++) {
-        unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
-        unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
-        unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0;
-        unsigned h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
-        unsigned n0 = h1 ^ c[1] ^ k0, n1 = l1, n2 = h0 ^ c[3] ^ k1, n3 = l0;
-        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
-AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j) {
-    unsigned c[4] = {(unsigned)env, (unsigned)t, (unsigned)(j >> 2), (unsigned)((unsigned long long)t >> 32)};
-    philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32));
-    unsigned x = c[j & 3];
-    return (float)(x >> 8) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
-}
+// (philox4x32_10, philox_action: avr_math.h)
 
 enum { MODE_STEP = 0, MODE_STEP_RANDOM = 1, MODE_SETTLE = 2, MODE_SUBSTEP = 3 };
 

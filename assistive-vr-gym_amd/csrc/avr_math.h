@@ -90,3 +90,25 @@ AVR_DI int wave_argmax(float v, int idx) {
     }
     return idx;
 }
+
+// Philox4x32-10 (the synthetic action stream, examples/random_actions.py semantics): action j of
+// env `env` at step t ~ U(-1, 1), keyed by (seed, env, t); _lib.random_actions is the host mirror
+AVR_DI void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1) {
+    for (int r = 0; r < 10; r++) {
+        unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
+        unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
+        unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0;
+        unsigned h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+        unsigned n0 = h1 ^ c[1] ^ k0, n1 = l1, n2 = h0 ^ c[3] ^ k1, n3 = l0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+AVR_DI float philox_action(unsigned long long seed, int env, long long t, int j) {
+    unsigned c[4] = {(unsigned)env, (unsigned)t, (unsigned)(j >> 2), (unsigned)((unsigned long long)t >> 32)};
+    philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32));
+    unsigned x = c[j & 3];
+    return (float)(x >> 8) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
+}

@@ -42,6 +42,11 @@ TASKS = {
     # set: 2252 + 28 B each way) + obs 24 + reward + done + 2 info + action in
     'BedBathingPR2-v0': dict(task=2, bytes=2280 * 2 + 120 + 28 + 112, settle=0, substeps=5, iters=50, pool=128,
                              workload='BedBathingPR2-v0, %d envs/GPU, wiping targets + tool-human closest distance, random actions'),
+    # DressingJaco (build-defined, include/avr_dressing.h): the 1104-word state block in and out once
+    # (it stays in registers / LDS across the 100 cloth sub-steps of one launch) + action + obs 24,
+    # reward, done, info 2; BASELINE configs[4] runs 2048 envs
+    'DressingJaco-v0': dict(task=3, bytes=1104 * 4 * 2 + 28 + 112, settle=0, substeps=100, iters=0, pool=128, envs=2048,
+                            workload='DressingJaco-v0, %d envs/GPU, mass-spring sleeve (128 particles) with penalty cloth-arm contact, random actions'),
 }
 VALU_CYC = 2.0          # v_fma_f32 wave64 issue throughput, cycles (MI355X_MICROARCH.md cycle table)
 SIMDS, CLOCK_HZ = 1024, 2.4e9
@@ -56,6 +61,9 @@ def layout_bytes_per_env_step(L):
 def reset_pool(task, A, md, ids, impairment, device=0):
     """Reset states of the bench's env pool; the PR2 tasks' base-pose search runs on the device
     (avr_base_search) with the reference's 100 attempts of 200 IK iterations, on this rank's GPU."""
+    if task == 3:
+        from avr import reset_dressing as RD
+        return RD.batch_reset_states(A, md, 1001, ids)
     if task in (1, 2):
         from avr import _lib
         sim = _lib.Sim(md, 1, device=device)
@@ -101,7 +109,8 @@ def cpu_baseline(name, md, A, seconds, threads, impairment):
 def pmc_summary(name, kernels, ms_per_step, E):
     """HBM traffic and SQ issue figures from the committed rocprofv3 PMC summary of this task's
     bench (profiles/pmc_<task>.json, tools/rocpd_summary.py), if its kernel set and env count match."""
-    fname = {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json', 'BedBathingPR2-v0': 'pmc_bedbath.json'}[name]
+    fname = {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json', 'BedBathingPR2-v0': 'pmc_bedbath.json',
+             'DressingJaco-v0': 'pmc_dressing.json'}[name]
     path = os.path.join(ROOT, 'profiles', fname)
     if not os.path.exists(path):
         return None
@@ -134,7 +143,7 @@ def facade_bench(args):
     import numpy as np
     import torch
     from avr import env as EV
-    E = args.envs
+    E = args.envs if args.envs is not None else TASKS[args.task].get('envs', 4096)
     dev = torch.device('cuda', 0)
     v = EV.AVRTorchVecEnv(args.task, E, device=0, impairment=args.impairment)
     t0 = time.perf_counter()
@@ -217,10 +226,14 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
     from avr import dist as D
     T = TASKS[name]
     settle = T['settle'] if args.settle is None else args.settle
-    A = ABI.load_scene(T['task'])
+    if T['task'] == 3:
+        from avr import reset_dressing as RD
+        A = RD.dressing_scene()
+    else:
+        A = ABI.load_scene(T['task'])
     md = ABI.ModelDesc(A)
     L = md.layout
-    E = args.envs
+    E = args.envs if args.envs is not None else T.get('envs', 4096)
     # reset pool: distinct initial states for global env ids; tiled if pool < E
     pool = min(args.reset_pool or T['pool'], E)
     base_id, _ = D.shard(E, rank)
@@ -358,9 +371,10 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
     return out
 
 
-# the other single-GPU configs BASELINE.json names (configs[2], the PR2 variant of configs[3]),
+# the other single-GPU configs BASELINE.json names (configs[2], the PR2 variant of configs[3],
+# configs[4] as the build-defined DressingJaco),
 # timed after the headline in the same default run: extra keys of the one JSON line
-OTHER_TASKS = ('ScratchItchPR2-v0', 'BedBathingPR2-v0')
+OTHER_TASKS = ('ScratchItchPR2-v0', 'BedBathingPR2-v0', 'DressingJaco-v0')
 OTHER_KEYS = ('value', 'unit', 'steps', 'warmup', 'ms_per_step', 'config', 'roofline', 'nan_or_overflow_envs', 'flagged_envs_by_bit',
               'cpu_baseline')
 
@@ -378,13 +392,14 @@ def policy_eval_bench(args):
     pol = PE.ActorCritic(L.OBS_DIM, L.ACT_DIM)
     rms = PE.RunningMeanStd((L.OBS_DIM,))
     t0 = time.perf_counter()
-    r = PE.evaluate(name, pol, rms, n_envs=args.envs, steps=200, deterministic=False, device=0)
+    E = args.envs if args.envs is not None else TASKS[name].get('envs', 4096)
+    r = PE.evaluate(name, pol, rms, n_envs=E, steps=200, deterministic=False, device=0)
     total = time.perf_counter() - t0
     out = {'metric': 'policy-eval env-steps/sec (avr.policy_eval.evaluate: enjoy_vr.py loop, fresh action tensor per step)',
-           'value': args.envs * 200 / r['loop_s'], 'unit': 'env-steps/s', 'n_gpus': 1, 'steps': 200, 'warmup': 0,
+           'value': E * 200 / r['loop_s'], 'unit': 'env-steps/s', 'n_gpus': 1, 'steps': 200, 'warmup': 0,
            'ms_per_step': r['loop_s'] / 200 * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
            'data': 'synthetic policy (random-init MLP actor-critic), stochastic actions',
-           'config': {'workload': '%s, %d envs, policy evaluation harness' % (name, args.envs), 'task': name, 'envs_per_gpu': args.envs},
+           'config': {'workload': '%s, %d envs, policy evaluation harness' % (name, E), 'task': name, 'envs_per_gpu': E},
            'graph_captures': r['graph_captures'], 'total_s_with_env_creation_and_reset': total,
            'mean_return': float(np.mean(r['returns']))}
     print(json.dumps(out), flush=True)
@@ -396,7 +411,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default: the config\'s, 4096; DressingJaco 2048)')
     ap.add_argument('--settle', type=int, default=None, help='reset settle frames (FeedingJaco 100, ScratchItch 0)')
     ap.add_argument('--gather-every', type=int, default=16)
     ap.add_argument('--cpu-seconds', type=float, default=15.0)

@@ -21,6 +21,7 @@ extern "C" {
 #define AVR_TASK_FEEDING 0       /* FeedingJaco-v0   (feeding.py, feeding_robots.py:7-9)       */
 #define AVR_TASK_SCRATCH 1       /* ScratchItchPR2-v0 (scratch_itch.py, scratch_itch_robots.py) */
 #define AVR_TASK_BEDBATH 2       /* BedBathingPR2-v0  (bed_bathing.py, bed_bathing_robots.py)   */
+#define AVR_TASK_DRESSING 3      /* DressingJaco-v0: build-defined (include/avr_dressing.h)       */
 
 /* ==== FeedingJaco-v0 layout ==== */
 /* ---- capacities (compile-time; checked against the model at create time) ---- */

@@ -1,0 +1,384 @@
+/* avr_oracle_dressing.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the DressingJaco-v0 step
+ * (a build-defined task: include/avr_dressing.h), the checker of the gfx950
+ * kernel (assistive-vr-gym_amd/csrc/avr_dressing.hip).  Imported only by tests/, smoke() and
+ * bench.py's cpu_baseline leg.  Built in fp64 (default) and fp32 (-DAVR_ORACLE_FLOAT).
+ *
+ * No parity anchor beyond this restatement: the reference holds no dressing task, only
+ * the hooks the task is built on -- the cloth spheres (human_creation.py:90-95,136-141), the
+ * dressing-force term (env.py:433-434) and Util.sleeve_on_arm_reward (util.py:179-252), which
+ * dr_sleeve_on_arm below restates line by line.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/avr_model.h"
+#include "../include/avr_dressing.h"
+
+#ifdef AVR_ORACLE_FLOAT
+typedef float real;
+#define R(x) ((float)(x))
+#else
+typedef double real;
+#define R(x) ((double)(x))
+#endif
+#define EXPORT __attribute__((visibility("default")))
+#define NP AVR_DR_NP
+#define NR AVR_DR_RINGS
+#define NS AVR_DR_SEGS
+
+typedef struct { real x, y, z; } v3;
+typedef struct { real x, y, z, w; } qt;
+static inline v3 V(real x, real y, real z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 scl(v3 a, real s) { return V(a.x * s, a.y * s, a.z * s); }
+static inline real dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 crs(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static inline real len(v3 a) { return sqrt(dot(a, a)); }
+static inline v3 ld3(const real *p) { return V(p[0], p[1], p[2]); }
+static inline void st3(real *p, v3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+static inline qt Q(real x, real y, real z, real w) { qt r = {x, y, z, w}; return r; }
+static inline qt qmul(qt a, qt b) {
+    return Q(a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+             a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z);
+}
+static inline v3 qrot(qt q, v3 v) {
+    const v3 u = V(q.x, q.y, q.z);
+    const v3 t = scl(crs(u, v), 2);
+    return add(add(v, scl(t, q.w)), crs(u, t));
+}
+
+/* Jaco chain (the FeedingJaco scene's robot; avr_model_desc rl_* arrays) */
+#define MAXL 20
+typedef struct {
+    int nl, tool, arm_dof[7];
+    int parent[MAXL], jtype[MAXL], dof[MAXL];
+    v3 jpos[MAXL], axis[MAXL], compos[MAXL];
+    qt jquat[MAXL], comquat[MAXL];
+    v3 base_p;
+    qt base_q;
+    real lower[7], upper[7];
+} chain_t;
+
+typedef struct avr_oracle {
+    chain_t c;
+    int n, threads;
+    real *state;
+    char err[128];
+} avr_oracle;
+
+/* COM frames of the tool link and of link 0 (the 'torso' of the observation, feeding.py:124) */
+static void chain_fk(const chain_t *c, const real *q7, v3 *tool_p, qt *tool_q, v3 *torso_p) {
+    v3 lp[MAXL];
+    qt lq[MAXL];
+    real q[MAXL] = {0};
+    for (int i = 0; i < 7; i++) q[c->arm_dof[i]] = q7[i];
+    for (int i = 0; i < c->nl; i++) {
+        const int p = c->parent[i];
+        const v3 pp = p < 0 ? c->base_p : lp[p];
+        const qt pq = p < 0 ? c->base_q : lq[p];
+        v3 tp = add(pp, qrot(pq, c->jpos[i]));
+        qt tq = qmul(pq, c->jquat[i]);
+        if (c->jtype[i] == AVR_J_REVOLUTE) {
+            const real a = q[c->dof[i]] * R(0.5);
+            const real s = sin(a);
+            tq = qmul(tq, Q(c->axis[i].x * s, c->axis[i].y * s, c->axis[i].z * s, cos(a)));
+        }
+        lp[i] = tp;
+        lq[i] = tq;
+    }
+    *tool_p = add(lp[c->tool], qrot(lq[c->tool], c->compos[c->tool]));
+    *tool_q = qmul(lq[c->tool], c->comquat[c->tool]);
+    *torso_p = add(lp[0], qrot(lq[0], c->compos[0]));
+}
+
+/* closest point on segment ab to x */
+static v3 seg_closest(v3 a, v3 b, v3 x) {
+    const v3 ab = sub(b, a);
+    const real l2 = dot(ab, ab);
+    real t = l2 > 0 ? dot(sub(x, a), ab) / l2 : 0;
+    t = t < 0 ? 0 : t > 1 ? 1 : t;
+    return add(a, scl(ab, t));
+}
+
+/* penalty contact force on a particle at x with velocity v against a sphere at c (radius r) */
+static v3 contact(v3 x, v3 v, v3 c, real r) {
+    const v3 d = sub(x, c);
+    const real dist = len(d);
+    const real pen = r + R(AVR_DR_THICK) - dist;
+    if (!(pen > 0) || !(dist > R(1e-9))) return V(0, 0, 0);
+    const v3 n = scl(d, 1 / dist);
+    const real vn = dot(v, n);
+    const real f = R(AVR_DR_K_CONTACT) * pen - R(AVR_DR_C_CONTACT) * (vn < 0 ? vn : 0);
+    return scl(n, f);
+}
+
+static const int NB_DK[12] = {0, 0, 1, -1, 1, 1, -1, -1, 0, 0, 2, -2};
+static const int NB_DJ[12] = {1, -1, 0, 0, 1, -1, 1, -1, 2, -2, 0, 0};
+
+/* one cloth sub-step of one env: x, v [NP] (in/out), cuff ring targets tgt [NS]; returns the
+ * summed contact-force magnitude (the dressing forces, env.py:433-434) */
+static real cloth_substep(v3 *x, v3 *v, const v3 *tgt, const real *geo, real dt) {
+    const real m = R(AVR_DR_MASS) / NP;
+    const real pi = R(3.14159265358979323846);
+    const real L_ring = 2 * R(AVR_DR_RADIUS) * sin(pi / NS), L_ax = R(AVR_DR_SPACING);
+    const real L_ring2 = 2 * R(AVR_DR_RADIUS) * sin(2 * pi / NS);
+    const real L_sh = sqrt(L_ring * L_ring + L_ax * L_ax);
+    v3 F[NP];
+    real ftot = 0;
+    for (int i = NS; i < NP; i++) {
+        const int k = i / NS, j = i % NS;
+        v3 f = V(0, 0, R(AVR_DR_GRAVITY) * m);
+        f = sub(f, scl(v[i], R(AVR_DR_AIR)));
+        for (int s = 0; s < 12; s++) {
+            const int kk = k + NB_DK[s];
+            if (kk < 0 || kk >= NR) continue;
+            const int jj = (j + NB_DJ[s] + NS) % NS;
+            const int o = kk * NS + jj;
+            const real ks = s < 4 ? (s < 2 ? R(AVR_DR_K_STRUCT) : R(AVR_DR_K_STRUCT)) : s < 8 ? R(AVR_DR_K_SHEAR) : R(AVR_DR_K_BEND);
+            const real L0 = s < 2 ? L_ring : s < 4 ? L_ax : s < 8 ? L_sh : s < 10 ? L_ring2 : 2 * L_ax;
+            const v3 d = sub(x[o], x[i]);
+            const real l = len(d);
+            if (!(l > R(1e-9))) continue;
+            const v3 u = scl(d, 1 / l);
+            const real fs = ks * (l - L0) + R(AVR_DR_DAMP) * dot(sub(v[o], v[i]), u);
+            f = add(f, scl(u, fs));
+        }
+        /* penalty contact with the left arm: capsules (upper arm, forearm), hand sphere, cloth spheres */
+        v3 fc = V(0, 0, 0);
+        fc = add(fc, contact(x[i], v[i], seg_closest(ld3(geo + 12), ld3(geo + 15), x[i]), geo[18]));
+        fc = add(fc, contact(x[i], v[i], seg_closest(ld3(geo + 19), ld3(geo + 22), x[i]), geo[25]));
+        fc = add(fc, contact(x[i], v[i], ld3(geo + 9), geo[26]));
+        fc = add(fc, contact(x[i], v[i], ld3(geo + 0), geo[27]));
+        fc = add(fc, contact(x[i], v[i], ld3(geo + 3), geo[28]));
+        fc = add(fc, contact(x[i], v[i], ld3(geo + 6), geo[29]));
+        ftot += len(fc);
+        F[i] = add(f, fc);
+    }
+    for (int i = 0; i < NS; i++) {                 /* the held cuff: kinematic */
+        v[i] = scl(sub(tgt[i], x[i]), 1 / dt);
+        x[i] = tgt[i];
+    }
+    for (int i = NS; i < NP; i++) {
+        v[i] = add(v[i], scl(F[i], dt / m));
+        x[i] = add(x[i], scl(v[i], dt));
+    }
+    return ftot;
+}
+
+/* Util.line_intersects_triangle (util.py:179-186) */
+static real svol(v3 a, v3 b, v3 c, v3 d) { return R(1.0 / 6.0) * dot(crs(sub(b, a), sub(c, a)), sub(d, a)); }
+static int sgn(real x) { return (x > 0) - (x < 0); }
+static int line_tri(v3 p0, v3 p1, v3 p2, v3 q0, v3 q1) {
+    if (sgn(svol(q0, p0, p1, p2)) != sgn(svol(q1, p0, p1, p2))) {
+        const int a = sgn(svol(q0, q1, p0, p1)), b = sgn(svol(q0, q1, p1, p2)), c = sgn(svol(q0, q1, p2, p0));
+        if (a == b && b == c) return 1;
+    }
+    return 0;
+}
+static v3 nrm(v3 a) { return scl(a, 1 / len(a)); }
+
+/* Util.sleeve_on_arm_reward (util.py:188-252): out = {forearm_in, upperarm_in, distance_along_forearm,
+ * distance_along_upperarm}; the sleeve's two triangles are ring 0's and the last ring's particles
+ * 0, 5, 10; hand / elbow / shoulder radii: the hand sphere and the elbow / shoulder cloth spheres */
+static void dr_sleeve_on_arm(const v3 *x, const real *geo, real *out, v3 *hand_end_o, v3 *elbow_end_o, v3 *shoulder_end_o, v3 *center_o) {
+    const v3 sh = ld3(geo), el = ld3(geo + 3), wr = ld3(geo + 6);
+    const real hand_r = geo[26], elbow_r = geo[28], shoulder_r = geo[27];
+    const v3 hand_end = add(wr, scl(scl(sub(wr, el), 1 / len(sub(wr, el))), hand_r * 2));
+    const v3 elbow_end = add(el, scl(scl(sub(el, wr), 1 / len(sub(wr, el))), elbow_r));
+    const v3 shoulder_end = add(sh, scl(scl(sub(sh, el), 1 / len(sub(sh, el))), shoulder_r));
+    const int tj[3] = {0, 5, 10};
+    v3 P[6];
+    for (int t = 0; t < 3; t++) { P[t] = x[tj[t]]; P[3 + t] = x[(NR - 1) * NS + tj[t]]; }
+    int res[2];
+    for (int seg = 0; seg < 2; seg++) {
+        const v3 a = seg == 0 ? hand_end : elbow_end, b = seg == 0 ? elbow_end : shoulder_end;
+        const v3 o = seg == 0 ? elbow_end : shoulder_end;
+        const v3 normal = nrm(seg == 0 ? sub(hand_end, elbow_end) : sub(elbow_end, shoulder_end));
+        const v3 tangent = nrm(crs(V(1, 1, 0), normal));
+        const v3 binormal = nrm(crs(tangent, normal));
+        int tp = 0, tn = 0, bp = 0, bn = 0;
+        for (int k = 0; k < 6; k++) {
+            const real t = dot(tangent, sub(P[k], o)), bb = dot(binormal, sub(P[k], o));
+            tp |= t > 0; tn |= t < 0; bp |= bb > 0; bn |= bb < 0;
+        }
+        const int above_below = tp && tn && bp && bn;
+        const int i1 = line_tri(P[0], P[1], P[2], a, b), i2 = line_tri(P[3], P[4], P[5], a, b);
+        res[seg] = above_below && (i1 || i2);
+    }
+    v3 c = V(0, 0, 0);
+    for (int k = 0; k < 6; k++) c = add(c, P[k]);
+    c = scl(c, R(1.0 / 6.0));
+    out[0] = res[0]; out[1] = res[1];
+    out[2] = len(sub(c, hand_end));
+    out[3] = len(sub(c, el));
+    *hand_end_o = hand_end; *elbow_end_o = elbow_end; *shoulder_end_o = shoulder_end; *center_o = c;
+}
+
+static qt qnlerp(qt a, qt b, real s) {
+    if (a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w < 0) b = Q(-b.x, -b.y, -b.z, -b.w);
+    qt r = Q(a.x + (b.x - a.x) * s, a.y + (b.y - a.y) * s, a.z + (b.z - a.z) * s, a.w + (b.w - a.w) * s);
+    const real n = 1 / sqrt(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+    return Q(r.x * n, r.y * n, r.z * n, r.w * n);
+}
+
+/* the env's step: take_step (env.py:274-337 for the arm), 5 frames x 2 robot sub-steps x 10 cloth
+ * sub-steps, then the task glue (obs 24, reward, done, info) */
+static void env_step(const chain_t *c, real *st, const float *act, int settle, float *obs, float *rew, uint8_t *done, float *info) {
+    real asq = 0;
+    if (!settle) {
+        for (int i = 0; i < 7; i++) {
+            const real a_raw = act[i];
+            asq += a_raw * a_raw;
+            real a = (a_raw < -1 ? -1 : a_raw > 1 ? 1 : a_raw) * R(0.05);
+            real qn = st[AVR_DR_S_Q + i];
+            for (int it = 0; it < AVR_DR_FRAME_SKIP; it++) {
+                if (qn + a < c->lower[i]) a = 0;
+                if (qn + a > c->upper[i]) a = 0;
+                qn += a;
+            }
+            st[AVR_DR_S_QT + i] = qn;
+        }
+    }
+    v3 x[NP], v[NP];
+    for (int i = 0; i < NP; i++) { x[i] = ld3(st + AVR_DR_S_X + 4 * i); v[i] = ld3(st + AVR_DR_S_V + 4 * i); }
+    v3 tp0 = ld3(st + AVR_DR_S_TOOL), torso;
+    qt tq0 = Q(st[AVR_DR_S_TOOL + 3], st[AVR_DR_S_TOOL + 4], st[AVR_DR_S_TOOL + 5], st[AVR_DR_S_TOOL + 6]);
+    const real pi = R(3.14159265358979323846);
+    v3 ringl[NS];
+    for (int j = 0; j < NS; j++) {
+        const real th = 2 * pi * j / NS;
+        ringl[j] = V(R(AVR_DR_RADIUS) * cos(th), R(AVR_DR_RADIUS) * sin(th), 0);
+    }
+    const real dtc = R(AVR_DR_FRAME) / (AVR_DR_RSUB * AVR_DR_CSUB);
+    real ftot = 0, speed = 0;
+    const int frames = settle ? 0 : AVR_DR_FRAME_SKIP;
+    for (int f = 0; f < frames; f++)
+        for (int r = 0; r < AVR_DR_RSUB; r++) {
+            real q[7];
+            for (int i = 0; i < 7; i++) {
+                q[i] = st[AVR_DR_S_Q + i] + R(AVR_DR_KP) * (st[AVR_DR_S_QT + i] - st[AVR_DR_S_Q + i]);
+                st[AVR_DR_S_Q + i] = q[i];
+            }
+            v3 tp1;
+            qt tq1;
+            chain_fk(c, q, &tp1, &tq1, &torso);
+            for (int cs = 0; cs < AVR_DR_CSUB; cs++) {
+                const real s = (real)(cs + 1) / AVR_DR_CSUB;
+                const v3 p = add(tp0, scl(sub(tp1, tp0), s));
+                const qt qq = qnlerp(tq0, tq1, s);
+                v3 tgt[NS];
+                for (int j = 0; j < NS; j++) tgt[j] = add(p, qrot(qq, ringl[j]));
+                ftot = cloth_substep(x, v, tgt, st + AVR_DR_S_GEO, dtc);
+            }
+            speed = len(sub(tp1, tp0)) / (R(AVR_DR_FRAME) / AVR_DR_RSUB);
+            tp0 = tp1;
+            tq0 = tq1;
+        }
+    {
+        real q[7];
+        for (int i = 0; i < 7; i++) q[i] = st[AVR_DR_S_Q + i];
+        v3 tpx;
+        qt tqx;
+        chain_fk(c, q, &tpx, &tqx, &torso);
+    }
+    for (int i = 0; i < NP; i++) { st3(st + AVR_DR_S_X + 4 * i, x[i]); st3(st + AVR_DR_S_V + 4 * i, v[i]); }
+    st3(st + AVR_DR_S_TOOL, tp0);
+    st[AVR_DR_S_TOOL + 3] = tq0.x; st[AVR_DR_S_TOOL + 4] = tq0.y; st[AVR_DR_S_TOOL + 5] = tq0.z; st[AVR_DR_S_TOOL + 6] = tq0.w;
+    real *T = st + AVR_DR_S_TASK;
+    if (!settle) T[AVR_DR_T_ITER] += 1;
+    else ftot = T[AVR_DR_T_FORCE];
+    real so[4];
+    v3 hand_end, elbow_end, shoulder_end, center;
+    dr_sleeve_on_arm(x, st + AVR_DR_S_GEO, so, &hand_end, &elbow_end, &shoulder_end, &center);
+    const real r_dress = so[0] > 0 ? so[2] + (so[1] > 0 ? so[3] : 0) : 0;
+    const real r_dist = -len(sub(tp0, shoulder_end));
+    const real reward = R(AVR_DR_W_DISTANCE) * r_dist + R(AVR_DR_W_ACTION) * (-asq) + R(AVR_DR_W_DRESS) * r_dress +
+                        R(AVR_DR_W_VELOCITY) * (-speed) + R(AVR_DR_W_FORCE) * (-ftot);
+    T[AVR_DR_T_FORCE] = ftot;
+    T[AVR_DR_T_FOREARM] = so[0];
+    T[AVR_DR_T_SUCCESS] = so[1];
+    int bad = 0;
+    for (int i = 0; i < AVR_DR_STATE_WORDS; i++)
+        if (!isfinite(st[i])) bad = 1;
+    if (bad) T[AVR_DR_T_FLAGS] = (real)((int)T[AVR_DR_T_FLAGS] | 1);
+    float *o = obs;
+    const v3 a0 = sub(tp0, torso), a1 = sub(center, hand_end), a2 = sub(center, elbow_end), a3 = sub(center, shoulder_end);
+    o[0] = a0.x; o[1] = a0.y; o[2] = a0.z;
+    o[3] = tq0.x; o[4] = tq0.y; o[5] = tq0.z; o[6] = tq0.w;
+    o[7] = a1.x; o[8] = a1.y; o[9] = a1.z;
+    o[10] = a2.x; o[11] = a2.y; o[12] = a2.z;
+    o[13] = a3.x; o[14] = a3.y; o[15] = a3.z;
+    for (int i = 0; i < 7; i++) o[16 + i] = st[AVR_DR_S_Q + i];
+    o[23] = ftot;
+    *rew = settle ? 0.f : (float)reward;
+    *done = T[AVR_DR_T_ITER] >= AVR_DR_MAX_STEPS;
+    info[0] = ftot;
+    info[1] = so[1];
+}
+
+EXPORT int avr_oracle_state_words(void) { return AVR_DR_STATE_WORDS; }
+
+EXPORT int avr_oracle_create(const avr_model_desc *d, int n_envs, avr_oracle **out) {
+    if (!d || !out || n_envs <= 0 || d->n_links > MAXL || d->n_arm != 7) return -1;
+    avr_oracle *o = (avr_oracle *)calloc(1, sizeof(avr_oracle));
+    chain_t *c = &o->c;
+    c->nl = d->n_links;
+    c->tool = d->tool_link;
+    for (int i = 0; i < 7; i++) {
+        c->arm_dof[i] = d->arm_dofs[i];
+        c->lower[i] = R(d->arm_lower[i]);
+        c->upper[i] = R(d->arm_upper[i]);
+    }
+    for (int i = 0; i < c->nl; i++) {
+        c->parent[i] = d->rl_parent[i]; c->jtype[i] = d->rl_jtype[i]; c->dof[i] = d->rl_dof[i];
+        c->jpos[i] = V(R(d->rl_jpos[3 * i]), R(d->rl_jpos[3 * i + 1]), R(d->rl_jpos[3 * i + 2]));
+        c->jquat[i] = Q(R(d->rl_jquat[4 * i]), R(d->rl_jquat[4 * i + 1]), R(d->rl_jquat[4 * i + 2]), R(d->rl_jquat[4 * i + 3]));
+        c->axis[i] = V(R(d->rl_axis[3 * i]), R(d->rl_axis[3 * i + 1]), R(d->rl_axis[3 * i + 2]));
+        c->compos[i] = V(R(d->rl_com_pos[3 * i]), R(d->rl_com_pos[3 * i + 1]), R(d->rl_com_pos[3 * i + 2]));
+        c->comquat[i] = Q(R(d->rl_com_quat[4 * i]), R(d->rl_com_quat[4 * i + 1]), R(d->rl_com_quat[4 * i + 2]), R(d->rl_com_quat[4 * i + 3]));
+    }
+    c->base_p = V(R(d->robot_base[0]), R(d->robot_base[1]), R(d->robot_base[2]));
+    c->base_q = Q(R(d->robot_base[3]), R(d->robot_base[4]), R(d->robot_base[5]), R(d->robot_base[6]));
+    o->n = n_envs;
+    o->threads = 1;
+    o->state = (real *)calloc((size_t)n_envs * AVR_DR_STATE_WORDS, sizeof(real));
+    *out = o;
+    return 0;
+}
+
+EXPORT int avr_oracle_destroy(avr_oracle *o) {
+    if (!o) return -1;
+    free(o->state);
+    free(o);
+    return 0;
+}
+EXPORT const char *avr_oracle_last_error(avr_oracle *o) { return o ? o->err : "null"; }
+EXPORT int avr_oracle_set_threads(avr_oracle *o, int n) { if (o) o->threads = n > 0 ? n : 1; return 0; }
+EXPORT int avr_oracle_set_state(avr_oracle *o, const double *s) {
+    for (size_t i = 0; i < (size_t)o->n * AVR_DR_STATE_WORDS; i++) o->state[i] = R(s[i]);
+    return 0;
+}
+EXPORT int avr_oracle_get_state(avr_oracle *o, double *s) {
+    for (size_t i = 0; i < (size_t)o->n * AVR_DR_STATE_WORDS; i++) s[i] = o->state[i];
+    return 0;
+}
+EXPORT int avr_oracle_step(avr_oracle *o, const float *act, float *obs, float *rew, uint8_t *done, float *info) {
+#pragma omp parallel for num_threads(o->threads) schedule(dynamic, 1)
+    for (int e = 0; e < o->n; e++)
+        env_step(&o->c, o->state + (size_t)e * AVR_DR_STATE_WORDS, act + 7 * (size_t)e, 0, obs + (size_t)e * AVR_DR_OBS_DIM, rew + e, done + e,
+                 info + 2 * (size_t)e);
+    return 0;
+}
+/* the observation of the current state (no stepping): avr_settle(0) */
+EXPORT int avr_oracle_settle(avr_oracle *o, int frames, float *obs) {
+    if (frames != 0) { strcpy(o->err, "DressingJaco has no settle frames"); return -1; }
+    for (int e = 0; e < o->n; e++) {
+        float r, inf[2];
+        uint8_t d;
+        env_step(&o->c, o->state + (size_t)e * AVR_DR_STATE_WORDS, 0, 1, obs + (size_t)e * AVR_DR_OBS_DIM, &r, &d, inf);
+    }
+    return 0;
+}

@@ -19,7 +19,7 @@ def build():
 
 
 def _load(precision, task=0):
-    name = 'libavr_oracle%s%s.so' % ({1: '_scratch', 2: '_bedbath'}.get(task, ''), '' if precision == 'f64' else '_f32')
+    name = 'libavr_oracle%s%s.so' % ({1: '_scratch', 2: '_bedbath', 3: '_dressing'}.get(task, ''), '' if precision == 'f64' else '_f32')
     path = os.path.join(HERE, name)
     if not os.path.exists(path):
         build()
@@ -31,6 +31,12 @@ def _load(precision, task=0):
     lib.avr_oracle_get_state.argtypes = [vp, vp]
     lib.avr_oracle_settle.argtypes = [vp, C.c_int, vp]
     lib.avr_oracle_step.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.avr_oracle_set_threads.argtypes = [vp, C.c_int]
+    lib.avr_oracle_last_error.argtypes = [vp]
+    lib.avr_oracle_last_error.restype = C.c_char_p
+    lib.avr_oracle_state_words.restype = C.c_int
+    if task == 3:           # DressingJaco (oracle/avr_oracle_dressing.c): the step API only
+        return lib
     lib.avr_oracle_substep.argtypes = [vp, C.c_double]
     lib.avr_oracle_stats.argtypes = [vp, vp]
     lib.avr_oracle_narrowphase.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_double, vp]
@@ -67,7 +73,7 @@ class Oracle:
             raise RuntimeError('avr_oracle_create failed: %d' % rc)
         self.h = h
         self.words = self.lib.avr_oracle_state_words()
-        self.obs_dim = {1: 30, 2: 24}.get(self.task, 25)
+        self.obs_dim = {1: 30, 2: 24, 3: 24}.get(self.task, 25)
 
     def set_threads(self, n):
         self.lib.avr_oracle_set_threads(self.h, int(n))
