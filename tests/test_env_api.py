@@ -9,12 +9,14 @@ from avr import _abi as ABI
 
 
 def test_registry_has_every_reference_id():
-    # ids registered by assistive_gym/__init__.py (49 ids: 4 tasks x {PR2, Jaco} x 6 variants + HumanTesting)
-    assert len(E.REGISTRY) == 49
+    # ids registered by assistive_gym/__init__.py (49 ids: 4 tasks x {PR2, Jaco} x 6 variants + HumanTesting),
+    # plus BASELINE's DressingJaco-v0 (build-defined: the reference has no dressing task)
+    assert len(E.REGISTRY) == 50
+    assert E.REGISTRY['DressingJaco-v0'] == ('dressing', 'jaco', True)
     assert E.REGISTRY['FeedingJaco-v0'] == ('feeding', 'jaco', True)
     assert E.REGISTRY['ScratchItchPR2-v0'] == ('scratch_itch', 'pr2', True)
     assert E.REGISTRY['BedBathingPR2-v0'] == ('bed_bathing', 'pr2', True)
-    assert sum(v[2] for v in E.REGISTRY.values()) == 3
+    assert sum(v[2] for v in E.REGISTRY.values()) == 4
     for k in E.REGISTRY:
         assert re.match(r'^[A-Za-z0-9]+-v0$', k)
 
