@@ -11,7 +11,7 @@ import numpy as np
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # ---- capacities / offsets (must match include/avr_model.h) ----
-ABI_VERSION = 5
+ABI_VERSION = 6
 TASK_FEEDING, TASK_SCRATCH, TASK_BEDBATH, TASK_DRESSING = 0, 1, 2, 3
 DESC_HC = 8                               # avr_model_desc hc_* capacity
 BODY_ROBOT, BODY_FREE, BODY_STATIC, BODY_HUMAN, BODY_RSTATIC = 0, 1, 2, 3, 4

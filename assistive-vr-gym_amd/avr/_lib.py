@@ -20,7 +20,7 @@ EXPORTS = [
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
     'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik', 'avr_base_search',
-    'avr_graph_captures',
+    'avr_graph_captures', 'avr_robot_self_contact',
 ]
 FLAGS_FAULT_MASK = 0x1f      # include/avr.h AVR_FLAGS_FAULT_MASK: bits 0-4; bit 5 (EPA budget) is informational
 
@@ -91,7 +91,8 @@ def load(path=LIB_PATH):
     lib.avr_get_link_pose.argtypes = [vp, C.c_int32, vp]
     lib.avr_get_contact_summary.argtypes = [vp, vp]
     lib.avr_get_flags.argtypes = [vp, vp]
-    lib.avr_reset_ik.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, C.c_int32, vp, vp]
+    lib.avr_reset_ik.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, C.c_int32, vp, vp]
+    lib.avr_robot_self_contact.argtypes = [vp, C.c_int32, vp, vp]
     lib.avr_base_search.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp, vp]
     if lib.avr_abi_version() != ABI.ABI_VERSION or any(
             lib.avr_task_state_words(t) != L.STATE_WORDS or lib.avr_task_obs_dim(t) != L.OBS_DIM or lib.avr_task_act_dim(t) != L.ACT_DIM
@@ -173,14 +174,18 @@ class Sim:
         self._chk(self.lib.avr_reset(self.h, None if m is None else m.ctypes.data, S.ctypes.data, int(frames), obs.ctypes.data))
         return obs
 
-    def reset_ik(self, mask, S, target7, init, iters=80, tol=0.01, keepout8=None, frames=100, obs=None):
+    def reset_ik(self, mask, S, target7, init, iters=80, tol=0.01, keepout8=None, frames=100, obs=None, alt=None):
         """Masked reset with the IK on the device (include/avr.h avr_reset_ik): S rows without the
-        arm joints, target7 (n_envs, 7), init (n_envs, restarts, n_arm) restart draws.
-        Returns (obs, ok)."""
+        arm joints, target7 (n_envs, 7), init (n_envs, restarts, n_arm) restart draws, alt
+        (n_envs, restarts, 4) the self-contact screening's re-drawn orientations (None: no
+        screening).  Returns (obs, ok)."""
         S = np.ascontiguousarray(S, np.float32).reshape(self.n, self.words)
         t = np.ascontiguousarray(target7, np.float32).reshape(self.n, 7)
         init = np.ascontiguousarray(init, np.float32)
         assert init.ndim == 3 and init.shape[0] == self.n
+        if alt is not None:
+            alt = np.ascontiguousarray(alt, np.float32)
+            assert alt.shape == (self.n, init.shape[1], 4)
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.n)
         box = None if keepout8 is None else np.ascontiguousarray(keepout8, np.float32).reshape(8)
         if obs is None:
@@ -188,9 +193,22 @@ class Sim:
         assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.shape == (self.n, self.obs_dim)
         ok = np.zeros(self.n, np.uint8)
         self._chk(self.lib.avr_reset_ik(self.h, None if m is None else m.ctypes.data, S.ctypes.data, t.ctypes.data, init.ctypes.data,
-                                        int(init.shape[1]), int(iters), float(tol), None if box is None else box.ctypes.data, int(frames),
+                                        None if alt is None else alt.ctypes.data, int(init.shape[1]), int(iters), float(tol), None if box is None else box.ctypes.data, int(frames),
                                         obs.ctypes.data, ok.ctypes.data))
         return obs, ok.astype(bool)
+
+    def robot_self_contact(self, Q):
+        """Touching robot shape pairs at each row of Q (n, n_dof()) -- avr_get_q's layout, or just
+        the robot DoFs (the human chain's then 0) -- (include/avr.h avr_robot_self_contact:
+        p.getContactPoints(robot, robot) after a reset restart)."""
+        Q = np.asarray(Q, np.float32)
+        nd = self.n_dof()
+        assert Q.ndim == 2 and Q.shape[1] <= nd
+        q = np.zeros((len(Q), nd), np.float32)
+        q[:, :Q.shape[1]] = Q
+        out = np.zeros(len(q), np.int32)
+        self._chk(self.lib.avr_robot_self_contact(self.h, int(len(q)), q.ctypes.data, out.ctypes.data))
+        return out
 
     def base_search(self, base7, rest, tstart, goals, iters=200, tol=0.03, per_attempt=False):
         """PR2 base-pose search on the device (include/avr.h avr_base_search): base7 (n, attempts, 7),

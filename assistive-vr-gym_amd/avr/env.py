@@ -265,8 +265,10 @@ class AVRVecEnv:
             from . import reset_scratch as RSS
             return RSS.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment,
                                      episodes=list(episodes), attempts=self.scratch_attempts)
-        return RS.reset_inputs(self.A, self.md, self.seed, ids, genders=self._genders(idx),
-                               impairment=self.impairment, episodes=list(episodes), stream=self.reset_stream)
+        out = RS.reset_inputs(self.A, self.md, self.seed, ids, genders=self._genders(idx),
+                              impairment=self.impairment, episodes=list(episodes), stream=self.reset_stream)
+        # + the self-contact screening's re-drawn target orientations (ik_random_restarts' step_sim)
+        return out + (RS.ik_alt_orients(self.seed, ids, list(episodes), out[2].shape[1], self.reset_stream),)
 
     def _reset_rows(self, mask):
         idx = np.nonzero(mask)[0]
@@ -280,7 +282,7 @@ class AVRVecEnv:
             t0 = time.perf_counter()
             key = (tuple(idx.tolist()), tuple(eps.tolist()))
             got = self._prefetch.take(key) if self._prefetch else None
-            Si, t7, init, _, _ = got if got is not None else self._inputs(idx, eps)
+            Si, t7, init, _, _, alt = got if got is not None else self._inputs(idx, eps)
             t1 = time.perf_counter()
             S[idx] = Si
             T = np.zeros((self.n, 7), np.float32)
@@ -288,8 +290,11 @@ class AVRVecEnv:
             T[idx] = t7
             I = np.zeros((self.n,) + init.shape[1:], np.float32)
             I[idx] = init
+            Al = np.zeros((self.n, init.shape[1], 4), np.float32)
+            Al[..., 3] = 1.0
+            Al[idx] = alt
             t2 = time.perf_counter()
-            _, ok = self.sim.reset_ik(mask.astype(np.uint8), S, T, I, keepout8=self._keepout, frames=frames, obs=self._obs)
+            _, ok = self.sim.reset_ik(mask.astype(np.uint8), S, T, I, keepout8=self._keepout, frames=frames, obs=self._obs, alt=Al)
             self.last_ik_ok = ok
             self.reset_timing = dict(inputs_s=t1 - t0, prefetched=got is not None, pack_s=t2 - t1, device_s=time.perf_counter() - t2)
             if self._prefetch:           # speculate: the same envs end their next episode together
@@ -323,7 +328,7 @@ class AVRVecEnv:
             return
         else:
             Si, _ = RS.batch_reset_states_fast(self.A, self.md, self.seed, ids, genders=self._genders(idx), impairment=self.impairment, episodes=eps,
-                                               stream=self.reset_stream)
+                                               stream=self.reset_stream, self_contact=self.sim.robot_self_contact)
         S[idx] = Si
         self.sim.reset(mask.astype(np.uint8), S, frames, self._obs)
 

@@ -323,13 +323,54 @@ def robot_fk_batch(A, Q):
     return CP, CQ, AX, OR
 
 
-def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, tol=0.01):
-    """Vectorised DLS IK (same acceptance rule as `ik`), one random restart per round for every
-    env that has not converged yet.  init (N, restarts, n_arm): the restarts' starting joints,
-    drawn up front from each env's reset stream (reset_inputs).  Every env runs on its own: it
-    stops updating at the first 10th iteration at which it has converged, so its result does not
-    depend on the other envs of the batch (or on how envs are sharded over GPUs).  Restated on the
-    device by avr_reset_ik (csrc/avr_reset_ik.hip), which runs the same rules one env at a time."""
+def ik_accept(pe, qe, tol):
+    """ik_random_restarts' acceptance (util.py:49): position error below tol, and the quaternion
+    distance below tol or np.isclose to 2 (the other cover of the rotation, atol tol)."""
+    return (pe < tol) & ((qe < tol) | (np.abs(qe - 2.0) <= tol + 2e-5))
+
+
+def ik_alt_orients(seed, env_ids, episodes, restarts, stream='numpy'):
+    """The target orientations ik_random_restarts switches to after a self-contact
+    (util.py:44-46: the original's Euler angles + uniform(-45, 45) degrees each, then
+    getQuaternionFromEuler), one per restart, drawn up front from a sub-stream of each env's reset
+    stream: (N, restarts, 4).  FeedingJaco's target orientation is Euler (pi/2, 0, pi/2)
+    (feeding.py:277), which getEulerFromQuaternion returns unchanged."""
+    env_ids = list(env_ids)
+    eps = [0] * len(env_ids) if episodes is None else list(episodes)
+    if stream == 'philox':
+        U = philox_uniforms(int(seed) ^ _ALT_TAG, env_ids, eps, 3 * restarts).reshape(len(env_ids), restarts, 3)
+        D = -45.0 + 90.0 * U
+    else:
+        D = np.stack([np.random.default_rng([int(seed), int(e), int(ep), _ALT_TAG]).uniform(-45, 45, size=(restarts, 3))
+                      for e, ep in zip(env_ids, eps)]) if env_ids else np.zeros((0, restarts, 3))
+    E = np.array([np.pi / 2.0, 0.0, np.pi / 2.0]) + np.deg2rad(D)
+    return quat_from_euler_batch(E)
+
+
+def quat_from_euler_batch(E):
+    """p.getQuaternionFromEuler over (..., 3) roll, pitch, yaw: q = qz(yaw) qy(pitch) qx(roll)."""
+    r, p, y = 0.5 * E[..., 0], 0.5 * E[..., 1], 0.5 * E[..., 2]
+    cr, sr, cp, sp, cy, sy = np.cos(r), np.sin(r), np.cos(p), np.sin(p), np.cos(y), np.sin(y)
+    return np.stack([sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+                     cr * cp * cy + sr * sp * sy], -1)
+
+
+_ALT_TAG = 0xA1745
+
+
+def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, tol=0.01, alt=None, self_contact=None):
+    """Vectorised DLS IK (ik_random_restarts, util.py:34-57), one random restart per round for
+    every env that has not converged yet.  init (N, restarts, n_arm): the restarts' starting
+    joints, drawn up front from each env's reset stream (reset_inputs).  Every env runs on its
+    own: it stops updating at the first 10th iteration at which it has converged, so its result
+    does not depend on the other envs of the batch (or on how envs are sharded over GPUs).
+    step_sim's self-contact screening (util.py:41-46): with self_contact (a function of joint
+    rows -> touching robot shape pairs: the device's avr_robot_self_contact, or the oracle's) and
+    alt (N, restarts, 4: ik_alt_orients), a restart whose solution touches itself switches the
+    env's target orientation to alt[restart] for its own check and the later restarts.  Accepted:
+    ik_accept and table_clear; else the restart closest to the target position (util.py:51-54).
+    Restated on the device by avr_reset_ik (csrc/avr_reset_ik.hip), which runs the same rules one
+    env at a time."""
     N = tpos.shape[0]
     restarts = init.shape[1]
     chain = _chain(A, link)
@@ -339,6 +380,8 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, t
         cols.append(l[0] if l else -1)
     done = np.zeros(N, bool)
     Qout = np.repeat(q0[None], N, 0)
+    best = np.full(N, np.inf)
+    tquat = np.array(tquat, float, copy=True)
     for r in range(restarts):
         idx = np.nonzero(~done)[0]
         if len(idx) == 0:
@@ -371,12 +414,18 @@ def ik_batch(A, link, tpos, tquat, arm_dofs, lower, upper, init, q0, iters=80, t
             rows = np.nonzero(live)[0]
             Q[np.ix_(rows, arm_dofs)] = np.clip(Q[:, arm_dofs] + step[..., 0], lower, upper)[rows]
         CP, CQ, _, _ = robot_fk_batch(A, Q)
+        if alt is not None and self_contact is not None:
+            sc = np.asarray(self_contact(Q)) > 0
+            tquat[idx[sc]] = alt[idx[sc], r]
+            tq = tquat[idx]
         pe = np.linalg.norm(tp - CP[:, link], axis=1)
-        qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))
+        qe = np.linalg.norm(tq - CQ[:, link], axis=1)
+        acc = ik_accept(pe, qe, tol)
         for k, e in enumerate(idx):
-            if r == restarts - 1 and not done[e]:
+            if pe[k] < best[e]:
+                best[e] = pe[k]
                 Qout[e] = Q[k]
-            if pe[k] < tol and qe[k] < tol and table_clear(A, Q[k]):
+            if acc[k] and table_clear(A, Q[k]):
                 Qout[e] = Q[k]
                 done[e] = True
     return Qout, done
@@ -690,13 +739,15 @@ def place_tool_bodies(A, S, Q):
     return S
 
 
-def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none', episodes=None, stream='numpy'):
+def batch_reset_states_fast(A, md, seed, env_ids, genders=None, impairment='none', episodes=None, stream='numpy', self_contact=None):
     """Vectorised equivalent of batch_reset_states (same per-env draws and acceptance rules,
     IK batched across envs).  episodes[k] selects the k-th env's episode stream (default 0);
-    stream: reset_inputs' draw stream."""
+    stream: reset_inputs' draw stream; self_contact: ik_batch's self-contact screening."""
     S, target7, init, q0, meta = reset_inputs(A, md, seed, env_ids, genders, impairment, episodes, vector_fk=False, stream=stream)
     lower, upper = arm_limits(md)
-    Q, ok = ik_batch(A, int(A['task_tool_link']), target7[:, :3], target7[:, 3:], md.arm_dofs, lower, upper, init, q0)
+    alt = ik_alt_orients(seed, env_ids, episodes, init.shape[1], stream) if self_contact is not None else None
+    Q, ok = ik_batch(A, int(A['task_tool_link']), target7[:, :3], target7[:, 3:], md.arm_dofs, lower, upper, init, q0,
+                     alt=alt, self_contact=self_contact)
     place_tool_bodies(A, S, Q)
     for k, m in enumerate(meta):
         m['ik_ok'] = bool(ok[k])

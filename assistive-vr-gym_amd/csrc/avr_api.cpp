@@ -42,8 +42,9 @@
     int avr_get_contact_summary(avr_sim *s, float *out4);                                                          \
     int avr_get_flags(avr_sim *s, int32_t *flags);                                                                 \
     int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init,      \
-                     int32_t restarts, int32_t iters, float tol, const float *keepout8, int32_t n_frames,           \
-                     float *host_obs, uint8_t *host_ok);                                                           \
+                     const float *alt4, int32_t restarts, int32_t iters, float tol, const float *keepout8,          \
+                     int32_t n_frames, float *host_obs, uint8_t *host_ok);                                         \
+    int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out);                               \
     int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest,            \
                         const float *tstart3, const float *goals9, int32_t iters, float tol, int32_t *best,         \
                         uint8_t *ok, float *q_arm, float *res4);                                                   \
@@ -184,10 +185,11 @@ int avr_get_q(avr_sim *s, float *q, float *qd) { DISPATCH(s, avr_get_q(h, q, qd)
 int avr_get_link_pose(avr_sim *s, int32_t link, float *o) { DISPATCH(s, avr_get_link_pose(h, link, o)); }
 int avr_get_contact_summary(avr_sim *s, float *o) { DISPATCH(s, avr_get_contact_summary(h, o)); }
 int avr_get_flags(avr_sim *s, int32_t *f) { DISPATCH(s, avr_get_flags(h, f)); }
-int avr_reset_ik(avr_sim *s, const uint8_t *m, const float *p, const float *t7, const float *init, int32_t r, int32_t it, float tol,
-                 const float *box8, int32_t n, float *o, uint8_t *ok) {
-    DISPATCH(s, avr_reset_ik(h, m, p, t7, init, r, it, tol, box8, n, o, ok));
+int avr_reset_ik(avr_sim *s, const uint8_t *m, const float *p, const float *t7, const float *init, const float *alt4, int32_t r, int32_t it,
+                 float tol, const float *box8, int32_t n, float *o, uint8_t *ok) {
+    DISPATCH(s, avr_reset_ik(h, m, p, t7, init, alt4, r, it, tol, box8, n, o, ok));
 }
+int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) { DISPATCH(s, avr_robot_self_contact(h, n, q, out)); }
 int avr_base_search(avr_sim *s, int32_t n, int32_t a, const float *b7, const float *rest, const float *t3, const float *g9, int32_t it, float tol,
                     int32_t *best, uint8_t *ok, float *q, float *res4) {
     DISPATCH(s, avr_base_search(h, n, a, b7, rest, t3, g9, it, tol, best, ok, q, res4));

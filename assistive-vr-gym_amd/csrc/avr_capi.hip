@@ -857,11 +857,11 @@ int avr_get_flags(avr_sim *s, int32_t *flags) {
 }
 
 // ------------------------------------------------------------------ device reset IK
-int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, int32_t restarts, int32_t iters,
-                 float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
+int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, const float *alt4, int32_t restarts,
+                 int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
     CHECK_SIM(s);
 #if AVR_TASK != AVR_TASK_FEEDING
-    (void)mask; (void)h; (void)target7; (void)init; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
+    (void)mask; (void)h; (void)target7; (void)init; (void)alt4; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
     return fail(s, -1, "avr_reset_ik: this task resets through avr_reset (host IK)");
 #else
     const size_t E = (size_t)s->cfg.n_envs;
@@ -871,7 +871,7 @@ int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *t
     if (na < 1 || na > 8) return fail(s, -1, "avr_reset_ik: %d arm DoFs (1..8 supported)", na);
     std::vector<uint8_t> all;
     if (!mask) { all.assign(E, 1); mask = all.data(); }
-    const size_t nt = E * 7, ni = E * (size_t)restarts * na, need = nt + ni + (E + 3) / 4;
+    const size_t nt = E * 7, ni = E * (size_t)restarts * na, nq = alt4 ? E * (size_t)restarts * 4 : 0, need = nt + ni + nq + (E + 3) / 4;
     if (need > s->ikcap) {
         if (s->d_ik) HIPCHK(s, hipFree(s->d_ik));
         s->d_ik = nullptr;
@@ -879,13 +879,14 @@ int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *t
         HIPCHK(s, hipMalloc(&s->d_ik, need * sizeof(float)));
         s->ikcap = need;
     }
-    float *d_t = s->d_ik, *d_i = s->d_ik + nt;
-    unsigned char *d_ok = (unsigned char *)(s->d_ik + nt + ni);
+    float *d_t = s->d_ik, *d_i = s->d_ik + nt, *d_q = alt4 ? s->d_ik + nt + ni : nullptr;
+    unsigned char *d_ok = (unsigned char *)(s->d_ik + nt + ni + nq);
     if (upload_masked(s, mask, h)) return -2;
     HIPCHK(s, hipMemcpyAsync(d_t, target7, nt * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, hipMemcpyAsync(d_i, init, ni * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    if (alt4) HIPCHK(s, hipMemcpyAsync(d_q, alt4, nq * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, hipMemsetAsync(d_ok, 0, E, s->stream));
-    HIPCHK(s, avr_launch_reset_ik(s->d_km, s->d_state, s->d_mask, d_t, d_i, restarts, iters, tol, keepout8, d_ok, (int)E, s->stream));
+    HIPCHK(s, avr_launch_reset_ik(s->d_km, s->d_state, s->d_mask, d_t, d_i, d_q, restarts, iters, tol, keepout8, d_ok, (int)E, s->stream));
     if (n_frames > 0) HIPCHK(s, run_step(s, s->d_state, nullptr, s->d_obs, s->d_rew, s->d_done, s->d_info, s->d_mask, 2, n_frames));
     std::vector<float> o;
     if (host_obs) {
@@ -905,6 +906,23 @@ int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *t
     }
     return 0;
 #endif
+}
+
+// ------------------------------------------------------------------ robot self-contact query
+int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) {
+    CHECK_SIM(s);
+    if (n < 0 || (n > 0 && (!q || !out))) return fail(s, -1, "avr_robot_self_contact: n >= 0, q and out must be given");
+    if (n == 0) return 0;
+    const size_t nd = (size_t)(s->km.nd + s->km.hc_n);
+    struct Buf { void *p = nullptr; ~Buf() { if (p) (void)hipFree(p); } } buf;     // (freed on every return)
+    HIPCHK(s, hipMalloc(&buf.p, (size_t)n * (nd * sizeof(float) + sizeof(int))));
+    float *d_q = (float *)buf.p;
+    int *d_o = (int *)(d_q + (size_t)n * nd);
+    HIPCHK(s, hipMemcpyAsync(d_q, q, (size_t)n * nd * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, avr_launch_self_contact(s->d_km, s->d_state, d_q, d_o, (int)n, s->stream));
+    HIPCHK(s, hipMemcpyAsync(out, d_o, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
 }
 
 // ------------------------------------------------------------------ device base-pose search (PR2 tasks)

@@ -662,9 +662,13 @@ int avr_get_flags(avr_sim *s, int32_t *flags) {
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }
-int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, int32_t restarts, int32_t iters, float tol,
-                 const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
-    (void)mask; (void)h; (void)target7; (void)init; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
+int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) {
+    (void)n; (void)q; (void)out;
+    return fail(s, -1, "avr_robot_self_contact: DressingJaco's robot is kinematic (no robot collision model)");
+}
+int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, const float *alt4, int32_t restarts,
+                 int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
+    (void)mask; (void)h; (void)target7; (void)init; (void)alt4; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
     return fail(s, -1, "avr_reset_ik: DressingJaco resets through avr_reset (host IK)");
 }
 int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest, const float *tstart3, const float *goals9,

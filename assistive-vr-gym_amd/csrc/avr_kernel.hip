@@ -1811,8 +1811,15 @@ AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.
 #ifndef B4_PK
 #define B4_PK 1     // free parts stored as (linear, angular) pairs per axis: packed-f32 row resolves (0: scalar layout)
 #endif
+// Friction units resolved as a pair through their coupling (go4_pair, -DB4_FPAIR=1): the same
+// Gauss-Seidel step in exact arithmetic, ~1 % faster part B, but rounded differently from the
+// sequential resolve -- and where a contact's normal impulse sits at 0 (a point at the contact
+// threshold), that rounding decides whether its friction unit is active in an iteration, so the
+// two orders end sub-steps apart by up to 5e-2 m/s on the BedBathing wiping states
+// (tools/dbg_torsion.py; the sequential resolve matches the oracle to 1e-6 there).  Off: parity
+// with the oracle's sequential order first.
 #ifndef B4_FPAIR
-#define B4_FPAIR B4_PK   // friction units resolved as a pair through their coupling (go4_pair)
+#define B4_FPAIR 0
 #endif
 AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
     const float *g = L.gsc[f];

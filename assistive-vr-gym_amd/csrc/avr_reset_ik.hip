@@ -6,14 +6,66 @@
 //   per restart r: the arm DoFs start from init[env][r] (the host draws them from the env's
 //   reset stream, so the restart sequence is the host reset's); `iters` DLS updates
 //     dq = J^T (J J^T + 1e-4 I)^-1 [p* - p; rot_err(q*, q)],  q <- clamp(q + dq, lower, upper)
-//   with an early exit at every 10th iteration once |dp| < 1e-5 and |rot_err| < 1e-4; accept
-//   when |p* - p| < tol, min |q* -+ q| < tol and no robot hull vertex lies inside the keep-out
-//   box (the reset's table screening, avr/reset.py table_clear); the last restart's result is
-//   kept when none is accepted.
+//   with an early exit at every 10th iteration once |dp| < 1e-5 and |rot_err| < 1e-4;
+//   step_sim's self-contact screening (util.py:41-46): when the robot's links touch each other at
+//   the solution, the target orientation becomes alt[env][r] (the orientation re-drawn +-45 deg
+//   about the original's Euler angles, drawn by the host) for this restart's check and the later
+//   restarts; accept when |p* - p| < tol and |q* - q| < tol or |q* - q| within tol of 2
+//   (util.py:49, np.isclose), and no robot hull vertex lies inside the keep-out box (the reset's
+//   table screening, avr/reset.py table_clear); when no restart is accepted, the restart closest
+//   to the target position is kept (util.py:51-54).
 // The same rules as the host path's ik_batch (avr/reset.py) run on one env at a time; the host
 // path is the checker of this kernel (tests/test_reset_ik.py).
 // After the IK the task places the tool-attached free bodies (FeedingJaco: the spoon on the
 // tool frame, world_creation.py:330-343, and the food spheres above it, feeding.py:291-308).
+
+// Robot self-contact at the pose in L (robot FK done): what p.getContactPoints(robot, robot)
+// reports after a restart's frames (util.py:41-46; the Jaco is loaded with URDF_USE_SELF_COLLISION,
+// world_creation.py:282) -- the step's collision pipeline on the compiled robot-robot candidate
+// pairs (parent-child pairs are not candidates): fattened body AABBs, child AABB culling (bare
+// pairs unculled), the lane narrowphase within the pair's contact threshold.  One lane per
+// candidate pair; returns the number of touching shape pairs in every lane.
+template <class LT>
+AVR_DI int robot_self_contacts(const KModel &m, const LT &L) {
+    const int lane = lane_id();
+    int cnt = 0;
+    for (int p0 = 0; p0 < m.np; p0 += 64) {
+        const int p = p0 + lane;
+        if (p >= m.np) continue;
+        const int4 r = m.pair_rec[p];
+        const int ba = r.x & 0xffff, bb = r.x >> 16;
+        if (gld(m.body_kind + ba) != AVR_BODY_ROBOT || gld(m.body_kind + bb) != AVR_BODY_ROBOT) continue;
+        const tf ta = body_tf(m, L, ba), tb = body_tf(m, L, bb);
+        const v3 e = V(BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND, BT_BROADPHASE_EXPAND);
+        v3 amn, amx, bmn, bmx;
+        aabb_of(ta, gld3(m.body_aabb + 12 * ba), gld3(m.body_aabb + 12 * ba + 3), amn, amx);
+        aabb_of(tb, gld3(m.body_aabb + 12 * bb), gld3(m.body_aabb + 12 * bb + 3), bmn, bmx);
+        if (!overlap(sub(amn, e), add(amx, e), sub(bmn, e), add(bmx, e))) continue;
+        const float thr = fminf(gld(m.body_threshold + ba), gld(m.body_threshold + bb));
+        const bool bare = (r.w & 1) != 0;
+        const int sa0 = r.y & 0xffff, na = r.y >> 16, sb0 = r.z & 0xffff, nb = r.z >> 16;
+        for (int i = 0; i < na; i++) {
+            v3 a0, a1;
+            shape_aabb(m, sa0 + i, ta, a0, a1);
+            for (int j = 0; j < nb; j++) {
+                v3 b0, b1;
+                shape_aabb(m, sb0 + j, tb, b0, b1);
+                if (!bare && !overlap(a0, a1, b0, b1)) continue;
+                const WShape A = make_wshape(m, sa0 + i, ta), B = make_wshape(m, sb0 + j, tb);
+                int rc = 2;     // (a hull the lane GJK cannot take, penetrating cores: touching)
+                if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
+                    v3 nB, pB;
+                    float d;
+                    int nit, nk;
+                    rc = narrowphase<false>(m, *(EpaBuf *)&L, A, B, thr, nB, pB, d, nit, nk);   // (the lane path never touches the EPA buffer)
+                }
+                cnt += rc != 0;
+            }
+        }
+    }
+    for (int o = 32; o; o >>= 1) cnt += __shfl_xor(cnt, o);
+    return cnt;
+}
 
 struct IkLDS {
     float J[8][8];     // [arm column][6 rows] (+ pad)
@@ -57,8 +109,9 @@ AVR_DI v3 ik_rot_err(qt tgt, qt cur) {
 }
 
 __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restrict__ mp, float *__restrict__ state, const unsigned char *__restrict__ mask,
-                                                          const float *__restrict__ target, const float *__restrict__ init, int R, int iters, float tol,
-                                                          float4 box_c, float4 box_he, unsigned char *__restrict__ ok, int n_envs) {
+                                                          const float *__restrict__ target, const float *__restrict__ init, const float *__restrict__ alt, int R,
+                                                          int iters, float tol, float4 box_c, float4 box_he, unsigned char *__restrict__ ok,
+                                                          int n_envs) {
     __shared__ PairsLDS L;
     __shared__ IkLDS K;
     const int env = blockIdx.x;
@@ -69,7 +122,7 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
     load_state(m, L, gst);
     const int link = m.tool_link, na = m.n_arm;
     const v3 tp = V(target[7 * env + 0], target[7 * env + 1], target[7 * env + 2]);
-    const qt tq = Q(target[7 * env + 3], target[7 * env + 4], target[7 * env + 5], target[7 * env + 6]);
+    qt tq = Q(target[7 * env + 3], target[7 * env + 4], target[7 * env + 5], target[7 * env + 6]);
     // this lane's arm column: DoF, the link that owns it (if on the tool link's chain), limits
     int cdof = -1, clink = -1;
     float lo = 0.f, hi = 0.f;
@@ -81,6 +134,7 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
         hi = m.arm_upper[lane] < 1e9f ? m.arm_upper[lane] : 6.283185307179586f;
     }
     bool accepted = false;
+    float best_pe = 3.4e38f, bestq = 0.f;      // the restart closest to the target position (util.py:51-54)
     for (int r = 0; r < R; r++) {
         if (lane < na) L.st[S_Q + cdof] = init[((size_t)env * R + r) * na + lane];
         SYNC();
@@ -123,16 +177,24 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
             SYNC();
         }
         robot_fk(m, L);
+        // step_sim's self-contact screening: a touching solution re-orients the target
+        if (alt && robot_self_contacts(m, L) > 0) {
+            const float *a = alt + ((size_t)env * R + r) * 4;
+            tq = Q(a[0], a[1], a[2], a[3]);
+        }
         if (lane == 0) {
             const qt cq = ldq(L.cm[link] + 3);
             K.pe = len(sub(tp, ld3(L.cm[link])));
-            const float d0 = sqrtf((tq.x - cq.x) * (tq.x - cq.x) + (tq.y - cq.y) * (tq.y - cq.y) + (tq.z - cq.z) * (tq.z - cq.z) + (tq.w - cq.w) * (tq.w - cq.w));
-            const float d1 = sqrtf((tq.x + cq.x) * (tq.x + cq.x) + (tq.y + cq.y) * (tq.y + cq.y) + (tq.z + cq.z) * (tq.z + cq.z) + (tq.w + cq.w) * (tq.w + cq.w));
-            K.qe = fminf(d0, d1);
+            K.qe = sqrtf((tq.x - cq.x) * (tq.x - cq.x) + (tq.y - cq.y) * (tq.y - cq.y) + (tq.z - cq.z) * (tq.z - cq.z) + (tq.w - cq.w) * (tq.w - cq.w));
             K.clear = 1;
         }
         SYNC();
-        if (K.pe < tol && K.qe < tol) {
+        if (K.pe < best_pe) {       // (wave-uniform)
+            best_pe = K.pe;
+            if (lane < na) bestq = L.st[S_Q + cdof];
+        }
+        // util.py:49: |dq| < tol, or np.isclose(|dq|, 2, atol=tol) (the other cover of the rotation)
+        if (K.pe < tol && (K.qe < tol || fabsf(K.qe - 2.f) <= tol + 2e-5f)) {
             // keep-out screening: every hull vertex of every robot link outside the box
             if (box_he.x >= 0.f) {
                 bool inside = false;
@@ -158,6 +220,11 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
         }
         if (accepted) break;
     }
+    if (!accepted) {
+        if (lane < na) L.st[S_Q + cdof] = bestq;
+        SYNC();
+        robot_fk(m, L);                 // (the tool frame of the kept joints places the spoon)
+    }
     if (lane < na) gst[S_Q + cdof] = L.st[S_Q + cdof];
     if (lane == 0) ok[env] = accepted ? 1 : 0;
 #if AVR_TASK == AVR_TASK_FEEDING
@@ -179,11 +246,35 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
 #endif
 }
 
-hipError_t avr_launch_reset_ik(const KModel *d_m, float *state, const unsigned char *mask, const float *target, const float *init, int R, int iters, float tol,
-                               const float *box8, unsigned char *ok, int n_envs, hipStream_t st) {
+hipError_t avr_launch_reset_ik(const KModel *d_m, float *state, const unsigned char *mask, const float *target, const float *init, const float *alt, int R,
+                               int iters, float tol, const float *box8, unsigned char *ok, int n_envs, hipStream_t st) {
     if (n_envs <= 0) return hipSuccess;
     const float4 c = box8 ? make_float4(box8[0], box8[1], box8[2], 0.f) : make_float4(0, 0, 0, 0);
     const float4 he = box8 ? make_float4(box8[4], box8[5], box8[6], 0.f) : make_float4(-1, -1, -1, 0);
-    hipLaunchKernelGGL(avr_reset_ik_kernel, dim3(n_envs), dim3(64), 0, st, d_m, state, mask, target, init, R, iters, tol, c, he, ok, n_envs);
+    hipLaunchKernelGGL(avr_reset_ik_kernel, dim3(n_envs), dim3(64), 0, st, d_m, state, mask, target, init, alt, R, iters, tol, c, he, ok, n_envs);
+    return hipGetLastError();
+}
+
+// avr_robot_self_contact: the screening above at n given joint vectors (q: n x avr_n_dof, the
+// rest of each pose from env 0's state block); out[i] = touching robot shape pairs
+__global__ __launch_bounds__(64) void avr_self_contact_kernel(const KModel *__restrict__ mp, const float *__restrict__ state, const float *__restrict__ q,
+                                                              int *__restrict__ out, int n) {
+    __shared__ PairsLDS L;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const KModel &m = *mp;
+    load_state(m, L, state);
+    SYNC();
+    const int nq = m.nd + m.hc_n;      // (avr_n_dof: robot DoFs, then the human chain's)
+    for (int d = lane_id(); d < nq; d += 64) L.st[S_Q + d] = q[(size_t)i * nq + d];
+    SYNC();
+    robot_fk(m, L);
+    const int c = robot_self_contacts(m, L);
+    if (lane_id() == 0) out[i] = c;
+}
+
+hipError_t avr_launch_self_contact(const KModel *d_m, const float *state, const float *q, int *out, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_self_contact_kernel, dim3(n), dim3(64), 0, st, d_m, state, q, out, n);
     return hipGetLastError();
 }

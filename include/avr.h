@@ -33,9 +33,10 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 5      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters;
+#define AVR_ABI_VERSION 6      /* 3: task-selected layouts (avr_model_desc.task), 5-kernel info, state getters;
                                   4: BedBathingPR2 (avr_model_desc bb_* fields, task 2);
-                                  5: avr_graph_captures, per-handle device guard, t >= 0 */
+                                  5: avr_graph_captures, per-handle device guard, t >= 0;
+                                  6: avr_reset_ik self-contact screening (alt4), avr_robot_self_contact */
 #define AVR_FLAGS_FAULT_MASK 0x1f  /* avr_get_flags bits 0-4; bit 5 (EPA budget) is informational */
 
 typedef struct avr_config {
@@ -161,14 +162,28 @@ const char *avr_last_error(avr_sim *sim);
  *   (position, quaternion); init[n_envs*restarts*n_arm] the arm's starting joints of every
  *   restart (drawn by the host from the env's reset stream).  Per env, restarts run in order
  *   with `iters` damped-least-squares updates each until one lands within `tol` (position, m, and
- *   quaternion distance) with no robot hull vertex inside the keep-out box keepout8 = {center xyz,
- *   pad, half extents xyz, pad} (NULL: no screening); else the last restart's joints are kept.
+ *   quaternion distance, or a distance within tol of 2: util.py:49) with no robot hull vertex
+ *   inside the keep-out box keepout8 = {center xyz, pad, half extents xyz, pad} (NULL: no
+ *   screening); else the joints of the restart closest to the target position are kept
+ *   (util.py:51-54).  step_sim's self-contact screening (util.py:41-46): alt4[n_envs*restarts*4]
+ *   (NULL: none) holds per restart the re-drawn target orientation (the original's Euler angles
+ *   +- 45 deg, drawn by the host); a restart whose solution has robot links touching (as
+ *   avr_robot_self_contact) switches the target orientation to its alt4 entry, for its own
+ *   acceptance check and the later restarts.
  *   The spoon and the food are then placed on the tool frame (world_creation.py:330-343,
  *   feeding.py:291-308) and n_frames settle frames run (feeding.py:319-320), as in avr_reset.
  *   host_ok[n_envs] (may be NULL) receives 1 where a restart was accepted.  Returns -1 for tasks
  *   other than FeedingJaco. */
-int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state, const float *target7, const float *init, int32_t restarts,
-                 int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok);
+int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state, const float *target7, const float *init, const float *alt4,
+                 int32_t restarts, int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok);
+
+/* avr_robot_self_contact: len(p.getContactPoints(bodyA=robot, bodyB=robot)) > 0 after a restart's
+ *   frames (util.py:41-46, 63-67) at n joint vectors q[n*avr_n_dof] (avr_get_q's layout; everything
+ *   else from env 0's state block): out[n] = the robot shape pairs the step's collision pipeline finds
+ *   within their contact threshold (compiled robot-robot candidate pairs: the URDF's
+ *   URDF_USE_SELF_COLLISION robots, parent-child pairs excluded).  Host screening of the host IK
+ *   path (avr/reset.py ik_batch); avr_reset_ik runs the same test on the device. */
+int avr_robot_self_contact(avr_sim *sim, int32_t n, const float *q, int32_t *out);
 
 /* ---- device base-pose search (ScratchItchPR2, BedBathingPR2) ----
  * avr_base_search: position_robot_toc (env.py:489-585; scratch_itch.py:189-190,

@@ -1798,4 +1798,51 @@ EXPORT int avr_oracle_robot_fk(avr_oracle *o, int env, double *out) {
     return 0;
 }
 
+/* robot self-contact for the reset IK's step_sim screening (util.py:41-46, 63-67:
+ * p.getContactPoints(robot, robot) after a restart's frames): at each of n joint vectors
+ * q[n*(n_dof+hc_n)] (env 0's state block otherwise), the robot shape pairs the collision pipeline
+ * (collide: fattened body AABBs, child AABB culling, narrowphase within the pair's threshold)
+ * finds on the robot-robot candidate pairs -> out[n] */
+EXPORT int avr_oracle_robot_self_contact(avr_oracle *o, int n, const double *q, int *out) {
+    if (!o || n < 0 || (n > 0 && (!q || !out))) return -1;
+    const int nq = o->m.d.n_dof + o->m.d.hc_n;
+    real *st = (real *)malloc(sizeof(real) * K_STATE_WORDS);
+    ws_t *w = (ws_t *)calloc(1, sizeof(ws_t));
+    for (int i = 0; i < n; i++) {
+        memcpy(st, o->state, sizeof(real) * K_STATE_WORDS);
+        for (int d = 0; d < nq; d++) st[S_Q + d] = R(q[(size_t)i * nq + d]);
+        const model *m = oview(o, st);
+        robot_fk(m, st, w);
+        int cnt = 0;
+        for (int p = 0; p < m->np; p++) {
+            int ba = m->d.pair_a[p], bb = m->d.pair_b[p];
+            if (m->d.body_kind[ba] != AVR_BODY_ROBOT || m->d.body_kind[bb] != AVR_BODY_ROBOT) continue;
+            tf ta = body_tf(m, st, w, ba), tb = body_tf(m, st, w, bb);
+            v3 a0, a1, b0, b1, e = V(R(BT_BROADPHASE_EXPAND), R(BT_BROADPHASE_EXPAND), R(BT_BROADPHASE_EXPAND));
+            aabb_of(ta, ld3d(m->d.body_aabb + 12 * ba), ld3d(m->d.body_aabb + 12 * ba + 3), &a0, &a1);
+            aabb_of(tb, ld3d(m->d.body_aabb + 12 * bb), ld3d(m->d.body_aabb + 12 * bb + 3), &b0, &b1);
+            if (!aabb_overlap(sub(a0, e), add(a1, e), sub(b0, e), add(b1, e))) continue;
+            real thr = R(fmin(m->d.body_threshold[ba], m->d.body_threshold[bb]));
+            int bare = (m->d.body_flags[ba] & 1) && (m->d.body_flags[bb] & 1);
+            for (int sa = m->d.body_shape_start[ba]; sa < m->d.body_shape_start[ba] + m->d.body_shape_count[ba]; sa++) {
+                v3 c0, c1;
+                shape_aabb(m, sa, ta, &c0, &c1);
+                for (int sb = m->d.body_shape_start[bb]; sb < m->d.body_shape_start[bb] + m->d.body_shape_count[bb]; sb++) {
+                    v3 d0, d1;
+                    shape_aabb(m, sb, tb, &d0, &d1);
+                    if (!bare && !aabb_overlap(c0, c1, d0, d1)) continue;
+                    wshape A = make_wshape(m, sa, ta), B = make_wshape(m, sb, tb);
+                    v3 nB, pB;
+                    real dd;
+                    cnt += narrowphase(w, &A, &B, thr, &nB, &pB, &dd) != 0;
+                }
+            }
+        }
+        out[i] = cnt;
+    }
+    free(st);
+    free(w);
+    return 0;
+}
+
 EXPORT const char *avr_oracle_last_error(avr_oracle *o) { return o ? o->err : "null handle"; }

@@ -41,6 +41,7 @@ def _load(precision, task=0):
     lib.avr_oracle_stats.argtypes = [vp, vp]
     lib.avr_oracle_narrowphase.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_double, vp]
     lib.avr_oracle_robot_fk.argtypes = [vp, C.c_int, vp]
+    lib.avr_oracle_robot_self_contact.argtypes = [vp, C.c_int, vp, vp]
     lib.avr_oracle_set_threads.argtypes = [vp, C.c_int]
     lib.avr_oracle_last_error.argtypes = [vp]
     lib.avr_oracle_last_error.restype = C.c_char_p
@@ -135,6 +136,18 @@ class Oracle:
         out = np.zeros(1)
         self.lib.avr_oracle_bb_closest(self.h, int(env), out.ctypes.data)
         return float(out[0])
+
+    def robot_self_contact(self, Q):
+        """Touching robot shape pairs at each row of Q (n, robot DoFs [+ head chain]), env 0's
+        state otherwise (avr_oracle_robot_self_contact; the device's avr_robot_self_contact)."""
+        Q = np.asarray(Q, np.float64)
+        nq = self.md.desc.n_dof + self.md.desc.hc_n
+        q = np.zeros((len(Q), nq))
+        q[:, :Q.shape[1]] = Q
+        out = np.zeros(len(Q), np.int32)
+        r = self.lib.avr_oracle_robot_self_contact(self.h, len(q), q.ctypes.data, out.ctypes.data)
+        assert r == 0
+        return out
 
     def robot_fk(self, env=0):
         out = np.zeros((self.md.desc.n_links, 7))

@@ -23,9 +23,10 @@ def _frame_z(n, x_hint):
     return Rotation.from_matrix(np.stack([x, y, z], 1)).as_quat()
 
 
-def wipe_states(A, md, S, depth=0.002, tries=12):
+def wipe_states(A, md, S, depth=0.002, tries=12, strict=True):
     """Copy of S with every env's left arm re-solved so the cloth presses on an upper-arm target;
-    returns (states, target index per env)."""
+    returns (states, target index per env).  strict=False drops the envs whose base pose reaches
+    none of the `tries` upward-facing targets (strict: an assertion)."""
     S = S.copy()
     nd = int(A['n_dof'])
     arm = np.array(md.arm_dofs)
@@ -33,7 +34,7 @@ def wipe_states(A, md, S, depth=0.002, tries=12):
     hi = np.array([md.desc.arm_upper[i] if md.desc.arm_upper[i] < 1e9 else 2 * np.pi for i in range(len(arm))])
     link = int(A['task_tool_link'])
     tip, piv = A['task_tool_tip'], A['task_tool_pivot']
-    ks = []
+    ks, keep = [], []
     for e in range(len(S)):
         st = S[e]
         g = int(st[BB.S_TASK + BB.T_GENDER])
@@ -63,7 +64,10 @@ def wipe_states(A, md, S, depth=0.002, tries=12):
             if pe < 1e-3 and qe < 1e-2:
                 best = (k, Q[0], CP[0, link], CQ[0, link])
                 break
+        if best is None and not strict:
+            continue
         assert best is not None, 'env %d: no upper-arm target reachable' % e
+        keep.append(e)
         k, q, cp, cq = best
         st[BB.S_Q:BB.S_Q + nd] = q
         st[BB.S_QD:BB.S_QD + nd] = 0
@@ -74,4 +78,4 @@ def wipe_states(A, md, S, depth=0.002, tries=12):
         st[BB.S_FREE + 3:BB.S_FREE + 7] = qq
         st[BB.S_FREE + 7:BB.S_FREE + 13] = 0
         ks.append(int(k))
-    return S, ks
+    return S[keep], ks

@@ -509,25 +509,36 @@ def test_coop_capped_env_drift_vs_oracle(lib_and_scene):
     manifold points) and on the fp64 and fp32 oracles (every pair solved each sub-step).  The
     capped env's arm stays within the stated bound of the uncapped oracle,
     and the budget's deviation is of the size of the fp32-vs-fp64 chaos of the same contact state."""
-    from avr import _lib
+    from avr import _abi as ABI, _lib
     from oracle.oracle import Oracle
     A, md = lib_and_scene
     bad = np.load(os.path.join(HERE, 'feeding_arm_in_wheelchair.npy')).astype(np.float32)
-    sim = make_sim(md, 1)
-    sim.set_state(bad)
+    sim = make_sim(md, 2)
+    # env 1: the same state with the budget's persistence counter (T_COOPN) started far below its
+    # threshold, so that it never engages: every penetrating pair solved, as the oracle does
+    S2 = np.repeat(bad.reshape(1, -1), 2, 0)
+    S2[1, ABI.S_TASK + ABI.T_COOPN] = -1e9
+    sim.set_state(S2)
     o64, o32 = Oracle(md, 1, 'f64'), Oracle(md, 1, 'f32')
     o64.set_state(bad.astype(np.float64)); o32.set_state(bad.astype(np.float64))
-    dq_cap = dq_32 = 0.0
+    dq_cap = dq_full = dq_32 = 0.0
     capped = False
     for t in range(20):
         a = _lib.random_actions(1001, np.arange(1), t)
-        sim.step(a); o64.step(a); o32.step(a)
+        sim.step(np.repeat(a, 2, 0)); o64.step(a); o32.step(a)
         G, C, C32 = sim.get_state(), o64.get_state(), o32.get_state()
         dq_cap = max(dq_cap, float(np.abs(G[0, :7] - C[0, :7]).max()))
+        dq_full = max(dq_full, float(np.abs(G[1, :7] - C[0, :7]).max()))
         dq_32 = max(dq_32, float(np.abs(C32[0, :7] - C[0, :7]).max()))
-        capped = capped or bool(sim.get_flags()[0] & 32)
+        fl = sim.get_flags()
+        capped = capped or bool(fl[0] & 32)
+        assert not fl[1] & 32
     sim.close()
-    print('capped env: max |dq| GPU(capped) vs fp64 oracle %.3g rad, fp32 vs fp64 oracle %.3g rad' % (dq_cap, dq_32))
+    print('capped env: max |dq| vs the fp64 oracle over 20 steps: GPU with the EPA budget %.3g rad, GPU without it %.3g rad, '
+          'fp32 oracle %.3g rad' % (dq_cap, dq_full, dq_32))
     assert capped
     assert np.all(np.isfinite(G))
-    assert dq_cap < 0.05, dq_cap
+    # The arm driven into the wheelchair's hulls is chaotic: fp32 rounding alone (the fp32 oracle,
+    # the unbudgeted GPU run) moves it by tenths of a radian in 20 steps.  The stated bound
+    # (DESIGN.md section 8): the budgeted env stays within 3x the larger unbudgeted fp32 deviation.
+    assert dq_cap <= 3.0 * max(dq_full, dq_32), (dq_cap, dq_full, dq_32)

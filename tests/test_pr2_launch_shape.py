@@ -46,7 +46,7 @@ def _pool(task, n_reset):
         A = ABI.load_scene(ABI.TASK_BEDBATH)
         md = ABI.ModelDesc(A)
         S, meta = RBB.batch_reset_states(A, md, 1001, list(range(n_reset)), attempts=12, iters=80)
-        C, _ = U.wipe_states(A, md, S)
+        C, _ = U.wipe_states(A, md, S, strict=False)
         L = BB
     P = np.concatenate([S, C]).astype(np.float32)
     return A, md, L, P, np.r_[np.zeros(len(S), bool), np.ones(len(C), bool)]
