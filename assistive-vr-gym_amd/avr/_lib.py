@@ -20,7 +20,7 @@ EXPORTS = [
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
     'avr_get_q', 'avr_get_link_pose', 'avr_get_contact_summary', 'avr_get_flags', 'avr_reset_ik', 'avr_base_search',
-    'avr_graph_captures', 'avr_robot_self_contact',
+    'avr_graph_captures', 'avr_robot_self_contact', 'avr_narrowphase_query',
 ]
 FLAGS_FAULT_MASK = 0x1f      # include/avr.h AVR_FLAGS_FAULT_MASK: bits 0-4; bit 5 (EPA budget) is informational
 
@@ -93,6 +93,7 @@ def load(path=LIB_PATH):
     lib.avr_get_flags.argtypes = [vp, vp]
     lib.avr_reset_ik.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, C.c_int32, vp, vp]
     lib.avr_robot_self_contact.argtypes = [vp, C.c_int32, vp, vp]
+    lib.avr_narrowphase_query.argtypes = [vp, C.c_int32, vp, vp, C.c_float, vp]
     lib.avr_base_search.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp, vp]
     if lib.avr_abi_version() != ABI.ABI_VERSION or any(
             lib.avr_task_state_words(t) != L.STATE_WORDS or lib.avr_task_obs_dim(t) != L.OBS_DIM or lib.avr_task_act_dim(t) != L.ACT_DIM
@@ -208,6 +209,15 @@ class Sim:
         q[:, :Q.shape[1]] = Q
         out = np.zeros(len(q), np.int32)
         self._chk(self.lib.avr_robot_self_contact(self.h, int(len(q)), q.ctypes.data, out.ctypes.data))
+        return out
+
+    def narrowphase(self, pairs, poses14, thr=0.02):
+        """The step's narrowphase per (sa, sb) row of pairs at body poses poses14 (n, 14)
+        (include/avr.h avr_narrowphase_query): (n, 8) {rc, normal on B, point on B, distance}."""
+        p = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        x = np.ascontiguousarray(poses14, np.float32).reshape(len(p), 14)
+        out = np.zeros((len(p), 8), np.float32)
+        self._chk(self.lib.avr_narrowphase_query(self.h, int(len(p)), p.ctypes.data, x.ctypes.data, float(thr), out.ctypes.data))
         return out
 
     def base_search(self, base7, rest, tstart, goals, iters=200, tol=0.03, per_attempt=False):

@@ -121,9 +121,11 @@ def settled_arms(A, md, device=0, frames=None, runner=None):
     process on the device (runner: a function (S, frames) -> settled S, e.g. the oracle's, for
     tests).  The settle has no random input: its result depends on the gender alone."""
     frames = md.params['settle_frames'] if frames is None else frames
-    key = (id(A), frames, runner is None)
-    if key in _SETTLED:
-        return _SETTLED[key]
+    # cached per scene object (held in the entry, so its id cannot be reused by another scene)
+    # and device; a runner's result is not cached
+    key = (id(A), frames, device)
+    if runner is None and key in _SETTLED and _SETTLED[key][0] is A:
+        return _SETTLED[key][1]
     S = settle_states(A, md, ('male', 'female'))
     if runner is None:
         from . import _lib
@@ -141,7 +143,8 @@ def settled_arms(A, md, device=0, frames=None, runner=None):
     for k, g in enumerate(('male', 'female')):
         out[g] = (St[k, BB.S_Q + nd:BB.S_Q + nd + len(ARM_CHAIN)].copy(),
                   St[k, BB.S_HUMAN:BB.S_HUMAN + 7 * BB.MAX_HUMAN].reshape(BB.MAX_HUMAN, 7).copy())
-    _SETTLED[key] = out
+    if runner is None:
+        _SETTLED[key] = (A, out)
     return out
 
 

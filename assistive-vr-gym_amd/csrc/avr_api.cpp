@@ -45,6 +45,8 @@
                      const float *alt4, int32_t restarts, int32_t iters, float tol, const float *keepout8,          \
                      int32_t n_frames, float *host_obs, uint8_t *host_ok);                                         \
     int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out);                               \
+    int avr_narrowphase_query(avr_sim *s, int32_t n, const int32_t *pairs, const float *poses14, float thr,         \
+                              float *out8);                                                                        \
     int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest,            \
                         const float *tstart3, const float *goals9, int32_t iters, float tol, int32_t *best,         \
                         uint8_t *ok, float *q_arm, float *res4);                                                   \
@@ -190,6 +192,9 @@ int avr_reset_ik(avr_sim *s, const uint8_t *m, const float *p, const float *t7, 
     DISPATCH(s, avr_reset_ik(h, m, p, t7, init, alt4, r, it, tol, box8, n, o, ok));
 }
 int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) { DISPATCH(s, avr_robot_self_contact(h, n, q, out)); }
+int avr_narrowphase_query(avr_sim *s, int32_t n, const int32_t *pairs, const float *poses14, float thr, float *out8) {
+    DISPATCH(s, avr_narrowphase_query(h, n, pairs, poses14, thr, out8));
+}
 int avr_base_search(avr_sim *s, int32_t n, int32_t a, const float *b7, const float *rest, const float *t3, const float *g9, int32_t it, float tol,
                     int32_t *best, uint8_t *ok, float *q, float *res4) {
     DISPATCH(s, avr_base_search(h, n, a, b7, rest, t3, g9, it, tol, best, ok, q, res4));

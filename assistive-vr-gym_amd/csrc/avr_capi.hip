@@ -64,13 +64,19 @@ struct avr_sim {
 // return: scratch buffers allocated lazily (hipMalloc) land on the handle's GPU whatever device
 // the caller (or another handle, or torch) made current.
 struct DevGuard {
-    int prev = -1, dev;
-    explicit DevGuard(int d) : dev(d) {
-        if (hipGetDevice(&prev) != hipSuccess || prev == d) prev = -1;
-        else (void)hipSetDevice(d);
+    // makes device d current for the call and restores the caller's; an out-of-range d (a handle
+    // whose avr_create failed) is left alone, and a failed switch does not leave its error behind
+    // for the next hipGetLastError of a launch check
+    int prev = -1;
+    explicit DevGuard(int d) {
+        int n = 0, cur = -1;
+        if (d < 0 || hipGetDeviceCount(&n) != hipSuccess || d >= n || hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
+        if (cur == d) return;
+        if (hipSetDevice(d) == hipSuccess) prev = cur;
+        else (void)hipGetLastError();
     }
     ~DevGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (prev >= 0 && hipSetDevice(prev) != hipSuccess) (void)hipGetLastError();
     }
 };
 
@@ -921,6 +927,25 @@ int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) 
     HIPCHK(s, hipMemcpyAsync(d_q, q, (size_t)n * nd * sizeof(float), hipMemcpyHostToDevice, s->stream));
     HIPCHK(s, avr_launch_self_contact(s->d_km, s->d_state, d_q, d_o, (int)n, s->stream));
     HIPCHK(s, hipMemcpyAsync(out, d_o, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ narrowphase query (test hook)
+int avr_narrowphase_query(avr_sim *s, int32_t n, const int32_t *pairs, const float *poses14, float thr, float *out8) {
+    CHECK_SIM(s);
+    if (n < 0 || (n > 0 && (!pairs || !poses14 || !out8))) return fail(s, -1, "avr_narrowphase_query: n >= 0, pairs, poses14 and out8 must be given");
+    for (int32_t i = 0; i < 2 * n; i++)
+        if (pairs[i] < 0 || pairs[i] >= s->km.ns) return fail(s, -1, "avr_narrowphase_query: shape %d out of range", (int)pairs[i]);
+    if (n == 0) return 0;
+    struct Buf { void *p = nullptr; ~Buf() { if (p) (void)hipFree(p); } } buf;
+    HIPCHK(s, hipMalloc(&buf.p, (size_t)n * (2 * sizeof(int) + 22 * sizeof(float))));
+    int *d_p = (int *)buf.p;
+    float *d_x = (float *)(d_p + 2 * (size_t)n), *d_o = d_x + 14 * (size_t)n;
+    HIPCHK(s, hipMemcpyAsync(d_p, pairs, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(d_x, poses14, 14 * (size_t)n * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, avr_launch_np_query(s->d_km, d_p, d_x, thr, d_o, (int)n, s->stream));
+    HIPCHK(s, hipMemcpyAsync(out8, d_o, 8 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
 }

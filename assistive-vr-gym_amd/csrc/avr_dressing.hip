@@ -387,13 +387,19 @@ struct avr_sim {
 };
 
 struct DevGuard {
+    // makes device d current for the call and restores the caller's; an out-of-range d (a handle
+    // whose avr_create failed) is left alone, and a failed switch does not leave its error behind
+    // for the next hipGetLastError of a launch check
     int prev = -1;
     explicit DevGuard(int d) {
-        if (hipGetDevice(&prev) != hipSuccess || prev == d) prev = -1;
-        else (void)hipSetDevice(d);
+        int n = 0, cur = -1;
+        if (d < 0 || hipGetDeviceCount(&n) != hipSuccess || d >= n || hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
+        if (cur == d) return;
+        if (hipSetDevice(d) == hipSuccess) prev = cur;
+        else (void)hipGetLastError();
     }
     ~DevGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (prev >= 0 && hipSetDevice(prev) != hipSuccess) (void)hipGetLastError();
     }
 };
 
@@ -661,6 +667,10 @@ int avr_get_flags(avr_sim *s, int32_t *flags) {
     HIPCHK(s, hipMemcpyAsync(flags, s->d_query, (size_t)E * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
     return 0;
+}
+int avr_narrowphase_query(avr_sim *s, int32_t n, const int32_t *pairs, const float *poses14, float thr, float *out8) {
+    (void)n; (void)pairs; (void)poses14; (void)thr; (void)out8;
+    return fail(s, -1, "avr_narrowphase_query: DressingJaco has no rigid collision model");
 }
 int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) {
     (void)n; (void)q; (void)out;

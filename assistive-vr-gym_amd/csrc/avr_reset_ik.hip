@@ -278,3 +278,33 @@ hipError_t avr_launch_self_contact(const KModel *d_m, const float *state, const 
     hipLaunchKernelGGL(avr_self_contact_kernel, dim3(n), dim3(64), 0, st, d_m, state, q, out, n);
     return hipGetLastError();
 }
+
+// avr_narrowphase_query (test hook): the step's wave-cooperative narrowphase (closed forms, GJK
+// with margins, EPA for penetrating cores) between shapes sa and sb at given body poses, one
+// wave per query -> {rc, normal on B xyz, point on B xyz, distance}
+__global__ __launch_bounds__(64) void avr_np_query_kernel(const KModel *__restrict__ mp, const int *__restrict__ pairs, const float *__restrict__ poses,
+                                                          float thr, float *__restrict__ out, int n) {
+    __shared__ EpaBuf E;
+    const int q = blockIdx.x;
+    if (q >= n) return;
+    const KModel &m = *mp;
+    const float *pa = poses + 14 * (size_t)q, *pb = pa + 7;
+    tf ta, tb;
+    ta.p = V(pa[0], pa[1], pa[2]); ta.q = Q(pa[3], pa[4], pa[5], pa[6]);
+    tb.p = V(pb[0], pb[1], pb[2]); tb.q = Q(pb[3], pb[4], pb[5], pb[6]);
+    const WShape A = make_wshape(m, pairs[2 * q], ta), B = make_wshape(m, pairs[2 * q + 1], tb);
+    v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+    float d = 0.f;
+    int nit, nk;
+    const int rc = narrowphase<true>(m, E, A, B, thr, nB, pB, d, nit, nk);
+    if (lane_id() == 0) {
+        float *o = out + 8 * (size_t)q;
+        o[0] = (float)rc; o[1] = nB.x; o[2] = nB.y; o[3] = nB.z; o[4] = pB.x; o[5] = pB.y; o[6] = pB.z; o[7] = d;
+    }
+}
+
+hipError_t avr_launch_np_query(const KModel *d_m, const int *pairs, const float *poses, float thr, float *out, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_np_query_kernel, dim3(n), dim3(64), 0, st, d_m, pairs, poses, thr, out, n);
+    return hipGetLastError();
+}

@@ -185,6 +185,14 @@ int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state,
  *   path (avr/reset.py ik_batch); avr_reset_ik runs the same test on the device. */
 int avr_robot_self_contact(avr_sim *sim, int32_t n, const float *q, int32_t *out);
 
+/* avr_narrowphase_query (test hook): the step's narrowphase between shapes pairs[2i] and
+ *   pairs[2i+1] (indices into the model's shapes) on body poses poses14[14i..] (A's body:
+ *   position, quaternion xyzw; then B's), contact threshold thr -> out8[8i..] = {rc (0 none,
+ *   1 contact, 2 unresolved), normal on B xyz, point on B xyz, signed distance}.  The shape-level
+ *   counterpart of p.getClosestPoints / the contact a pair adds to its manifold (btGjkEpa2 [ext]);
+ *   lets the GJK / EPA be checked against the oracle pair by pair. */
+int avr_narrowphase_query(avr_sim *sim, int32_t n, const int32_t *pairs, const float *poses14, float thr, float *out8);
+
 /* ---- device base-pose search (ScratchItchPR2, BedBathingPR2) ----
  * avr_base_search: position_robot_toc (env.py:489-585; scratch_itch.py:189-190,
  *   bed_bathing.py:317) for n envs on the device, one lane per (env, attempt).  Host buffers:

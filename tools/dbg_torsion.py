@@ -12,7 +12,12 @@ import bedbath_util as BU
 BB = ABI.BB
 A0 = dict(np.load(os.path.join(os.path.dirname(ABI.__file__), 'data', 'bed_bathing_pr2.npz')))
 md0 = ABI.ModelDesc(A0)
-S, meta = RBB.batch_reset_states(A0, md0, 1001, list(range(8)))
+if os.environ.get('DBG_FIXTURE'):      # tests/test_bedbath.py's states: arms settled by the fp64 oracle
+    import test_bedbath as TB
+    settled = RBB.settled_arms(A0, md0, runner=TB._oracle_runner(md0))
+    S, meta = RBB.batch_reset_states(A0, md0, 1001, list(range(8)), attempts=12, iters=80, settled=settled)
+else:
+    S, meta = RBB.batch_reset_states(A0, md0, 1001, list(range(8)))
 W, ks = BU.wipe_states(A0, md0, S)
 nd = int(A0['n_dof'])
 for variant in ('compiled', 'zero'):
@@ -36,6 +41,9 @@ for variant in ('compiled', 'zero'):
         dqd = np.abs(G[:, BB.S_QD:BB.S_QD + nd] - C[:, BB.S_QD:BB.S_QD + nd]).max(1)
         df = np.abs(G[:, BB.S_FREE:BB.S_FREE + 13] - C[:, BB.S_FREE:BB.S_FREE + 13]).max(1)
         ncg, ncc = G[:, BB.S_TASK + BB.T_NCP], C[:, BB.S_TASK + BB.T_NCP]
+        wb = slice(BB.S_TASK + BB.T_WIPE, BB.S_TASK + BB.T_WIPE + 6)
+        print('wipe bits equal', [bool(np.array_equal(G[e, wb], C[e, wb].astype(np.float32))) for e in range(len(W))],
+              G[:, wb][:, 0].astype(int).tolist(), C[:, wb][:, 0].astype(int).tolist())
         print(variant, what, 'dq', np.array2string(dq, precision=2), 'dqd', np.array2string(dqd, precision=2), 'dfree', np.array2string(df, precision=2),
               'ncp', ncg.astype(int).tolist(), ncc.astype(int).tolist(), flush=True)
         sim.close()
