@@ -68,6 +68,7 @@ struct EnvLDS {
     float gsc[MAXF][4];     // 1/sqrt(m), sqrt of the inverse principal inertias (mass-normalised rows)
     float h[MAXD], qdd[MAXD];
     int nsp, nap, n_nc, n_c, flags, gender;
+    int n_t;                // (K_TORSION) contacts with torsional rows
     int nla, nda;           // articulated links / DoFs of this env (the head chain counts under 'tremor')
 #ifdef AVR_PROF
     unsigned long long prof[AVR_PROF_SLOTS];
@@ -1792,6 +1793,7 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 #define WS_XCC 3     // diagnostic builds: XCD that ran part A
 #define WS_NROB 4    // int bits: robot parts (slots) of the row set
 #define WS_COOPROT 5 // int bits: rotation of the capped cooperative-pair window (np_coop)
+#define WS_NT 6      // int bits: (K_TORSION) contacts with torsional rows (rows n_nc + 3 n_c ..)
 #define WS_VQ 16     // [MAXD] unconstrained robot velocities
 #define WS_FV (WS_VQ + 16 * NDL)     // [MAXF][4] unconstrained free-body linear velocities
 #define WS_FW (WS_FV + 4 * MAXF)     // [MAXF][4] angular
@@ -2030,12 +2032,16 @@ AVR_DI void body_endpoint(const KModel &m, const EnvLDS &L, int b, int &kind, in
 }
 
 // Contact rows: one lane per contact point; contact c owns rows n_nc + c (normal),
-// n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions) and (K_TORSION)
-// n_nc + 3 n_c + 3c + {0,1,2}: the torsional rows -- spinning about the normal, rolling about the
-// two friction directions; angular-only Jacobians, limits +-coefficient x normal impulse, no
-// positional term (btMultiBodyConstraintSolver::addMultiBodyTorsionalFrictionConstraint [ext]).
-// Their coefficients combine the bodies' as btManifoldResult does (roll_A fric_B + roll_B fric_A,
-// clamped to 10); a row whose coefficient is 0 is a null record.
+// n_nc + n_c + 2c + {0,1} (frictions along btPlaneSpace1 directions) and (K_TORSION, contacts
+// whose rolling or spinning coefficient is positive, the t-th of them) n_nc + 3 n_c + 3t + {0,1,2}:
+// the torsional rows -- spinning about the normal, rolling about the two friction directions;
+// angular-only Jacobians, limits +-coefficient x normal impulse, no positional term
+// (btMultiBodyConstraintSolver::addMultiBodyTorsionalFrictionConstraint [ext]).  Their
+// coefficients combine the bodies' as btManifoldResult does (roll_A fric_B + roll_B fric_A, clamped
+// to 10); a row whose coefficient is 0 (only one of the two positive) is a null record.  The normal
+// record's 4th word (unused by the normal resolve) holds t + 1 (0: no torsional rows), so part B
+// sweeps only the torsional rows that exist.  Robot parts: 3 slots per robot contact, 6 with
+// torsional rows.
 
 // btManifoldResult::calculateCombinedRollingFriction / SpinningFriction [ext]
 AVR_DI float torsion_coeff(const float *c, const KModel &m, int ba, int bb) {
@@ -2046,7 +2052,8 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
     const int lane = lane_id();
     const int ncp = (int)L.st[S_TASK + T_NCP];
     const float erp = m.erp;
-    int nrob = n_nc;                                 // robot parts: nc rows first, then 3 per robot contact
+    int nrob = n_nc;                                 // robot parts: nc rows first, then 3 (6) per robot contact
+    int nt = 0;                                      // contacts with torsional rows so far
     for (int base = 0; base < ncp; base += 64) {
         const int i = base + lane;
         const bool act = i < ncp;
@@ -2057,10 +2064,25 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         body_endpoint(m, L, ba, kA, iA);
         body_endpoint(m, L, bb, kB, iB);
         const bool rob = kA == 1 || kB == 1;
-        int tot;
-        const int pre = ballot_prefix(act && rob, &tot);
-        const int slot0 = nrob + K_CROWS * pre;
-        nrob += K_CROWS * tot;
+#if K_TORSION
+        const float spin = torsion_coeff(m.body_spinning, m, ba, bb), roll = torsion_coeff(m.body_rolling, m, ba, bb);
+        const bool trs = act && (spin > 0.f || roll > 0.f);
+#else
+        constexpr bool trs = false;
+#endif
+        const int nrow = trs ? 6 : 3;
+        // robot slots: an inclusive scan of each lane's slot count
+        const int wgt = act && rob ? nrow : 0;
+        int incl = wgt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const int slot0 = nrob + incl - wgt;
+        nrob += __shfl(incl, 63, 64);
+        int ttot;
+        const int ti = nt + ballot_prefix(trs, &ttot);
+        nt += ttot;
         if (!act) continue;
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
@@ -2071,15 +2093,12 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         float fric = fminf(gld(m.body_friction + (ba)) * gld(m.body_friction + (bb)), 10.f);
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
-#if K_TORSION
-        const float spin = torsion_coeff(m.body_spinning, m, ba, bb), roll = torsion_coeff(m.body_rolling, m, ba, bb);
-#endif
 #pragma unroll 1
-        for (int k = 0; k < K_CROWS; k++) {
+        for (int k = 0; k < nrow; k++) {
             const int kd = k < 3 ? k : k - 3;
             v3 dir = kd == 0 ? n : (kd == 1 ? t1 : t2);
             const int slot = rob ? slot0 + k : -1;
-            float *w = row_crec(rows, k == 0 ? i : k < 3 ? ncp + 2 * i + (k - 1) : 3 * ncp + 3 * i + (k - 3));
+            float *w = row_crec(rows, k == 0 ? i : k < 3 ? ncp + 2 * i + (k - 1) : 3 * ncp + 3 * ti + (k - 3));
             float den = 0.f, rel = 0.f;
 #if K_TORSION
             // torsional rows (k >= 3): angular axis dir, no linear part
@@ -2138,7 +2157,8 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 else poserr = -pen * erp / dt;
                 rhs = (poserr + velerr) * inv;
             }
-            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs; w[3] = tor ? tcoef : fric;
+            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs;
+            w[3] = tor ? tcoef : k == 0 ? (trs ? (float)(ti + 1) : 0.f) : fric;
 #if B4_FPAIR
             if (k == 2) {
                 // the friction unit's coupling c = J_2 M^-1 J_1^T (its second row's 4th header word,
@@ -2160,7 +2180,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
 #endif
         }
     }
-    if (lane == 0) L.n_c = ncp;
+    if (lane == 0) { L.n_c = ncp; L.n_t = nt; }
     return nrob;
 }
 
@@ -2230,7 +2250,10 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     SYNC();
     PROF_STOP(8, ps);
     // hand-over to part B
-    if (lane == 0) { ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); ws[WS_NROB] = __int_as_float(n_rob); }
+    if (lane == 0) {
+        ws[WS_NNC] = __int_as_float(n_nc); ws[WS_NC] = __int_as_float(L.n_c); ws[WS_NROB] = __int_as_float(n_rob);
+        ws[WS_NT] = __int_as_float(K_TORSION ? L.n_t : 0);
+    }
     if (lane < MAXD) ws[WS_VQ + lane] = lane < L.nda ? L.vq[lane] : 0.f;
     if (lane < m.nf) {
         st3(ws + WS_FV + 4 * lane, ld3(L.fv[lane]));
@@ -2987,6 +3010,7 @@ typedef unsigned u3v __attribute__((ext_vector_type(3)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 AVR_DI f4v bld4(rsrc_t r, int o) { u4v x = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0); return *(f4v *)&x; }
 AVR_DI f2v bld2(rsrc_t r, int o) { u2v x = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0); return *(f2v *)&x; }
+AVR_DI float bld1(rsrc_t r, int o) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0)); }
 #if NDL == 2
 typedef f4v rv_t;           // a lane's robot-part words: (J, M^-1 J^T) of DoF sl, then of DoF sl + 16
 #define RVB 16              // bytes per lane in a robot part
@@ -3120,6 +3144,8 @@ struct CLds {
         return *(const lds_rv *)(blk + b);
     }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
+    // (K_TORSION) contact c's torsional index + 1 (0: none), its normal record's 4th word
+    AVR_DI int tor_of(int c) const { return (int)*(const lds_f *)(blk + cn + CRW * 4 * c + 20); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
         const unsigned b = own_b(A), r = rob_b(A);
         own_at(A, b); own_at(B, b + CRW * 4);
@@ -3152,6 +3178,7 @@ struct CGlb {
     AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + ROBW * 4 * s : B4_OOB; }
     AVR_DI rv_t rob_at(int b) const { return rload(rs, b); }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
+    AVR_DI int tor_of(int c) const { return (int)bld1(rs, cn + CRW * 4 * c + 12); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
         const int b = own_b(A), r = rob_b(A);
         own_at(A, b); own_at(B, b + CRW * 4);
@@ -3312,7 +3339,7 @@ struct TorSrc {
 #endif
 
 template <int DN, int DC, class NS, class CS>
-AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
+AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, lds_i *tlist, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename NS::Row NR;
     typedef typename CS::Row CR;
     const int sl = lane_id() & 15;
@@ -3392,14 +3419,34 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, int n_
         }
 #if K_TORSION
         // torsional rows after the frictions (btMultiBodyConstraintSolver::solveSingleIteration
-        // [ext]), for the same active contacts; null records (coefficient 0) resolve to delta 0
+        // [ext]), for the active contacts that have them, in contact order: their (contact,
+        // torsional index) pairs compacted from the active list, then one flat sweep, step j = row
+        // j mod 3 of the j / 3-th such contact; a row carries its contact's normal impulse (its
+        // limits are +-coefficient x that impulse)
         {
+            int tt = 0;
+            for (int u0 = 0; u0 < tmax; u0 += 16) {
+                const int u = u0 + sl;
+                const int cl = list[u < t ? u : 0];
+                const int c = u < t ? cl : 0;
+                const int tv = cs.tor_of(c);                 // (read unconditionally, record 0 past the list)
+                const bool a = u < t && tv > 0;
+                const unsigned long long b = __ballot(a);
+                const unsigned gm = (unsigned)(b >> (lane_id() & 48)) & 0xffffu;
+                if (a) tlist[tt + __popc(gm & ((1u << sl) - 1u))] = c | (tv - 1) << 8;
+                tt += __popc(gm);
+            }
+            int ttmax = tt;
+            ttmax = max(ttmax, __shfl_xor(ttmax, 16));
+            ttmax = max(ttmax, __shfl_xor(ttmax, 32));
+            ttmax = uni(ttmax);
             const TorSrc<CS> ts{cs};
-            sweep4<DC, false>(ts, 3 * tmax, [&](TorRow<CS> &R, int j) {
+            sweep4<DC, false>(ts, 3 * ttmax, [&](TorRow<CS> &R, int j) {
                 const int u = j / 3, k = j - 3 * u;
-                const bool v = u < t;
-                const int c = list[v ? u : 0];
-                cs.set(R, v, cs.ct + 3 * CRW * 4 * c + CRW * 4 * k, cs.ipt + 3 * c + k);
+                const bool v = u < tt;
+                const int e = tlist[v ? u : 0];
+                const int c = e & 255, ti = e >> 8;
+                cs.set(R, v, cs.ct + 3 * CRW * 4 * ti + CRW * 4 * k, cs.ipt + 3 * ti + k);
                 const float x = cs.ipn[v ? c : 0];      // (read unconditionally)
                 R.in = v ? x : 0.f;
             }, [&](const TorRow<CS> &R) {
@@ -3445,7 +3492,9 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     float *st = state + (size_t)ev * K_STATE_WORDS;
     const int n_nc = live ? __float_as_int(wsg[WS_NNC]) : 0, n_c = live ? __float_as_int(wsg[WS_NC]) : 0;
     const int n_rob = live ? __float_as_int(wsg[WS_NROB]) : 0;
-    const int n_rows = n_nc + K_CROWS * n_c, n_rc = max(n_rob - n_nc, 0);
+    const int n_t = live && K_TORSION ? __float_as_int(wsg[WS_NT]) : 0;       // contacts with torsional rows
+    const int n_cr = 3 * n_c + 3 * n_t;                                        // contact records
+    const int n_rows = n_nc + n_cr, n_rc = max(n_rob - n_nc, 0);
     auto wmax = [&](int x) { x = max(x, __shfl_xor(x, 16)); x = max(x, __shfl_xor(x, 32)); return uni(x); };
     const int nnc_max = wmax(n_nc), nc_max = wmax(n_c);
     // the row buffer of every env as one buffer resource; this env's records at byte eo
@@ -3456,7 +3505,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     SYNC();
 #endif
     // pack the groups' regions; stage every row (B4_NC_LDS) or the contact rows when all four fit
-    const int szA = al4(n_rows + 2) + al4(n_c), szB = K_CROWS * n_c * CRW + n_rc * ROBW;
+    const int szA = al4(n_rows + 2) + (K_TORSION ? 2 : 1) * al4(n_c), szB = n_cr * CRW + n_rc * ROBW;
 #if B4_NC_LDS
     const int szF = szB + n_nc * (RWC + ROBW);
     const int f0 = __shfl(szA + szF, 0), f1 = __shfl(szA + szF, 16), f2 = __shfl(szA + szF, 32), f3 = __shfl(szA + szF, 48);
@@ -3477,9 +3526,10 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     base += LN_HEAD;
     lds_f *imp = blk + base;
     lds_i *list = (lds_i *)(imp + al4(n_rows + 2));
+    lds_i *tlist = list + al4(n_c);     // (K_TORSION) active contacts with torsional rows
     // LDS regions: contact records at cw, then (full) the non-contact records at nw, then the
     // robot parts at rw (full: every slot's; otherwise the robot-contact slots')
-    const int cw = base + szA, nw = cw + K_CROWS * n_c * CRW, rw = full ? nw + n_nc * RWC : nw;
+    const int cw = base + szA, nw = cw + n_cr * CRW, rw = full ? nw + n_nc * RWC : nw;
     // starting impulses: non-contact rows and frictions 0, normal rows the cached impulse x the
     // warm-start factor; null slots 0.  The cached impulses are loaded here and stored after the
     // staging loads below have been issued (one memory round trip for both).
@@ -3493,7 +3543,7 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
     }
     for (int i = lane; i < LN_HEAD; i += 64) blk[i] = 0.f;        // null rows, zero parts
     if (in_lds) {   // contact records, (full) non-contact records, robot parts: 8 loads in flight per lane
-        const int n4r = K_CROWS * n_c * (CRW / 4), n4n = full ? n_nc * (RWC / 4) : 0, n4s = (full ? n_rob : n_rc) * (ROBW / 4);
+        const int n4r = n_cr * (CRW / 4), n4n = full ? n_nc * (RWC / 4) : 0, n4s = (full ? n_rob : n_rc) * (ROBW / 4);
         const int n4a = n4r + n4n, n4 = n4a + n4s, so = full ? ro : ro + n_nc * ROBW * 4;
         const int m4 = wmax(n4);
         lds_f4 *l0 = (lds_f4 *)(blk + cw);
@@ -3527,11 +3577,11 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
         const NcLds nl{(lds_c *)blk, 4 * nw + 8, rob, imp, nullip};
         if (wmax(n_rc) > 0) {
             CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
-            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, tlist, n_nc, n_c, nnc_max, nc_max, d);
             rcb = 1;
         } else {
             CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
-            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DNL, B4_DC>(m, nl, cs, list, tlist, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else
 #endif
@@ -3540,16 +3590,16 @@ AVR_DI void substep_b4_block(const KModel &m, float *__restrict__ state, const u
         const unsigned cn = 4 * cw - 8, cf = cn + 4 * CRW * n_c, ct = cf + 8 * CRW * n_c, rob = 4 * (rw - (n_nc + 1) * ROBW) + RVB * sl;
         if (wmax(n_rc) > 0) {
             CLds<true> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
-            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, tlist, n_nc, n_c, nnc_max, nc_max, d);
             rcb = 1;
         } else {
             CLds<false> cs{(lds_c *)blk, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
-            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+            units = pgs4<B4_DN, B4_DC>(m, ns, cs, list, tlist, n_nc, n_c, nnc_max, nc_max, d);
         }
     } else {
         const int cn = eo + CR_BASE * 4, cf = cn + 4 * CRW * n_c, ct = cf + 8 * CRW * n_c, rob = ro - ROBW * 4 + RVB * sl;
         CGlb cs{rs, cn, cf, rob, ipn, ipf, nullip, ct, ipt};
-        units = pgs4<B4_DN, B4_DG>(m, ns, cs, list, n_nc, n_c, nnc_max, nc_max, d);
+        units = pgs4<B4_DN, B4_DG>(m, ns, cs, list, tlist, n_nc, n_c, nnc_max, nc_max, d);
     }
     (void)units; (void)rcb;
     // normal impulses back to the manifold points (warm start + normalForce)
