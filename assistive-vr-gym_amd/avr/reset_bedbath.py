@@ -182,7 +182,8 @@ def prepare_reset(A, md, seed, env_ids, genders=None, episodes=None, attempts=10
         S[idx, BB.S_Q + nd:BB.S_Q + nd + len(qc)] = qc
     lo, hi = arm_limits(md)
     tstart, base, rest = base_search_draws(rngs, attempts, lo, hi, (0, 0, 0), np.repeat(START_GOAL[None], N, 0))
-    return dict(S=S, genders=gl, goals=goals, tstart=tstart, base=base, rest=rest)
+    retry = dict(seed=seed, env_ids=env_ids, episodes=eps, pos_offset=(0, 0, 0))
+    return dict(S=S, genders=gl, goals=goals, tstart=tstart, base=base, rest=rest, retry=retry)
 
 
 def finish_reset(A, md, P, iters=200, sim=None):
@@ -193,7 +194,7 @@ def finish_reset(A, md, P, iters=200, sim=None):
     gl = P['genders']
     N = len(S)
     nd = int(A['n_dof'])
-    bp, bq, Qa, _, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim)
+    bp, bq, Qa, _, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim, P.get('retry'))
     for d in md.finger_dofs:                                           # set_gripper_open_position(0.2, set_instantly)
         Qa[:, d] = md.params['finger_target']
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)

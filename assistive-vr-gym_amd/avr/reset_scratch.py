@@ -208,20 +208,52 @@ def position_robot_toc(A, md, rngs, human_goals, attempts=100, iters=200, tstart
     return base_search(A, md, tstart, base, rest, human_goals, iters, sim)
 
 
-def base_search(A, md, tstart, base, rest, human_goals, iters=200, sim=None):
+RETRY_BLOCKS = 10      # position_robot_toc keeps drawing until a start goal is reached (env.py:509); capped here
+_RETRY_TAG = 0x7E7
+
+
+def _retry_draws(retry, env_rows, k, attempts, lo, hi, tstart):
+    """Block k of further attempts for the given rows of a batch: drawn from a sub-stream of each
+    env's reset stream (seed, env id, episode, tag + k)."""
+    rngs = [np.random.default_rng([int(retry['seed']), int(retry['env_ids'][r]), int(retry['episodes'][r]), _RETRY_TAG + k]) for r in env_rows]
+    _, base, rest = base_search_draws(rngs, attempts, lo, hi, retry['pos_offset'], tstart[env_rows])
+    return base, rest
+
+
+def base_search(A, md, tstart, base, rest, human_goals, iters=200, sim=None, retry=None):
     """The search of position_robot_toc on drawn attempts (base_search_draws): on the device when
-    sim is given, else here in fp64.  Returns (base_pos, base_quat, arm q, start target, ok)."""
+    sim is given, else here in fp64.  retry (dict: seed, env_ids, episodes, pos_offset): an env
+    none of whose attempts reaches the start goal draws further blocks of attempts and takes the
+    first that does, as the reference's `while iteration < attempts or best_position is None`
+    (env.py:509) -- up to RETRY_BLOCKS blocks, then the closest attempt of the first block.
+    Returns (base_pos, base_quat, arm q, start target, ok)."""
     N, attempts = base.shape[:2]
     nd = int(A['n_dof'])
     arm = np.array(md.arm_dofs)
     if sim is not None:
         best, ok, qa = sim.base_search(base, rest, tstart, human_goals, iters=iters, tol=0.03)
+        bsel = base[np.arange(N), best].copy()
+        if retry is not None:
+            lo, hi = arm_limits(md)
+            for k in range(RETRY_BLOCKS):
+                rows = np.nonzero(~ok)[0]
+                if not len(rows):
+                    break
+                b2, r2 = _retry_draws(retry, rows, k, attempts, lo, hi, tstart)
+                _, _, _, res = sim.base_search(b2, r2, tstart[rows], human_goals[rows], iters=iters, tol=0.03, per_attempt=True)
+                hit = res[..., 0] > 0
+                for j, e in enumerate(rows):
+                    if not hit[j].any():
+                        continue
+                    a = int(np.argmax(hit[j]))              # the first attempt that reaches the start goal
+                    _, ok1, q1 = sim.base_search(b2[j:j + 1, a:a + 1], r2[j:j + 1, a:a + 1], tstart[e:e + 1], human_goals[e:e + 1],
+                                                 iters=iters, tol=0.03)
+                    bsel[e], qa[e], ok[e] = b2[j, a], q1[0], bool(ok1[0])
         out_q = np.zeros((N, nd))
         for d in md.finger_dofs:
             out_q[:, d] = md.params['finger_target']
         out_q[:, arm] = qa
-        b = base[np.arange(N), best]
-        return b[:, :3].copy(), b[:, 3:].copy(), out_q, tstart, ok
+        return bsel[:, :3].copy(), bsel[:, 3:].copy(), out_q, tstart, ok
     res = base_search_host(A, md, base, rest, tstart, human_goals, iters)
     goals, manip, pe, Qs = res
     out_bp, out_bq, out_q, ok = np.zeros((N, 3)), np.zeros((N, 4)), np.zeros((N, nd)), np.zeros(N, bool)
@@ -236,6 +268,19 @@ def base_search(A, md, tstart, base, rest, human_goals, iters=200, sim=None):
         else:
             ok[e] = True
         out_bp[e], out_bq[e], out_q[e] = base[e, best, :3], base[e, best, 3:], Qs[e, best]
+    if retry is not None:
+        lo, hi = arm_limits(md)
+        for k in range(RETRY_BLOCKS):
+            rows = np.nonzero(~ok)[0]
+            if not len(rows):
+                break
+            b2, r2 = _retry_draws(retry, rows, k, attempts, lo, hi, tstart)
+            g2, _, _, Q2 = base_search_host(A, md, b2, r2, tstart[rows], human_goals[rows], iters)
+            for j, e in enumerate(rows):
+                hit = g2[j] > 0
+                if hit.any():
+                    a = int(np.argmax(hit))
+                    out_bp[e], out_bq[e], out_q[e], ok[e] = b2[j, a, :3], b2[j, a, 3:], Q2[j, a], True
     return out_bp, out_bq, out_q, tstart, ok
 
 
@@ -388,7 +433,8 @@ def prepare_reset(A, md, seed, env_ids, genders=None, impairment='random', episo
     S[:, t + SI.T_TARGET:t + SI.T_TARGET + 3] = lp[:, :3] + _qrot(lp[:, 3:], on_arm)
     for k in range(N):
         meta[k].update(limb=int(limbs[k]), start_goal=tstart[k])
-    return dict(S=S, meta=meta, goals=goals, tstart=tstart, base=base, rest=rest)
+    retry = dict(seed=seed, env_ids=env_ids, episodes=eps, pos_offset=(0.1, 0, 0))
+    return dict(S=S, meta=meta, goals=goals, tstart=tstart, base=base, rest=rest, retry=retry)
 
 
 def finish_reset(A, md, P, iters=200, sim=None):
@@ -397,7 +443,7 @@ def finish_reset(A, md, P, iters=200, sim=None):
     S, meta = P['S'].copy(), [dict(m) for m in P['meta']]
     N = len(S)
     nd = int(A['n_dof'])
-    bp, bq, Qa, tstart, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim)
+    bp, bq, Qa, tstart, ok = base_search(A, md, P['tstart'], P['base'], P['rest'], P['goals'], iters, sim, P.get('retry'))
     CP, CQ, _, _ = arm_fk(A, Qa, bp, bq)
     link = int(A['task_tool_link'])
     S[:, SI.S_RBASE:SI.S_RBASE + 3] = bp

@@ -387,17 +387,23 @@ AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
 // DoF of link j sees the moment about its joint origin of every force in its subtree,
 // h_j = ax_j . sum_k (N_k + (c_k - o_j) x F_k) (revolute; ax_j . sum_k F_k prismatic), which is what
 // the recursion (F_p += F_k, N_p += N_k + (c_k - c_p) x F_k) evaluates.
+// (the ancestors of a link, root first: a per-lane bit loop over its ancestor mask, whose trip
+// count is the link's depth rather than the link count; kernel a 0.182 -> 0.178 ms per 4096-env
+// launch, bit-identical)
 AVR_DI v3 anc_sum(const KModel &m, unsigned am, const float (*T)[4], int nla, v3 acc) {
-    for (int k = 0; k < nla; k++) {
-        const f4v t = *(const lds_f4 *)T[k];
-        if ((am >> k) & 1u) acc = add(acc, V(t.x, t.y, t.z));
+    (void)m; (void)nla;
+    for (unsigned dm = am; dm; dm &= dm - 1u) {
+        const f4v t = *(const lds_f4 *)T[__builtin_ctz(dm)];
+        acc = add(acc, V(t.x, t.y, t.z));
     }
     return acc;
 }
 AVR_DI v3 anc_sum3(const KModel &m, unsigned am, const float (*A)[4], const float (*B)[4], const float (*C)[4], int nla, v3 acc) {
-    for (int k = 0; k < nla; k++) {
+    (void)m; (void)nla;
+    for (unsigned dm = am; dm; dm &= dm - 1u) {
+        const int k = __builtin_ctz(dm);
         const f4v a = *(const lds_f4 *)A[k], b = *(const lds_f4 *)B[k], c = *(const lds_f4 *)C[k];
-        if ((am >> k) & 1u) acc = add(add(add(acc, V(a.x, a.y, a.z)), V(b.x, b.y, b.z)), V(c.x, c.y, c.z));
+        acc = add(add(add(acc, V(a.x, a.y, a.z)), V(b.x, b.y, b.z)), V(c.x, c.y, c.z));
     }
     return acc;
 }

@@ -176,3 +176,56 @@ def test_scratch_env_rollover_uses_device_search():
         assert np.all(np.isfinite(o)) and np.all(np.isfinite(r))
     finally:
         env.close()
+
+
+def test_retry_until_a_start_goal_is_reached():
+    """position_robot_toc keeps drawing bases until one reaches the start goal (`while iteration <
+    attempts or best_position is None`, env.py:509): with 2 attempts per env, the envs whose two
+    bases both miss draw further blocks and take the first base that reaches it; envs that
+    succeeded in the first block are untouched."""
+    from avr import reset_scratch as RSS
+    A = ABI.load_scene(ABI.TASK_SCRATCH)
+    md = ABI.ModelDesc(A)
+    P = RSS.prepare_reset(A, md, 1001, list(range(8)), attempts=2)
+    P0 = dict(P)
+    P0.pop('retry')
+    S0, m0 = RSS.finish_reset(A, md, P0, iters=60)
+    S1, m1 = RSS.finish_reset(A, md, P, iters=60)
+    ok0 = np.array([m['base_ok'] for m in m0])
+    ok1 = np.array([m['base_ok'] for m in m1])
+    assert (~ok0).any(), 'the 2-attempt search should miss for some env'
+    assert ok1.all() and np.all(ok1 >= ok0)
+    np.testing.assert_array_equal(S1[ok0], S0[ok0])
+    L = ABI.SI
+    link = int(A['task_tool_link'])
+    nd = int(A['n_dof'])
+    for e in np.nonzero(~ok0)[0]:
+        st = S1[e]
+        CP, _, _, _ = RSS.arm_fk(A, st[L.S_Q:L.S_Q + nd][None], st[L.S_RBASE:L.S_RBASE + 3][None], st[L.S_RBASE + 3:L.S_RBASE + 7][None])
+        assert np.linalg.norm(CP[0, link] - P['tstart'][e]) < 0.03
+
+
+@pytest.mark.gpu
+def test_device_search_retries_until_a_start_goal_is_reached():
+    from avr import _lib, reset_scratch as RSS
+    A = ABI.load_scene(ABI.TASK_SCRATCH)
+    md = ABI.ModelDesc(A)
+    P = RSS.prepare_reset(A, md, 1001, list(range(16)), attempts=2)
+    P0 = dict(P)
+    P0.pop('retry')
+    sim = _lib.Sim(md, 16)
+    try:
+        S0, m0 = RSS.finish_reset(A, md, P0, iters=60, sim=sim)
+        S1, m1 = RSS.finish_reset(A, md, P, iters=60, sim=sim)
+    finally:
+        sim.close()
+    ok0 = np.array([m['base_ok'] for m in m0])
+    ok1 = np.array([m['base_ok'] for m in m1])
+    assert (~ok0).any() and ok1.all()
+    np.testing.assert_array_equal(S1[ok0], S0[ok0])
+    L = ABI.SI
+    link, nd = int(A['task_tool_link']), int(A['n_dof'])
+    for e in np.nonzero(~ok0)[0]:
+        st = S1[e]
+        CP, _, _, _ = RSS.arm_fk(A, st[L.S_Q:L.S_Q + nd][None], st[L.S_RBASE:L.S_RBASE + 3][None], st[L.S_RBASE + 3:L.S_RBASE + 7][None])
+        assert np.linalg.norm(CP[0, link] - P['tstart'][e]) < 0.031
