@@ -2518,10 +2518,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
 
 // Sub-step part A1: one 64-lane block per env -- forward kinematics, body frames, broadphase,
 // shape-pair list (collide_pairs) into the env's collision scratch.
-__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
-                                                                         const unsigned char *__restrict__ mask, int env0, int n_envs) {
-    __shared__ PairsLDS L;
-    AVR_ENV_GUARD();
+AVR_DI void pairs_env(const KModel &m, PairsLDS &L, float *__restrict__ state, int env) {
     float *gst = state + (size_t)env * K_STATE_WORDS;
     // the packed shape info, staged in LDS for the pair enumeration (loads issued first, their
     // LDS stores after the kinematics)
@@ -2542,6 +2539,13 @@ __global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const K
     for (int i = lane_id(); i < L.nla * 4; i += 64) { cs[CS_AX + i] = (&L.ax[0][0])[i]; cs[CS_ORG + i] = (&L.org[0][0])[i]; }
     collide_pairs(m, L, cs);
     prof_flush(m, L, env);
+}
+
+__global__ __launch_bounds__(64) AVR_KATTR void avr_substep_pairs_kernel(const KModel *__restrict__ mp, float *__restrict__ state,
+                                                                         const unsigned char *__restrict__ mask, int env0, int n_envs) {
+    __shared__ PairsLDS L;
+    AVR_ENV_GUARD();
+    pairs_env(m, L, state, env);
 }
 
 // Sphere against convex hull (most of the scene's shape pairs: food against the spoon's and the
@@ -2760,13 +2764,8 @@ AVR_DI int np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot, int bu
 #ifndef NP_WAVES
 #define NP_WAVES 4
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
-                                                             int n_envs) {
-    const KModel &m = *mp;
+AVR_DI void np_list(const KModel &m, const unsigned char *__restrict__ mask, int eb, int list, int n_envs, float2 *ent, float (*btfs)[MAXB * 8]) {
     const int lane = lane_id();
-    const int list = (blockIdx.x >> 3) & 1;
-    const int eb = env0 + 8 * NP_ENVS * (blockIdx.x >> 4) + (blockIdx.x & 7);
-    if (eb >= n_envs) return;
     // items per env (0 past the end or masked out), prefix over the block's envs
     int pre[NP_ENVS + 1];
     pre[0] = 0;
@@ -2795,8 +2794,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
     };
     // the block's list entries (concatenated over its envs) and its envs' body frames, staged in
     // LDS in one round trip: a refill then reads its entry and frames from LDS
-    __shared__ float2 ent[NP_ENVS * MAXSP];
-    __shared__ float btfs[NP_ENVS][MAXB * 8];
 #pragma unroll
     for (int k = 0; k < NP_ENVS; k++) {
         const int e = eb + 8 * k;
@@ -2808,7 +2805,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
         r2l((float *)ent + 2 * pre[k], te, 2 * nk);
         r2l(btfs[k], tb, m.nb * 8);
     }
-    __syncthreads();
+    SYNC();
     auto entry = [&](int j) { const float2 x = ent[j]; return make_int2(__float_as_int(x.x), __float_as_int(x.y)); };
 #ifdef AVR_WAVETIME   // [3][eb] (list-0 block, list-1 block) durations in 100 MHz ticks
     struct WtNp {
@@ -2895,6 +2892,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) 
         pcount(39, __popcll(__ballot(pk >= 0 && pk < 3)));
 #endif
     }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP_WAVES))) void avr_narrowphase_kernel(const KModel *__restrict__ mp, const unsigned char *__restrict__ mask, int env0,
+                                                             int n_envs) {
+    const int list = (blockIdx.x >> 3) & 1;
+    const int eb = env0 + 8 * NP_ENVS * (blockIdx.x >> 4) + (blockIdx.x & 7);
+    if (eb >= n_envs) return;
+    __shared__ float2 ent[NP_ENVS * MAXSP];
+    __shared__ float btfs[NP_ENVS][MAXB * 8];
+    np_list(*mp, mask, eb, list, n_envs, ent, btfs);
 }
 
 // AVR_COOP_KERNEL 1: the wave-cooperative pairs run in a kernel of their own between the

@@ -17,7 +17,7 @@ timeout -k 10 600 python3 bench.py --task $TASK > gpurun_out/prof/bench_full.log
 rc=$?
 (rocm-smi --showclocks --showuse --showpower 2>&1 || true) > gpurun_out/prof/smi_after.txt
 # summaries on the box (the rocpd databases are too large to copy back), then drop the databases
-PS=gpurun_out/psum_${TAG:-r03}; mkdir -p $PS && AVR_PROF_OUT=$PS python3 tools/rocpd_summary.py gpurun_out/prof ${TAG:-r03} 4096 $TASK > $PS/summary.txt 2>&1
+PS=gpurun_out/psum_${TAG:-r03}; mkdir -p $PS && AVR_PROF_OUT=$PS python3 tools/rocpd_summary.py gpurun_out/prof ${TAG:-r03} ${ENVS:-4096} $TASK > $PS/summary.txt 2>&1
 cp gpurun_out/prof/*.txt gpurun_out/prof/*.log $PS/ 2>/dev/null
 rm -rf gpurun_out/prof
 tail -1 $PS/bench_full.log | cut -c1-600

@@ -26,6 +26,8 @@ SUBSTEPS = {'FeedingJaco-v0': 10, 'ScratchItchPR2-v0': 5, 'BedBathingPR2-v0': 5}
 
 
 def step_kernels(task):
+    if task == 'DressingJaco-v0':          # one launch per gym step (csrc/avr_dressing.hip)
+        return {'avr_dress_step_kernel': 1}
     n = SUBSTEPS[task]
     return {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n,
             'avr_substep_a_kernel': n, 'avr_substep_b4_kernel': n, 'avr_task_kernel': 1}
@@ -77,7 +79,7 @@ def main(pdir, tag, envs=4096, groups=None, task='FeedingJaco-v0'):
     STEP_KERNELS = step_kernels(task)
     # the bench runs min(4, envs / 1024) env groups: every kernel of the step is dispatched once
     # per group, over that group's share of the envs
-    groups = groups or max(1, min(4, envs // 1024))
+    groups = groups or (1 if task == 'DressingJaco-v0' else max(1, min(4, envs // 1024)))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.environ.get('AVR_PROF_OUT') or os.path.join(root, 'profiles')   # (on the GPU box: a gpurun_out/ dir)
     os.makedirs(prof, exist_ok=True)
@@ -113,7 +115,7 @@ def main(pdir, tag, envs=4096, groups=None, task='FeedingJaco-v0'):
         out['hbm_bytes_per_step'] = fb + wb
         out['hbm_bytes_per_env_step'] = (fb + wb) / envs
         out['correction'] = 'FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; median per-dispatch value x dispatches per step (launches x env groups)'
-        json.dump(out, open(os.path.join(prof, {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json'}.get(task, 'pmc_bedbath.json')), 'w'), indent=1)
+        json.dump(out, open(os.path.join(prof, {'FeedingJaco-v0': 'pmc_traffic.json', 'ScratchItchPR2-v0': 'pmc_scratch.json', 'DressingJaco-v0': 'pmc_dressing.json'}.get(task, 'pmc_bedbath.json')), 'w'), indent=1)
     json.dump(out, open(os.path.join(prof, '%s_pmc.json' % tag), 'w'), indent=1)
     print(json.dumps(out, indent=1))
 
