@@ -777,6 +777,7 @@ def build_pr2():
             cp, cq = G.tf_mul(P[i], Q[i], L.com_pos, L.com_quat)
             for s in urdf_shapes(L):
                 s.pos, s.quat = G.tf_mul(cp, cq, s.pos, s.quat)
+                s.urdf_link = i
                 shapes.append(s)
         groups.append((name, shapes))
     L15 = links[dfs[PR2_TORSO_LINK][0]['child']]
@@ -784,6 +785,31 @@ def build_pr2():
     # base_footprint: inertial origin 0, so PyBullet's base (COM) pose is the URDF root frame
     assert np.allclose(rootL.com_pos, 0)
     return rob, groups, torso_com, sub
+
+
+def pr2_frozen_joints():
+    """The PR2 joints the build holds at the reset pose (every joint outside the left arm's
+    subtree), in the base_footprint frame: per DFS index the parent, the joint type (J_*), the
+    joint origin and the world axis at the reset pose.  The reference drives them with PyBullet's
+    default velocity motors (world_creation.py:187); tests/test_pr2_frozen_branches.py sets the
+    contact impulses the build's rollouts put on these joints against those motors' limit."""
+    links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, PR2_URDF))
+    P, Q = pr2_fk(dfs, {j: v for j, v in zip(PR2_RIGHT_ARM, PR2_RIGHT_ARM_RESET)})
+    sub = {PR2_LEFT_ROOT}
+    for i in range(PR2_LEFT_ROOT + 1, len(dfs)):
+        if dfs[i][1] in sub:
+            sub.add(i)
+    n = len(dfs)
+    parent, jtype = np.full(n, -1, np.int32), np.zeros(n, np.int32)
+    axis = np.zeros((n, 3))
+    for i, (J, par) in enumerate(dfs):
+        parent[i] = par
+        if i in sub:
+            continue
+        jtype[i] = {'fixed': J_FIXED, 'revolute': J_REVOLUTE, 'continuous': J_REVOLUTE, 'prismatic': J_PRISMATIC}[J['type']]
+        if jtype[i] != J_FIXED:
+            axis[i] = G.quat_rotate(Q[i], J['axis'] / max(np.linalg.norm(J['axis']), 1e-12))
+    return dict(pr2_parent=parent, pr2_jtype=jtype, pr2_jorigin=P.copy(), pr2_jaxis=axis)
 
 
 def build_composite_tool(rel, tip_link):
@@ -1098,7 +1124,7 @@ def to_arrays(S):
         for s in b['shapes']:
             c, h = s.local_aabb()
             row = dict(kind=s.kind, body=len(b_start) - 1, pos=s.pos, quat=s.quat, margin=s.margin,
-                       gender=s.gender, aabb=np.concatenate([c, h]))
+                       gender=s.gender, aabb=np.concatenate([c, h]), link=getattr(s, 'urdf_link', -1))
             if s.kind == SPHERE:
                 row['param'] = [s.radius, 0, 0, 0]
             elif s.kind == CAPSULE:
@@ -1131,6 +1157,8 @@ def to_arrays(S):
     A['shape_param'] = np.array([r['param'] for r in shape_rows], float)
     A['shape_margin'] = np.array([r['margin'] for r in shape_rows])
     A['shape_aabb'] = np.array([r['aabb'] for r in shape_rows])
+    if any(r['link'] >= 0 for r in shape_rows):       # (robot-fixed PR2 geometry: the URDF link of each shape)
+        A['shape_urdf_link'] = np.array([r['link'] for r in shape_rows], np.int32)
     A['hull_verts'] = np.array(hv).reshape(-1, 3)
     A['pair_a'] = np.array([p[0] for p in S.pairs], np.int32)
     A['pair_b'] = np.array([p[1] for p in S.pairs], np.int32)
@@ -1199,6 +1227,7 @@ def compile_scratch(out_dir=DATA_DIR):
     A['task_limbs'] = np.array([[[li, ln, r] for li, ln, r in t['limbs'][g]] for g in ('male', 'female')], float)
     A['n_rstatic'] = np.int32(len(S.rstatic))
     A['rl_urdf'] = np.array(S.robot['urdf'], np.int32)
+    A.update(pr2_frozen_joints())
     path = os.path.join(out_dir, 'scratch_itch_pr2.npz')
     np.savez_compressed(path, **A)
     return path, A
@@ -1223,6 +1252,7 @@ def compile_bedbath(out_dir=DATA_DIR):
     A['task_human_body0'] = np.int32(S.human_body[S.human_slots[0]])
     A['n_rstatic'] = np.int32(len(S.rstatic))
     A['rl_urdf'] = np.array(S.robot['urdf'], np.int32)
+    A.update(pr2_frozen_joints())
     # wipe targets [gender][k] = (x, y, z in the limb frame, limb 0 upper arm / 1 forearm)
     T = np.zeros((2, 160, 4))
     NT = np.zeros((2, 2), np.int32)
