@@ -343,13 +343,15 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
                      'sq_by_kernel': pmc.get('sq') if pmc else None,
                      'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': 'one env-step = 1 take_step + %d x (%s) + 1 task launch; '
+                     'scope': ('one env-step = one dress_step launch (the gym step\'s %d sub-steps inside it); ' % T['substeps']
+                               if name == 'DressingJaco-v0' else
+                               'one env-step = 1 take_step + %d x (%s) + 1 task launch; ' % (
+                                   T['substeps'], ', '.join(k[4:-7] for k in kernels if k not in ('avr_take_step_kernel', 'avr_task_kernel')))) +
                               'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
                               'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
                               'sequences, so its stream time per step is below the summed durations; traffic = PMC HBM bytes of the '
                               'step and valu_busy = PMC VALU instructions x %.0f cycles / (%d SIMDs x %.1f GHz x ms_per_step), both from '
                               'the task\'s committed rocprofv3 summary (%s)' % (
-                                  T['substeps'], ', '.join(k[4:-7] for k in kernels if k not in ('avr_take_step_kernel', 'avr_task_kernel')),
                                   VALU_CYC, SIMDS, CLOCK_HZ / 1e9, pmc['source'] if pmc else 'none matching'),
                      'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(L),
                      'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
