@@ -224,7 +224,7 @@ class AVRVecEnv:
         if self.task == ABI.TASK_BEDBATH:          # the reset's arm settle, once per gender (device)
             from . import reset_bedbath as RBB
             RBB.settled_arms(self.A, self.md, device)
-        self._prefetch = _Prefetch(self._inputs) if (prefetch and (self.device_ik or self.device_search)) else None
+        self._prefetch = _Prefetch(self._inputs) if (prefetch and (self.device_ik or self.device_search or self.task == ABI.TASK_DRESSING)) else None
         self.last_ik_ok = None
         self.reset_timing = None
 
@@ -302,11 +302,17 @@ class AVRVecEnv:
             return
         ids = [self.env_offset + int(i) for i in idx]
         if self.task == ABI.TASK_DRESSING:
+            # the whole reset is host work (prefetched like the others' host parts)
             t0 = time.perf_counter()
-            Si, _ = self._inputs(idx, eps)
+            key = (tuple(idx.tolist()), tuple(eps.tolist()))
+            got = self._prefetch.take(key) if self._prefetch else None
+            Si, _ = got if got is not None else self._inputs(idx, eps)
+            t1 = time.perf_counter()
+            if self._prefetch:
+                self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
             S[idx] = Si
             self.sim.reset(mask.astype(np.uint8), S, 0, self._obs)
-            self.reset_timing = dict(host_s=time.perf_counter() - t0)
+            self.reset_timing = dict(host_s=t1 - t0, prefetched=got is not None, device_s=time.perf_counter() - t1)
             return
         if self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH):
             # host part (prefetched on a background thread during the previous episode when the

@@ -68,11 +68,33 @@ def arm_geometry(A, gender, qh):
 
 
 def _frame_z(z, x_hint):
-    z = z / np.linalg.norm(z)
-    x = x_hint - np.dot(x_hint, z) * z
-    x /= np.linalg.norm(x)
+    """Quaternions (N, 4) of the frames whose z axes are z (N, 3), x axes the projection of x_hint."""
     from scipy.spatial.transform import Rotation
-    return Rotation.from_matrix(np.stack([x, np.cross(z, x), z], 1)).as_quat()
+    z = z / np.linalg.norm(z, axis=-1, keepdims=True)
+    x = x_hint - np.sum(x_hint * z, -1, keepdims=True) * z
+    x /= np.linalg.norm(x, axis=-1, keepdims=True)
+    return Rotation.from_matrix(np.stack([x, np.cross(z, x), z], -1)).as_quat()
+
+
+def arm_geometry_batch(A, gender, QH):
+    """arm_geometry for many envs of one gender: QH (N, n_joints) -> (N, 32)."""
+    from .reset_scratch import human_link_poses_batch
+    _, _, P, Q = human_link_poses_batch(A, gender, QH)
+    N = len(QH)
+    geo = np.zeros((N, 32))
+    geo[:, 0:3], geo[:, 3:6], geo[:, 6:9] = P[:, SH_LINK], P[:, EL_LINK], P[:, WR_LINK]
+    s = _slot_shape(A, HAND_LINK, gender)
+    geo[:, 9:12] = P[:, HAND_LINK] + RS._qrot(Q[:, HAND_LINK], np.broadcast_to(A['shape_pose'][s][:3], (N, 3)))
+    for off, link in ((12, UA_LINK), (19, FA_LINK)):
+        s = _slot_shape(A, link, gender)
+        sp = A['shape_pose'][s]
+        c = P[:, link] + RS._qrot(Q[:, link], np.broadcast_to(sp[:3], (N, 3)))
+        q = RS._qmul(Q[:, link], np.broadcast_to(sp[3:], (N, 4)))
+        ax = RS._qrot(q, np.broadcast_to([0, 0, 1.0], (N, 3))) * A['shape_param'][s][1]    # GEOM_CAPSULE: z-aligned
+        geo[:, off:off + 3], geo[:, off + 3:off + 6], geo[:, off + 6] = c + ax, c - ax, A['shape_param'][s][0]
+    geo[:, 26] = A['shape_param'][_slot_shape(A, HAND_LINK, gender)][0]
+    geo[:, 27:30] = CLOTH_SPHERE_R[gender]
+    return geo
 
 
 def arm_limits(md):
@@ -82,46 +104,56 @@ def arm_limits(md):
     return arm, lo, hi
 
 
-def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01):
+def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01, res=1e-4):
     """Vectorised damped-least-squares IK of the tool link's COM frame (RS.ik_batch's update rule)
     with per-env restarts init (N, R, 7); no collision screening (the robot is kinematic here).
-    Returns (Q (N, ndof), ok (N,))."""
+    A row stops iterating once its position error and rotation angle are both below `res`
+    (calculateInverseKinematics' residualThreshold role); the first restart that meets `tol`
+    is kept, else the last one.  Returns (Q (N, ndof), ok (N,))."""
     N, R, _ = init.shape
     nd = int(A['n_dof'])
     chain = RS._chain(A, link)
     cols = [[k for k in chain if A['rl_dof'][k] == d][0] for d in arm]
+    conj = np.array([-1, -1, -1, 1.0])
     Qout = np.zeros((N, nd))
     done = np.zeros(N, bool)
     for r in range(R):
         idx = np.nonzero(~done)[0]
         if not len(idx):
             break
-        Q = np.zeros((len(idx), nd))
-        Q[:, arm] = init[idx, r]
-        tp, tq = tpos[idx], tquat[idx]
-        for it in range(iters):
+        Qr = np.zeros((len(idx), nd))
+        Qr[:, arm] = init[idx, r]
+        act = np.arange(len(idx))                  # rows of Qr still iterating
+        for it in range(iters + 1):
+            Q = Qr[act]
             CP, CQ, AX, OR = RS.robot_fk_batch(A, Q)
+            tp, tq = tpos[idx[act]], tquat[idx[act]]
             ep = tp - CP[:, link]
-            dq = RS._qmul(tq, CQ[:, link] * np.array([-1, -1, -1, 1.0]))
+            dq = RS._qmul(tq, CQ[:, link] * conj)
             dq = np.where(dq[:, 3:4] < 0, -dq, dq)
             s = np.linalg.norm(dq[:, :3], axis=1)
             ang = 2.0 * np.arctan2(s, dq[:, 3])
+            live = (np.linalg.norm(ep, axis=1) >= res) | (ang >= res)
+            if it == iters or not live.any():
+                break
+            act, Q, ep, dq, s, ang = act[live], Q[live], ep[live], dq[live], s[live], ang[live]
+            CP, AX, OR = CP[live], AX[live], OR[live]
             er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
-            J = np.zeros((len(idx), 6, len(arm)))
+            J = np.zeros((len(act), 6, len(arm)))
             for c, l in enumerate(cols):
                 J[:, :3, c] = RS._cross(AX[:, l], CP[:, link] - OR[:, l])
                 J[:, 3:, c] = AX[:, l]
             JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
             step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, np.concatenate([ep, er], 1)[..., None])
-            Q[:, arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
-        CP, CQ, _, _ = RS.robot_fk_batch(A, Q)
+            Qr[act[:, None], arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
+        CP, CQ, _, _ = RS.robot_fk_batch(A, Qr)
+        tp, tq = tpos[idx], tquat[idx]
         pe = np.linalg.norm(tp - CP[:, link], axis=1)
         qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))
         good = (pe < tol) & (qe < tol)
-        for k, e in enumerate(idx):
-            if good[k] or r == R - 1:
-                Qout[e] = Q[k]
-                done[e] = good[k]
+        take = good | (r == R - 1)
+        Qout[idx[take]] = Qr[take]
+        done[idx[take]] = good[take]
     return Qout, done
 
 
@@ -137,6 +169,16 @@ def cloth_rest(p_tool, q_tool):
     return X.reshape(-1, 3)
 
 
+def cloth_rest_batch(P, Qt):
+    """cloth_rest for many tool frames: P (N, 3), Qt (N, 4) -> (N, NP, 3)."""
+    N = len(P)
+    th = 2 * np.pi * np.arange(DR.SEGS) / DR.SEGS
+    ring = np.stack([DR.RADIUS * np.cos(th), DR.RADIUS * np.sin(th), np.zeros(DR.SEGS)], 1)
+    loc = (ring[None] - np.arange(DR.RINGS)[:, None, None] * np.array([0, 0, DR.SPACING])).reshape(-1, 3)
+    Rm = np.stack([G.quat_to_mat(q) for q in Qt])
+    return P[:, None] + np.einsum('nij,pj->npi', Rm, loc)
+
+
 def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restarts=8):
     """(S (N, STATE_WORDS) float64, meta) for the global env ids."""
     n = len(env_ids)
@@ -144,31 +186,35 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restar
     arm, lo, hi = arm_limits(md)
     tool = int(A['task_tool_link'])
     S = np.zeros((n, DR.STATE_WORDS))
-    tpos = np.zeros((n, 3)); tquat = np.zeros((n, 4))
     init = np.zeros((n, restarts, len(arm)))
-    meta = []
-    for k, e in enumerate(env_ids):
+    jit = np.zeros((n, 3))
+    gl, QH = [], []
+    for k, e in enumerate(env_ids):              # the per-env draws, in the stream's order
         rng = RS._rng(seed, e, episodes[k])
         g = genders[k] if genders is not None else ('male' if rng.integers(2) == 0 else 'female')
-        qh = RS.human_joint_angles(A, g, rng)
-        geo = arm_geometry(A, g, qh)
-        el, wr = geo[3:6], geo[6:9]
-        u = (wr - el) / np.linalg.norm(wr - el)
-        hand_end = wr + u * geo[26] * 2                        # util.py:191
-        tpos[k] = hand_end + u * 0.06 + rng.uniform(-0.02, 0.02, 3)
-        tquat[k] = _frame_z(-u, np.array([0, 0, 1.0]))
+        QH.append(RS.human_joint_angles(A, g, rng))
+        jit[k] = rng.uniform(-0.02, 0.02, 3)
         init[k] = rng.uniform(lo, hi, size=(restarts, len(arm)))
-        S[k, DR.S_GEO:DR.S_GEO + 32] = geo
-        S[k, DR.S_TASK + DR.T_GENDER] = 0 if g == 'male' else 1
-        meta.append(dict(gender=g, impairment='none'))
+        gl.append(g)
+    gl = np.array(gl)
+    geo = np.zeros((n, 32))
+    for g in ('male', 'female'):
+        sel = np.nonzero(gl == g)[0]
+        if len(sel):
+            geo[sel] = arm_geometry_batch(A, g, np.array([QH[k] for k in sel]))
+    el, wr = geo[:, 3:6], geo[:, 6:9]
+    u = (wr - el) / np.linalg.norm(wr - el, axis=1, keepdims=True)
+    hand_end = wr + u * geo[:, 26:27] * 2                  # util.py:191
+    tpos = hand_end + u * 0.06 + jit
+    tquat = _frame_z(-u, np.array([0, 0, 1.0]))
+    S[:, DR.S_GEO:DR.S_GEO + 32] = geo
+    S[:, DR.S_TASK + DR.T_GENDER] = (gl == 'female').astype(float)
     Q, ok = ik_batch(A, tool, tpos, tquat, arm, lo, hi, init)
     CP, CQ, _, _ = RS.robot_fk_batch(A, Q)
-    for k in range(n):
-        S[k, DR.S_Q:DR.S_Q + 7] = Q[k, arm]
-        S[k, DR.S_QT:DR.S_QT + 7] = Q[k, arm]
-        S[k, DR.S_TOOL:DR.S_TOOL + 3] = CP[k, tool]
-        S[k, DR.S_TOOL + 3:DR.S_TOOL + 7] = CQ[k, tool]
-        X = cloth_rest(CP[k, tool], CQ[k, tool])
-        S[k, DR.S_X:DR.S_X + 4 * DR.NP].reshape(DR.NP, 4)[:, :3] = X
-        meta[k]['ik_ok'] = bool(ok[k])
+    S[:, DR.S_Q:DR.S_Q + 7] = Q[:, arm]
+    S[:, DR.S_QT:DR.S_QT + 7] = Q[:, arm]
+    S[:, DR.S_TOOL:DR.S_TOOL + 3] = CP[:, tool]
+    S[:, DR.S_TOOL + 3:DR.S_TOOL + 7] = CQ[:, tool]
+    S[:, DR.S_X:DR.S_X + 4 * DR.NP].reshape(n, DR.NP, 4)[:, :, :3] = cloth_rest_batch(CP[:, tool], CQ[:, tool])
+    meta = [dict(gender=str(gl[k]), impairment='none', ik_ok=bool(ok[k])) for k in range(n)]
     return S, meta
