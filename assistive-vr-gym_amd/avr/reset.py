@@ -276,15 +276,24 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, impairment='none'):
 
 # ----------------------------------------------------------------------------- batched reset
 def _qmul(a, b):
+    a, b = np.asarray(a), np.asarray(b)
     ax, ay, az, aw = a[..., 0], a[..., 1], a[..., 2], a[..., 3]
     bx, by, bz, bw = b[..., 0], b[..., 1], b[..., 2], b[..., 3]
-    return np.stack([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
-                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz], -1)
+    out = np.empty(np.broadcast_shapes(a.shape, b.shape))
+    out[..., 0] = aw * bx + ax * bw + ay * bz - az * by
+    out[..., 1] = aw * by - ax * bz + ay * bw + az * bx
+    out[..., 2] = aw * bz + ax * by - ay * bx + az * bw
+    out[..., 3] = aw * bw - ax * bx - ay * by - az * bz
+    return out
 
 
 def _cross(a, b):
-    return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1], a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
-                     a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
+    a, b = np.asarray(a), np.asarray(b)
+    out = np.empty(np.broadcast_shapes(a.shape, b.shape))
+    out[..., 0] = a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1]
+    out[..., 1] = a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2]
+    out[..., 2] = a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]
+    return out
 
 
 def _qrot(q, v):
