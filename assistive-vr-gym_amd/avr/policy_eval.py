@@ -40,6 +40,16 @@ class RunningMeanStd:
         self.count = tot
 
 
+class DeviceRMS:
+    """ob_rms's mean / variance as device tensors, converted once: torch.as_tensor of a numpy
+    array is a pageable host-to-device copy, which waits for the stream's queued work and would
+    stop the stepping loop from running ahead of the GPU if it happened every step."""
+
+    def __init__(self, ob_rms, device, dtype=torch.float32):
+        self.mean = torch.as_tensor(ob_rms.mean, dtype=dtype, device=device)
+        self.var = torch.as_tensor(ob_rms.var, dtype=dtype, device=device)
+
+
 def normalize(obs, ob_rms):
     """VecNormalize in eval mode (enjoy_vr.py:85-88): obs are not used to update ob_rms."""
     m = torch.as_tensor(ob_rms.mean, dtype=obs.dtype, device=obs.device)
@@ -87,11 +97,42 @@ def load_policy(path, device='cpu'):
     return pol, rms
 
 
-def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=True, setup=None, device=0, seed=1001):
+def _graphed_policy(actor_critic, ob_rms, obs, hxs, masks, deterministic):
+    """The policy forward captured once into a torch CUDA (HIP) graph with static obs / masks
+    buffers; returns step(obs, masks) -> action (a fresh tensor per step), or None when capture is
+    unavailable.  Sampling inside the graph draws from the default generator's Philox stream,
+    whose offset the replays advance."""
+    try:
+        s_obs, s_masks = obs.clone(), masks.clone()
+        side = torch.cuda.Stream(device=obs.device)
+        side.wait_stream(torch.cuda.current_stream(obs.device))
+        with torch.cuda.stream(side), torch.no_grad():
+            for _ in range(3):                      # warm-up (library handles, workspaces) off the capture
+                actor_critic.act(normalize(s_obs, ob_rms), hxs, s_masks, deterministic=deterministic)
+        torch.cuda.current_stream(obs.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g), torch.no_grad():
+            _, s_act, _, _ = actor_critic.act(normalize(s_obs, ob_rms), hxs, s_masks, deterministic=deterministic)
+    except Exception:
+        return None
+
+    def step(o, m):
+        s_obs.copy_(o)
+        s_masks.copy_(m)
+        g.replay()
+        return s_act.clone()
+    return step
+
+
+def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=True, setup=None, device=0, seed=1001, graph=True):
     """Run one 200-step trial in each of n_envs envs (enjoy_vr.py:92-116 per env) and return
     per-env episode return, mean total_force_on_human and final task_success, plus the stepping
     loop's wall time (policy forward + env.step, synchronised at both ends) as loop_s.
-    setup: dict(gender, participant, policy_name[, hipbone_to_mouth_height]) for env.setup."""
+    setup: dict(gender, participant, policy_name[, hipbone_to_mouth_height]) for env.setup.
+    graph: replay the policy forward (normalisation + act) as one captured graph: its ~30 small
+    kernels run back to back between two env steps, and each of them would otherwise add a
+    dispatch gap to the GPU's critical path (the env step waits for the action); eager if the
+    capture fails."""
     from .env import AVRTorchVecEnv
     env = AVRTorchVecEnv(env_id, n_envs, device=device, seed=seed, auto_reset=False)
     try:
@@ -102,14 +143,19 @@ def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=T
         hxs = torch.zeros(n_envs, actor_critic.recurrent_hidden_state_size, device=dev)
         masks = torch.zeros(n_envs, 1, device=dev)
         obs = env.reset()[:, :env.obs_robot_len]
+        ob_rms = DeviceRMS(ob_rms, dev, obs.dtype)
         ret = torch.zeros(n_envs, device=dev)
         force = torch.zeros(n_envs, device=dev)
         info = None
+        policy = _graphed_policy(actor_critic, ob_rms, obs, hxs, masks, deterministic) if graph else None
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(steps):
-            with torch.no_grad():
-                _, action, _, hxs = actor_critic.act(normalize(obs, ob_rms), hxs, masks, deterministic=deterministic)
+            if policy is not None:
+                action = policy(obs, masks)
+            else:
+                with torch.no_grad():
+                    _, action, _, hxs = actor_critic.act(normalize(obs, ob_rms), hxs, masks, deterministic=deterministic)
             obs, rew, done, info = env.step(action)
             obs = obs[:, :env.obs_robot_len]
             masks = (~done).float()[:, None]
@@ -119,6 +165,6 @@ def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=T
         loop_s = time.perf_counter() - t0
         return dict(returns=ret.cpu().numpy(), mean_force=(force / steps).cpu().numpy(),
                     task_success=info['task_success'].cpu().numpy() if info is not None else None, done=done.cpu().numpy(),
-                    loop_s=loop_s, graph_captures=env.sim.graph_captures())
+                    loop_s=loop_s, graph_captures=env.sim.graph_captures(), policy_graph=policy is not None)
     finally:
         env.close()

@@ -402,7 +402,7 @@ def policy_eval_bench(args):
            'ms_per_step': r['loop_s'] / 200 * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
            'data': 'synthetic policy (random-init MLP actor-critic), stochastic actions',
            'config': {'workload': '%s, %d envs, policy evaluation harness' % (name, E), 'task': name, 'envs_per_gpu': E},
-           'graph_captures': r['graph_captures'], 'total_s_with_env_creation_and_reset': total,
+           'graph_captures': r['graph_captures'], 'policy_graph': r.get('policy_graph'), 'total_s_with_env_creation_and_reset': total,
            'mean_return': float(np.mean(r['returns']))}
     print(json.dumps(out), flush=True)
 
