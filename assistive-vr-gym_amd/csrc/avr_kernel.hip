@@ -60,8 +60,6 @@ struct EnvLDS {
     float st[S_CP];     // state words before the contact cache; the cache lives in global memory
     float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
     float btf[MAXB][8];
-    float Mi[MAXD][MAXD];   // Cholesky factor of the mass matrix (lower)
-    float Minv[MAXD][MAXD]; // its inverse
     float vq[MAXD];
     float fv[MAXF][4], fw[MAXF][4];
     float Iinv[MAXF][12];   // world inverse inertia (row-major 3x3)
@@ -73,14 +71,25 @@ struct EnvLDS {
 #ifdef AVR_PROF
     unsigned long long prof[AVR_PROF_SLOTS];
 #endif
+#ifdef AVR_PAD_A_WORDS
+    float pad_a[AVR_PAD_A_WORDS];   // (occupancy experiments: extra LDS per kernel-a block)
+#endif
+    // Phase-overlaid storage (kernel a's LDS footprint sets how many env groups' launches can be
+    // resident at once): the contact update's pool is dead once the new pool is
+    // in global memory; the mass matrix's Cholesky factor is dead once M^-1 is formed, before the
+    // RNEA (and the row enumeration after it) uses its temporaries; M^-1 lives until the rows.
     union __attribute__((aligned(16))) {
         struct {                           // contact update (part A3)
             float ocp[K_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
             int okey[K_MAX_CONTACTS];                   // its (sa | sb << 16) keys
         } k;
-        struct {
-            float rn[6][MAXL][4];          // RNEA temporaries: omega, v_com, alpha, a_com, F, N
+        struct {                           // dynamics and rows
+            union {
+                float rn[6][MAXL][4];      // RNEA temporaries: omega, v_com, alpha, a_com, F, N
+                float Mi[MAXD][MAXD];      // Cholesky factor of the mass matrix (lower)
+            };
             float iw[MAXL][8];             // world inertia (xx yy zz xy xz yz), mass
+            float Minv[MAXD][MAXD];        // M^-1
         } d;
     } u;
 };
@@ -242,15 +251,15 @@ AVR_DI void chol_solve_block(const EnvLDS &L, int c, float *x) {
     for (int i = B0; i < B1; i++) {
         float s = i == c ? 1.f : 0.f;
 #pragma unroll
-        for (int k = B0; k < i; k++) s -= L.Mi[i][k] * y[k];
-        y[i] = s / L.Mi[i][i];
+        for (int k = B0; k < i; k++) s -= L.u.d.Mi[i][k] * y[k];
+        y[i] = s / L.u.d.Mi[i][i];
     }
 #pragma unroll
     for (int i = B1 - 1; i >= B0; i--) {
         float s = y[i];
 #pragma unroll
-        for (int k = i + 1; k < B1; k++) s -= L.Mi[k][i] * x[k];
-        x[i] = s / L.Mi[i][i];
+        for (int k = i + 1; k < B1; k++) s -= L.u.d.Mi[k][i] * x[k];
+        x[i] = s / L.u.d.Mi[i][i];
     }
 }
 
@@ -294,8 +303,8 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
                 s += mi * dot(lina, linb) + dot(Ia, angb);
             }
         } else if (a == b) s = 1.f;
-        L.Mi[a][b] = s;
-        if (a != b) L.Mi[b][a] = 0.f;
+        L.u.d.Mi[a][b] = s;
+        if (a != b) L.u.d.Mi[b][a] = 0.f;
     }
     SYNC();
     PROF_STOP(24, pm);
@@ -317,11 +326,11 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
             const bool live = rob ? jj < K_ND : (jj < NH && i < MAXD);
             float s = 0.f, t = 0.f;
             if (live) {
-                s = L.Mi[j][j];
-                for (int k = k0; k < j; k++) s -= L.Mi[j][k] * L.Mi[j][k];
+                s = L.u.d.Mi[j][j];
+                for (int k = k0; k < j; k++) s -= L.u.d.Mi[j][k] * L.u.d.Mi[j][k];
                 if (i > j) {
-                    t = L.Mi[i][j];
-                    for (int k = k0; k < j; k++) t -= L.Mi[i][k] * L.Mi[j][k];
+                    t = L.u.d.Mi[i][j];
+                    for (int k = k0; k < j; k++) t -= L.u.d.Mi[i][k] * L.u.d.Mi[j][k];
                 }
             }
             // every column's diagonal is positive in exact arithmetic; a lane of either block reports
@@ -329,8 +338,8 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
             if (bad) ok = 0;
             const float d = sqrtf(fmaxf(s, 1e-30f));
             SYNC();
-            if (live && i > j) L.Mi[i][j] = t / d;
-            if (live && i == j) L.Mi[j][j] = d;
+            if (live && i > j) L.u.d.Mi[i][j] = t / d;
+            if (live && i == j) L.u.d.Mi[j][j] = d;
             SYNC();
         }
     }
@@ -342,7 +351,7 @@ AVR_DI bool robot_mass_matrix(const KModel &m, EnvLDS &L) {
         if (lane < K_ND) chol_solve_block<0, K_ND>(L, lane, x);
         else chol_solve_block<K_ND, MAXD>(L, lane, x);
 #pragma unroll
-        for (int k = 0; k < MAXD; k++) L.Minv[k][lane] = x[k];
+        for (int k = 0; k < MAXD; k++) L.u.d.Minv[k][lane] = x[k];
     }
     SYNC();
     PROF_STOP(26, pm);
@@ -360,9 +369,9 @@ AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
     // 1.31M env-steps/s, BedBathing 1.35M -> 1.55M; FeedingJaco unchanged)
     int z = 0;
     asm volatile("" : "+v"(z));
-    const float *Mv = &L.Minv[0][0] + z;
+    const float *Mv = &L.u.d.Minv[0][0] + z;
 #else
-    const float *Mv = &L.Minv[0][0];
+    const float *Mv = &L.u.d.Minv[0][0];
 #endif
 #pragma unroll
     for (int i = 0; i < MAXD; i++) {
@@ -1943,8 +1952,8 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         const float sg = kind == 1 ? -1.f : 1.f;
         float J[MAXD], MJ[MAXD];
 #pragma unroll
-        for (int d = 0; d < MAXD; d++) { J[d] = d == dof ? sg : 0.f; MJ[d] = sg * L.Minv[d][dof]; }
-        const float den = L.Minv[dof][dof];
+        for (int d = 0; d < MAXD; d++) { J[d] = d == dof ? sg : 0.f; MJ[d] = sg * L.u.d.Minv[d][dof]; }
+        const float den = L.u.d.Minv[dof][dof];
         const float inv = den > BT_DENOM_EPS ? 1.f / den : 1.f;
         const float rel = sg * L.vq[dof];
         float *w = row_rec(m, rows, lane);
@@ -2206,6 +2215,10 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     PROF_STOP(0, ps);
     collide_contacts(m, L, cs, gst + S_CP);
     PROF_STOP(13, ps);
+#ifdef AVR_LDS_POISON   // (the dynamics overlay the contact update's storage: re-poison it)
+    for (int i = lane; i < (int)(sizeof(L.u) / 4); i += 64) ((float *)&L.u)[i] = __int_as_float(-1);
+    SYNC();
+#endif
     // unconstrained velocities
     bool ok = robot_mass_matrix(m, L);
     PROF_START(pbias);
@@ -2213,7 +2226,7 @@ AVR_DI bool substep_a(const KModel &m, EnvLDS &L, float dt, float *gst, float *w
     PROF_STOP(27, pbias);
     if (lane < MAXD) {                      // qdd = -M^-1 h, one lane per DoF
         float s = 0.f;
-        for (int k = 0; k < L.nda; k++) s -= L.Minv[lane][k] * L.h[k];
+        for (int k = 0; k < L.nda; k++) s -= L.u.d.Minv[lane][k] * L.h[k];
         L.qdd[lane] = s;
     }
     SYNC();

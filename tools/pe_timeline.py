@@ -22,6 +22,11 @@ def analyze(d):
     cols = [r[1] for r in c.execute('pragma table_info(kernels)')]
     rows = c.execute('select name, start, "end" from kernels order by start').fetchall()
     print('columns', cols[:12])
+    if os.environ.get('DUMP'):
+        t0 = rows[0][1]
+        mid = len(rows) // 4
+        for r in rows[mid:mid + 160]:
+            print('%10.1f %8.1f %s' % ((r[1] - t0) / 1e3, (r[2] - r[1]) / 1e3, r[0][:70]))
     takes = [i for i, r in enumerate(rows) if 'avr_take_step_kernel' in r[0]]
     # one take_step per env group: a step starts at the first of a cluster
     steps = [i for k, i in enumerate(takes) if k == 0 or rows[i][1] - rows[takes[k - 1]][1] > 500e3]
