@@ -124,15 +124,15 @@ def _graphed_policy(actor_critic, ob_rms, obs, hxs, masks, deterministic):
     return step
 
 
-def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=True, setup=None, device=0, seed=1001, graph=True):
+def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=True, setup=None, device=0, seed=1001, graph=False):
     """Run one 200-step trial in each of n_envs envs (enjoy_vr.py:92-116 per env) and return
     per-env episode return, mean total_force_on_human and final task_success, plus the stepping
     loop's wall time (policy forward + env.step, synchronised at both ends) as loop_s.
     setup: dict(gender, participant, policy_name[, hipbone_to_mouth_height]) for env.setup.
-    graph: replay the policy forward (normalisation + act) as one captured graph: its ~30 small
-    kernels run back to back between two env steps, and each of them would otherwise add a
-    dispatch gap to the GPU's critical path (the env step waits for the action); eager if the
-    capture fails."""
+    graph: replay the policy forward (normalisation + act) as one captured graph (eager if the
+    capture fails).  Off by default: measured at 4096 envs it made the loop slower (7.09 vs 6.49
+    ms per step, tools/pe_breakdown.py) -- the eager kernels are short, and the copies into the
+    graph's static buffers add to the chain the env step waits on."""
     from .env import AVRTorchVecEnv
     env = AVRTorchVecEnv(env_id, n_envs, device=device, seed=seed, auto_reset=False)
     try:
