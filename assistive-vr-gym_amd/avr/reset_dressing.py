@@ -104,57 +104,77 @@ def arm_limits(md):
     return arm, lo, hi
 
 
-def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01, res=1e-6):
+def _dls(A, link, cols, arm, lo, hi, Qr, tpos, tquat, iters, res):
+    """Damped-least-squares iterations on the rows of Qr (in place) towards the tool poses
+    (tpos, tquat); a row stops once its position error and rotation angle are below res."""
+    conj = np.array([-1, -1, -1, 1.0])
+    act = np.arange(len(Qr))                       # rows still iterating
+    for it in range(iters + 1):
+        Q = Qr[act]
+        CP, CQ, AX, OR = RS.robot_fk_batch(A, Q)
+        tp, tq = tpos[act], tquat[act]
+        ep = tp - CP[:, link]
+        dq = RS._qmul(tq, CQ[:, link] * conj)
+        dq = np.where(dq[:, 3:4] < 0, -dq, dq)
+        s = np.linalg.norm(dq[:, :3], axis=1)
+        ang = 2.0 * np.arctan2(s, dq[:, 3])
+        live = (np.linalg.norm(ep, axis=1) >= res) | (ang >= res)
+        if it == iters or not live.any():
+            break
+        act, Q, ep, dq, s, ang = act[live], Q[live], ep[live], dq[live], s[live], ang[live]
+        CP, AX, OR = CP[live], AX[live], OR[live]
+        er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
+        J = np.zeros((len(act), 6, len(arm)))
+        for c, l in enumerate(cols):
+            J[:, :3, c] = RS._cross(AX[:, l], CP[:, link] - OR[:, l])
+            J[:, 3:, c] = AX[:, l]
+        JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
+        step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, np.concatenate([ep, er], 1)[..., None])
+        Qr[act[:, None], arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
+    CP, CQ, _, _ = RS.robot_fk_batch(A, Qr)
+    return CP[:, link], CQ[:, link]
+
+
+def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01, res=1e-6, split=2):
     """Vectorised damped-least-squares IK of the tool link's COM frame (RS.ik_batch's update rule)
     with per-env restarts init (N, R, 7); no collision screening (the robot is kinematic here).
-    A row stops iterating once its position error and rotation angle are both below `res`
+    A row stops iterating once its position error and rotation angle are below `res`
     (calculateInverseKinematics' residualThreshold role; at 1e-6 the joint angles stay within
     ~4e-6 rad of running all 150 iterations); the first restart that meets `tol` is kept, else
-    the last one.  Returns (Q (N, ndof), ok (N,))."""
+    the last one.  The first `split` restarts run in turn over the envs still unsolved; the rest
+    run side by side for the few envs left (rows are independent, so the result is the same as
+    running them in turn, with far fewer passes).  Returns (Q (N, ndof), ok (N,))."""
     N, R, _ = init.shape
     nd = int(A['n_dof'])
     chain = RS._chain(A, link)
     cols = [[k for k in chain if A['rl_dof'][k] == d][0] for d in arm]
-    conj = np.array([-1, -1, -1, 1.0])
     Qout = np.zeros((N, nd))
     done = np.zeros(N, bool)
+
+    def accept(P, Qq, tp, tq):
+        pe = np.linalg.norm(tp - P, axis=1)
+        qe = np.minimum(np.linalg.norm(tq - Qq, axis=1), np.linalg.norm(tq + Qq, axis=1))
+        return (pe < tol) & (qe < tol)
     for r in range(R):
         idx = np.nonzero(~done)[0]
         if not len(idx):
             break
-        Qr = np.zeros((len(idx), nd))
-        Qr[:, arm] = init[idx, r]
-        act = np.arange(len(idx))                  # rows of Qr still iterating
-        for it in range(iters + 1):
-            Q = Qr[act]
-            CP, CQ, AX, OR = RS.robot_fk_batch(A, Q)
-            tp, tq = tpos[idx[act]], tquat[idx[act]]
-            ep = tp - CP[:, link]
-            dq = RS._qmul(tq, CQ[:, link] * conj)
-            dq = np.where(dq[:, 3:4] < 0, -dq, dq)
-            s = np.linalg.norm(dq[:, :3], axis=1)
-            ang = 2.0 * np.arctan2(s, dq[:, 3])
-            live = (np.linalg.norm(ep, axis=1) >= res) | (ang >= res)
-            if it == iters or not live.any():
-                break
-            act, Q, ep, dq, s, ang = act[live], Q[live], ep[live], dq[live], s[live], ang[live]
-            CP, AX, OR = CP[live], AX[live], OR[live]
-            er = np.where(s[:, None] > 1e-12, dq[:, :3] / np.maximum(s, 1e-12)[:, None] * ang[:, None], 0.0)
-            J = np.zeros((len(act), 6, len(arm)))
-            for c, l in enumerate(cols):
-                J[:, :3, c] = RS._cross(AX[:, l], CP[:, link] - OR[:, l])
-                J[:, 3:, c] = AX[:, l]
-            JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
-            step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, np.concatenate([ep, er], 1)[..., None])
-            Qr[act[:, None], arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
-        CP, CQ, _, _ = RS.robot_fk_batch(A, Qr)
-        tp, tq = tpos[idx], tquat[idx]
-        pe = np.linalg.norm(tp - CP[:, link], axis=1)
-        qe = np.minimum(np.linalg.norm(tq - CQ[:, link], axis=1), np.linalg.norm(tq + CQ[:, link], axis=1))
-        good = (pe < tol) & (qe < tol)
-        take = good | (r == R - 1)
-        Qout[idx[take]] = Qr[take]
-        done[idx[take]] = good[take]
+        rs = [r] if r < split else list(range(r, R))
+        n = len(idx)
+        Qr = np.zeros((n * len(rs), nd))            # restart-major rows
+        Qr[:, arm] = np.concatenate([init[idx, q] for q in rs])
+        tp, tq = np.tile(tpos[idx], (len(rs), 1)), np.tile(tquat[idx], (len(rs), 1))
+        P, Qq = _dls(A, link, cols, arm, lo, hi, Qr, tp, tq, iters, res)
+        good = accept(P, Qq, tp, tq).reshape(len(rs), n)
+        Qr = Qr.reshape(len(rs), n, nd)
+        first = np.where(good.any(0), good.argmax(0), len(rs) - 1)    # first good restart, else the last
+        pick = Qr[first, np.arange(n)]
+        ok = good[first, np.arange(n)]
+        take = ok | (rs[-1] == R - 1)
+        Qout[idx[take]] = pick[take]
+        done[idx[take]] = ok[take]
+        if len(rs) > 1:
+            break
     return Qout, done
 
 
