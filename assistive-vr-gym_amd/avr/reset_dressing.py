@@ -104,6 +104,32 @@ def arm_limits(md):
     return arm, lo, hi
 
 
+def _fk_chain(A, Q, link):
+    """RS.robot_fk_batch restricted to the chain root .. `link` (the same operations in the same
+    order for those links; other links are left zero): (CP, CQ, AX, OR) (N, n_links, .)."""
+    N = Q.shape[0]
+    nl = int(A['n_links'])
+    chain = sorted(int(k) for k in RS._chain(A, link))
+    bp = np.broadcast_to(A['robot_base'][:3], (N, 3))
+    bq = np.broadcast_to(A['robot_base'][3:], (N, 4))
+    LP = np.zeros((N, nl, 3)); LQ = np.zeros((N, nl, 4))
+    CP = np.zeros((N, nl, 3)); CQ = np.zeros((N, nl, 4))
+    AX = np.zeros((N, nl, 3)); OR = np.zeros((N, nl, 3))
+    for i in chain:
+        p = A['rl_parent'][i]
+        pp, pq = (bp, bq) if p < 0 else (LP[:, p], LQ[:, p])
+        tp = pp + RS._qrot(pq, np.broadcast_to(A['rl_jpos'][i], (N, 3)))
+        tq = RS._qmul(pq, np.broadcast_to(A['rl_jquat'][i], (N, 4)))
+        OR[:, i] = tp
+        AX[:, i] = RS._qrot(tq, np.broadcast_to(A['rl_axis'][i], (N, 3)))
+        if A['rl_jtype'][i] == 1:
+            tq = RS._qmul(tq, RS._qaxis(np.broadcast_to(A['rl_axis'][i], (N, 3)), Q[:, A['rl_dof'][i]]))
+        LP[:, i], LQ[:, i] = tp, tq
+    CP[:, link] = LP[:, link] + RS._qrot(LQ[:, link], np.broadcast_to(A['rl_com_pos'][link], (N, 3)))
+    CQ[:, link] = RS._qmul(LQ[:, link], np.broadcast_to(A['rl_com_quat'][link], (N, 4)))
+    return CP, CQ, AX, OR
+
+
 def _dls(A, link, cols, arm, lo, hi, Qr, tpos, tquat, iters, res):
     """Damped-least-squares iterations on the rows of Qr (in place) towards the tool poses
     (tpos, tquat); a row stops once its position error and rotation angle are below res."""
@@ -111,7 +137,7 @@ def _dls(A, link, cols, arm, lo, hi, Qr, tpos, tquat, iters, res):
     act = np.arange(len(Qr))                       # rows still iterating
     for it in range(iters + 1):
         Q = Qr[act]
-        CP, CQ, AX, OR = RS.robot_fk_batch(A, Q)
+        CP, CQ, AX, OR = _fk_chain(A, Q, link)
         tp, tq = tpos[act], tquat[act]
         ep = tp - CP[:, link]
         dq = RS._qmul(tq, CQ[:, link] * conj)
@@ -131,7 +157,7 @@ def _dls(A, link, cols, arm, lo, hi, Qr, tpos, tquat, iters, res):
         JJ = J @ np.transpose(J, (0, 2, 1)) + 1e-4 * np.eye(6)[None]
         step = np.transpose(J, (0, 2, 1)) @ np.linalg.solve(JJ, np.concatenate([ep, er], 1)[..., None])
         Qr[act[:, None], arm] = np.clip(Q[:, arm] + step[..., 0], lo, hi)
-    CP, CQ, _, _ = RS.robot_fk_batch(A, Qr)
+    CP, CQ, _, _ = _fk_chain(A, Qr, link)
     return CP[:, link], CQ[:, link]
 
 
