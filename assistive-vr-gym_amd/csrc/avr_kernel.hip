@@ -58,7 +58,7 @@ typedef const __attribute__((address_space(1))) f2v *gf2p;
 #define AVR_PROF_SLOTS 48   // diagnostic build: per-env cycle / event counters (tools/prof_phases.py)
 struct EnvLDS {
     float st[S_CP];     // state words before the contact cache; the cache lives in global memory
-    float lk[MAXL][8], cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
+    float cm[MAXL][8], ax[MAXL][4], org[MAXL][4];
     float btf[MAXB][8];
     float vq[MAXD];
     float fv[MAXF][4], fw[MAXF][4];
@@ -78,7 +78,10 @@ struct EnvLDS {
     // resident at once): the contact update's pool is dead once the new pool is
     // in global memory; the mass matrix's Cholesky factor is dead once M^-1 is formed, before the
     // RNEA (and the row enumeration after it) uses its temporaries; M^-1 lives until the rows.
+    // robot_fk's joint frames (lk) are its own scratch (dead when it returns; kernel a, which gets
+    // its frames from the pair kernel, never runs it, and no caller holds u data across it).
     union __attribute__((aligned(16))) {
+        float lk[MAXL][8];                 // robot_fk: joint frames + joint value
         struct {                           // contact update (part A3)
             float ocp[K_MAX_CONTACTS * AVR_CP_WORDS];   // previous contact pool, updated in place
             int okey[K_MAX_CONTACTS];                   // its (sa | sb << 16) keys
@@ -154,6 +157,10 @@ static_assert(MAXSH % 64 == 0, "shape info staged 64 per pass");
 template <class LT>
 AVR_DI int lgo(const LT &L, const KModel &m) { return L.gender * m.nla; }   // gendered table offset
 
+// robot_fk's joint-frame scratch: a member of EnvLDS's phase union, of PairsLDS's FK struct
+AVR_DI float (*lk_of(EnvLDS &L))[8] { return L.u.lk; }
+AVR_DI float (*lk_of(PairsLDS &L))[8] { return L.lk; }
+
 template <class LT>
 AVR_DI void robot_fk(const KModel &m, LT &L) {
     const int i = lane_id();
@@ -173,8 +180,8 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
         const int dof = gld(m.rl_dof + (i));
         const float qv = dof >= 0 ? L.st[S_Q + dof] : 0.f;
         const qt qj = jt == AVR_J_REVOLUTE ? qaxis(axl, qv) : Q(0, 0, 0, 1);
-        sttf(L.lk[i], jo);
-        L.lk[i][7] = qv;
+        sttf(lk_of(L)[i], jo);
+        lk_of(L)[i][7] = qv;
         stq(L.cm[i], qj);
         st3(L.cm[i] + 4, axl);
         L.cm[i][7] = (float)jt;
@@ -191,8 +198,8 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
 #endif
         for (unsigned b = am; b; b &= b - 1u) {
             const int k = __builtin_ctz(b);
-            const tf jo = ldtf(L.lk[k]);
-            const float qv = L.lk[k][7];
+            const tf jo = ldtf(lk_of(L)[k]);
+            const float qv = lk_of(L)[k][7];
             const qt qj = ldq(L.cm[k]);
             const v3 ax = ld3(L.cm[k] + 4);
             const int jt = (int)L.cm[k][7];
@@ -207,7 +214,7 @@ AVR_DI void robot_fk(const KModel &m, LT &L) {
     if (mine) {
         st3(L.org[i], org);
         st3(L.ax[i], axw);
-        sttf(L.lk[i], t);
+        sttf(lk_of(L)[i], t);
         sttf(L.cm[i], tfmul(t, com));
     }
     SYNC();
