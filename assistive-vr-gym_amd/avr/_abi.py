@@ -76,26 +76,9 @@ SI = _scratch_layout()
 BB = _scratch_layout(TASK_BEDBATH)
 
 
-def _header_defines(path, prefix):
-    """Numeric #defines NAME -> value of a C header (the constants shared with the kernels)."""
-    import re
-    env = {}
-    for line in open(path):
-        m = re.match(r'#define\s+(%s\w+)\s+(.+?)\s*(/\*.*)?$' % prefix, line)
-        if not m:
-            continue
-        expr = m.group(2)
-        for k in sorted(env, key=len, reverse=True):
-            expr = expr.replace(k, repr(env[k]))
-        try:
-            env[m.group(1)] = eval(expr, {'__builtins__': {}})
-        except Exception:
-            pass
-    return env
-
-
-# DressingJaco-v0 (build-defined, include/avr_dressing.h): its constants and state layout
-_DRH = _header_defines(os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), 'include', 'avr_dressing.h'), 'AVR_DR_')
+# DressingJaco-v0 (build-defined, include/avr_dressing.h): its constants and state layout, from
+# the module avr.build generates from the header (so the package needs no header at import time)
+from ._dressing_consts import DEFINES as _DRH  # noqa: E402
 DR = _Layout(TASK=TASK_DRESSING, ACT_DIM=7, INFO_DIM=2, **{k[len('AVR_DR_'):]: v for k, v in _DRH.items()})
 DR.STATE_WORDS = _DRH['AVR_DR_STATE_WORDS']
 DR.OBS_DIM = _DRH['AVR_DR_OBS_DIM']

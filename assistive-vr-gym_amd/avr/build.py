@@ -126,11 +126,49 @@ def build_wavetime(force=False):
     return build_lib(force=force, extra=('-DAVR_WAVETIME',), out=os.path.join(HERE, 'libavr_wt.so'))
 
 
+def header_defines(path, prefix):
+    """Numeric #defines NAME -> value of a C header (the constants shared with the kernels)."""
+    import re
+    env = {}
+    for line in open(path):
+        m = re.match(r'#define\s+(%s\w+)\s+(.+?)\s*(/\*.*)?$' % prefix, line)
+        if not m:
+            continue
+        expr = m.group(2)
+        for k in sorted(env, key=len, reverse=True):
+            expr = expr.replace(k, repr(env[k]))
+        try:
+            env[m.group(1)] = eval(expr, {'__builtins__': {}})
+        except Exception:
+            pass
+    return env
+
+
+DRESSING_HEADER = os.path.join(ROOT, 'include', 'avr_dressing.h')
+DRESSING_CONSTS = os.path.join(HERE, '_dressing_consts.py')
+
+
+def dressing_consts_source():
+    d = header_defines(DRESSING_HEADER, 'AVR_DR_')
+    lines = ['"""DressingJaco-v0 constants (include/avr_dressing.h), generated by avr.build.write_dressing_consts();',
+             'tests/test_dressing.py checks them against the header.  Do not edit by hand."""', '', 'DEFINES = {']
+    lines += ['    %r: %r,' % (k, v) for k, v in d.items()]
+    return '\n'.join(lines + ['}']) + '\n'
+
+
+def write_dressing_consts():
+    """Regenerate avr/_dressing_consts.py from include/avr_dressing.h when they differ."""
+    src = dressing_consts_source()
+    if not os.path.exists(DRESSING_CONSTS) or open(DRESSING_CONSTS).read() != src:
+        open(DRESSING_CONSTS, 'w').write(src)
+
+
 def build_oracle():
     subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
 
 
 def build_all(force=False):
+    write_dressing_consts()
     build_lib(force=force)
     build_poison(force=force)
     build_oracle()

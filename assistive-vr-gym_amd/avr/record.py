@@ -17,10 +17,23 @@
     exactly as a live episode's;
   * replay_vr_savemeta.py (observations, rewards, actions, forces, task success of every
     recording) -> savemeta().
+
+Reference-format recordings (a participant directory the reference wrote: setup.pkl,
+actions.pkl, frame_%d.bullet; feeding.py:50-54,146-157,322-330, scratch_itch.py:136-144,268-272,
+bed_bathing.py:163-170,352-356) are read by load_reference_pickle -- a restricted unpickler that
+executes nothing from the file: it admits lists, tuples, dicts, strings, numbers and numpy arrays
+/ scalars of numeric dtypes, rebuilt by this module's own constructors from the raw bytes; any
+other global refuses the file -- and replayed by ReferenceReplayEnv (replay_setup + reset + step,
+env.py:74-78, feeding.py:31-39): the recorded gender is set up, the episode starts from this
+build's reset for it, and the recorded actions are re-simulated.  The frame_%d.bullet states are
+Bullet serializer output and cannot be restored here, so the replayed trajectory is the
+re-simulation of the participant's actions, not the participant's recorded frames.
+savemeta_reference() is replay_vr_savemeta.py over such directories.
 """
 import glob
 import json
 import os
+import pickle
 
 import numpy as np
 
@@ -159,5 +172,240 @@ def savemeta(pattern, out=None, device=0):
             for k in ('observations', 'rewards', 'actions', 'forces', 'task_success'):
                 flat['%d_%s' % (i, k)] = v[k]
         flat['dirs'] = np.array(list(res))
+        np.savez(out, **flat)
+    return res
+
+
+# ---------------------------------------------------------------- reference-format recordings
+
+_NUMERIC_KINDS = 'biufc'
+
+
+class _DType:
+    """numpy.dtype(name, align, copy) as pickled; only numeric dtypes are admitted."""
+
+    def __init__(self, name, align=False, copy=True):
+        if not isinstance(name, str):
+            raise pickle.UnpicklingError('dtype spec %r' % (name,))
+        dt = np.dtype(name)
+        if dt.kind not in _NUMERIC_KINDS or dt.fields is not None or dt.subdtype is not None:
+            raise pickle.UnpicklingError('dtype %r is not a plain numeric dtype' % (name,))
+        self.dtype = dt
+
+    def __setstate__(self, state):
+        # (version, byteorder, subdescr, names, fields, elsize, alignment, flags)
+        if not isinstance(state, tuple) or len(state) < 2 or state[1] not in ('<', '>', '=', '|'):
+            raise pickle.UnpicklingError('dtype state %r' % (state,))
+        if state[2] is not None or state[3] is not None or state[4] is not None:
+            raise pickle.UnpicklingError('structured dtype')
+        if state[1] in '<>':
+            self.dtype = self.dtype.newbyteorder(state[1])
+
+
+def _as_dtype(d):
+    if isinstance(d, _DType):
+        return d.dtype
+    raise pickle.UnpicklingError('expected a dtype, got %r' % type(d))
+
+
+class _ArrayBuilder:
+    """numpy.core.multiarray._reconstruct(ndarray, (0,), b'b') + BUILD(state) as pickled
+    (protocols 0-4): the state carries shape, dtype, order and the raw bytes."""
+
+    def __init__(self, cls, shape, code):
+        if cls is not _NDARRAY:
+            raise pickle.UnpicklingError('only numpy.ndarray is reconstructed')
+        self.array = None
+
+    def __setstate__(self, state):
+        if not isinstance(state, tuple) or len(state) != 5:
+            raise pickle.UnpicklingError('ndarray state')
+        _, shape, dt, fortran, raw = state
+        dt = _as_dtype(dt)
+        if isinstance(raw, str):               # protocol 0-2 pickles carry the bytes as latin-1 text
+            raw = raw.encode('latin1')
+        if not isinstance(raw, (bytes, bytearray)):
+            raise pickle.UnpicklingError('ndarray data of type %r' % type(raw))
+        shape = tuple(int(s) for s in shape)
+        n = int(np.prod(shape)) if shape else 1
+        if n * dt.itemsize != len(raw):
+            raise pickle.UnpicklingError('ndarray of shape %s / %s with %d data bytes' % (shape, dt, len(raw)))
+        a = np.frombuffer(bytes(raw), dt, count=n).reshape(shape, order='F' if fortran else 'C')
+        self.array = a.astype(dt.newbyteorder('='), copy=True)
+
+
+def _frombuffer(buf, dt, shape, order):
+    """numpy.core.numeric._frombuffer as pickled by protocol 5 (in-band buffer)."""
+    dt = _as_dtype(dt)
+    raw = bytes(buf)
+    shape = tuple(int(s) for s in shape)
+    n = int(np.prod(shape)) if shape else 1
+    if n * dt.itemsize != len(raw) or order not in ('C', 'F'):
+        raise pickle.UnpicklingError('ndarray buffer')
+    return np.frombuffer(raw, dt, count=n).reshape(shape, order=order).astype(dt.newbyteorder('='), copy=True)
+
+
+def _scalar(dt, raw=None):
+    """numpy.core.multiarray.scalar(dtype, bytes): a numpy scalar (e.g. a float64 height)."""
+    dt = _as_dtype(dt)
+    if isinstance(raw, str):
+        raw = raw.encode('latin1')
+    if not isinstance(raw, (bytes, bytearray)) or len(raw) != dt.itemsize:
+        raise pickle.UnpicklingError('numpy scalar data')
+    return np.frombuffer(bytes(raw), dt, count=1)[0].astype(dt.newbyteorder('=')).item()
+
+
+def _codecs_encode(s, enc='utf-8'):
+    if enc != 'latin1' or not isinstance(s, str):
+        raise pickle.UnpicklingError('_codecs.encode(%r)' % enc)
+    return s.encode('latin1')
+
+
+_NDARRAY = object()
+_MODS = ('numpy.core.multiarray', 'numpy._core.multiarray')
+_SAFE = {('numpy', 'dtype'): _DType, ('numpy', 'ndarray'): _NDARRAY, ('_codecs', 'encode'): _codecs_encode}
+for _m in _MODS:
+    _SAFE[(_m, '_reconstruct')] = _ArrayBuilder
+    _SAFE[(_m, 'scalar')] = _scalar
+for _m in ('numpy.core.numeric', 'numpy._core.numeric'):
+    _SAFE[(_m, '_frombuffer')] = _frombuffer
+
+
+class _RestrictedUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        f = _SAFE.get((module, name))
+        if f is None:
+            raise pickle.UnpicklingError('%s.%s is not admitted by the recording reader' % (module, name))
+        return f
+
+    def persistent_load(self, pid):
+        raise pickle.UnpicklingError('persistent ids are not admitted')
+
+
+def _finish(x):
+    if isinstance(x, _ArrayBuilder):
+        if x.array is None:
+            raise pickle.UnpicklingError('ndarray without state')
+        return x.array
+    if isinstance(x, (_DType,)) or x is _NDARRAY:
+        raise pickle.UnpicklingError('stray numpy object')
+    if isinstance(x, list):
+        return [_finish(v) for v in x]
+    if isinstance(x, tuple):
+        return tuple(_finish(v) for v in x)
+    if isinstance(x, dict):
+        return {_finish(k): _finish(v) for k, v in x.items()}
+    if x is None or isinstance(x, (bool, int, float, complex, str, bytes, np.ndarray)):
+        return x
+    raise pickle.UnpicklingError('object of type %r' % type(x))
+
+
+def load_reference_pickle(path):
+    """Read a reference recording's pickle (setup.pkl / actions.pkl) without executing anything
+    from the file (see the module docstring); raises pickle.UnpicklingError on anything else."""
+    with open(path, 'rb') as f:
+        return _finish(_RestrictedUnpickler(f).load())
+
+
+def write_reference_recording(directory, robot_type, gender, hipbone_to_mouth_height, actions):
+    """Write setup.pkl and actions.pkl as the reference's VR episodes do (feeding.py:50-54,
+    328-329): [robot_type, gender, hipbone_to_mouth_height] and the list of 200 actions."""
+    os.makedirs(directory, exist_ok=True)
+    with open(os.path.join(directory, 'setup.pkl'), 'wb') as f:
+        pickle.dump([robot_type, gender, hipbone_to_mouth_height], f)
+    with open(os.path.join(directory, 'actions.pkl'), 'wb') as f:
+        pickle.dump([np.asarray(a, np.float32) for a in actions], f)
+
+
+_TASK_KEYS = (('scratch_itch', 'ScratchItch'), ('feeding', 'Feeding'), ('drinking', 'Drinking'), ('bed_bathing', 'BedBathing'))
+
+
+def reference_env_id(directory):
+    """The env id replay_vr_savemeta.py derives from a recording directory's name
+    (replay_vr_savemeta.py:20): task from 'scratch_itch' / 'feeding' / 'drinking' /
+    'bed_bathing', robot 'Jaco' if 'jaco' is in the name, else 'PR2'.  None: skipped."""
+    d = os.path.basename(os.path.normpath(directory))
+    for k, name in _TASK_KEYS:
+        if k in d:
+            return '%s%s-v0' % (name, 'Jaco' if 'jaco' in d else 'PR2')
+    return None
+
+
+class ReferenceReplayEnv:
+    """replay_setup(dir) + reset/step over a reference participant directory (setup.pkl,
+    actions.pkl).  reset() sets up the recorded gender and starts from this build's reset for it;
+    each step() re-simulates the next recorded action (the action passed in is ignored, as in
+    feeding.py:38); done after the last recorded action (feeding.py:79-80: 200).
+
+    The compiled humans have the reference's default proportions; a recording with another
+    hipbone_to_mouth_height raises NotImplementedError unless default_proportions=True, which
+    replays it on the default human (noted in `self.proportions`)."""
+
+    def __init__(self, directory, env_id=None, device=0, seed=1001, default_proportions=False):
+        from . import env as EV
+        self.directory = directory
+        self.env_id = env_id or reference_env_id(directory)
+        if self.env_id is None:
+            raise ValueError('%s: no task name in the directory name (replay_vr_savemeta.py:20)' % directory)
+        setup = load_reference_pickle(os.path.join(directory, 'setup.pkl'))
+        if not isinstance(setup, (list, tuple)) or len(setup) != 3:
+            raise ValueError('%s/setup.pkl: expected [robot_type, gender, hipbone_to_mouth_height]' % directory)
+        self.robot_type, self.gender, hip = setup
+        self.hipbone_to_mouth_height = None if hip is None else float(hip)
+        acts = load_reference_pickle(os.path.join(directory, 'actions.pkl'))
+        self.action_list = np.asarray([np.asarray(a, np.float32).reshape(-1) for a in acts], np.float32)
+        self.env = EV.AVRVecEnv(self.env_id, 1, device=device, seed=seed, auto_reset=False, prefetch=False)
+        if self.action_list.ndim != 2 or self.action_list.shape[1] != self.env.L.ACT_DIM:
+            raise ValueError('%s/actions.pkl: actions of shape %s, the task takes %d' % (directory, self.action_list.shape, self.env.L.ACT_DIM))
+        default = 0.6 if self.gender == 'male' else 0.54
+        self.proportions = 'recorded'
+        hip = self.hipbone_to_mouth_height
+        if hip is not None and abs(hip - default) > 1e-9:
+            if not default_proportions:
+                self.env.close()
+                raise NotImplementedError('%s: hipbone_to_mouth_height %.4f; only the default %.2f (%s) is compiled '
+                                          '(default_proportions=True replays on it)' % (directory, hip, default, self.gender))
+            hip, self.proportions = None, 'default (recorded %.4f)' % self.hipbone_to_mouth_height
+        self.env.setup(self.gender, -1, '', hip)
+        self.iteration = 0
+
+    def reset(self):
+        self.iteration = 0
+        return self.env.reset()
+
+    def step(self, action=None):
+        obs, rew, _, info = self.env.step(self.action_list[self.iteration][None])
+        self.iteration += 1
+        done = np.full(1, self.iteration >= len(self.action_list))
+        return obs, rew, done, info
+
+    def close(self):
+        self.env.close()
+
+
+def savemeta_reference(replay_dir, out=None, device=0, default_proportions=False):
+    """replay_vr_savemeta.py: every participant_*/* recording under replay_dir replayed; per
+    directory the observations, rewards, actions, total_force_on_human per step and the final
+    task_success (an .npz at `out`, not a pickle)."""
+    res = {}
+    for d in sorted(glob.glob(os.path.join(replay_dir, 'participant_*', '*'))):
+        if reference_env_id(d) is None or not os.path.exists(os.path.join(d, 'setup.pkl')):
+            continue
+        r = ReferenceReplayEnv(d, device=device, default_proportions=default_proportions)
+        r.reset()
+        obs, rews, forces, succ = [], [], [], 0.0
+        done = np.zeros(1, bool)
+        while not done.all():
+            o, rw, done, info = r.step()
+            obs.append(o[0]); rews.append(float(rw[0])); forces.append(float(info['total_force_on_human'][0]))
+            succ = float(info['task_success'][0])
+        res[d] = dict(env_id=r.env_id, observations=np.stack(obs), rewards=np.array(rews), actions=r.action_list,
+                      forces=np.array(forces), task_success=succ, proportions=r.proportions)
+        r.close()
+    if out:
+        flat = {'dirs': np.array(list(res))}
+        for i, v in enumerate(res.values()):
+            for k in ('observations', 'rewards', 'actions', 'forces', 'task_success'):
+                flat['%d_%s' % (i, k)] = np.asarray(v[k])
         np.savez(out, **flat)
     return res

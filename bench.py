@@ -101,6 +101,7 @@ def cpu_baseline(name, md, A, seconds, threads, impairment):
         if el >= seconds and steps >= 2:
             break
     return dict(value=n * steps / el, unit='env-steps/s', cores=threads, host_cpus=os.cpu_count(), kind='port',
+                short='%d envs x %d steps, fp64 oracle, %d OpenMP threads' % (n, steps, threads),
                 sample='%s, %d envs x %d gym steps (%.1f s) after a %d-frame settle; fp64 oracle, OpenMP over envs on %d threads '
                        '(the GPU box\'s CPU share, OMP_NUM_THREADS; os.cpu_count() reports the whole host)' % (
                            name, n, steps, el, T['settle'], threads))
@@ -331,54 +332,75 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
         'vs_baseline': None,
         'dtype': 'f32',
         'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the reset path (%d distinct per GPU, tiled)' % pool,
-        'config': {'workload': T['workload'] % E, 'task': name, 'envs_per_gpu': E,
-                   'impairment': args.impairment, 'tremor_fraction': n_tremor / pool,
-                   'global_envs': world * E, 'substeps_per_env_step': T['substeps'], 'solver_iterations': T['iters'],
-                   'parallelism': 'env-sharded x%d' % world, 'rollout_gather_every': G if world > 1 else None,
-                   'dist_backend': args.dist_backend if world > 1 else None,
-                   'env_groups': sim.env_groups()},
+        'config': {'workload': T['workload'] % E, 'task': name, 'envs_per_gpu': E, 'impairment': args.impairment,
+                   'parallelism': 'env-sharded x%d' % world, 'env_groups': sim.env_groups()},
         'roofline': {'bound': bound, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'fracs': fracs, 'limiter': limiter,
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'limiter': limiter,
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
-                     'sq_by_kernel': pmc.get('sq') if pmc else None,
-                     'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
-                     'scope': ('one env-step = one dress_step launch (the gym step\'s %d sub-steps inside it); ' % T['substeps']
-                               if name == 'DressingJaco-v0' else
-                               'one env-step = 1 take_step + %d x (%s) + 1 task launch; ' % (
-                                   T['substeps'], ', '.join(k[4:-7] for k in kernels if k not in ('avr_take_step_kernel', 'avr_task_kernel')))) +
-                              'achieved = algorithmic bytes of the step / summed launch durations, measured in a separate pass with '
-                              'one env group (per-kernel events need one stream); the timed loop runs env_groups concurrent launch '
-                              'sequences, so its stream time per step is below the summed durations; traffic = PMC HBM bytes of the '
-                              'step and valu_busy = PMC VALU instructions x %.0f cycles / (%d SIMDs x %.1f GHz x ms_per_step), both from '
-                              'the task\'s committed rocprofv3 summary (%s)' % (
-                                  VALU_CYC, SIMDS, CLOCK_HZ / 1e9, pmc['source'] if pmc else 'none matching'),
-                     'bytes_per_env_step': bpe, 'layout_bytes_per_env_step': layout_bytes_per_env_step(L),
-                     'step_kernel_ms': step_kernel_ms, 'stream_ms_per_step': kern_ms,
-                     'dominant_kernel': dominant, 'kernels': kernels},
+                     'bytes_per_env_step': bpe, 'dominant_kernel': dominant,
+                     'dominant_avg_ms': kernels[dominant]['avg_ms']},
         # fault bits only (bits 0-4); bit 5 (an env under the EPA budget) is informational
         'nan_or_overflow_envs': int(np.count_nonzero(flags & _lib.FLAGS_FAULT_MASK)),
-        'flagged_envs_by_bit': {fname: int(np.count_nonzero(flags & (1 << b))) for b, fname in enumerate(
-            ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full', 'coop_capped'))},
-        'reset_pool_sha1': pool_sha,
     }
+    # the long-form record (per-kernel tables, PMC issue shares, the scope of each figure) goes to
+    # a side file, so that the printed line stays within the driver's record
+    detail = {'task': name, 'value': value, 'ms_per_step': ms_per_step, 'roofline_fracs': fracs,
+              'traffic_GBs': (traffic * 1e-9 / (step_kernel_ms * 1e-3)) if traffic else None,
+              'sq_by_kernel': pmc.get('sq') if pmc else None, 'pmc_source': pmc['source'] if pmc else None,
+              'layout_bytes_per_env_step': layout_bytes_per_env_step(L), 'step_kernel_ms': step_kernel_ms,
+              'stream_ms_per_step': kern_ms, 'kernels': kernels, 'scope': SCOPE,
+              'config': dict(out['config'], tremor_fraction=n_tremor / pool, global_envs=world * E,
+                             substeps_per_env_step=T['substeps'], solver_iterations=T['iters'],
+                             rollout_gather_every=G if world > 1 else None,
+                             dist_backend=args.dist_backend if world > 1 else None),
+              'flagged_envs_by_bit': {fname: int(np.count_nonzero(flags & (1 << b))) for b, fname in enumerate(
+                  ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full', 'coop_capped'))},
+              'reset_pool_sha1': pool_sha}
     sim.close()
     if rank == 0 and world == 1 and cpu_seconds > 0:
         # the host threads this process may use: OMP_NUM_THREADS (the GPU box's CPU share, 16 per
         # GPU; os.cpu_count() reports the whole machine there), else every CPU of this host
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-        out['cpu_baseline'] = cpu_baseline(name, md, A, cpu_seconds, max(1, threads), args.impairment)
+        cb = cpu_baseline(name, md, A, cpu_seconds, max(1, threads), args.impairment)
+        detail['cpu_baseline'] = cb
+        out['cpu_baseline'] = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind')}
+        out['cpu_baseline']['sample'] = cb['short']
     elif rank == 0:
         out['cpu_baseline'] = None
-    return out
+    return out, detail
 
 
 # the other single-GPU configs BASELINE.json names (configs[2], the PR2 variant of configs[3],
 # configs[4] as the build-defined DressingJaco),
 # timed after the headline in the same default run: extra keys of the one JSON line
 OTHER_TASKS = ('ScratchItchPR2-v0', 'BedBathingPR2-v0', 'DressingJaco-v0')
-OTHER_KEYS = ('value', 'unit', 'steps', 'warmup', 'ms_per_step', 'config', 'roofline', 'nan_or_overflow_envs', 'flagged_envs_by_bit',
-              'cpu_baseline')
+OTHER_KEYS = ('value', 'ms_per_step', 'steps', 'nan_or_overflow_envs', 'cpu_baseline')
+ROOF_KEYS = ('frac', 'achieved', 'traffic', 'valu_busy', 'limiter', 'dominant_kernel', 'dominant_avg_ms')
+# what each figure covers (kept out of the printed line, written to the detail file)
+SCOPE = ('one env-step = one gym step of one env: 1 take_step + S x (pairs, narrowphase, a, b4) + 1 task launch '
+         '(DressingJaco: one dress_step launch); achieved = algorithmic bytes of the step (SURVEY 8(d)) / summed launch '
+         'durations, measured with HIP events on the sim stream in a separate pass with one env group; the timed loop runs '
+         'env_groups concurrent launch sequences; traffic = PMC HBM bytes per step (FETCH_SIZE x 2 + WRITE_SIZE) and '
+         'valu_busy = PMC VALU instructions x %.0f cycles / (%d SIMDs x %.1f GHz x ms_per_step), both from the task\'s committed '
+         'rocprofv3 summary under profiles/' % (VALU_CYC, SIMDS, CLOCK_HZ / 1e9))
+DETAIL_PATH = os.environ.get('AVR_BENCH_DETAIL', os.path.join(ROOT, 'gpurun_out', 'bench_detail.json'))
+
+
+def compact_other(o):
+    c = {k: o[k] for k in OTHER_KEYS}
+    c['envs'] = o['config']['envs_per_gpu']
+    c['roofline'] = {k: o['roofline'][k] for k in ROOF_KEYS}
+    return c
+
+
+def write_detail(details):
+    try:
+        os.makedirs(os.path.dirname(DETAIL_PATH), exist_ok=True)
+        with open(DETAIL_PATH, 'w') as f:
+            json.dump(details, f, indent=1)
+        return os.path.relpath(DETAIL_PATH, ROOT)
+    except OSError:
+        return None
 
 
 def policy_eval_bench(args):
@@ -460,14 +482,17 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_seconds
-    out = run_task(args.task, args, args.steps, args.warmup, world, rank, local, dist, gloo, dev, cpu_s)
+    out, det = run_task(args.task, args, args.steps, args.warmup, world, rank, local, dist, gloo, dev, cpu_s)
+    details = [det]
     if rank == 0 and world == 1 and args.task == 'FeedingJaco-v0' and args.other_steps > 0:
         out['other_tasks'] = {}
         for name in OTHER_TASKS:
-            o = run_task(name, args, args.other_steps, args.warmup, world, rank, local, dist, gloo, dev, min(cpu_s, 5.0))
-            out['other_tasks'][name] = {k: o[k] for k in OTHER_KEYS}
+            o, det = run_task(name, args, args.other_steps, args.warmup, world, rank, local, dist, gloo, dev, min(cpu_s, 5.0))
+            out['other_tasks'][name] = compact_other(o)
+            details.append(det)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        out['detail'] = write_detail(details)
+        print(json.dumps(out, separators=(',', ':')), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -106,6 +106,15 @@ typedef double real;
 #endif
 
 /* ---------------------------------------------------------------- assumed Bullet constants */
+/* Precision probe build (-DAVR_ORACLE_PROBE, tools only): the fp64 oracle with chosen stage
+ * outputs rounded to float (avr_oracle_probe_mask bits), to find where fp32 rounding is amplified */
+#ifdef AVR_ORACLE_PROBE
+static unsigned probe_mask;
+#define PRB(k, x) ((probe_mask >> (k) & 1) ? (real)(float)(x) : (x))
+#else
+#define PRB(k, x) (x)
+#endif
+#define PRB3(k, v) V(PRB(k, (v).x), PRB(k, (v).y), PRB(k, (v).z))
 #define BT_ANGULAR_MOTION_THRESHOLD (0.5 * 1.5707963267948966) /* btMultiBody quat update   */
 #define BT_BROADPHASE_EXPAND 0.02      /* gContactBreakingThreshold AABB fattening           */
 #define BT_DENOM_EPS 1e-12             /* SIMD_EPSILON guard on jacDiagABInv (double build)  */
@@ -286,6 +295,11 @@ static void robot_fk(const model *m, real *st, ws_t *w) {
         else if (m->jtype[i] == AVR_J_PRISMATIC) t.p = add(t.p, scl(w->ax[i], st[S_Q + dof]));
         w->lk[i] = t;
         w->cm[i] = tfmul(t, m->com[i]);
+#ifdef AVR_ORACLE_PROBE
+        w->org[i] = PRB3(0, w->org[i]); w->ax[i] = PRB3(0, w->ax[i]);
+        w->cm[i].p = PRB3(0, w->cm[i].p);
+        w->cm[i].q = Q(PRB(0, w->cm[i].q.x), PRB(0, w->cm[i].q.y), PRB(0, w->cm[i].q.z), PRB(0, w->cm[i].q.w));
+#endif
     }
     if (m->hc)
         for (int k = 0; k < m->d.hc_n; k++) {
@@ -342,6 +356,9 @@ static int robot_mass_matrix(const model *m, ws_t *w) {
             }
         }
     }
+#ifdef AVR_ORACLE_PROBE
+    for (int a = 0; a < nd; a++) for (int b = 0; b <= a; b++) M[a][b] = PRB(2, M[a][b]);
+#endif
     /* Cholesky M = L L^T (lower) */
     for (int j = 0; j < nd; j++) {
         real s = M[j][j];
@@ -355,6 +372,9 @@ static int robot_mass_matrix(const model *m, ws_t *w) {
             w->Mi[i][j] = t / d;
         }
     }
+#ifdef AVR_ORACLE_PROBE
+    for (int a = 0; a < nd; a++) for (int b = 0; b <= a; b++) w->Mi[a][b] = PRB(3, w->Mi[a][b]);
+#endif
     return 0;
 }
 
@@ -371,6 +391,9 @@ static void chol_solve(const model *m, const ws_t *w, const real *b, real *x) {
         for (int k = i + 1; k < nd; k++) s -= w->Mi[k][i] * x[k];
         x[i] = s / w->Mi[i][i];
     }
+#ifdef AVR_ORACLE_PROBE
+    for (int i = 0; i < nd; i++) x[i] = PRB(4, x[i]);
+#endif
 }
 
 /* Bias forces h(q,qd) by recursive Newton-Euler in world frame: Coriolis/centrifugal,
@@ -999,7 +1022,7 @@ static real ep_denom(const model *m, int kind, const real *J, const real *MJ) {
 
 static void ep_apply(const model *m, ws_t *w, int kind, int idx, const real *MJ, real imp) {
     if (kind == 1) {
-        for (int d = 0; d < m->nd; d++) w->dq[d] += MJ[d] * imp;
+        for (int d = 0; d < m->nd; d++) w->dq[d] = PRB(8, w->dq[d] + MJ[d] * imp);
     } else if (kind == 2) {
         w->dfv[idx] = add(w->dfv[idx], scl(ld3(MJ), imp));
         w->dfw[idx] = add(w->dfw[idx], scl(ld3(MJ + 3), imp));
@@ -1007,8 +1030,11 @@ static void ep_apply(const model *m, ws_t *w, int kind, int idx, const real *MJ,
 }
 
 static void row_finish(const model *m, ws_t *w, row_t *r) {
+#ifdef AVR_ORACLE_PROBE
+    for (int i = 0; i < K_MAX_DOF; i++) { r->JA[i] = PRB(6, r->JA[i]); r->JB[i] = PRB(6, r->JB[i]); r->MA[i] = PRB(6, r->MA[i]); r->MB[i] = PRB(6, r->MB[i]); }
+#endif
     real den = ep_denom(m, r->kindA, r->JA, r->MA) + ep_denom(m, r->kindB, r->JB, r->MB);
-    r->inv = den > R(BT_DENOM_EPS) ? 1 / den : 1;
+    r->inv = den > R(BT_DENOM_EPS) ? PRB(6, 1 / den) : 1;
 }
 
 static real row_relvel(const model *m, const ws_t *w, const row_t *r) {
@@ -1188,7 +1214,7 @@ static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
         real velerr = -rel, poserr = 0;
         if (pen > 0) velerr -= pen / dt;
         else poserr = -pen * erp / dt;
-        r->rhs = (poserr + velerr) * r->inv;
+        r->rhs = PRB(9, (poserr + velerr) * r->inv);
         r->lo = 0; r->hi = R(1e10);
         r->cp = i;
         r->imp = c[AVR_CP_IMP] * ws;                               /* warm start */
@@ -1236,8 +1262,8 @@ static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
 }
 
 static void resolve(const model *m, ws_t *w, row_t *r) {
-    real dv = ep_dot(m, w, r->kindA, r->idxA, r->JA, 1) + ep_dot(m, w, r->kindB, r->idxB, r->JB, 1);
-    real delta = r->rhs - dv * r->inv;
+    real dv = PRB(7, ep_dot(m, w, r->kindA, r->idxA, r->JA, 1) + ep_dot(m, w, r->kindB, r->idxB, r->JB, 1));
+    real delta = PRB(7, r->rhs - dv * r->inv);
     real sum = r->imp + delta;
     if (sum < r->lo) { delta = r->lo - r->imp; r->imp = r->lo; }
     else if (sum > r->hi) { delta = r->hi - r->imp; r->imp = r->hi; }
@@ -1335,7 +1361,11 @@ static void collide(avr_oracle *o, real *st, ws_t *w) {
         wshape A = make_wshape(m, sa, w->body[ba]), B = make_wshape(m, sb, w->body[bb]);
         v3 nB, pB;
         real d;
-        if (narrowphase(w, &A, &B, thr, &nB, &pB, &d)) manifold_add(&M, sa, sb, p, w->body[ba], w->body[bb], nB, pB, d, thr);
+        int hit = narrowphase(w, &A, &B, thr, &nB, &pB, &d);
+#ifdef AVR_ORACLE_PROBE
+        nB = PRB3(1, nB); pB = PRB3(1, pB); d = PRB(1, d);
+#endif
+        if (hit) manifold_add(&M, sa, sb, p, w->body[ba], w->body[bb], nB, pB, d, thr);
         manifold_refresh(&M, w->body[ba], w->body[bb], thr);
         for (int k = 0; k < M.n; k++) {
             if (nnew >= K_MAX_CONTACTS) { st[S_TASK + T_FLAGS] = (real)((int)st[S_TASK + T_FLAGS] | 2); break; }
@@ -1354,7 +1384,7 @@ static int substep(avr_oracle *o, real *st, ws_t *w, real dt) {
     if (robot_mass_matrix(m, w)) return -1;
     real h[K_MAX_DOF] = {0}, qdd[K_MAX_DOF] = {0}, nh[K_MAX_DOF] = {0};
     robot_bias(m, st, w, h);
-    for (int d = 0; d < m->nd; d++) nh[d] = -h[d];
+    for (int d = 0; d < m->nd; d++) nh[d] = -PRB(5, h[d]);
     chol_solve(m, w, nh, qdd);
     real vmax = R(m->d.max_coord_vel);
     for (int d = 0; d < m->nd; d++) {
@@ -1599,6 +1629,9 @@ static int env_step(avr_oracle *o, int e, const float *act, float *obs, float *r
 
 /* ---------------------------------------------------------------- public API */
 #define EXPORT __attribute__((visibility("default")))
+#ifdef AVR_ORACLE_PROBE
+EXPORT void avr_oracle_probe_mask(unsigned m) { probe_mask = m; }
+#endif
 
 static void *dupa(const void *p, size_t n) {
     void *r = malloc(n ? n : 1);

@@ -296,3 +296,9 @@ def test_dressing_facade_contract():
     assert o.shape == (24,) and info['obs_robot_len'] == 24 and info['action_robot_len'] == 7
     assert np.isfinite(r) and not d
     e.close()
+
+def test_generated_constants_match_the_header():
+    """avr/_dressing_consts.py (what the package imports) is include/avr_dressing.h parsed by
+    avr.build: the package needs no header at import time, and the two cannot drift."""
+    from avr import build as B
+    assert open(B.DRESSING_CONSTS).read() == B.dressing_consts_source()

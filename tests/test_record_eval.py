@@ -132,3 +132,80 @@ def test_policy_evaluation_harness(tmp_path):
     assert np.all(np.isfinite(a['returns'])) and a['done'].all()
     np.testing.assert_array_equal(a['returns'], b['returns'])          # deterministic policy, same reset streams
     assert a['task_success'].shape == (16,)
+
+
+# ------------------------------------------------------------------ reference-format recordings
+class _Evil:
+    def __reduce__(self):
+        return (os.system, ('echo not-run',))
+
+
+@pytest.mark.parametrize('proto', [0, 2, 3, 4, 5])
+def test_reference_pickle_reader_reads_setup_and_actions(tmp_path, proto):
+    """setup.pkl / actions.pkl as the reference writes them (feeding.py:50-54, 328-329), every
+    pickle protocol: strings, floats, numpy float scalars and float32 action arrays come back."""
+    import pickle
+    rng = np.random.default_rng(proto)
+    acts = [rng.uniform(-1, 1, 7).astype(np.float32) for _ in range(200)]
+    with open(tmp_path / 'setup.pkl', 'wb') as f:
+        pickle.dump(['jaco', 'female', np.float64(0.54)], f, protocol=proto)
+    with open(tmp_path / 'actions.pkl', 'wb') as f:
+        pickle.dump(acts, f, protocol=proto)
+    setup = R.load_reference_pickle(str(tmp_path / 'setup.pkl'))
+    assert setup == ['jaco', 'female', 0.54]
+    got = R.load_reference_pickle(str(tmp_path / 'actions.pkl'))
+    assert len(got) == 200 and all(g.dtype == np.float32 and np.array_equal(g, a) for g, a in zip(got, acts))
+    big = np.arange(12, dtype='>f8').reshape(3, 4)          # byte order and Fortran layout survive
+    with open(tmp_path / 'x.pkl', 'wb') as f:
+        pickle.dump({'a': (big, np.asfortranarray(big))}, f, protocol=proto)
+    x = R.load_reference_pickle(str(tmp_path / 'x.pkl'))
+    assert np.array_equal(x['a'][0], big) and np.array_equal(x['a'][1], big)
+
+
+def test_reference_pickle_reader_refuses_code_and_object_arrays(tmp_path):
+    import pickle
+    for k, obj in enumerate([[_Evil()], np.array([{'a': 1}], dtype=object), {1, 2}, SimpleNamespace(a=1)]):
+        p = tmp_path / ('e%d.pkl' % k)
+        with open(p, 'wb') as f:
+            pickle.dump(obj, f)
+        with pytest.raises(pickle.UnpicklingError):
+            R.load_reference_pickle(str(p))
+
+
+def test_reference_env_id_from_directory_name():
+    """replay_vr_savemeta.py:20's naming rule."""
+    f = R.reference_env_id
+    assert f('participant_3/feeding_vr_data_jaco_ppo_participant_3_2019-01-01') == 'FeedingJaco-v0'
+    assert f('participant_3/scratch_itch_vr_data_pr2_x') == 'ScratchItchPR2-v0'
+    assert f('participant_3/bed_bathing_vr_data_pr2_x') == 'BedBathingPR2-v0'
+    assert f('participant_3/drinking_vr_data_jaco_x') == 'DrinkingJaco-v0'
+    assert f('participant_3/other') is None
+
+
+@pytest.mark.gpu
+def test_reference_recording_replays_its_actions(tmp_path):
+    """A participant directory in the reference's format (setup.pkl, actions.pkl; feeding.py:
+    146-157) replayed as replay_vr_savemeta.py does: the recorded gender is set up, the 200
+    recorded actions are re-simulated from this build's reset (frame_%d.bullet cannot be restored
+    without Bullet's serializer), and the result equals a live episode driven by the same actions
+    from the same reset."""
+    from avr import env as EV
+    rng = np.random.default_rng(3)
+    acts = [rng.uniform(-1, 1, 7).astype(np.float32) for _ in range(200)]
+    d = tmp_path / 'participant_1' / 'feeding_vr_data_jaco_ppo_participant_1'
+    R.write_reference_recording(str(d), 'jaco', 'female', 0.54, acts)
+    res = R.savemeta_reference(str(tmp_path), out=str(tmp_path / 'meta.npz'))
+    (k, v), = res.items()
+    assert v['env_id'] == 'FeedingJaco-v0' and v['observations'].shape == (200, 25) and v['proportions'] == 'recorded'
+    live = EV.AVRVecEnv('FeedingJaco-v0', 1, auto_reset=False, prefetch=False)
+    live.setup('female', -1, '')
+    live.reset()
+    assert int(live.get_state()[0, ABI.S_TASK + ABI.T_GENDER]) == 1
+    rews = [float(live.step(a[None])[1][0]) for a in acts]
+    live.close()
+    np.testing.assert_array_equal(np.array(rews, np.float32), v['rewards'].astype(np.float32))
+    z = np.load(str(tmp_path / 'meta.npz'), allow_pickle=False)
+    assert z['0_actions'].shape == (200, 7)
+    R.write_reference_recording(str(d), 'jaco', 'female', 0.571, acts)
+    with pytest.raises(NotImplementedError):
+        R.ReferenceReplayEnv(str(d))
