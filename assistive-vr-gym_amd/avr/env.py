@@ -179,8 +179,9 @@ class AVRVecEnv:
 
     impairment: 'random' (the tasks' own setting, feeding.py:175 / scratch_itch.py:178: none /
     limits / weakness / tremor, one draw per episode), a fixed one of those four, or 'no_tremor'.
-    reset_ik: 'device' (default: FeedingJaco's IK through avr_reset_ik, the PR2 tasks' base-pose
-    search through avr_base_search) or 'host' (the fp64 host restatements, then avr_reset).
+    reset_ik: 'device' (default: FeedingJaco's and DressingJaco's IK through avr_reset_ik, the PR2
+    tasks' base-pose search through avr_base_search) or 'host' (the fp64 host restatements, then
+    avr_reset).
     reset_stream: FeedingJaco's reset draws, 'philox' (counter-based, vectorised; default) or
     'numpy' (the per-env Generator stream of the bench's reset pools and the golden fixtures).
     """
@@ -203,6 +204,7 @@ class AVRVecEnv:
         self.task = self.md.task
         self.L = self.md.layout
         self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'
+        self.device_dress_ik = self.task == ABI.TASK_DRESSING and reset_ik == 'device'
         self.device_search = self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH) and reset_ik == 'device'
         self.scratch_attempts, self.scratch_iters = scratch_attempts, scratch_iters
         self.reset_stream = reset_stream
@@ -256,7 +258,8 @@ class AVRVecEnv:
         ids = [self.env_offset + int(i) for i in idx]
         if self.task == ABI.TASK_DRESSING:
             from . import reset_dressing as RD
-            return RD.batch_reset_states(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes))
+            P = RD.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes))
+            return P if self.device_dress_ik else RD.finish_reset(self.A, self.md, P)
         if self.task == ABI.TASK_BEDBATH:
             from . import reset_bedbath as RBB
             return RBB.prepare_reset(self.A, self.md, self.seed, ids, genders=self._genders(idx), episodes=list(episodes),
@@ -302,16 +305,28 @@ class AVRVecEnv:
             return
         ids = [self.env_offset + int(i) for i in idx]
         if self.task == ABI.TASK_DRESSING:
-            # the whole reset is host work (prefetched like the others' host parts)
+            # host draws (prefetched like the others' host parts), then the IK on the device
+            # (avr_reset_ik) or, with reset_ik='host', the host IK and avr_reset
             t0 = time.perf_counter()
             key = (tuple(idx.tolist()), tuple(eps.tolist()))
             got = self._prefetch.take(key) if self._prefetch else None
-            Si, _ = got if got is not None else self._inputs(idx, eps)
+            P = got if got is not None else self._inputs(idx, eps)
             t1 = time.perf_counter()
             if self._prefetch:
                 self._prefetch.start((key[0], tuple((eps + 1).tolist())), idx, eps + 1)
-            S[idx] = Si
-            self.sim.reset(mask.astype(np.uint8), S, 0, self._obs)
+            if self.device_dress_ik:
+                Si, tpos, tquat, init, _ = P
+                S[idx] = Si
+                T = np.zeros((self.n, 7), np.float32)
+                T[:, 6] = 1.0
+                T[idx, :3], T[idx, 3:] = tpos, tquat
+                I = np.zeros((self.n,) + init.shape[1:], np.float32)
+                I[idx] = init
+                _, ok = self.sim.reset_ik(mask.astype(np.uint8), S, T, I, iters=150, tol=0.01, frames=0, obs=self._obs)
+                self.last_ik_ok = ok
+            else:
+                S[idx] = P[0]
+                self.sim.reset(mask.astype(np.uint8), S, 0, self._obs)
             self.reset_timing = dict(host_s=t1 - t0, prefetched=got is not None, device_s=time.perf_counter() - t1)
             return
         if self.task in (ABI.TASK_SCRATCH, ABI.TASK_BEDBATH):

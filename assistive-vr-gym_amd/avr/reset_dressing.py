@@ -11,7 +11,8 @@ Per env (numpy Generator keyed by (seed, env id, episode), like the other tasks'
     (jittered), the tool frame's z axis pointing back along the forearm towards the elbow; the
     Jaco's arm joints by damped least squares to that tool pose (random restarts, as the other
     resets' IK, util.py:34-105 semantics) -- the robot is kinematic in this task, so no collision
-    screening applies;
+    screening applies.  prepare_reset draws everything on the host; the IK then runs on the device
+    (avr_reset_ik, the facade's default) or on the host (finish_reset, the checker);
   * the sleeve in its rest shape: ring k centred k * spacing beyond the cuff, away from the arm.
 """
 import numpy as np
@@ -161,26 +162,32 @@ def _dls(A, link, cols, arm, lo, hi, Qr, tpos, tquat, iters, res):
     return CP[:, link], CQ[:, link]
 
 
+def ik_accept(P, Qq, tp, tq, tol):
+    """util.py:49's acceptance of a restart: position error below tol and the orientation's
+    quaternion distance below tol or np.isclose to 2 (the other cover of the rotation, atol tol)."""
+    pe = np.linalg.norm(tp - P, axis=1)
+    qd = np.linalg.norm(tq - Qq, axis=1)
+    return (pe < tol) & ((qd < tol) | np.isclose(qd, 2.0, atol=tol)), pe
+
+
 def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01, res=1e-6, split=2):
     """Vectorised damped-least-squares IK of the tool link's COM frame (RS.ik_batch's update rule)
     with per-env restarts init (N, R, 7); no collision screening (the robot is kinematic here).
     A row stops iterating once its position error and rotation angle are below `res`
     (calculateInverseKinematics' residualThreshold role; at 1e-6 the joint angles stay within
-    ~4e-6 rad of running all 150 iterations); the first restart that meets `tol` is kept, else
-    the last one.  The first `split` restarts run in turn over the envs still unsolved; the rest
-    run side by side for the few envs left (rows are independent, so the result is the same as
-    running them in turn, with far fewer passes).  Returns (Q (N, ndof), ok (N,))."""
+    ~4e-6 rad of running all 150 iterations); the first restart that meets util.py:49's rule
+    (ik_accept) is kept, else the restart closest to the target position (util.py:51-54).  The
+    first `split` restarts run in turn over the envs still unsolved; the rest run side by side for
+    the few envs left (rows are independent, so the result is the same as running them in turn,
+    with far fewer passes).  The device restatement is avr_reset_ik (csrc/avr_dressing.hip).
+    Returns (Q (N, ndof), ok (N,))."""
     N, R, _ = init.shape
     nd = int(A['n_dof'])
     chain = RS._chain(A, link)
     cols = [[k for k in chain if A['rl_dof'][k] == d][0] for d in arm]
     Qout = np.zeros((N, nd))
     done = np.zeros(N, bool)
-
-    def accept(P, Qq, tp, tq):
-        pe = np.linalg.norm(tp - P, axis=1)
-        qe = np.minimum(np.linalg.norm(tq - Qq, axis=1), np.linalg.norm(tq + Qq, axis=1))
-        return (pe < tol) & (qe < tol)
+    best = np.full(N, np.inf)                     # closest restart so far (util.py:51-54)
     for r in range(R):
         idx = np.nonzero(~done)[0]
         if not len(idx):
@@ -191,14 +198,14 @@ def ik_batch(A, link, tpos, tquat, arm, lo, hi, init, iters=150, tol=0.01, res=1
         Qr[:, arm] = np.concatenate([init[idx, q] for q in rs])
         tp, tq = np.tile(tpos[idx], (len(rs), 1)), np.tile(tquat[idx], (len(rs), 1))
         P, Qq = _dls(A, link, cols, arm, lo, hi, Qr, tp, tq, iters, res)
-        good = accept(P, Qq, tp, tq).reshape(len(rs), n)
+        good, pe = ik_accept(P, Qq, tp, tq, tol)
+        good, pe = good.reshape(len(rs), n), pe.reshape(len(rs), n)
         Qr = Qr.reshape(len(rs), n, nd)
-        first = np.where(good.any(0), good.argmax(0), len(rs) - 1)    # first good restart, else the last
-        pick = Qr[first, np.arange(n)]
-        ok = good[first, np.arange(n)]
-        take = ok | (rs[-1] == R - 1)
-        Qout[idx[take]] = pick[take]
-        done[idx[take]] = ok[take]
+        for k in range(len(rs)):                    # restarts in order: first accepted, else the closest
+            take = ~done[idx] & (good[k] | (pe[k] < best[idx]))
+            Qout[idx[take]] = Qr[k, take]
+            best[idx[take]] = np.where(good[k, take], -1.0, pe[k, take])
+            done[idx[good[k]]] = True
         if len(rs) > 1:
             break
     return Qout, done
@@ -226,12 +233,14 @@ def cloth_rest_batch(P, Qt):
     return P[:, None] + np.einsum('nij,pj->npi', Rm, loc)
 
 
-def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restarts=8):
-    """(S (N, STATE_WORDS) float64, meta) for the global env ids."""
+def prepare_reset(A, md, seed, env_ids, genders=None, episodes=None, restarts=8):
+    """The host part of a reset: per-env draws (gender, the seated human's joints, the start-pose
+    jitter, the IK restarts) and the arm geometry.  Returns (S (N, STATE_WORDS) with the geometry and
+    gender words set and no arm / sleeve yet, tpos (N, 3), tquat (N, 4), init (N, restarts, 7),
+    genders); finish_reset (host IK) or avr_reset_ik (device) completes it."""
     n = len(env_ids)
     episodes = [0] * n if episodes is None else list(episodes)
     arm, lo, hi = arm_limits(md)
-    tool = int(A['task_tool_link'])
     S = np.zeros((n, DR.STATE_WORDS))
     init = np.zeros((n, restarts, len(arm)))
     jit = np.zeros((n, 3))
@@ -256,6 +265,16 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restar
     tquat = _frame_z(-u, np.array([0, 0, 1.0]))
     S[:, DR.S_GEO:DR.S_GEO + 32] = geo
     S[:, DR.S_TASK + DR.T_GENDER] = (gl == 'female').astype(float)
+    return S, tpos, tquat, init, gl
+
+
+def finish_reset(A, md, P):
+    """The host IK (ik_batch) and the sleeve in its rest shape on the tool frame: (S, meta)."""
+    S, tpos, tquat, init, gl = P
+    S = S.copy()
+    n = len(S)
+    arm, lo, hi = arm_limits(md)
+    tool = int(A['task_tool_link'])
     Q, ok = ik_batch(A, tool, tpos, tquat, arm, lo, hi, init)
     CP, CQ, _, _ = RS.robot_fk_batch(A, Q)
     S[:, DR.S_Q:DR.S_Q + 7] = Q[:, arm]
@@ -265,3 +284,8 @@ def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restar
     S[:, DR.S_X:DR.S_X + 4 * DR.NP].reshape(n, DR.NP, 4)[:, :, :3] = cloth_rest_batch(CP[:, tool], CQ[:, tool])
     meta = [dict(gender=str(gl[k]), impairment='none', ik_ok=bool(ok[k])) for k in range(n)]
     return S, meta
+
+
+def batch_reset_states(A, md, seed, env_ids, genders=None, episodes=None, restarts=8):
+    """(S (N, STATE_WORDS) float64, meta) for the global env ids: prepare_reset + the host IK."""
+    return finish_reset(A, md, prepare_reset(A, md, seed, env_ids, genders, episodes, restarts))

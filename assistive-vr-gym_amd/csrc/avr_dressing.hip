@@ -25,6 +25,11 @@
 #include "../../include/avr.h"
 #include "../../include/avr_dressing.h"
 
+// No contraction anywhere in this file: every multiply and add rounds on its own, in the order the
+// fp32 oracle (oracle/avr_oracle_dressing.c, gcc, no FMA) writes them, so the kernel and the fp32
+// oracle round alike and the contact-free sleeve matches it to the last bits (tests/test_dressing.py).
+#pragma clang fp contract(off)
+
 namespace avr_dressing {
 #include "avr_math.h"
 
@@ -40,6 +45,9 @@ struct DrModel {
     float jpos[DR_MAXL][4], jquat[DR_MAXL][4], axis[DR_MAXL][4], compos[DR_MAXL][4], comquat[DR_MAXL][4];
     float base_p[4], base_q[4], lower[8], upper[8];
     float ring[DR_NS][4];            // the held cuff's particles in the tool frame
+    float l_ring, l_ring2, l_sh, pmass;   // spring rest lengths and particle mass, rounded as the fp32 oracle's
+    int chain_n, chain[DR_MAXL];     // the tool link's chain, root first (the reset IK's kinematics)
+    int col[7];                      // chain position of arm joint c's link (Jacobian column c)
     unsigned long long seed;
     int env_offset;
 };
@@ -65,8 +73,9 @@ AVR_DI void dr_fk(const DrModel &m, const float *q7, v3 &tool_p, qt &tool_q, v3 
                 const int aj = m.ajoint[i];
                 const float qa = aj >= 0 ? F.q[aj] : 0.f;
                 const float h = qa * 0.5f;
-                const float sn = sinf(h);
-                tq = qmul(tq, Q(m.axis[i][0] * sn, m.axis[i][1] * sn, m.axis[i][2] * sn, cosf(h)));
+                // (double sin / cos rounded once to float: what the fp32 oracle's sin() of a float returns)
+                const float sn = (float)sin((double)h);
+                tq = qmul(tq, Q(m.axis[i][0] * sn, m.axis[i][1] * sn, m.axis[i][2] * sn, (float)cos((double)h)));
             }
             F.lp[i] = make_float4(tp.x, tp.y, tp.z, 0.f);
             F.lq[i] = make_float4(tq.x, tq.y, tq.z, tq.w);
@@ -111,12 +120,9 @@ __constant__ int c_nb_dk[12] = {0, 0, 1, -1, 1, 1, -1, -1, 0, 0, 2, -2};
 __constant__ int c_nb_dj[12] = {1, -1, 0, 0, 1, -1, 1, -1, 2, -2, 0, 0};
 
 // force on free particle i (ring k = i / NS >= 1) from the published positions / velocities
-AVR_DI v3 dr_force(int i, v3 x, v3 v, const float4 *X, const float4 *Vv, const float *geo, float &fc_mag) {
-    const float m = (float)AVR_DR_MASS / DR_NP;
-    const float pi = 3.14159265358979323846f;
-    const float L_ring = 2.f * (float)AVR_DR_RADIUS * sinf(pi / DR_NS), L_ax = (float)AVR_DR_SPACING;
-    const float L_ring2 = 2.f * (float)AVR_DR_RADIUS * sinf(2.f * pi / DR_NS);
-    const float L_sh = sqrtf(L_ring * L_ring + L_ax * L_ax);
+AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const float4 *Vv, const float *geo, float &fc_mag) {
+    const float m = M.pmass;
+    const float L_ring = M.l_ring, L_ax = (float)AVR_DR_SPACING, L_ring2 = M.l_ring2, L_sh = M.l_sh;
     const int k = i / DR_NS, j = i % DR_NS;
     v3 f = V(0, 0, (float)AVR_DR_GRAVITY * m);
     f = sub(f, scl(v, (float)AVR_DR_AIR));
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                                                             long long t, float *__restrict__ obs, float *__restrict__ rew,
                                                             unsigned char *__restrict__ done, float *__restrict__ info, int n_envs) {
     __shared__ float4 X[DR_NP], Vv[DR_NP];
-    __shared__ float red[64];
+    __shared__ float red[DR_NP];
     __shared__ FkLds fk;
     const int env = blockIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
     const bool pinned = i0 < DR_NS;             // ring 0: lanes 0..15's first particle
     const v3 ringl = ld3(m.ring[i0 & (DR_NS - 1)]);
     const float dtc = (float)AVR_DR_FRAME / (AVR_DR_RSUB * AVR_DR_CSUB);
-    const float minv_dt = dtc / ((float)AVR_DR_MASS / DR_NP);
+    const float minv_dt = dtc / m.pmass;
     float ftot = st[AVR_DR_S_TASK + AVR_DR_T_FORCE], speed = 0.f;
     const int frames = mode == DR_MODE_OBS ? 0 : AVR_DR_FRAME_SKIP;
     for (int f = 0; f < frames; f++)
@@ -266,11 +272,12 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                 Vv[i1] = make_float4(v1.x, v1.y, v1.z, 0.f);
                 __syncthreads();
                 float fm0 = 0.f, fm1 = 0.f;
-                const v3 F0 = pinned ? V(0, 0, 0) : dr_force(i0, x0, v0, X, Vv, geo, fm0);
-                const v3 F1 = dr_force(i1, x1, v1, X, Vv, geo, fm1);
+                const v3 F0 = pinned ? V(0, 0, 0) : dr_force(m, i0, x0, v0, X, Vv, geo, fm0);
+                const v3 F1 = dr_force(m, i1, x1, v1, X, Vv, geo, fm1);
                 // the dressing forces' sum over the free particles, at the step's last cloth sub-step
+                // (summed in particle order, as the oracle's loop)
                 const bool last = f == frames - 1 && r == AVR_DR_RSUB - 1 && cs == AVR_DR_CSUB - 1;
-                if (last) red[lane] = fm0 + fm1;
+                if (last) { red[i0] = fm0; red[i1] = fm1; }
                 __syncthreads();
                 if (pinned) {
                     const float s = (float)(cs + 1) / AVR_DR_CSUB;
@@ -287,7 +294,7 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                 x1 = add(x1, scl(v1, dtc));
                 if (last) {
                     float s = 0.f;
-                    for (int k = 0; k < 64; k++) s += red[k];
+                    for (int k = DR_NS; k < DR_NP; k++) s += red[k];
                     ftot = s;
                 }
                 __syncthreads();
@@ -349,6 +356,171 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
     }
 }
 
+// ------------------------------------------------------------------------------------------ reset IK
+// The reset's inverse kinematics on the device (the host restatement, avr/reset_dressing.py
+// ik_batch, is the checker): damped least squares of the tool link's COM frame towards the start
+// pose, per restart from its own random joint vector (util.py:34-105 ik_random_restarts: the
+// first restart whose pose meets the tolerance is kept -- |dp| < tol and |dq| < tol or
+// np.isclose(|dq|, 2, atol=tol), util.py:49 -- else the restart closest to the target position,
+// util.py:51-54).  Each iteration: J (6 x 7, the arm joints' columns), (J J^T + 1e-4 I) y = e by
+// Cholesky, q += J^T y clipped to the limits; a restart stops once its position error and rotation
+// angle are below res (calculateInverseKinematics' residual threshold role).  One block per env,
+// lane r runs restart r (serial FK of the tool chain in registers); then the block writes the arm,
+// its motor targets, the tool frame and the sleeve in its rest shape (ring k centred k * spacing
+// along -z of the tool frame, avr/reset_dressing.py cloth_rest).
+// the tool COM frame and, per arm joint a, its joint origin and world axis (the Jacobian's
+// columns); the chain loop is unrolled to its capacity so every array index is a constant
+AVR_DI void ik_fk(const DrModel &m, const float *q7, v3 &cp, qt &cq, v3 *ORa, v3 *AXa) {
+    v3 p = ld3(m.base_p);
+    qt q = ldq(m.base_q);
+    for (int c = 0; c < m.chain_n; c++) {
+        const int i = m.chain[c];
+        const v3 tp = add(p, qrot(q, ld3(m.jpos[i])));
+        qt tq = qmul(q, ldq(m.jquat[i]));
+        const v3 ax = qrot(tq, ld3(m.axis[i]));
+        const int aj = m.ajoint[i];
+        float qa = 0.f;
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+            if (aj == k) { qa = q7[k]; ORa[k] = tp; AXa[k] = ax; }
+        if (m.jtype[i] == AVR_J_REVOLUTE) {
+            const float h = 0.5f * qa, sn = sinf(h);
+            tq = qmul(tq, Q(m.axis[i][0] * sn, m.axis[i][1] * sn, m.axis[i][2] * sn, cosf(h)));
+        }
+        p = tp;
+        q = tq;
+    }
+    cp = add(p, qrot(q, ld3(m.compos[m.tool])));
+    cq = qmul(q, ldq(m.comquat[m.tool]));
+}
+
+__global__ __launch_bounds__(64) void avr_dress_reset_ik_kernel(const DrModel *__restrict__ mp, float *__restrict__ state, const unsigned char *__restrict__ mask,
+                                                                const float *__restrict__ target7, const float *__restrict__ init, int restarts, int iters,
+                                                                float tol, unsigned char *__restrict__ ok_out, int n_envs) {
+    __shared__ float rq[64][8];      // per restart: q[7], position error
+    __shared__ int acc[64];
+    __shared__ float pose[8];
+    const int env = blockIdx.x, lane = threadIdx.x;
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const DrModel &m = *mp;
+    const float *t7 = target7 + (size_t)env * 7;
+    const v3 tpos = V(t7[0], t7[1], t7[2]);
+    const qt tq = Q(t7[3], t7[4], t7[5], t7[6]);
+    const float res = 1e-6f, lam = 1e-4f;
+    if (lane < restarts) {
+        float q[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) q[k] = init[((size_t)env * restarts + lane) * 7 + k];
+        v3 OR[7], AX[7];
+        v3 cp;
+        qt cq;
+        for (int it = 0; it <= iters; it++) {
+            ik_fk(m, q, cp, cq, OR, AX);
+            const v3 ep = sub(tpos, cp);
+            qt dq = qmul(tq, Q(-cq.x, -cq.y, -cq.z, cq.w));
+            if (dq.w < 0.f) dq = Q(-dq.x, -dq.y, -dq.z, -dq.w);
+            const float sv = sqrtf(dq.x * dq.x + dq.y * dq.y + dq.z * dq.z);
+            const float ang = 2.f * atan2f(sv, dq.w);
+            if ((len(ep) < res && ang < res) || it == iters) break;
+            const v3 er = sv > 1e-12f ? scl(V(dq.x, dq.y, dq.z), ang / sv) : V(0, 0, 0);
+            float J[6][7];
+#pragma unroll
+            for (int c = 0; c < 7; c++) {
+                const v3 a = AX[c], l = crs(a, sub(cp, OR[c]));
+                J[0][c] = l.x; J[1][c] = l.y; J[2][c] = l.z; J[3][c] = a.x; J[4][c] = a.y; J[5][c] = a.z;
+            }
+            float Am[6][6], e[6] = {ep.x, ep.y, ep.z, er.x, er.y, er.z};
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = 0; j <= i; j++) {
+                    float t = i == j ? lam : 0.f;
+#pragma unroll
+                    for (int c = 0; c < 7; c++) t += J[i][c] * J[j][c];
+                    Am[i][j] = t;
+                }
+            // Cholesky A = L L^T (lower, in place), then L L^T y = e
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                float d = Am[j][j];
+#pragma unroll
+                for (int k = 0; k < j; k++) d -= Am[j][k] * Am[j][k];
+                d = sqrtf(fmaxf(d, 1e-30f));
+                Am[j][j] = d;
+#pragma unroll
+                for (int i = j + 1; i < 6; i++) {
+                    float t = Am[i][j];
+#pragma unroll
+                    for (int k = 0; k < j; k++) t -= Am[i][k] * Am[j][k];
+                    Am[i][j] = t / d;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                float t = e[i];
+#pragma unroll
+                for (int k = 0; k < i; k++) t -= Am[i][k] * e[k];
+                e[i] = t / Am[i][i];
+            }
+#pragma unroll
+            for (int i = 5; i >= 0; i--) {
+                float t = e[i];
+#pragma unroll
+                for (int k = i + 1; k < 6; k++) t -= Am[k][i] * e[k];
+                e[i] = t / Am[i][i];
+            }
+#pragma unroll
+            for (int c = 0; c < 7; c++) {
+                float st = 0.f;
+#pragma unroll
+                for (int i = 0; i < 6; i++) st += J[i][c] * e[i];
+                q[c] = fminf(fmaxf(q[c] + st, m.lower[c]), m.upper[c]);
+            }
+        }
+        ik_fk(m, q, cp, cq, OR, AX);
+        const float pe = len(sub(tpos, cp));
+        const float qd = sqrtf((tq.x - cq.x) * (tq.x - cq.x) + (tq.y - cq.y) * (tq.y - cq.y) + (tq.z - cq.z) * (tq.z - cq.z) + (tq.w - cq.w) * (tq.w - cq.w));
+        acc[lane] = pe < tol && (qd < tol || fabsf(qd - 2.f) <= tol + 1e-5f * 2.f);
+#pragma unroll
+        for (int k = 0; k < 7; k++) rq[lane][k] = q[k];
+        rq[lane][7] = pe;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        int pick = -1;
+        for (int r = 0; r < restarts && pick < 0; r++)
+            if (acc[r]) pick = r;
+        const bool good = pick >= 0;
+        if (!good) {
+            pick = 0;
+            for (int r = 1; r < restarts; r++)
+                if (rq[r][7] < rq[pick][7]) pick = r;
+        }
+        float *st = state + (size_t)env * DR_W;
+        float q[7];
+        for (int k = 0; k < 7; k++) { q[k] = rq[pick][k]; st[AVR_DR_S_Q + k] = q[k]; st[AVR_DR_S_QT + k] = q[k]; }
+        v3 OR[7], AX[7], cp;
+        qt cq;
+        ik_fk(m, q, cp, cq, OR, AX);
+        st3(st + AVR_DR_S_TOOL, cp);
+        stq(st + AVR_DR_S_TOOL + 3, cq);
+        pose[0] = cp.x; pose[1] = cp.y; pose[2] = cp.z; pose[3] = cq.x; pose[4] = cq.y; pose[5] = cq.z; pose[6] = cq.w;
+        ok_out[env] = good;
+    }
+    __syncthreads();
+    const v3 cp = V(pose[0], pose[1], pose[2]);
+    const qt cq = Q(pose[3], pose[4], pose[5], pose[6]);
+    float *st = state + (size_t)env * DR_W;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int i = lane + 64 * h, k = i / DR_NS, j = i % DR_NS;
+        const v3 x = add(cp, qrot(cq, V(m.ring[j][0], m.ring[j][1], -(float)k * (float)AVR_DR_SPACING)));
+        float *px = st + AVR_DR_S_X + 4 * i, *pv = st + AVR_DR_S_V + 4 * i;
+        px[0] = x.x; px[1] = x.y; px[2] = x.z; px[3] = 0.f;
+        pv[0] = 0.f; pv[1] = 0.f; pv[2] = 0.f; pv[3] = 0.f;
+    }
+}
+
 __global__ void avr_dress_copy_masked_kernel(float *state, const float *src, const unsigned char *mask, int n_envs) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < (size_t)n_envs * DR_W && mask[i / DR_W]) state[i] = src[i];
@@ -378,6 +550,9 @@ struct avr_sim {
     DrModel *d_m;
     hipStream_t stream;
     float *d_state, *d_stage, *d_act, *d_obs, *d_rew, *d_info, *d_query;
+    float *d_ik;                 // reset IK inputs: target frames [E][7], then restarts [E][R][7] (grow-only)
+    size_t ik_cap;
+    unsigned char *d_ok;
     unsigned char *d_done, *d_mask;
     hipEvent_t ev0, ev1;
     int prof;
@@ -459,12 +634,35 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
             m.comquat[i][k] = (float)d->rl_com_quat[4 * i + k];
         }
     }
+    {
+        int rev[DR_MAXL], n = 0;
+        for (int k = m.tool; k >= 0 && n < DR_MAXL; k = m.parent[k]) rev[n++] = k;
+        m.chain_n = n;
+        for (int c = 0; c < n; c++) m.chain[c] = rev[n - 1 - c];
+        for (int a = 0; a < 7; a++) {
+            m.col[a] = -1;
+            for (int c = 0; c < n; c++)
+                if (m.ajoint[m.chain[c]] == a) m.col[a] = c;
+            if (m.col[a] < 0) return fail(s, -2, "DressingJaco: arm joint %d is not on the tool link's chain", a);
+        }
+    }
     for (int k = 0; k < 3; k++) m.base_p[k] = (float)d->robot_base[k];
     for (int k = 0; k < 4; k++) m.base_q[k] = (float)d->robot_base[3 + k];
-    for (int j = 0; j < DR_NS; j++) {
-        const double th = 2.0 * 3.14159265358979323846 * j / DR_NS;
-        m.ring[j][0] = (float)(AVR_DR_RADIUS * cos(th));
-        m.ring[j][1] = (float)(AVR_DR_RADIUS * sin(th));
+    // the cuff ring, rest lengths and particle mass rounded exactly as the fp32 oracle computes them
+    // (float operands, double sin / cos / sqrt rounded to float; avr_oracle_dressing.c cloth_substep
+    // and env_step)
+    {
+        const float pi = (float)3.14159265358979323846, rad = (float)AVR_DR_RADIUS, L_ax = (float)AVR_DR_SPACING;
+        for (int j = 0; j < DR_NS; j++) {
+            const float th = 2 * pi * j / DR_NS;
+            m.ring[j][0] = (float)((double)rad * cos((double)th));
+            m.ring[j][1] = (float)((double)rad * sin((double)th));
+        }
+        m.l_ring = (float)((double)(2 * rad) * sin((double)(pi / DR_NS)));
+        m.l_ring2 = (float)((double)(2 * rad) * sin((double)(2 * pi / DR_NS)));
+        const float ls2 = m.l_ring * m.l_ring + L_ax * L_ax;
+        m.l_sh = (float)sqrt((double)ls2);
+        m.pmass = (float)AVR_DR_MASS / DR_NP;
     }
     m.seed = cfg->seed;
     m.env_offset = cfg->env_offset;
@@ -482,6 +680,7 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
     HIPCHK(s, hipMalloc(&s->d_query, E * 7 * 2 * sizeof(float)));
     HIPCHK(s, hipMalloc(&s->d_done, E));
     HIPCHK(s, hipMalloc(&s->d_mask, E));
+    HIPCHK(s, hipMalloc(&s->d_ok, E));
     HIPCHK(s, hipEventCreate(&s->ev0));
     HIPCHK(s, hipEventCreate(&s->ev1));
     return 0;
@@ -491,7 +690,7 @@ int avr_destroy(avr_sim *s) {
     if (!s) return -1;
     DevGuard dg(s->cfg.device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    void *ptrs[] = {s->d_m, s->d_state, s->d_stage, s->d_act, s->d_obs, s->d_rew, s->d_info, s->d_query, s->d_done, s->d_mask};
+    void *ptrs[] = {s->d_m, s->d_state, s->d_stage, s->d_act, s->d_obs, s->d_rew, s->d_info, s->d_query, s->d_done, s->d_mask, s->d_ik, s->d_ok};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -678,8 +877,41 @@ int avr_robot_self_contact(avr_sim *s, int32_t n, const float *q, int32_t *out) 
 }
 int avr_reset_ik(avr_sim *s, const uint8_t *mask, const float *h, const float *target7, const float *init, const float *alt4, int32_t restarts,
                  int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok) {
-    (void)mask; (void)h; (void)target7; (void)init; (void)alt4; (void)restarts; (void)iters; (void)tol; (void)keepout8; (void)n_frames; (void)host_obs; (void)host_ok;
-    return fail(s, -1, "avr_reset_ik: DressingJaco resets through avr_reset (host IK)");
+    CHECK_SIM(s);
+    const size_t E = (size_t)s->cfg.n_envs;
+    if (!h || !target7 || !init) return fail(s, -1, "avr_reset_ik: host_state, target7 and init are required");
+    if (alt4 || keepout8) return fail(s, -1, "avr_reset_ik: DressingJaco's robot is kinematic (no self-contact screening, no keep-out box)");
+    if (n_frames != 0) return fail(s, -1, "avr_reset_ik: DressingJaco has no settle frames");
+    if (restarts < 1 || restarts > 64) return fail(s, -1, "avr_reset_ik: restarts %d outside 1..64", (int)restarts);
+    if (iters < 0) return fail(s, -1, "avr_reset_ik: iters %d < 0", (int)iters);
+    std::vector<uint8_t> all;
+    if (!mask) { all.assign(E, 1); mask = all.data(); }
+    const size_t need = E * 7 + E * (size_t)restarts * 7;
+    if (need > s->ik_cap) {
+        if (s->d_ik) HIPCHK(s, hipFree(s->d_ik));
+        s->d_ik = nullptr;
+        HIPCHK(s, hipMalloc(&s->d_ik, need * sizeof(float)));
+        s->ik_cap = need;
+    }
+    if (upload_masked(s, mask, h)) return -2;
+    HIPCHK(s, hipMemcpyAsync(s->d_ik, target7, E * 7 * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemcpyAsync(s->d_ik + E * 7, init, E * (size_t)restarts * 7 * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s, hipMemsetAsync(s->d_ok, 0, E, s->stream));
+    hipLaunchKernelGGL(avr_dress_reset_ik_kernel, dim3(s->cfg.n_envs), dim3(64), 0, s->stream, s->d_m, s->d_state, s->d_mask, s->d_ik, s->d_ik + E * 7,
+                       (int)restarts, (int)iters, tol, s->d_ok, s->cfg.n_envs);
+    HIPCHK(s, hipGetLastError());
+    HIPCHK(s, launch(s, nullptr, s->d_mask, DR_MODE_OBS, 0, s->d_obs, s->d_rew, s->d_done, s->d_info));
+    std::vector<float> o(E * AVR_DR_OBS_DIM);
+    std::vector<uint8_t> ok(E);
+    HIPCHK(s, hipMemcpyAsync(o.data(), s->d_obs, o.size() * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(ok.data(), s->d_ok, E, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    for (size_t e = 0; e < E; e++)
+        if (mask[e]) {
+            if (host_obs) memcpy(host_obs + e * AVR_DR_OBS_DIM, o.data() + e * AVR_DR_OBS_DIM, AVR_DR_OBS_DIM * sizeof(float));
+            if (host_ok) host_ok[e] = ok[e];
+        }
+    return 0;
 }
 int avr_base_search(avr_sim *s, int32_t n, int32_t attempts, const float *base7, const float *rest, const float *tstart3, const float *goals9,
                     int32_t iters, float tol, int32_t *best, uint8_t *ok, float *q_arm, float *res4) {

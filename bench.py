@@ -202,7 +202,7 @@ def facade_bench(args):
            'data': 'synthetic: torch uniform(-1, 1) actions on the device; resets drawn per env and episode',
            'config': {'workload': args.task + ', %d envs, gym facade with rollover' % E, 'task': args.task, 'envs_per_gpu': E,
                       'impairment': args.impairment,
-                      'reset_ik': ('device IK' if v.device_ik else 'device base-pose search' if v.device_search else 'host')},
+                      'reset_ik': ('device IK' if (v.device_ik or v.device_dress_ik) else 'device base-pose search' if v.device_search else 'host')},
            'rollovers_timed': roll, 'env_steps_per_s_between_rollovers': E / no_roll, 'between_rollovers_steps': K,
            'between_rollovers_host_ms_per_step': [round(float(np.median(host_ms)), 3), round(float(np.max(host_ms)), 3)],
            'rollover_ms': float(np.mean(t_roll) * 1e3) if roll else None,
