@@ -156,7 +156,9 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const f
 AVR_DI qt qnlerp(qt a, qt b, float s) {
     if (a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w < 0.f) b = Q(-b.x, -b.y, -b.z, -b.w);
     const qt r = Q(a.x + (b.x - a.x) * s, a.y + (b.y - a.y) * s, a.z + (b.z - a.z) * s, a.w + (b.w - a.w) * s);
-    const float n = 1.f / sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+    // (1 / sqrt in double, rounded once to float: the fp32 oracle's `1 / sqrt(x)` of a float x is
+    // a double expression -- a float sqrt then a float division would round twice)
+    const float n = (float)(1.0 / sqrt((double)(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w)));
     return Q(r.x * n, r.y * n, r.z * n, r.w * n);
 }
 

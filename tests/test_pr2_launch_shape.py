@@ -21,8 +21,6 @@ from avr import _abi as ABI
 pytestmark = pytest.mark.gpu
 
 SI, BB = ABI.SI, ABI.BB
-PICK = np.array([0, 1, 31, 32, 33, 511, 512, 1023, 1024, 1025, 1055, 1056, 1500, 2047, 2048, 2049, 2079, 2080,
-                 2500, 3071, 3072, 3073, 3103, 3104, 3500, 3800, 4000, 4063, 4064, 4090, 4094, 4095])
 
 
 def _oracle(md, n, precision):
@@ -56,55 +54,96 @@ def _wipe_bits(St, L):
     return St[:, L.S_TASK + L.T_WIPE:L.S_TASK + L.T_WIPE + 6]
 
 
+def _picks(n_pool, n_first_contact):
+    """32 picks of the 4096-env launch (env e holds pool state e mod n_pool): every env group's
+    first and last env, part-B block boundaries, and one env of every contact state spread over
+    the four groups, the last pool state (the scratcher pressed hardest) at every group end."""
+    reset = [0, 1, 32, 33, 511, 512, 1024, 1025, 2048, 2049, 3072, 4064]
+    contact = [n_first_contact + k + n_pool * (8 * k + 3) for k in range(n_pool - n_first_contact)]
+    ends = [1023, 2047, 3071, 4095]
+    P = np.array(sorted(set(reset + contact + ends)))
+    assert len(P) == 32 and P.max() < 4096
+    return P
+
+
+def _perturbed(S, L, nd, rng, eps):
+    """S with the joint angles and the tool's position moved by eps N(0, 1): rounding-level
+    perturbations that show how far fp32 rounding alone can carry a state in a few steps."""
+    X = S.astype(np.float64).copy()
+    X[:, L.S_Q:L.S_Q + nd] += eps * rng.standard_normal((len(X), nd))
+    X[:, L.S_FREE:L.S_FREE + 3] += eps * rng.standard_normal((len(X), 3))
+    return X
+
+
 @pytest.mark.parametrize('task', [ABI.TASK_SCRATCH, ABI.TASK_BEDBATH], ids=['ScratchItchPR2', 'BedBathingPR2'])
 def test_launch_shape_sampled_envs_match_oracle(task):
+    """32 sampled envs of the bench's launch against the fp64 oracle over 5 gym steps.  The GPU is
+    one fp32 realisation of each env; an ensemble of fp32 oracles started from rounding-level
+    perturbations of the same states (1e-6 on the joint angles and the tool position) measures how
+    far fp32 rounding alone carries each env from the fp64 oracle.  Each pick is held to the
+    one-step tolerances, or -- where the ensemble itself spreads further (a contact bifurcation) --
+    to twice the ensemble's own deviation; no pick is excepted."""
     from avr import _lib
-    A, md, L, P, _ = _pool(task, 16)
+    A, md, L, P, is_c = _pool(task, 16)
     E = 4096
-    P = P[:31] if len(P) % 2 == 0 else P    # (an odd pool: the picks at block boundaries see different states)
-    S = np.tile(P, (E // len(P) + 1, 1))[:E]
+    n_pool, n_first_contact = len(P), int(np.argmax(is_c))
+    PICK = _picks(n_pool, n_first_contact)
+    S = np.tile(P, (E // n_pool + 1, 1))[:E]
+    n = len(PICK)
+    n_contact_picks = int(is_c[PICK % n_pool].sum())
     sim = _lib.Sim(md, E)
     assert sim.env_groups() == 4
     sim.set_state(S)
-    o, op = _oracle(md, len(PICK), 'f64'), _oracle(md, len(PICK), 'f64')
-    o.set_state(S[PICK].astype(np.float64)); op.set_state(S[PICK].astype(np.float64))
     nd = md.n_dof + (int(A['hc_n']) if task == ABI.TASK_SCRATCH else 0)
+    o = _oracle(md, n, 'f64')
+    o.set_state(S[PICK].astype(np.float64))
+    rng = np.random.default_rng(9)
+    ens = []
+    for j in range(5):                     # the fp32 oracle itself, then four perturbed starts
+        e = _oracle(md, n, 'f32')
+        e.set_state(S[PICK].astype(np.float64) if j == 0 else _perturbed(S[PICK], L, nd, rng, 1e-6))
+        ens.append(e)
     od = L.OBS_DIM - 1                     # the kinematic part of the obs (the last word is the tool force)
-    n = len(PICK)
-    w = dict(dq=np.zeros(n), obs=np.zeros(n), rew=np.zeros(n), force=np.zeros(n))
-    spread = np.zeros(n)
+    keys = ('dq', 'obs', 'rew', 'force')
+    w = {k: np.zeros(n) for k in keys}     # GPU vs fp64
+    s = {k: np.zeros(n) for k in keys}     # fp32 ensemble vs fp64
     same = np.ones(n, bool)
     ncp = 0
-    rng = np.random.default_rng(9)
     for t in range(5):
         a = _lib.random_actions(1001, np.arange(E), t) * 0.2
         ob, r, d, i = sim.step(a)
         oc, rc, dc, ic = o.step(a[PICK])
-        op.step((a[PICK] + 1e-4 * rng.standard_normal((n, a.shape[1]))).astype(np.float32))
-        G, C = sim.get_state()[PICK], o.get_state()
-        w['dq'] = np.maximum(w['dq'], np.abs(G[:, :nd] - C[:, :nd]).max(1))
-        w['obs'] = np.maximum(w['obs'], np.abs(ob[PICK, :od] - oc[:, :od]).max(1))
-        w['rew'] = np.maximum(w['rew'], np.abs(r[PICK] - rc) / (1.0 + np.abs(rc)))
-        w['force'] = np.maximum(w['force'], np.abs(ob[PICK, od] - oc[:, od]) / (1.0 + np.abs(oc[:, od])))
-        spread = np.maximum(spread, np.abs(op.get_state()[:, :nd] - C[:, :nd]).max(1))
+        C = o.get_state()
+        G = sim.get_state()[PICK]
+
+        def dev(acc, X, obx, rx):
+            acc['dq'] = np.maximum(acc['dq'], np.abs(X[:, :nd] - C[:, :nd]).max(1))
+            acc['obs'] = np.maximum(acc['obs'], np.abs(obx[:, :od] - oc[:, :od]).max(1))
+            acc['rew'] = np.maximum(acc['rew'], np.abs(rx - rc) / (1.0 + np.abs(rc)))
+            acc['force'] = np.maximum(acc['force'], np.abs(obx[:, od] - oc[:, od]) / (1.0 + np.abs(oc[:, od])))
+        dev(w, G, ob[PICK], r[PICK])
+        for e in ens:
+            eo, er, _, _ = e.step(a[PICK])
+            dev(s, e.get_state(), eo, er)
         assert np.array_equal(d[PICK], dc)
-        same &= i[PICK, 1] == ic[:, 1]                                            # task_success
-        same &= G[:, L.S_TASK + L.T_SUCCESS] == C[:, L.S_TASK + L.T_SUCCESS].astype(np.float32)
+        calm_now = s['dq'] < 1e-4
+        same &= ~calm_now | (i[PICK, 1] == ic[:, 1])                                           # task_success
+        same &= ~calm_now | (G[:, L.S_TASK + L.T_SUCCESS] == C[:, L.S_TASK + L.T_SUCCESS].astype(np.float32))
         if task == ABI.TASK_BEDBATH:
-            same &= np.all(_wipe_bits(G, L) == _wipe_bits(C, L).astype(np.float32), axis=1)
+            same &= ~calm_now | np.all(_wipe_bits(G, L) == _wipe_bits(C, L).astype(np.float32), axis=1)
         ncp += int(np.count_nonzero(G[:, L.S_TASK + L.T_NCP]))
     sim.close()
-    # a pick whose own oracle moves by more than 1e-3 under a 1e-4 perturbation of its actions sits
-    # at a contact bifurcation (e.g. the scratcher pressed hard into the arm: a wrist joint ends at
-    # 0.86 or 0.36 rad depending on the fifth decimal of the action); the rest are held to the
-    # one-step tolerances, up to two picks: the fp32 GJK / EPA misses ~1 % of penetrating
-    # box-capsule queries (test_narrowphase_pairs.py), and a contact pick makes tens per step
-    calm = spread < 1e-3
-    ok = same & (w['dq'] < 1e-3) & (w['obs'] < 2e-3) & (w['rew'] < 2e-3) & (w['force'] < 5e-2)
-    print('launch shape', task, {k: float(v[calm & ok].max()) for k, v in w.items()}, 'sensitive picks', int((~calm).sum()),
-          'calm picks off', [(int(PICK[k]), float(w['dq'][k])) for k in np.nonzero(calm & ~ok)[0]], 'contact env-steps', ncp)
-    assert ncp > 0 and calm.sum() >= n // 2, spread
-    assert (calm & ~ok).sum() <= 2, w
+    tol = dict(dq=1e-3, obs=2e-3, rew=2e-3, force=5e-2)
+    bound = {k: np.maximum(tol[k], 2.0 * s[k]) for k in keys}
+    ok = same & np.all([w[k] <= bound[k] for k in keys], axis=0)
+    chaotic = s['dq'] >= 0.5 * tol['dq']
+    print('launch shape', task, 'picks', n, 'contact picks', n_contact_picks, 'contact env-steps', ncp,
+          'chaotic picks (fp32 ensemble >= 5e-4 rad)', [(int(PICK[k]), float(s['dq'][k]), float(w['dq'][k])) for k in np.nonzero(chaotic)[0]])
+    print('  calm picks: max GPU dev', {k: float(w[k][~chaotic].max()) for k in keys}, 'max ensemble dev', {k: float(s[k][~chaotic].max()) for k in keys})
+    print('  failing picks', [(int(PICK[k]), {q: (float(w[q][k]), float(bound[q][k])) for q in keys}) for k in np.nonzero(~ok)[0]])
+    assert n_contact_picks >= 16 and ncp >= 60, (n_contact_picks, ncp)
+    assert chaotic.sum() <= n // 4, 'the ensemble bound would carry too many picks'
+    assert ok.all()
 
 
 def _episode(task, sim_or_oracle, L, ids, steps, gpu):
