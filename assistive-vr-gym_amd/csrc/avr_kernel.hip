@@ -1789,8 +1789,12 @@ AVR_DI v3 iinv_mul(const EnvLDS &L, int f, v3 a) {
 //   w8..13 free A Jacobian (lin, ang)   w14..19 free B Jacobian
 // Contact rows (row n_nc + k, k = c for contact c's normal, n_c + 2c + {0,1} for its frictions)
 // have 16-word records at word CR_BASE + 16 k:
-//   w0 ownership mask | (robot slot + 1) << 20   w1 inv   w2 rhs   w3 friction coefficient
+//   w0 ownership mask | (robot slot + 1) << 20   w1 inv   w2 rhs   w3 see below
 //   w4..9 free A Jacobian   w10..15 free B Jacobian
+// w3: normal rows the residual limit (BT_RESIDUAL_SQRT inv), a friction unit's first row its
+// friction coefficient, its second row its own residual limit (and the second row's w0, which the
+// resolve does not read, the first row's limit); torsional rows their coefficient.  (K_TORSION) a
+// normal record's w0 also carries the contact's torsional index + 1 in bits 2..19 (0: none).
 // (normal rows clamp to [0, 1e10], frictions to +-friction * normal impulse; the normal row's
 // starting impulse is the manifold point's cached impulse x warm-start factor, read by part B
 // from the contact pool).  Rows with an articulated endpoint own a robot part (slot): 16 (J[d],
@@ -1845,6 +1849,10 @@ AVR_DI float *row_rob(const KModel &m, float *base, int slot) { return base + m.
 #ifndef B4_FPAIR
 #define B4_FPAIR 0
 #endif
+#if B4_FPAIR
+#error "B4_FPAIR: the second friction row's 4th header word now holds its residual limit, not the coupling"
+#endif
+static_assert(!K_TORSION || MAXF == 1, "the torsional index shares the normal header's word 0 with a 1-body ownership mask");
 AVR_DI void put_free(const EnvLDS &L, int f, float *w, v3 jl, v3 ja) {
     const float *g = L.gsc[f];
     const qt q = ldq(L.st + S_FREE + AVR_FB_WORDS * f + 3);
@@ -1861,8 +1869,12 @@ AVR_DI void put_free_zero(float *w) {
 #pragma unroll
     for (int k = 0; k < 6; k++) w[k] = 0.f;
 }
+// PyBullet's solverResidualThreshold (1e-7 on the largest squared row residual of a PGS iteration,
+// the row's impulse change over its jacDiagABInv; oracle/avr_oracle.c BT_RESIDUAL_THRESHOLD): a row
+// has converged when |delta| <= sqrt(1e-7) inv.  Kernel a stores that limit with every row.
+#define BT_RESIDUAL_SQRT 3.16227766e-4f
 AVR_DI void put_hdr(float *w, int info, float inv, float rhs, float lo, float hi, int slot) {
-    w[0] = __int_as_float(info); w[1] = __int_as_float(slot + 1); w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = 0.f; w[7] = 0.f;
+    w[0] = __int_as_float(info); w[1] = __int_as_float(slot + 1); w[2] = inv; w[3] = rhs; w[4] = lo; w[5] = hi; w[6] = BT_RESIDUAL_SQRT * inv; w[7] = 0.f;
 }
 AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 #if NDL == 2
@@ -2115,6 +2127,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         float fric = fminf(gld(m.body_friction + (ba)) * gld(m.body_friction + (bb)), 10.f);
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
+        float rlim1 = 0.f;                           // the first friction row's residual limit
 #pragma unroll 1
         for (int k = 0; k < nrow; k++) {
             const int kd = k < 3 ? k : k - 3;
@@ -2179,8 +2192,11 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 else poserr = -pen * erp / dt;
                 rhs = (poserr + velerr) * inv;
             }
-            w[0] = __int_as_float(info | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs;
-            w[3] = tor ? tcoef : k == 0 ? (trs ? (float)(ti + 1) : 0.f) : fric;
+            const float rlim = BT_RESIDUAL_SQRT * inv;
+            const int tword = K_TORSION && k == 0 && trs ? (ti + 1) << 2 : 0;    // (K_TORSION: MAXF 1, own bits 0-1)
+            w[0] = k == 2 ? rlim1 : __int_as_float(info | tword | ((slot + 1) << CI_SLOT)); w[1] = inv; w[2] = rhs;
+            w[3] = tor ? tcoef : k == 1 ? fric : rlim;
+            if (k == 1) rlim1 = rlim;
 #if B4_FPAIR
             if (k == 2) {
                 // the friction unit's coupling c = J_2 M^-1 J_1^T (its second row's 4th header word,
@@ -3087,7 +3103,7 @@ static_assert(2 * MAXF <= CI_SLOT && MAXNC + K_CROWS * K_MAX_CONTACTS < (1 << (3
 // impulse slots: the second row's loads are the first's plus immediate offsets.
 
 // non-contact rows: buffer loads (they stay L2-resident)
-struct NcRow { int o; lds_f *ip; f4v h0; f2v h1; float imp; f2v j0, j1, j2; rv_t r; };
+struct NcRow { int o; lds_f *ip; f4v h0, h1; float imp; f2v j0, j1, j2; rv_t r; };   // h1: lo, hi, residual limit
 struct NcSrc {
     typedef NcRow Row;
     static constexpr bool robot_parts = true;
@@ -3095,7 +3111,7 @@ struct NcSrc {
     int eo, ro;                // this env's records / robot parts (byte offsets)
     lds_f *ip0, *nullip;       // impulse slots: row 0, null rows
     AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
-    AVR_DI void hdr(Row &R) const { R.h0 = bld4(rs, R.o); R.h1 = bld2(rs, R.o + 16); R.imp = *R.ip; }
+    AVR_DI void hdr(Row &R) const { R.h0 = bld4(rs, R.o); R.h1 = bld3(rs, R.o + 16); R.imp = *R.ip; }
     AVR_DI void parts(Row &R) const {
         const int o = own_of(__float_as_int(R.h0.x));     // endpoint A at word 8, B at word 14
         const int b = o ? R.o + 8 + 24 * o : B4_OOB;
@@ -3125,7 +3141,8 @@ struct NcLds {
     AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : LNB_NCNULL; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const {
         R.h0 = *(const lds_f4 *)(blk + R.o - 8);
-        R.h1 = *(const lds_f2 *)(blk + R.o + 8);
+        const f2v a = *(const lds_f2 *)(blk + R.o + 8);
+        R.h1.x = a.x; R.h1.y = a.y; R.h1.z = *(const lds_f *)(blk + R.o + 16);
         R.imp = *R.ip;
     }
     AVR_DI void parts(Row &R) const {
@@ -3161,12 +3178,8 @@ struct CLds {
         R.h.x = a.x; R.h.y = a.y; R.h.z = q[2];
         R.imp = *R.ip;
     }
-    AVR_DI void hdr2(Row &B, const Row &A) const {   // a unit's second row: inv, rhs, coupling (the rest is the first row's)
-        const lds_f *q = (const lds_f *)(blk + A.wb + 8 + CRW * 4);
-        B.h.y = q[1]; B.h.z = q[2];
-#if B4_FPAIR
-        B.h.w = q[3];
-#endif
+    AVR_DI void hdr2(Row &B, const Row &A) const {   // a unit's second row: the first row's residual limit, inv, rhs, its own limit
+        B.h = *(const lds_f4 *)(blk + A.wb + 8 + CRW * 4);
         B.imp = A.ip[1];
     }
     AVR_DI unsigned own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.wb + 24 * o : LNB_ZERO; }
@@ -3178,7 +3191,7 @@ struct CLds {
     }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
     // (K_TORSION) contact c's torsional index + 1 (0: none), its normal record's 4th word
-    AVR_DI int tor_of(int c) const { return (int)*(const lds_f *)(blk + cn + CRW * 4 * c + 20); }
+    AVR_DI int tor_of(int c) const { return (int)((unsigned)__float_as_int(*(const lds_f *)(blk + cn + CRW * 4 * c + 8)) >> 2 & 0x3ffffu); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
         const unsigned b = own_b(A), r = rob_b(A);
         own_at(A, b); own_at(B, b + CRW * 4);
@@ -3201,17 +3214,13 @@ struct CGlb {
     AVR_DI void set(Row &R, bool v, int o, lds_f *ip) const { R.o = v ? o : B4_OOB; R.ip = v ? ip : nullip; }
     AVR_DI void hdr(Row &R) const { R.h = bld4(rs, R.o); R.imp = *R.ip; }
     AVR_DI void hdr3(Row &R) const { R.h = bld3(rs, R.o); R.imp = *R.ip; }
-#if B4_FPAIR
-    AVR_DI void hdr2(Row &B, const Row &A) const { const f4v a = bld3(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.h.w = a.z; B.imp = A.ip[1]; }
-#else
-    AVR_DI void hdr2(Row &B, const Row &A) const { const f2v a = bld2(rs, A.o + CRW * 4 + 4); B.h.y = a.x; B.h.z = a.y; B.imp = A.ip[1]; }
-#endif
+    AVR_DI void hdr2(Row &B, const Row &A) const { B.h = bld4(rs, A.o + CRW * 4); B.imp = A.ip[1]; }
     AVR_DI int own_b(const Row &R) const { const int o = own_of(__float_as_int(R.h.x)); return o ? R.o - 8 + 24 * o : B4_OOB; }
     AVR_DI void own_at(Row &R, int b) const { R.j0 = bld2(rs, b); R.j1 = bld2(rs, b + 8); R.j2 = bld2(rs, b + 16); }
     AVR_DI int rob_b(const Row &R) const { const int s = (int)((unsigned)__float_as_int(R.h.x) >> CI_SLOT); return s ? rob + ROBW * 4 * s : B4_OOB; }
     AVR_DI rv_t rob_at(int b) const { return rload(rs, b); }
     AVR_DI void parts(Row &R) const { own_at(R, own_b(R)); R.r = rob_at(rob_b(R)); }
-    AVR_DI int tor_of(int c) const { return (int)bld1(rs, cn + CRW * 4 * c + 12); }
+    AVR_DI int tor_of(int c) const { return (int)((unsigned)__float_as_int(bld1(rs, cn + CRW * 4 * c)) >> 2 & 0x3ffffu); }
     AVR_DI void unit_parts(Row &A, Row &B) const {
         const int b = own_b(A), r = rob_b(A);
         own_at(A, b); own_at(B, b + CRW * 4);
@@ -3232,9 +3241,11 @@ AVR_DI float row16_sum(float x) {
 // resolve one row with its current impulse; returns the new impulse.  The fused multiply-adds
 // are spelled out and nothing else may contract: every unrolled copy of a row resolve (and every
 // pipeline depth) then rounds the same way, so an env's results do not depend on which copy
-// resolves its rows or on the row counts of the other envs in its wavefront.
+// resolves its rows or on the row counts of the other envs in its wavefront.  With acc, the lanes
+// of a row whose impulse change exceeds its residual limit rl (BT_RESIDUAL_SQRT inv: the row has not
+// converged, solverResidualThreshold) are or-ed into acc.
 template <bool RP, class R>
-AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi) {
+AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, float hi, float rl = 0.f, unsigned long long *acc = nullptr) {
 #pragma clang fp contract(off)
 #if B4_PK
     // the same products and roundings as below, two per packed instruction: parts are stored as
@@ -3252,6 +3263,7 @@ AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, f
     const float dv = row16_sum(s.x + s.y);
     const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
     const float delta = ni - imp;
+    if (acc) *acc |= __ballot(fabsf(delta) > rl);
     const f2v dd = {delta, delta};
     d.v1 = __builtin_elementwise_fma(X.j0, dd, d.v1);
     d.v2 = __builtin_elementwise_fma(X.j1, dd, d.v2);
@@ -3273,6 +3285,7 @@ AVR_DI float go4(const R &X, DV &d, float imp, float inv, float rhs, float lo, f
     const float dv = row16_sum(p + q);
     const float ni = __builtin_amdgcn_fmed3f(imp + fmaf(-dv, inv, rhs), lo, hi);
     const float delta = ni - imp;
+    if (acc) *acc |= __ballot(fabsf(delta) > rl);
     d.vx = fmaf(X.j0.x, delta, d.vx); d.vy = fmaf(X.j0.y, delta, d.vy); d.vz = fmaf(X.j1.x, delta, d.vz);
     d.wx = fmaf(X.j1.y, delta, d.wx); d.wy = fmaf(X.j2.x, delta, d.wy); d.wz = fmaf(X.j2.y, delta, d.wz);
     if (RP) d.rq = fmaf(X.r.y, delta, d.rq);
@@ -3371,6 +3384,13 @@ struct TorSrc {
 };
 #endif
 
+// the largest of the four groups' values, wave-uniform
+AVR_DI int wave_max4(int x) {
+    x = max(x, __shfl_xor(x, 16));
+    x = max(x, __shfl_xor(x, 32));
+    return uni(x);
+}
+
 template <int DN, int DC, class NS, class CS>
 AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, lds_i *tlist, int n_nc, int n_c, int nnc_max, int nc_max, DV &d) {
     typedef typename NS::Row NR;
@@ -3387,31 +3407,36 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, lds_i 
     // is also the rows' starting impulse
     sweep4<DC, true>(cs, nc_max, at_n, [&](const CR &R) { (void)go4<CS::robot_parts>(R, d, 0.f, R.h.y, R.h.z, R.imp, R.imp); });
     int units = 0;      // friction units swept (diagnostics)
+    // solverResidualThreshold: a group whose rows all stayed within their residual limits in an
+    // iteration is done -- its rows are null rows from then on (Bullet leaves that solve group's
+    // PGS loop), and the wave leaves the loop once its four groups are done
+    bool done = false;
     for (int it = 0; it < m.iters; it++) {
+        const int a_nc = done ? 0 : n_nc, a_c = done ? 0 : n_c;         // this iteration's rows
+        const int anc_max = wave_max4(a_nc), ac_max = wave_max4(a_c);
+        unsigned long long acc = 0ull;      // lanes of groups with a row above its residual limit
         // non-contact rows, the sweep direction alternating per iteration
         const bool fwd = (it & 1) != 0;
         const int r0 = fwd ? 0 : n_nc - 1, sg = fwd ? 1 : -1;
         const int ob = ns.eo + r0 * (RWC * 4);
         lds_f *ib = ns.ip0 + r0;
-        sweep4<DN, false>(ns, nnc_max, [&](NR &R, int j) { ns.set(R, j < n_nc, ob + sg * j * (RWC * 4), ib + sg * j); },
-                          [&](const NR &R) { *R.ip = go4<true>(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y); });
-        sweep4<DC, true>(cs, nc_max, at_n, [&](const CR &R) { *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f); });
+        sweep4<DN, false>(ns, anc_max, [&](NR &R, int j) { ns.set(R, j < a_nc, ob + sg * j * (RWC * 4), ib + sg * j); },
+                          [&](const NR &R) { *R.ip = go4<true>(R, d, R.imp, R.h0.z, R.h0.w, R.h1.x, R.h1.y, R.h1.z, &acc); });
+        auto at_na = [&](CR &R, int j) { cs.set(R, j < a_c, cs.cn + CRW * 4 * j, cs.ipn + j); };
+        sweep4<DC, false>(cs, ac_max, at_na, [&](const CR &R) { *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, 0.f, 1e10f, R.h.w, &acc); });
         // active contacts (positive normal impulse) of each group, in contact order
         int t = 0;
-        for (int c0 = 0; c0 < nc_max; c0 += 16) {
+        for (int c0 = 0; c0 < ac_max; c0 += 16) {
             const int c = c0 + sl;
-            const bool a = c < n_c && cs.ipn[c < n_c ? c : 0] > 0.f;
+            const bool a = c < a_c && cs.ipn[c < a_c ? c : 0] > 0.f;
             const unsigned long long b = __ballot(a);
             const unsigned gm = (unsigned)(b >> (lane_id() & 48)) & 0xffffu;
             if (a) list[t + __popc(gm & ((1u << sl) - 1u))] = c;
             t += __popc(gm);
         }
-        int tmax = t;
-        tmax = max(tmax, __shfl_xor(tmax, 16));
-        tmax = max(tmax, __shfl_xor(tmax, 32));
-        tmax = uni(tmax);
+        const int tmax = wave_max4(t);
         units += tmax;
-        if (tmax == 0) continue;
+        if (tmax > 0) {
         // the same depth-DC pipeline over friction units; list entries are read one step before
         // the headers they address
         constexpr int K = 2 * DC + 1;
@@ -3431,8 +3456,8 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, lds_i 
             go4_pair<CS::robot_parts>(Y.a, Y.b, d, ia, ib, lim);
             Y.a.ip[0] = ia; Y.a.ip[1] = ib;
 #else
-            Y.a.ip[0] = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim);
-            Y.a.ip[1] = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim);
+            Y.a.ip[0] = go4<CS::robot_parts>(Y.a, d, Y.a.imp, Y.a.h.y, Y.a.h.z, -lim, lim, Y.b.h.x, &acc);
+            Y.a.ip[1] = go4<CS::robot_parts>(Y.b, d, Y.b.imp, Y.b.h.y, Y.b.h.z, -lim, lim, Y.b.h.w, &acc);
 #endif
         };
         // (whole rounds of K units, null units past the end, unconditional read-ahead: sweep4)
@@ -3484,10 +3509,13 @@ AVR_DI int pgs4(const KModel &m, const NS &ns, const CS &cs, lds_i *list, lds_i 
                 R.in = v ? x : 0.f;
             }, [&](const TorRow<CS> &R) {
                 const float lim = R.h.w * R.in;
-                *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, -lim, lim);
+                *R.ip = go4<CS::robot_parts>(R, d, R.imp, R.h.y, R.h.z, -lim, lim, BT_RESIDUAL_SQRT * R.h.y, &acc);
             });
         }
 #endif
+        }   // (tmax > 0)
+        done = done || ((acc >> (lane_id() & 48)) & 0xffffull) == 0ull;
+        if (__ballot(!done) == 0ull) break;
     }
     return units;
 }

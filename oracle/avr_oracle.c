@@ -118,6 +118,13 @@ static unsigned probe_mask;
 #define BT_ANGULAR_MOTION_THRESHOLD (0.5 * 1.5707963267948966) /* btMultiBody quat update   */
 #define BT_BROADPHASE_EXPAND 0.02      /* gContactBreakingThreshold AABB fattening           */
 #define BT_DENOM_EPS 1e-12             /* SIMD_EPSILON guard on jacDiagABInv (double build)  */
+/* PyBullet's solverResidualThreshold (btContactSolverInfo::m_leastSquaresResidualThreshold, which
+ * PhysicsServerCommandProcessor sets to 1e-7 [ext]): the PGS stops after the first iteration whose
+ * largest squared row residual -- the row's impulse change times its effective mass denominator,
+ * max over every row resolved in that iteration -- is at most this
+ * (btSequentialImpulseConstraintSolver::solveGroupCacheFriendlyIterations,
+ * btMultiBodyConstraintSolver::solveSingleIteration [ext]).  One solve group per env. */
+#define BT_RESIDUAL_THRESHOLD 1e-7
 #define BT_LARGE 1e18
 #define GJK_MAX_IT 64
 #define GJK_REL_EPS 1e-6
@@ -249,7 +256,7 @@ typedef struct {
     int nsp;
     int gender;
     real oldcp[K_MAX_CONTACTS * AVR_CP_WORDS];
-    long long stats_gjk, stats_epa, stats_rows;
+    long long stats_gjk, stats_epa, stats_rows, stats_iters, stats_solves;
 } ws_t;
 
 typedef struct avr_oracle {
@@ -1261,7 +1268,9 @@ static void build_contact_rows(const model *m, real *st, ws_t *w, real dt) {
     }
 }
 
-static void resolve(const model *m, ws_t *w, row_t *r) {
+/* one row resolve (btMultiBodyConstraintSolver::resolveSingleConstraintRowGeneric [ext]); returns
+ * the row's squared residual: (impulse change / jacDiagABInv)^2 */
+static real resolve(const model *m, ws_t *w, row_t *r) {
     real dv = PRB(7, ep_dot(m, w, r->kindA, r->idxA, r->JA, 1) + ep_dot(m, w, r->kindB, r->idxB, r->JB, 1));
     real delta = PRB(7, r->rhs - dv * r->inv);
     real sum = r->imp + delta;
@@ -1270,23 +1279,28 @@ static void resolve(const model *m, ws_t *w, row_t *r) {
     else r->imp = sum;
     ep_apply(m, w, r->kindA, r->idxA, r->MA, delta);
     ep_apply(m, w, r->kindB, r->idxB, r->MB, delta);
+    const real res = delta / r->inv;
+    return res * res;
 }
 
 static void solve(const model *m, ws_t *w) {
     int iters = m->d.solver_iterations;
+    w->stats_solves++;
+#define RES(x) do { const real r_ = (x); if (r_ > res) res = r_; } while (0)
     for (int it = 0; it < iters; it++) {
+        real res = 0;                       /* largest squared residual of this iteration */
         for (int j = 0; j < w->n_nc; j++) {
             int k = (it & 1) ? j : w->n_nc - 1 - j;
-            resolve(m, w, &w->rows[w->nc_idx[k]]);
+            RES(resolve(m, w, &w->rows[w->nc_idx[k]]));
         }
-        for (int j = 0; j < w->n_nrm; j++) resolve(m, w, &w->rows[w->nrm_idx[j]]);
+        for (int j = 0; j < w->n_nrm; j++) RES(resolve(m, w, &w->rows[w->nrm_idx[j]]));
         for (int j = 0; j < w->n_fr; j++) {
             row_t *f = &w->rows[w->fr_idx[j]];
             real nimp = w->rows[w->nrm_idx[f->normal_row]].imp;
             if (nimp > 0) {
                 f->lo = -f->fric * nimp;
                 f->hi = f->fric * nimp;
-                resolve(m, w, f);
+                RES(resolve(m, w, f));
             }
         }
         /* torsional friction rows after the lateral ones (solveSingleIteration [ext]), limits
@@ -1297,10 +1311,13 @@ static void solve(const model *m, ws_t *w) {
             if (nimp > 0) {
                 f->lo = -f->fric * nimp;
                 f->hi = f->fric * nimp;
-                resolve(m, w, f);
+                RES(resolve(m, w, f));
             }
         }
+        w->stats_iters++;
+        if (res <= R(BT_RESIDUAL_THRESHOLD)) break;     /* solverResidualThreshold */
     }
+#undef RES
 }
 
 /* ---------------------------------------------------------------- collision detection */
@@ -1800,9 +1817,13 @@ EXPORT int avr_oracle_substep(avr_oracle *o, double dt) {
     return 0;
 }
 
-EXPORT void avr_oracle_stats(avr_oracle *o, long long *out3) {
-    out3[0] = out3[1] = out3[2] = 0;
-    for (int e = 0; e < o->n_envs; e++) { out3[0] += o->ws[e].stats_gjk; out3[1] += o->ws[e].stats_epa; out3[2] += o->ws[e].stats_rows; }
+/* counters since creation: GJK runs, EPA runs, constraint rows built, PGS iterations run, PGS solves */
+EXPORT void avr_oracle_stats(avr_oracle *o, long long *out5) {
+    for (int k = 0; k < 5; k++) out5[k] = 0;
+    for (int e = 0; e < o->n_envs; e++) {
+        out5[0] += o->ws[e].stats_gjk; out5[1] += o->ws[e].stats_epa; out5[2] += o->ws[e].stats_rows;
+        out5[3] += o->ws[e].stats_iters; out5[4] += o->ws[e].stats_solves;
+    }
 }
 
 /* threads used by avr_oracle_step / avr_oracle_settle (OpenMP over envs; 1 = serial) */

@@ -540,3 +540,50 @@ def test_spinning_friction_torque_is_bounded_by_mu_n(scene, oracle_built):
         alpha = np.polyfit(np.arange(1, 21) * dt, np.array(ws), 1)[0]
         assert alpha == pytest.approx(want, abs=0.02 * mu_s * m * g / I), (spinning, alpha, want)
         assert np.all(np.array(ws) > 0)
+
+
+# ----------------------------------------------------------------------------- solver residual threshold
+def test_pgs_stops_at_the_residual_threshold(oracle_built):
+    """PyBullet's solverResidualThreshold (1e-7 on the largest squared row residual of a PGS
+    iteration, [ext]): one unsaturated motor row alone (the chain scene's weld rows have max force 0)
+    is met exactly by the first iteration, so the second changes nothing and the solve stops there:
+    2 iterations of the 10 allowed, every sub-step, and the motor's closed form still holds."""
+    import kat_scene as K
+    from oracle.oracle import Oracle
+    A = K.chain_scene([dict(parent=-1, axis=[0, 0, 1], jpos=[0, 0, 0], com_pos=[0.3, 0, 0], mass=2.0, inertia=[0.01, 0.02, 0.03])])
+    md = K.desc(A)
+    kp, q0, qs, dt = 0.1, 0.2, 1.0, 0.01
+    o = Oracle(md, 1)
+    o.set_state(K.state(md, [q0], kp=[kp], target=[qs], maximp=[1e6]))
+    for _ in range(20):
+        o.substep(dt)
+    st = o.stats()
+    assert st[4] == 20 and st[3] == 2 * 20, st
+    assert o.get_state()[0, ABI.S_Q] == pytest.approx(qs + (q0 - qs) * (1 - kp) ** 20, abs=1e-12)
+
+
+def test_pgs_iterations_used_per_task(scene, oracle_built):
+    """How many of their PGS iterations the tasks' solves use under the residual threshold: the
+    PR2 tasks' reset states (arm in free space, 50 allowed) stop well before 50; FeedingJaco's food
+    pile in the spoon never converges to 1e-7 within its 10 (measured: every solve runs all 10)."""
+    from oracle.oracle import Oracle
+    from avr import _lib
+    import scratch_util as U
+    A, md = U.scene()
+    S, _ = U.reset_states(A, md, range(4))
+    o = Oracle(md, 4)
+    o.set_state(S.astype(np.float64))
+    for t in range(5):
+        o.step(_lib.random_actions(1001, np.arange(4), t))
+    st = o.stats()
+    print('ScratchItchPR2: %.1f iterations per solve of 50' % (st[3] / st[4]))
+    assert st[4] == 4 * 5 * 5 and st[3] / st[4] < 25
+    A, md, S = _one_env_state(scene)
+    o = Oracle(md, 1)
+    o.set_state(S)
+    o.settle(20)
+    s0 = o.stats()
+    o.step(_lib.random_actions(1001, np.arange(1), 0))
+    st = o.stats() - s0
+    print('FeedingJaco: %.1f iterations per solve of 10' % (st[3] / st[4]))
+    assert st[4] == 10 and st[3] <= 10 * 10

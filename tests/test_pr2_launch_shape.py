@@ -6,12 +6,12 @@ configs[3]) at the bench's launch shape and over contact horizons, against the C
     the cloth pressed onto a wipe target), tiled; 32 sampled envs (every group, part-B block
     boundaries included) against the fp64 oracle over 5 gym steps: joint angles, observations,
     rewards, done and the task bookkeeping (success counts, wipe bits) per step;
-  * contact regime: 128 envs x 200 gym steps starting in contact, small random actions (x 0.2,
+  * contact regime: 512 envs x 200 gym steps starting in contact, small random actions (x 0.2,
     so the tool stays on the person), GPU vs the fp64 oracle.  Contact trajectories diverge at
     the rounding level (chaos), so the episode outcomes are compared statistically, as FeedingJaco's
-    (test_gpu_parity.py): mean episode reward (paired difference within 3 standard errors +
-    tolerance), scratches / wiped targets (task_success counters, scratch_itch.py:66-70 and
-    bed_bathing.py:97-125), contact-step counts and the final task_success flags.
+    (test_gpu_parity.py): mean episode reward, scratches / wiped targets (the task_success
+    counters, scratch_itch.py:66-70 and bed_bathing.py:97-125) and contact-step counts, each as a
+    paired difference within three standard errors.
 """
 import numpy as np
 import pytest
@@ -162,11 +162,17 @@ def _episode(task, sim_or_oracle, L, ids, steps, gpu):
 
 @pytest.mark.parametrize('task', [ABI.TASK_SCRATCH, ABI.TASK_BEDBATH], ids=['ScratchItchPR2', 'BedBathingPR2'])
 def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
+    """512 envs x 200 gym steps from the contact states (distinct action streams per env) on the GPU
+    and on the fp64 oracle.  Contact trajectories part at the rounding level (chaos), so episode
+    outcomes are compared as paired statistics: the mean episode reward, the scratch / wipe counter
+    (task_success before the threshold, scratch_itch.py:66-70, bed_bathing.py:97-125) and the
+    contact-step count each within three standard errors of the paired differences (plus a 1 %
+    allowance on the reward)."""
     from avr import _lib
     A, md, L, P, is_c = _pool(task, 16)
     C = P[is_c]
-    n = 128
-    S = np.tile(C, (n // len(C) + 1, 1))[:n]        # distinct action streams per env id
+    n = 512
+    S = np.tile(C, (n // len(C) + 1, 1))[:n]
     ids = np.arange(n)
     sim = _lib.Sim(md, n)
     sim.set_state(S)
@@ -175,15 +181,20 @@ def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
     Rg, Kg, G, ig = _episode(task, sim, L, ids, 200, True)
     Rc, Kc, Cs, ic = _episode(task, o, L, ids, 200, False)
     sim.close()
-    d = Rg - Rc
-    se = d.std(ddof=1) / np.sqrt(n)
-    sg, sc = G[:, L.S_TASK + L.T_SUCCESS], Cs[:, L.S_TASK + L.T_SUCCESS]
-    print('contact regime', task, 'reward mean gpu %.4f oracle %.4f diff %.4f se %.4f' % (Rg.mean(), Rc.mean(), d.mean(), se),
-          'success mean %.3f %.3f' % (sg.mean(), sc.mean()), 'contact steps %.2f %.2f' % (Kg.mean(), Kc.mean()),
-          'task_success %.3f %.3f' % (ig[:, 1].mean(), ic[:, 1].mean()))
+    sg, sc = G[:, L.S_TASK + L.T_SUCCESS].astype(np.float64), Cs[:, L.S_TASK + L.T_SUCCESS]
+
+    def paired(a, b):
+        d = a - b
+        return d.mean(), d.std(ddof=1) / np.sqrt(len(d))
+    dr, ser = paired(Rg, Rc)
+    ds, ses = paired(sg, sc)
+    dk, sek = paired(Kg, Kc)
+    print('contact regime', task, 'reward mean gpu %.4f oracle %.4f diff %.4f se %.4f' % (Rg.mean(), Rc.mean(), dr, ser),
+          'success counter %.3f %.3f diff %.3f se %.3f' % (sg.mean(), sc.mean(), ds, ses),
+          'contact steps %.2f %.2f diff %.2f se %.2f' % (Kg.mean(), Kc.mean(), dk, sek))
     assert np.all(np.isfinite(Rg)) and np.all(G[:, L.S_TASK + L.T_FLAGS].astype(np.int64) & 0x1f == 0)
     assert Kg.mean() > 5 and Kc.mean() > 5            # the episodes do run in contact
-    assert abs(d.mean()) < 3 * se + 0.05 * abs(Rc.mean()) + 0.5, (d.mean(), se)
-    assert abs(sg.mean() - sc.mean()) <= 0.1 * max(sc.mean(), 1.0) + 0.5, (sg.mean(), sc.mean())
-    assert abs(Kg.mean() - Kc.mean()) <= 0.1 * Kc.mean() + 2.0, (Kg.mean(), Kc.mean())
-    assert abs(ig[:, 1].mean() - ic[:, 1].mean()) <= 0.1
+    assert sc.mean() > 0.05                           # and score (scratches / wiped targets)
+    assert abs(dr) <= 3 * ser + 0.01 * abs(Rc.mean()), (dr, ser)
+    assert abs(ds) <= 3 * ses + 1e-9, (ds, ses)
+    assert abs(dk) <= 3 * sek + 1e-9, (dk, sek)
