@@ -109,13 +109,22 @@ def test_committed_bedbath_scene_matches_compiler(tmp_path):
 
 
 # ------------------------------------------------------------------ reset
+# The vector pins the MALE settle: our male settle lands within 0.012 rad of it, the female's
+# elbow 0.088 rad away (a shorter, lighter forearm rests at -0.585 rad, not -0.674): the reference
+# recorded it on the male model, and holds no female value.  The male bound (0.02) is tight
+# against how strongly the settle responds to the Bullet defaults the restatement assumes
+# (tools/bb_settle_sensitivity.py, profiles/r05_bb_settle_sensitivity.txt): erp 0.1 / 0.8 move
+# the male arm 0.072 / 0.20 rad from the vector, no damping or 0.1 damping 0.040 / 0.061, 10
+# solver iterations 0.061, warm start 0.1 0.017; the assumed set (erp 0.2, damping 0.04, 50
+# iterations, warm start 0.85) is the nearest.  The female bound is a plausibility check only.
 VR_TOL = {'male': 0.02, 'female': 0.1}
 
 
 def test_arm_settle_matches_reference_vr_pose(bb, settled):
     """The 100-frame drop of the right arm onto the mattress (bed_bathing.py:283-289), fp64 oracle,
     against the arm pose the reference hard-codes for its VR/replay bed bathing (male: 0.012 rad
-    with the bed's rolling / spinning friction, 0.046 without)."""
+    with the bed's rolling / spinning friction, 0.046 without; the female has no reference value,
+    see VR_TOL)."""
     for g in ('male', 'female'):
         q, slots = settled[g]
         assert np.abs(q - VR_ARM).max() < VR_TOL[g], (g, q)
@@ -226,11 +235,13 @@ def test_bedbath_one_substep_matches_oracle(bb, states):
 @pytest.mark.gpu
 def test_bedbath_200_steps_within_1e3(bb, states):
     """200 gym steps of full-scale random actions: every env the fp64 oracle itself holds to
-    1e-3 under a 1e-6 perturbation of its actions stays within 1e-3 rad of it (and its obs and
-    reward within 2e-3); an env the perturbation moves further has met a contact bifurcation (the
-    arm or the cloth striking the bed, whose rolling / spinning friction 5 locks the contact
-    either way) -- there the GPU stays within 20x that spread.  At most 2 of the 8 envs may be
-    such."""
+    1e-3 under a 1e-6 perturbation of its actions stays within 1e-3 rad of it, and its obs and
+    reward within 2e-3 or three times the perturbed oracle's own obs / reward spread (the PGS's
+    residual-threshold exit is a discrete decision: an iteration more or less moves a contact's
+    impulse at the 3e-4 velocity level, and the cloth's speed term of the reward follows); an env
+    the perturbation moves further has met a contact bifurcation (the arm or the cloth striking
+    the bed, whose rolling / spinning friction 5 locks the contact either way) -- there the GPU
+    stays within 20x that spread.  At most 2 of the 8 envs may be such."""
     from avr import _lib
     A, md = bb
     S, meta = states
@@ -241,23 +252,28 @@ def test_bedbath_200_steps_within_1e3(bb, states):
     assert np.abs(sim.settle(0) - o.settle(0)).max() < 1e-5
     rng = np.random.default_rng(5)
     w, spread, wobs, wrew = np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n)
+    sobs, srew = np.zeros(n), np.zeros(n)
     for t in range(200):
         a = _lib.random_actions(1001, np.arange(n), t)
         g = sim.step(a)
         c = o.step(a)
-        op.step((a + 1e-6 * rng.standard_normal(a.shape)).astype(np.float32))
+        cp = op.step((a + 1e-6 * rng.standard_normal(a.shape)).astype(np.float32))
         wobs = np.maximum(wobs, np.abs(g[0][:, :23] - c[0][:, :23]).max(1))
         wrew = np.maximum(wrew, np.abs(g[1] - c[1]))
+        sobs = np.maximum(sobs, np.abs(cp[0][:, :23] - c[0][:, :23]).max(1))
+        srew = np.maximum(srew, np.abs(cp[1] - c[1]))
         assert np.array_equal(g[2], c[2])
         if t % 20 == 19:
             G, C, Cp = sim.get_state()[:, :nd], o.get_state()[:, :nd], op.get_state()[:, :nd]
             w = np.maximum(w, np.abs(G - C).max(1))
             spread = np.maximum(spread, np.abs(Cp - C).max(1))
     sim.close()
-    print('bedbath 200 steps: GPU vs fp64 oracle %s, oracle spread under 1e-6 action noise %s' % (w, spread))
+    print('bedbath 200 steps: GPU vs fp64 oracle dq %s obs %s reward %s; oracle spread under 1e-6 action noise dq %s obs %s reward %s' % (
+        w, wobs, wrew, spread, sobs, srew))
     calm = spread < 1e-3
     assert calm.sum() >= n - 2, spread
-    assert np.all(w[calm] < 1e-3) and np.all(wobs[calm] < 2e-3) and np.all(wrew[calm] < 2e-3), (w, wobs, wrew)
+    assert np.all(w[calm] < 1e-3), w
+    assert np.all(wobs[calm] < np.maximum(2e-3, 3 * sobs[calm])) and np.all(wrew[calm] < np.maximum(2e-3, 3 * srew[calm])), (wobs, sobs, wrew, srew)
     assert np.all(w[~calm] <= 20 * spread[~calm]), (w, spread)
 
 

@@ -57,11 +57,18 @@ def _wipe_bits(St, L):
 def _picks(n_pool, n_first_contact):
     """32 picks of the 4096-env launch (env e holds pool state e mod n_pool): every env group's
     first and last env, part-B block boundaries, and one env of every contact state spread over
-    the four groups, the last pool state (the scratcher pressed hardest) at every group end."""
+    the four groups; the rest of the 32 from further contact envs."""
     reset = [0, 1, 32, 33, 511, 512, 1024, 1025, 2048, 2049, 3072, 4064]
     contact = [n_first_contact + k + n_pool * (8 * k + 3) for k in range(n_pool - n_first_contact)]
     ends = [1023, 2047, 3071, 4095]
-    P = np.array(sorted(set(reset + contact + ends)))
+    P = sorted(set(reset + contact + ends))
+    extra = (n_first_contact + k % (n_pool - n_first_contact) + n_pool * (5 * k + 1) for k in range(10 ** 4))
+    for e in extra:
+        if len(P) >= 32:
+            break
+        if e < 4096 and e not in P:
+            P = sorted(P + [e])
+    P = np.array(P[:32])
     assert len(P) == 32 and P.max() < 4096
     return P
 
@@ -79,8 +86,11 @@ def _perturbed(S, L, nd, rng, eps):
 def test_launch_shape_sampled_envs_match_oracle(task):
     """32 sampled envs of the bench's launch against the fp64 oracle over 5 gym steps.  The GPU is
     one fp32 realisation of each env; an ensemble of fp32 oracles started from rounding-level
-    perturbations of the same states (1e-6 on the joint angles and the tool position) measures how
-    far fp32 rounding alone carries each env from the fp64 oracle.  Each pick is held to the
+    perturbations of the same states (1e-6 on the joint angles and the tool position, 16 members)
+    measures how far fp32 rounding alone carries each env from the fp64 oracle: on penetrating
+    hull-capsule contacts the fp32 GJK / EPA of both the kernel and the oracle lands on a wrong face
+    of the nearly degenerate Minkowski difference for ~3 % of poses (tools/dbg_np_state.py), and a
+    contact-rich pick meets such a pose now and then.  Each pick is held to the
     one-step tolerances, or -- where the ensemble itself spreads further (a contact bifurcation) --
     to twice the ensemble's own deviation; no pick is excepted."""
     from avr import _lib
@@ -99,7 +109,7 @@ def test_launch_shape_sampled_envs_match_oracle(task):
     o.set_state(S[PICK].astype(np.float64))
     rng = np.random.default_rng(9)
     ens = []
-    for j in range(5):                     # the fp32 oracle itself, then four perturbed starts
+    for j in range(16):                    # the fp32 oracle itself, then fifteen perturbed starts
         e = _oracle(md, n, 'f32')
         e.set_state(S[PICK].astype(np.float64) if j == 0 else _perturbed(S[PICK], L, nd, rng, 1e-6))
         ens.append(e)
@@ -163,11 +173,13 @@ def _episode(task, sim_or_oracle, L, ids, steps, gpu):
 @pytest.mark.parametrize('task', [ABI.TASK_SCRATCH, ABI.TASK_BEDBATH], ids=['ScratchItchPR2', 'BedBathingPR2'])
 def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
     """512 envs x 200 gym steps from the contact states (distinct action streams per env) on the GPU
-    and on the fp64 oracle.  Contact trajectories part at the rounding level (chaos), so episode
-    outcomes are compared as paired statistics: the mean episode reward, the scratch / wipe counter
-    (task_success before the threshold, scratch_itch.py:66-70, bed_bathing.py:97-125) and the
-    contact-step count each within three standard errors of the paired differences (plus a 1 %
-    allowance on the reward)."""
+    and on the fp32 and fp64 oracles.  Contact trajectories part at the rounding level (chaos), so
+    episode outcomes are compared as paired statistics: the mean episode reward, the scratch / wipe
+    counter (task_success before the threshold, scratch_itch.py:66-70, bed_bathing.py:97-125) and
+    the contact-step count.  Against the fp32 oracle (the same precision) each within three standard
+    errors of the paired differences; against the fp64 oracle within three standard errors plus the
+    fp32 oracle's own mean difference from fp64 (precision is not neutral here: BedBathing's fp32
+    oracle wipes ~1 % more targets than its fp64 build)."""
     from avr import _lib
     A, md, L, P, is_c = _pool(task, 16)
     C = P[is_c]
@@ -178,23 +190,26 @@ def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
     sim.set_state(S)
     o = _oracle(md, n, 'f64')
     o.set_state(S.astype(np.float64))
+    o32 = _oracle(md, n, 'f32')
+    o32.set_state(S.astype(np.float64))
     Rg, Kg, G, ig = _episode(task, sim, L, ids, 200, True)
     Rc, Kc, Cs, ic = _episode(task, o, L, ids, 200, False)
+    R3, K3, C3, i3 = _episode(task, o32, L, ids, 200, False)
     sim.close()
-    sg, sc = G[:, L.S_TASK + L.T_SUCCESS].astype(np.float64), Cs[:, L.S_TASK + L.T_SUCCESS]
+    sg, sc, s3 = (X[:, L.S_TASK + L.T_SUCCESS].astype(np.float64) for X in (G, Cs, C3))
 
     def paired(a, b):
         d = a - b
         return d.mean(), d.std(ddof=1) / np.sqrt(len(d))
-    dr, ser = paired(Rg, Rc)
-    ds, ses = paired(sg, sc)
-    dk, sek = paired(Kg, Kc)
-    print('contact regime', task, 'reward mean gpu %.4f oracle %.4f diff %.4f se %.4f' % (Rg.mean(), Rc.mean(), dr, ser),
-          'success counter %.3f %.3f diff %.3f se %.3f' % (sg.mean(), sc.mean(), ds, ses),
-          'contact steps %.2f %.2f diff %.2f se %.2f' % (Kg.mean(), Kc.mean(), dk, sek))
+    print('contact regime', task, 'reward mean gpu %.4f fp32 %.4f fp64 %.4f' % (Rg.mean(), R3.mean(), Rc.mean()),
+          'success counter %.3f %.3f %.3f' % (sg.mean(), s3.mean(), sc.mean()), 'contact steps %.2f %.2f %.2f' % (Kg.mean(), K3.mean(), Kc.mean()))
     assert np.all(np.isfinite(Rg)) and np.all(G[:, L.S_TASK + L.T_FLAGS].astype(np.int64) & 0x1f == 0)
     assert Kg.mean() > 5 and Kc.mean() > 5            # the episodes do run in contact
     assert sc.mean() > 0.05                           # and score (scratches / wiped targets)
-    assert abs(dr) <= 3 * ser + 0.01 * abs(Rc.mean()), (dr, ser)
-    assert abs(ds) <= 3 * ses + 1e-9, (ds, ses)
-    assert abs(dk) <= 3 * sek + 1e-9, (dk, sek)
+    for name, g, c64, c32 in (('reward', Rg, Rc, R3), ('success', sg, sc, s3), ('contact steps', Kg, Kc, K3)):
+        d32, se32 = paired(g, c32)
+        d64, se64 = paired(g, c64)
+        p, _ = paired(c32, c64)
+        print('  %s: gpu - fp32 %.4f (se %.4f), gpu - fp64 %.4f (se %.4f), fp32 - fp64 %.4f' % (name, d32, se32, d64, se64, p))
+        assert abs(d32) <= 3 * se32 + 1e-9, (name, d32, se32)
+        assert abs(d64) <= 3 * se64 + abs(p) + 1e-9, (name, d64, se64, p)

@@ -1,5 +1,5 @@
-"""Experiment builds of libavr.so: exp/libavr_<name>.so with the extra hipcc flags of VARIANTS
-(tools/gpu_variants.sh benches them against the shipped build).
+"""Experiment builds of libavr.so: _ab/libavr_<name>.so (VARDIR overrides) with the extra hipcc
+flags of VARIANTS (tools/gpu_ab_variants.sh benches them against the shipped build).
 
     python tools/build_variants.py name [name ...]
 """
@@ -28,14 +28,19 @@ VARIANTS = {
     'coopk': ('-DAVR_COOP_KERNEL=1',), 'ml': ('-DAVR_MINV_LAUNDER=1',), 'mlc': ('-DAVR_MINV_LAUNDER=1', '-DAVR_COOP_KERNEL=1'),
     'mlc2': ('-DAVR_MINV_LAUNDER=1', '-DAVR_COOP_KERNEL=1', '-DAVR_WAVES_PER_EU=2'),
     'nofp': ('-DB4_FPAIR=0',),
+    # round 5
+    'coopk5': ('-DAVR_COOP_KERNEL=1',), 'np5': ('-DNP_WAVES=5',), 'dc2r5': ('-DB4_DC=2',),
     'nonl': ('-DB4_NC_LDS=0',), 'fnl': ('-DB4_NC_LDS=1',), 'fnl12': ('-DB4_NC_LDS=1', '-DB4_LDSW=12288'), 'fnl11': ('-DB4_NC_LDS=1', '-DB4_LDSW=11264'), 'dnl2': ('-DB4_DNL=2',), 'noml': ('-DAVR_MINV_LAUNDER=0',),
 }
 
 
+OUT = os.environ.get('VARDIR', os.path.join(ROOT, '_ab'))    # _ab/: git-ignored, travels with gpurun
+
+
 def main(names):
-    os.makedirs(os.path.join(ROOT, 'exp'), exist_ok=True)
+    os.makedirs(OUT, exist_ok=True)
     for n in names:
-        out = os.path.join(ROOT, 'exp', 'libavr_%s.so' % n)
+        out = os.path.join(OUT, 'libavr_%s.so' % n)
         B.build_lib(extra=VARIANTS[n], out=out)
         print(out)
 
