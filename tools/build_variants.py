@@ -29,6 +29,8 @@ VARIANTS = {
     'mlc2': ('-DAVR_MINV_LAUNDER=1', '-DAVR_COOP_KERNEL=1', '-DAVR_WAVES_PER_EU=2'),
     'nofp': ('-DB4_FPAIR=0',),
     # round 5
+    'noepa': ('-DAVR_COOP_CAP=0', '-DAVR_COOP_PERSIST=0'),     # diagnostic only: no EPA / cooperative pair ever runs
+    'noepawt': ('-DAVR_COOP_CAP=0', '-DAVR_COOP_PERSIST=0', '-DAVR_WAVETIME'),
     'coopk5': ('-DAVR_COOP_KERNEL=1',), 'np5': ('-DNP_WAVES=5',), 'dc2r5': ('-DB4_DC=2',),
     'nonl': ('-DB4_NC_LDS=0',), 'fnl': ('-DB4_NC_LDS=1',), 'fnl12': ('-DB4_NC_LDS=1', '-DB4_LDSW=12288'), 'fnl11': ('-DB4_NC_LDS=1', '-DB4_LDSW=11264'), 'dnl2': ('-DB4_DNL=2',), 'noml': ('-DAVR_MINV_LAUNDER=0',),
 }

@@ -6,7 +6,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'assistive-vr-gym_amd')); sys.path.insert(0, ROOT)
 from avr import _abi as ABI, reset as RS, _lib
-so = os.path.join(ROOT, 'assistive-vr-gym_amd', 'avr', sys.argv[2] if len(sys.argv) > 2 else 'libavr_wt.so')
+so = sys.argv[2] if len(sys.argv) > 2 and os.path.isabs(sys.argv[2]) else os.path.join(ROOT, "assistive-vr-gym_amd", "avr", sys.argv[2] if len(sys.argv) > 2 else "libavr_wt.so")
 _lib.LIB_PATH = so
 lib = _lib.load(so)
 lib.avr_set_profile_buffer.argtypes = [C.c_void_p, C.c_void_p]
