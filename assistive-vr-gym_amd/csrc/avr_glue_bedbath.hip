@@ -114,7 +114,9 @@ AVR_DI BBForces bb_forces(const KModel &m, EnvLDS &L, BBShared &B, const float *
 // min over the closest points of the tool and the human (bed_bathing.py:61): every tool shape
 // against every human shape of the env's gender, the signed distance of each pair (negative:
 // penetration) when within `closest_distance` (4.0); the narrowphase's lane path, then the
-// wave-cooperative path (EPA) for the penetrating pairs it hands on.  Poses: the state after the
+// wave-cooperative path (EPA) for the penetrating pairs it hands on.  A stalled lane GJK (rc 4)
+// is rerun on the cooperative fp32 GJK, not the double one the step uses (gjk_coop_d): its
+// registers would take this kernel from 211 to 256 VGPRs (one wave per SIMD; BedBathing -5 %).  Poses: the state after the
 // step (the tool's body frame, the human slots).
 AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
     const int lane = lane_id();
@@ -149,7 +151,7 @@ AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
                 int nit, nk;
                 const int rc = narrowphase<false>(m, E, A, Bs, thr, nB, pB, d, nit, nk);
                 if (rc == 1) dmin = fminf(dmin, d);
-                else if (rc == 2) coop = true;
+                else if (rc == 2 || rc == 4) coop = true;
             }
         }
         unsigned long long cm = __ballot(coop);

@@ -812,10 +812,137 @@ AVR_DI int simplex_closest(SX &S, v3 &vout, float lam[4]) {
     return 0;
 }
 
+// The cooperative GJK for the pairs whose fp32 lane GJK stalled (rc 4: hulls, boxes and capsules
+// against each other) solves for the simplex's closest point in double precision.
+// Its Voronoi-region tests and barycentric weights on thin simplices -- a scratcher or wiper lying
+// along a limb capsule, a box edge along a segment -- cancel catastrophically in fp32: the fp32
+// GJK stops on "no progress" with a wrong witness for ~3 % of such poses (normals off by up to 50
+// degrees, distances by a centimetre; tools/dbg_np_state.py, kernel and fp32 oracle alike at
+// different poses), where the fp64 oracle -- PyBullet itself runs in double -- converges.  The
+// simplex vertices (float supports, exactly representable in double) are unchanged; the Voronoi
+// tests and the barycentric solve run in double, and the closest point and its weights are
+// rounded to float (the rest of the iteration is the fp32 GJK's).
+struct d3 { double x, y, z; };
+AVR_DI d3 D3(v3 a) { return d3{(double)a.x, (double)a.y, (double)a.z}; }
+AVR_DI d3 dadd(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+AVR_DI d3 dsub(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+AVR_DI d3 dscl(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
+AVR_DI d3 dcrs(d3 a, d3 b) { return d3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+AVR_DI double ddot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+AVR_DI v3 dtof(d3 a) { return V((float)a.x, (float)a.y, (float)a.z); }
+
+AVR_DI d3 tri_cp_d(d3 A, d3 B, d3 C, int &used, double &la, double &lb, double &lc) {
+    d3 ab = dsub(B, A), ac = dsub(C, A), ap = dscl(A, -1.0);
+    double d1 = ddot(ab, ap), d2 = ddot(ac, ap);
+    la = lb = lc = 0.0;
+    if (d1 <= 0.0 && d2 <= 0.0) { used = 1; la = 1.0; return A; }
+    d3 bp = dscl(B, -1.0);
+    double d3_ = ddot(ab, bp), d4 = ddot(ac, bp);
+    if (d3_ >= 0.0 && d4 <= d3_) { used = 2; lb = 1.0; return B; }
+    double vc = d1 * d4 - d3_ * d2;
+    if (vc <= 0.0 && d1 >= 0.0 && d3_ <= 0.0) {
+        double v = d1 / (d1 - d3_);
+        used = 3; la = 1.0 - v; lb = v; return dadd(A, dscl(ab, v));
+    }
+    d3 cp = dscl(C, -1.0);
+    double d5 = ddot(ab, cp), d6 = ddot(ac, cp);
+    if (d6 >= 0.0 && d5 <= d6) { used = 4; lc = 1.0; return C; }
+    double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+        double wv = d2 / (d2 - d6);
+        used = 5; la = 1.0 - wv; lc = wv; return dadd(A, dscl(ac, wv));
+    }
+    double va = d3_ * d6 - d5 * d4;
+    if (va <= 0.0 && (d4 - d3_) >= 0.0 && (d5 - d6) >= 0.0) {
+        double wv = (d4 - d3_) / ((d4 - d3_) + (d5 - d6));
+        used = 6; lb = 1.0 - wv; lc = wv; return dadd(B, dscl(dsub(C, B), wv));
+    }
+    double den = 1.0 / (va + vb + vc);
+    double v = vb * den, wv = vc * den;
+    used = 7; la = 1.0 - v - wv; lb = v; lc = wv;
+    return dadd(A, dadd(dscl(ab, v), dscl(ac, wv)));
+}
+
+AVR_DI void tri_compact_d(Simplex &S, int used, double la, double lb, double lc, float lam[4]) {
+    switch (used) {
+    case 1: S.n = 1; lam[0] = (float)la; break;
+    case 2: sx_copy(S, 0, 1); S.n = 1; lam[0] = (float)lb; break;
+    case 4: sx_copy(S, 0, 2); S.n = 1; lam[0] = (float)lc; break;
+    case 3: S.n = 2; lam[0] = (float)la; lam[1] = (float)lb; break;
+    case 5: sx_copy(S, 1, 2); S.n = 2; lam[0] = (float)la; lam[1] = (float)lc; break;
+    case 6: sx_copy(S, 0, 1); sx_copy(S, 1, 2); S.n = 2; lam[0] = (float)lb; lam[1] = (float)lc; break;
+    default: S.n = 3; lam[0] = (float)la; lam[1] = (float)lb; lam[2] = (float)lc; break;
+    }
+}
+
+// the closest point of the simplex to the origin and its weights, computed in double and rounded
+// to float (the fp32 GJK's state; only the Voronoi tests and the barycentric solve need the
+// digits).  Wave-cooperative (every lane holds the same simplex): a tetrahedron's faces are tested
+// one per lane (lane f & 3: face f) and share one triangle solve with the 3-simplex case.
+AVR_DI int simplex_closest_d(Simplex &S, v3 &vout, float lam[4]) {
+    if (S.n == 1) { lam[0] = 1.f; vout = S.w[0]; return 0; }
+    if (S.n == 2) {
+        d3 A = D3(S.w[0]), B = D3(S.w[1]), ab = dsub(B, A);
+        double t = -ddot(A, ab), dd = ddot(ab, ab);
+        if (t <= 0.0 || dd <= 0.0) { S.n = 1; lam[0] = 1.f; vout = S.w[0]; return 0; }
+        if (t >= dd) { sx_copy(S, 0, 1); S.n = 1; lam[0] = 1.f; vout = S.w[0]; return 0; }
+        t /= dd;
+        lam[0] = (float)(1.0 - t); lam[1] = (float)t;
+        vout = dtof(dadd(A, dscl(ab, t)));
+        return 0;
+    }
+    const bool tet = S.n == 4;
+    // faces (0 1 2 | 3), (0 3 1 | 2), (0 2 3 | 1), (1 3 2 | 0); a triangle is face 0.  Vertices by
+    // selects between registers, not a lane-dependent index (that would put the simplex in scratch)
+    const int f = tet ? (lane_id() & 3) : 0;
+    const d3 W0 = D3(S.w[0]), W1 = D3(S.w[1]), W2 = D3(S.w[2]), W3 = D3(S.w[3]);
+    const bool f0 = f == 0, f1 = f == 1, f2 = f == 2;
+    const d3 A = f0 || f1 || f2 ? W0 : W1;
+    const d3 B = f0 ? W1 : f2 ? W2 : W3;
+    const d3 C = f0 ? W2 : f1 ? W1 : f2 ? W3 : W2;
+    bool outside = true;
+    if (tet) {
+        const d3 D = f0 ? W3 : f1 ? W2 : f2 ? W1 : W0;
+        const d3 n = dcrs(dsub(B, A), dsub(C, A));
+        const double sp = ddot(dscl(A, -1.0), n), sd = ddot(dsub(D, A), n);
+        outside = !(sd * sd < 1e-30) && sp * sd < 0.0;
+    }
+    int used;
+    double la, lb, lc;
+    const d3 cv = tri_cp_d(A, B, C, used, la, lb, lc);
+    if (!tet) {
+        vout = dtof(cv);
+        tri_compact_d(S, used, la, lb, lc, lam);
+        return 0;
+    }
+    if (!(__ballot(outside) & 0xfull)) { lam[0] = lam[1] = lam[2] = lam[3] = 0.f; vout = V(0, 0, 0); return 1; }
+    // the face with the smallest distance wins, the lowest index on ties (the serial loop's d2 <
+    // best over faces 0..3; a strict minimum in double that rounds to a float tie keeps the lower
+    // face, as a tie does)
+    const float d2 = outside ? (float)ddot(cv, cv) : BIGF;
+    float m = fminf(d2, __shfl_xor(d2, 1));
+    m = fminf(m, __shfl_xor(m, 2));
+    const int bf = __builtin_ctzll(__ballot(outside && d2 == m) & 0xfull);
+    const int bused = __shfl(used, bf);
+    const double bla = __shfl(la, bf), blb = __shfl(lb, bf), blc = __shfl(lc, bf);
+    vout = V(__shfl((float)cv.x, bf), __shfl((float)cv.y, bf), __shfl((float)cv.z, bf));
+    switch (bf) {
+    case 0: break;
+    case 1: sx_face1(S); break;
+    case 2: sx_copy(S, 1, 2); sx_copy(S, 2, 3); break;
+    default: sx_copy(S, 0, 1); sx_copy(S, 1, 3); break;
+    }
+    S.n = 3;
+    tri_compact_d(S, bused, bla, blb, blc, lam);
+    return 0;
+}
+
+#define GJK_NP_GAP 1e-4f     // lane GJK: largest duality gap (m) a no-progress stop may leave (gjk_lane)
 #define GJK_SEPARATED 0
 #define GJK_FAR 1
 #define GJK_PENETRATING 2
 #define GJK_UNFINISHED 3        // lane path only: iteration cap hit, finish on the cooperative path
+#define GJK_STALLED 4           // lane path only: no progress with an open duality gap, rerun in double (gjk_coop_d)
 // The lane-per-pair path runs at the pace of its slowest lane: pairs that have not converged
 // after GJK_LANE_IT iterations are handed to the wave-cooperative path, which reruns the same
 // GJK (same support tie-break, same arithmetic) to completion -- identical results.
@@ -828,23 +955,119 @@ AVR_DI int simplex_closest(SX &S, v3 &vout, float lam[4]) {
 #ifndef GJK_NB
 #define GJK_NB 4
 #endif
-template <bool COOP>
-AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
+AVR_DI int gjk_coop_d(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
     v3 v = sub(A.t.p, B.t.p);
     if (len2(v) < 1e-20f) v = V(1, 0, 0);
     S.n = 0;
     float lam[4] = {1, 0, 0, 0};
     float prev = BIGF;
     int status = GJK_SEPARATED;
-    const int max_it = COOP ? GJK_MAX_IT : GJK_LANE_IT;
-    bool converged = false;
-    for (int it = 0; it < max_it; it++) {
+    for (int it = 0; it < GJK_MAX_IT; it++) {
         nit = it + 1;
         v3 sa, sb;
-        if constexpr (COOP) support2<true>(m, A, scl(v, -1.f), B, v, sa, sb);
-        else { sa = support<COOP, GJK_NB>(m, A, scl(v, -1.f)); sb = support<COOP, GJK_NB>(m, B, v); }
+        support2<true>(m, A, scl(v, -1.f), B, v, sa, sb);
         v3 wv = sub(sa, sb);
         float vv = len2(v), vw = dot(v, wv);
+        if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
+        bool dup = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < S.n && S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
+        if (dup && S.n > 0) break;
+        if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) break;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k == S.n) { S.w[k] = wv; S.a[k] = sa; S.b[k] = sb; }
+        S.n++;
+        v3 nv;
+        if (simplex_closest_d(S, nv, lam)) { status = GJK_PENETRATING; break; }
+        float nvv = len2(nv);
+        if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; break; }
+        if (nvv >= prev) { v = nv; break; }
+        prev = nvv;
+        v = nv;
+    }
+    if (status == GJK_PENETRATING) return GJK_PENETRATING;
+    v3 a = V(0, 0, 0), b = V(0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < S.n) { a = add(a, scl(S.a[k], lam[k])); b = add(b, scl(S.b[k], lam[k])); }
+    pa = a; pb = b;
+    dist = len(sub(a, b));
+    return GJK_SEPARATED;
+}
+
+// the cooperative GJK in fp32 (pairs the lane path hands over for EPA or a big hull): the lane
+// path's arithmetic with both supports of an iteration issued together
+AVR_DI int gjk_coop_f(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
+    v3 v = sub(A.t.p, B.t.p);
+    if (len2(v) < 1e-20f) v = V(1, 0, 0);
+    S.n = 0;
+    float lam[4] = {1, 0, 0, 0};
+    float prev = BIGF;
+    int status = GJK_SEPARATED;
+    for (int it = 0; it < GJK_MAX_IT; it++) {
+        nit = it + 1;
+        v3 sa, sb;
+        support2<true>(m, A, scl(v, -1.f), B, v, sa, sb);
+        v3 wv = sub(sa, sb);
+        float vv = len2(v), vw = dot(v, wv);
+        if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
+        bool dup = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < S.n && S.w[k].x == wv.x && S.w[k].y == wv.y && S.w[k].z == wv.z) dup = true;
+        if (dup && S.n > 0) break;
+        if (S.n > 0 && vv - vw <= GJK_REL_EPS * vv) break;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k == S.n) { S.w[k] = wv; S.a[k] = sa; S.b[k] = sb; }
+        S.n++;
+        v3 nv;
+        if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; break; }
+        float nvv = len2(nv);
+        if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; break; }
+        if (nvv >= prev) { v = nv; break; }
+        prev = nvv;
+        v = nv;
+    }
+    if (status == GJK_PENETRATING) return GJK_PENETRATING;
+    v3 a = V(0, 0, 0), b = V(0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < S.n) { a = add(a, scl(S.a[k], lam[k])); b = add(b, scl(S.b[k], lam[k])); }
+    pa = a; pb = b;
+    dist = len(sub(a, b));
+    return GJK_SEPARATED;
+}
+
+// Lane path (one pair per lane, fp32).  A step that makes no progress ends it as in the oracle
+// only when the duality gap at the final direction is closed: the distance's upper and lower
+// bounds (|v| and v.w / |v|, one more support query) within GJK_NP_GAP.  Otherwise -- the fp32
+// symptom of a thin simplex whose closest point has lost its digits, see gjk_coop_d -- the pair is
+// handed to the cooperative GJK in double (rc 4).  Measured with the fp32 oracle: on the ScratchItch
+// state-27 neighbourhood (4000 jittered poses, tools/dbg_np_state.py) the 132 wrong answers all
+// stop on no progress with gaps of 1.3 - 37 mm, 90 % of the correct no-progress stops below 0.6 um;
+// in FeedingJaco runs 4.5 % of the no-progress stops (~0.1 % of GJK calls) exceed 0.1 mm.
+AVR_DI int gjk_lane(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit) {
+    v3 v = sub(A.t.p, B.t.p);
+    if (len2(v) < 1e-20f) v = V(1, 0, 0);
+    S.n = 0;
+    float lam[4] = {1, 0, 0, 0};
+    float prev = BIGF;
+    int status = GJK_SEPARATED;
+    bool converged = false, npc = false;
+    for (int it = 0; it < GJK_LANE_IT; it++) {
+        nit = it + 1;
+        v3 sa = support<false, GJK_NB>(m, A, scl(v, -1.f)), sb = support<false, GJK_NB>(m, B, v);
+        v3 wv = sub(sa, sb);
+        float vv = len2(v), vw = dot(v, wv);
+        if (npc) {      // the step before made no progress: keep its simplex if the gap is closed
+            const float gap = vv - vw;     // (|v| times the gap between the distance's bounds)
+            if (gap > 0.f && gap * gap > (GJK_NP_GAP * GJK_NP_GAP) * vv) return GJK_STALLED;
+            converged = true;
+            break;
+        }
         if (vw > 0.f && vw * vw > vv * maxdist2) return GJK_FAR;
         bool dup = false;
 #pragma unroll
@@ -860,11 +1083,11 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
         if (simplex_closest(S, nv, lam)) { status = GJK_PENETRATING; converged = true; break; }
         float nvv = len2(nv);
         if (nvv < 1e-14f * (1.f + len2(wv))) { status = GJK_PENETRATING; converged = true; break; }
-        if (nvv >= prev) { v = nv; converged = true; break; }
+        if (nvv >= prev) { v = nv; npc = true; continue; }     // (the gap check takes the next support)
         prev = nvv;
         v = nv;
     }
-    if (!COOP && !converged) return GJK_UNFINISHED;
+    if (!converged) return GJK_UNFINISHED;
     if (status == GJK_PENETRATING) return GJK_PENETRATING;
     v3 a = V(0, 0, 0), b = V(0, 0, 0);
 #pragma unroll
@@ -873,6 +1096,12 @@ AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2
     pa = a; pb = b;
     dist = len(sub(a, b));
     return GJK_SEPARATED;
+}
+
+template <bool COOP>
+AVR_DI int gjk(const KModel &m, const WShape &A, const WShape &B, float maxdist2, v3 &pa, v3 &pb, float &dist, Simplex &S, int &nit, bool dbl) {
+    if constexpr (COOP) return dbl ? gjk_coop_d(m, A, B, maxdist2, pa, pb, dist, S, nit) : gjk_coop_f(m, A, B, maxdist2, pa, pb, dist, S, nit);
+    else return gjk_lane(m, A, B, maxdist2, pa, pb, dist, S, nit);
 }
 
 // --------------------------------------------------------------------------- EPA (wave-cooperative)
@@ -1080,7 +1309,7 @@ AVR_DI int epa(const KModel &m, EpaBuf &L, const WShape &A, const WShape &B, con
 // 2 sphere-capsule, 3 GJK; unused outside the AVR_PROF build)
 template <bool COOP>
 AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape &B, float thr, v3 &nB, v3 &pB, float &dist, int &nit, int &kind,
-                       int *epa_budget = nullptr) {
+                       int *epa_budget = nullptr, bool dbl = false) {
     int ka = A.kind, kb = B.kind;
     nit = 0;
     kind = 3;
@@ -1153,9 +1382,10 @@ AVR_DI int narrowphase(const KModel &m, EpaBuf &E, const WShape &A, const WShape
     v3 pa, pb;
     float cd;
     Simplex S;
-    int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S, nit);
+    int st = gjk<COOP>(m, A, B, maxd * maxd, pa, pb, cd, S, nit, dbl);
     if (st == GJK_FAR) return 0;
     if (st == GJK_UNFINISHED) return 2;
+    if (st == GJK_STALLED) return 4;
     v3 n;
     float d;
     if (st == GJK_SEPARATED && cd > 1e-9f) {
@@ -2698,12 +2928,13 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
     float4 *o = (float4 *)(cs + CS_RES) + 2 * k;
     o[0] = make_float4(__int_as_float(rc), nB.x, nB.y, nB.z);
     o[1] = make_float4(pB.x, pB.y, pB.z, d);
-    if (rc == 2) cs[CS_COOP] = 1.f;      // (every writer stores the same value)
+    if (rc == 2 || rc == 4) cs[CS_COOP] = 1.f;      // (every writer stores the same value)
 }
 
 // the listed pairs (n of them) that the lane path left to the wave-cooperative narrowphase (rc 2:
-// a big hull without a support table, penetrating cores that need EPA, the lane iteration cap):
-// the whole wave runs narrowphase<true> on each, E = the env's EPA buffer
+// a big hull without a support table, penetrating cores that need EPA, the lane iteration cap;
+// rc 4: a lane GJK that stalled with an open duality gap, rerun in double -- gjk_coop_d): the
+// whole wave runs narrowphase<true> on each, E = the env's EPA buffer
 //
 // EPA budget (cap): an env whose penetrating hull pairs needed more than AVR_COOP_CAP EPAs in
 // each of its last AVR_COOP_PERSIST sub-steps (T_COOPN counts them) gets at most AVR_COOP_CAP per
@@ -2724,12 +2955,14 @@ AVR_DI void np_store(float *cs, int k, int rc, v3 nB, v3 pB, float d) {
 AVR_DI int np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot, int budget) {
     const int lane = lane_id();
     // the cooperative pairs of each 64-pair chunk, read once (the stores below rewrite CS_RES)
-    unsigned long long bm[MAXSP / 64];
+    unsigned long long bm[MAXSP / 64], bd[MAXSP / 64];
     int nco = 0;
 #pragma unroll
     for (int q = 0; q < MAXSP / 64; q++) {
         const int k = 64 * q + lane;
-        bm[q] = __ballot(k < n && __float_as_int(gld(cs + CS_RES + 8 * (k < n ? k : 0))) == 2);
+        const int rc = __float_as_int(gld(cs + CS_RES + 8 * (k < n ? k : 0)));
+        bm[q] = __ballot(k < n && (rc == 2 || rc == 4));
+        bd[q] = __ballot(k < n && rc == 4);
         nco += __popcll(bm[q]);
     }
     const int r0 = nco > 0 ? rot % nco : 0;
@@ -2758,7 +2991,7 @@ AVR_DI int np_coop(const KModel &m, float *cs, int n, EpaBuf &E, int rot, int bu
 #ifdef AVR_PROF
                 const unsigned long long c0t = __builtin_readcyclecounter();
 #endif
-                int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk, &budget);
+                int r2 = narrowphase<true>(m, E, A, B, thr, n2, p2, d2, nit, nk, &budget, (bd[q] >> j) & 1ull);
                 if (r2 == 3) { r2 = 0; skipped++; }
 #ifdef AVR_PROF
                 if (m.prof && lane == 0) {     // cooperative pairs, their GJK iterations, the time they took

@@ -20,15 +20,27 @@
 // tool frame, world_creation.py:330-343, and the food spheres above it, feeding.py:291-308).
 
 // Robot self-contact at the pose in L (robot FK done): what p.getContactPoints(robot, robot)
-// reports after a restart's frames (util.py:41-46; the Jaco is loaded with URDF_USE_SELF_COLLISION,
-// world_creation.py:282) -- the step's collision pipeline on the compiled robot-robot candidate
-// pairs (parent-child pairs are not candidates): fattened body AABBs, child AABB culling (bare
-// pairs unculled), the lane narrowphase within the pair's contact threshold.  One lane per
-// candidate pair; returns the number of touching shape pairs in every lane.
+// reports (the Jaco is loaded with URDF_USE_SELF_COLLISION, world_creation.py:282), at the IK
+// solution itself -- the reference asks after a restart's 5 simulated frames (util.py:41-46);
+// these are not simulated here, a known difference (host and device alike).  The step's
+// collision pipeline on the compiled robot-robot candidate pairs (parent-child pairs are not
+// candidates): fattened body AABBs, child AABB culling (bare pairs unculled), the lane
+// narrowphase within the pair's contact threshold, one lane per candidate pair; the pairs the
+// lane path hands on (rc 2: penetrating cores or a hull without a support table, rc 4: a stalled
+// GJK) are appended to Q and resolved by the wave-cooperative narrowphase (EPA, double GJK), as
+// the step resolves them.  A pair beyond Q's capacity counts as touching.  Returns the number of
+// touching shape pairs in every lane.
+struct SelfQ {
+    static constexpr int CAP = 64;
+    int n;
+    int2 e[CAP];       // (sa | sb << 16, ba | bb << 16 | rc 4 << 31)
+};
 template <class LT>
-AVR_DI int robot_self_contacts(const KModel &m, const LT &L) {
+AVR_DI int robot_self_contacts(const KModel &m, const LT &L, EpaBuf &E, SelfQ &Q) {
     const int lane = lane_id();
     int cnt = 0;
+    if (lane == 0) Q.n = 0;
+    SYNC();
     for (int p0 = 0; p0 < m.np; p0 += 64) {
         const int p = p0 + lane;
         if (p >= m.np) continue;
@@ -52,18 +64,36 @@ AVR_DI int robot_self_contacts(const KModel &m, const LT &L) {
                 shape_aabb(m, sb0 + j, tb, b0, b1);
                 if (!bare && !overlap(a0, a1, b0, b1)) continue;
                 const WShape A = make_wshape(m, sa0 + i, ta), B = make_wshape(m, sb0 + j, tb);
-                int rc = 2;     // (a hull the lane GJK cannot take, penetrating cores: touching)
+                int rc = 2;     // (a hull the lane GJK cannot take)
                 if (!((A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0))) {
                     v3 nB, pB;
                     float d;
                     int nit, nk;
-                    rc = narrowphase<false>(m, *(EpaBuf *)&L, A, B, thr, nB, pB, d, nit, nk);   // (the lane path never touches the EPA buffer)
+                    rc = narrowphase<false>(m, E, A, B, thr, nB, pB, d, nit, nk);   // (the lane path never touches the EPA buffer)
                 }
-                cnt += rc != 0;
+                if (rc == 2 || rc == 4) {
+                    const int k = atomicAdd(&Q.n, 1);
+                    if (k < SelfQ::CAP) Q.e[k] = make_int2((sa0 + i) | (sb0 + j) << 16, ba | bb << 16 | (rc == 4 ? (int)0x80000000u : 0));
+                    else cnt++;
+                } else cnt += rc != 0;
             }
         }
     }
     for (int o = 32; o; o >>= 1) cnt += __shfl_xor(cnt, o);
+    SYNC();
+    const int nq = min(Q.n, SelfQ::CAP);
+    for (int k = 0; k < nq; k++) {
+        const int2 q = Q.e[k];
+        const int ba = q.y & 0x7fff, bb = (q.y >> 16) & 0x7fff;
+        const float thr = fminf(gld(m.body_threshold + ba), gld(m.body_threshold + bb));
+        const WShape A = make_wshape(m, q.x & 0xffff, body_tf(m, L, ba)), B = make_wshape(m, q.x >> 16, body_tf(m, L, bb));
+        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+        float d = 0.f;
+        int nit, nk;
+        const int rc = narrowphase<true>(m, E, A, B, thr, nB, pB, d, nit, nk, nullptr, q.y < 0);
+        SYNC();
+        cnt += rc == 1;
+    }
     return cnt;
 }
 
@@ -114,6 +144,8 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
                                                           int n_envs) {
     __shared__ PairsLDS L;
     __shared__ IkLDS K;
+    __shared__ EpaBuf E;
+    __shared__ SelfQ SQ;
     const int env = blockIdx.x;
     if (env >= n_envs || !mask[env]) return;     // uniform over the block
     const KModel &m = *mp;
@@ -178,7 +210,7 @@ __global__ __launch_bounds__(64) void avr_reset_ik_kernel(const KModel *__restri
         }
         robot_fk(m, L);
         // step_sim's self-contact screening: a touching solution re-orients the target
-        if (alt && robot_self_contacts(m, L) > 0) {
+        if (alt && robot_self_contacts(m, L, E, SQ) > 0) {
             const float *a = alt + ((size_t)env * R + r) * 4;
             tq = Q(a[0], a[1], a[2], a[3]);
         }
@@ -260,6 +292,8 @@ hipError_t avr_launch_reset_ik(const KModel *d_m, float *state, const unsigned c
 __global__ __launch_bounds__(64) void avr_self_contact_kernel(const KModel *__restrict__ mp, const float *__restrict__ state, const float *__restrict__ q,
                                                               int *__restrict__ out, int n) {
     __shared__ PairsLDS L;
+    __shared__ EpaBuf E;
+    __shared__ SelfQ SQ;
     const int i = blockIdx.x;
     if (i >= n) return;
     const KModel &m = *mp;
@@ -269,7 +303,7 @@ __global__ __launch_bounds__(64) void avr_self_contact_kernel(const KModel *__re
     for (int d = lane_id(); d < nq; d += 64) L.st[S_Q + d] = q[(size_t)i * nq + d];
     SYNC();
     robot_fk(m, L);
-    const int c = robot_self_contacts(m, L);
+    const int c = robot_self_contacts(m, L, E, SQ);
     if (lane_id() == 0) out[i] = c;
 }
 
@@ -296,7 +330,14 @@ __global__ __launch_bounds__(64) void avr_np_query_kernel(const KModel *__restri
     v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
     float d = 0.f;
     int nit, nk;
-    const int rc = narrowphase<true>(m, E, A, B, thr, nB, pB, d, nit, nk);
+    // as the step runs it: a lane GJK that stalls with an open duality gap (rc 4) hands the pair
+    // to the cooperative GJK in double (np_coop); every other pair gets the cooperative fp32 path
+    // (sphere-hull pairs take the point-core lane GJK, ph_step, which hands nothing over this way)
+    const bool big = (A.nv > SMALL_NV && A.tab < 0) || (B.nv > SMALL_NV && B.tab < 0);
+    const bool sph = (A.kind == AVR_SPHERE && B.kind == AVR_HULL) || (A.kind == AVR_HULL && B.kind == AVR_SPHERE);
+    const bool dbl = !big && !sph && narrowphase<false>(m, E, A, B, thr, nB, pB, d, nit, nk) == 4;
+    nB = V(0, 0, 0); pB = V(0, 0, 0); d = 0.f;
+    const int rc = narrowphase<true>(m, E, A, B, thr, nB, pB, d, nit, nk, nullptr, dbl);
     if (lane_id() == 0) {
         float *o = out + 8 * (size_t)q;
         o[0] = (float)rc; o[1] = nB.x; o[2] = nB.y; o[3] = nB.z; o[4] = pB.x; o[5] = pB.y; o[6] = pB.z; o[7] = d;

@@ -177,8 +177,10 @@ const char *avr_last_error(avr_sim *sim);
 int avr_reset_ik(avr_sim *sim, const uint8_t *env_mask, const float *host_state, const float *target7, const float *init, const float *alt4,
                  int32_t restarts, int32_t iters, float tol, const float *keepout8, int32_t n_frames, float *host_obs, uint8_t *host_ok);
 
-/* avr_robot_self_contact: len(p.getContactPoints(bodyA=robot, bodyB=robot)) > 0 after a restart's
- *   frames (util.py:41-46, 63-67) at n joint vectors q[n*avr_n_dof] (avr_get_q's layout; everything
+/* avr_robot_self_contact: len(p.getContactPoints(bodyA=robot, bodyB=robot)) > 0 (util.py:41-46,
+ *   63-67) at n joint vectors q[n*avr_n_dof], evaluated at the joint vector itself: the reference
+ *   asks after a restart's 5 simulated frames, which are not simulated here -- a known difference,
+ *   the same on the host and device IK paths (avr_get_q's layout; everything
  *   else from env 0's state block): out[n] = the robot shape pairs the step's collision pipeline finds
  *   within their contact threshold (compiled robot-robot candidate pairs: the URDF's
  *   URDF_USE_SELF_COLLISION robots, parent-child pairs excluded).  Host screening of the host IK

@@ -184,10 +184,11 @@ def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
     and on the fp32 and fp64 oracles.  Contact trajectories part at the rounding level (chaos), so
     episode outcomes are compared as paired statistics: the mean episode reward, the scratch / wipe
     counter (task_success before the threshold, scratch_itch.py:66-70, bed_bathing.py:97-125) and
-    the contact-step count.  Against the fp32 oracle (the same precision) each within three standard
-    errors of the paired differences; against the fp64 oracle within three standard errors plus the
-    fp32 oracle's own mean difference from fp64 (precision is not neutral here: BedBathing's fp32
-    oracle wipes ~1 % more targets than its fp64 build)."""
+    the contact-step count, each within three standard errors of the paired differences plus the
+    fp32 oracle's own mean difference from fp64, against both oracles.  Precision is not neutral
+    here: BedBathing's fp32 oracle wipes ~2 % more targets than its fp64 build, mostly through fp32
+    GJK stops on thin hull-capsule simplices that the kernel hands to its double GJK (gjk_lane), so
+    the GPU may sit anywhere between the two oracles (measured: at the fp64 oracle)."""
     from avr import _lib
     A, md, L, P, is_c = _pool(task, 16)
     C = P[is_c]
@@ -219,5 +220,5 @@ def test_contact_regime_episode_statistics_vs_fp64_oracle(task):
         d64, se64 = paired(g, c64)
         p, _ = paired(c32, c64)
         print('  %s: gpu - fp32 %.4f (se %.4f), gpu - fp64 %.4f (se %.4f), fp32 - fp64 %.4f' % (name, d32, se32, d64, se64, p))
-        assert abs(d32) <= 3 * se32 + 1e-9, (name, d32, se32)
+        assert abs(d32) <= 3 * se32 + abs(p) + 1e-9, (name, d32, se32, p)
         assert abs(d64) <= 3 * se64 + abs(p) + 1e-9, (name, d64, se64, p)

@@ -19,7 +19,8 @@ __device__ __forceinline__ float row16(float x) { x += dpp(x, 8); x += dpp(x, 4)
 // 0: dependent fma chain; 1: dependent pk_fma chain; 2: dependent add_dpp chain; 3: row16 + fma;
 // 4: the go4 arithmetic chain (packed, as avr_kernel.hip B4_PK); 5: the same unpacked;
 // 6: 4 independent fma chains; 7: 4 independent pk chains; 8: dependent ds_read chain
-__global__ __launch_bounds__(64) void k(int mode, float *out, long long *cyc, float b, float c) {
+template <int mode>
+__global__ __launch_bounds__(64) void k(float *out, long long *cyc, float b, float c) {
 #pragma clang fp contract(off)
     __shared__ int lds[1024];
     const int l = threadIdx.x;
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(64) void k(int mode, float *out, long long *cyc, fl
     int ix = l;
     long long t0 = clock64();
     for (int it = 0; it < N; it++) {
-        switch (mode) {
+        switch (mode) {   // (compile-time: no branch in the timed loop)
         case 0:
 #pragma unroll
             for (int u = 0; u < 16; u++) x = __builtin_fmaf(x, b, c);
@@ -122,12 +123,13 @@ int main() {
     (void)hipMalloc(&out, nb * 64 * 4); (void)hipMalloc(&cyc, nb * 8);
     const char *nm[] = {"fma dep", "pk_fma dep", "add_dpp dep", "row16+fma", "go4 packed", "go4 unpacked", "4x fma indep", "4x pk_fma indep", "ds_read dep", "go4 quad_perm sum"};
     const int per[] = {16, 16, 16, 4, 4, 4, 16, 16, 16, 4};
+    void (*ks[])(float *, long long *, float, float) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>, k<9>};
     for (int mode = 0; mode < 10; mode++) {
         for (int blocks : {1, 1024}) {
             long long h[1024];
             double best = 1e30;
             for (int rep = 0; rep < 3; rep++) {
-                hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, mode, out, cyc, 0.999f, 1e-4f);
+                hipLaunchKernelGGL(ks[mode], dim3(blocks), dim3(64), 0, 0, out, cyc, 0.999f, 1e-4f);
                 (void)hipDeviceSynchronize();
                 (void)hipMemcpy(h, cyc, blocks * 8, hipMemcpyDeviceToHost);
                 double m = 0; for (int i = 0; i < blocks; i++) m += h[i]; m /= blocks;
