@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('AVR_LIB') or os.path.join(HERE, 'libavr.so')   # AVR_
 
 EXPORTS = [
     'avr_create', 'avr_destroy', 'avr_set_state', 'avr_get_state', 'avr_set_state_masked', 'avr_settle',
-    'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_random_actions_device', 'avr_sync',
+    'avr_step', 'avr_step_device', 'avr_step_random_device', 'avr_rollout_random_device', 'avr_random_actions_device', 'avr_sync',
     'avr_stream', 'avr_state_device_ptr', 'avr_n_envs', 'avr_env_groups', 'avr_state_words', 'avr_abi_version',
     'avr_kernel_info', 'avr_last_error', 'avr_substep', 'avr_reset', 'avr_profile_kernels', 'avr_kernel_times',
     'avr_hull_support_table', 'avr_task', 'avr_task_state_words', 'avr_task_obs_dim', 'avr_task_act_dim', 'avr_n_dof',
@@ -62,6 +62,7 @@ def load(path=LIB_PATH):
     lib.avr_step.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.avr_step_device.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.avr_step_random_device.argtypes = [vp, C.c_int64, vp, vp, vp, vp]
+    lib.avr_rollout_random_device.argtypes = [vp, C.c_int64, C.c_int32, vp, vp, vp, vp, C.c_int32]
     lib.avr_random_actions_device.argtypes = [vp, C.c_int64, vp]
     lib.avr_sync.argtypes = [vp]
     lib.avr_stream.argtypes = [vp]
@@ -258,6 +259,12 @@ class Sim:
 
     def step_random_device(self, t, d_obs=None, d_rew=None, d_done=None, d_info=None):
         self._chk(self.lib.avr_step_random_device(self.h, int(t), d_obs, d_rew, d_done, d_info))
+
+    def rollout_random_device(self, t0, n, d_obs=None, d_rew=None, d_done=None, d_info=None, stacked=False):
+        """n device-random steps from step index t0 (= n step_random_device calls, bit for bit); the
+        env groups are joined at the end only.  stacked: step k's outputs to slot k of [n, E, ...]
+        device arrays (all four required)."""
+        self._chk(self.lib.avr_rollout_random_device(self.h, int(t0), int(n), d_obs, d_rew, d_done, d_info, int(bool(stacked))))
 
     def random_actions_device(self, t, d_act):
         self._chk(self.lib.avr_random_actions_device(self.h, int(t), d_act))

@@ -33,6 +33,16 @@ def pack_rollout(roll, j, obs, rew, info, done):
     roll[j, :, -1] = done.to(roll.dtype)
 
 
+def pack_rollout_stacked(roll, obs, rew, info, done, m):
+    """roll[:m] (m, E, W) <- m steps of stacked outputs ([G, E, ...] device tensors); the rows past m
+    keep their previous contents (a short last chunk)."""
+    od = obs.shape[2]
+    roll[:m, :, :od] = obs[:m]
+    roll[:m, :, od] = rew[:m]
+    roll[:m, :, od + 1:od + 1 + ABI.INFO_DIM] = info[:m]
+    roll[:m, :, -1] = done[:m].to(roll.dtype)
+
+
 def gather_rollouts(roll, out=None, group=None):
     """All-gather every rank's roll (G, E, W) -> (G, world*E, W) in global env order."""
     import torch.distributed as dist

@@ -30,6 +30,8 @@
     int avr_substep(avr_sim *s, float dt);                                                                         \
     int avr_step_device(avr_sim *s, const float *d_act, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info); \
     int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);  \
+    int avr_rollout_random_device(avr_sim *s, int64_t t0, int32_t n, float *d_obs, float *d_rew, uint8_t *d_done,   \
+                                  float *d_info, int32_t stacked);                                                 \
     int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act);                                            \
     int avr_step(avr_sim *s, const float *act, float *obs, float *rew, uint8_t *done, float *info);                \
     int avr_sync(avr_sim *s);                                                                                      \
@@ -176,6 +178,9 @@ int avr_reset(avr_sim *s, const uint8_t *m, const float *p, int32_t n, float *o)
 int avr_step(avr_sim *s, const float *a, float *o, float *r, uint8_t *d, float *i) { DISPATCH(s, avr_step(h, a, o, r, d, i)); }
 int avr_step_device(avr_sim *s, const float *a, float *o, float *r, uint8_t *d, float *i) { DISPATCH(s, avr_step_device(h, a, o, r, d, i)); }
 int avr_step_random_device(avr_sim *s, int64_t t, float *o, float *r, uint8_t *d, float *i) { DISPATCH(s, avr_step_random_device(h, t, o, r, d, i)); }
+int avr_rollout_random_device(avr_sim *s, int64_t t0, int32_t n, float *o, float *r, uint8_t *d, float *i, int32_t stacked) {
+    DISPATCH(s, avr_rollout_random_device(h, t0, n, o, r, d, i, stacked));
+}
 int avr_random_actions_device(avr_sim *s, int64_t t, float *a) { DISPATCH(s, avr_random_actions_device(h, t, a)); }
 int avr_substep(avr_sim *s, float dt) { DISPATCH(s, avr_substep(h, dt)); }
 int avr_sync(avr_sim *s) { DISPATCH(s, avr_sync(h)); }

@@ -16,6 +16,7 @@
 
 #define AVR_MAX_GROUPS 8
 #define AVR_GRAPH_SLOTS 4
+#define AVR_ROLL_CHUNK 16      // steps per rollout graph replay (avr_rollout_random_device)
 
 struct avr_sim {
     avr_config cfg;
@@ -56,6 +57,17 @@ struct avr_sim {
     int use_graph;
     struct GraphSlot { hipGraph_t graph; hipGraphExec_t gexec; const void *key[5]; unsigned long long used; };
     GraphSlot gslot[AVR_GRAPH_SLOTS];
+    // rollouts (avr_rollout_random_device): graphs of AVR_ROLL_CHUNK steps (and of one step, for
+    // the remainder) in which every env group runs all its steps back to back on its own branch,
+    // with its own step counter advanced on the device before each step; the branches are
+    // forked and joined once per replay, not after every step
+    struct RollSlot {
+        hipGraph_t graph[2]; hipGraphExec_t gexec[2];                                       // branches: [chunk, 1 step]
+        hipGraph_t pgraph[2][2][AVR_MAX_GROUPS]; hipGraphExec_t pgexec[2][2][AVR_MAX_GROUPS];  // per group: [chunk, 1 step][copy][group]
+        const void *key[8];
+        unsigned long long used;
+    };
+    RollSlot rslot[AVR_GRAPH_SLOTS];
     unsigned long long gclock;
     long long n_captures;                  // diagnostics (avr_graph_captures)
 };
@@ -216,6 +228,7 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         s->ngroups = ng;
         const char *gr = getenv("AVR_GRAPH");
         s->use_graph = gr ? atoi(gr) : 1;
+
         HIPCHK(s, hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         for (int i = 1; i < ng; i++) {      // (group 0 runs on the handle's stream)
             HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));
@@ -489,9 +502,9 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         k.cscr = cscr;
     }
     {
-        long long *st = nullptr;
-        HIPCHK(s, hipMalloc(&st, sizeof(long long)));
-        HIPCHK(s, hipMemset(st, 0, sizeof(long long)));
+        long long *st = nullptr;      // per env group: the step index (take_step) and, in a rollout, the step's slot
+        HIPCHK(s, hipMalloc(&st, 2 * AVR_MAX_GROUPS * sizeof(long long)));
+        HIPCHK(s, hipMemset(st, 0, 2 * AVR_MAX_GROUPS * sizeof(long long)));
         s->allocs.push_back(st);
         k.step_t = st;
     }
@@ -510,6 +523,12 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
 }
 
 
+// env group g's first env (boundaries on multiples of 32 envs, one part-B block's share)
+static int group_bound(const avr_sim *s, int g) {
+    const int E = s->cfg.n_envs;
+    return g >= s->ngroups ? E : std::min(E, (int)(((long long)E * g / s->ngroups + 16) / 32 * 32));
+}
+
 // one launch sequence over all envs: on the handle's stream (1 group, or while per-kernel
 // timing is on), else split into env groups (boundaries on multiples of 32 envs, one part-B
 // block's share) whose sequences run concurrently: group 0 on the handle's stream itself, the
@@ -521,7 +540,7 @@ static hipError_t run_step_direct(avr_sim *s, float *state, const float *act, fl
     if (s->ngroups <= 1 || s->evlog.cap)
         return avr_launch_step(&s->km, s->d_km, state, act, obs, rew, done, info, mask, mode, t, 0, E, s->stream,
                                s->evlog.cap ? &s->evlog : nullptr);
-    auto bound = [&](int g) { return g >= s->ngroups ? E : std::min(E, (int)(((long long)E * g / s->ngroups + 16) / 32 * 32)); };
+    auto bound = [&](int g) { return group_bound(s, g); };
     hipError_t e = hipEventRecord(s->fork_ev, s->stream);
     if (e != hipSuccess) return e;
     for (int g = 1; g < s->ngroups; g++) {
@@ -535,6 +554,22 @@ static hipError_t run_step_direct(avr_sim *s, float *state, const float *act, fl
     for (int g = 1; g < s->ngroups; g++)
         if ((e = hipStreamWaitEvent(s->stream, s->join_ev[g], 0)) != hipSuccess) return e;
     return hipSuccess;
+}
+
+static void drop_roll(avr_sim::RollSlot &r) {
+    for (int c = 0; c < 2; c++) {
+        if (r.gexec[c]) (void)hipGraphExecDestroy(r.gexec[c]);
+        if (r.graph[c]) (void)hipGraphDestroy(r.graph[c]);
+        r.gexec[c] = nullptr; r.graph[c] = nullptr;
+        for (int p = 0; p < 2; p++)
+            for (int g = 0; g < AVR_MAX_GROUPS; g++) {
+                if (r.pgexec[c][p][g]) (void)hipGraphExecDestroy(r.pgexec[c][p][g]);
+                if (r.pgraph[c][p][g]) (void)hipGraphDestroy(r.pgraph[c][p][g]);
+                r.pgexec[c][p][g] = nullptr; r.pgraph[c][p][g] = nullptr;
+            }
+    }
+    memset(r.key, 0, sizeof(r.key));
+    r.used = 0;
 }
 
 static void drop_graph(avr_sim::GraphSlot &g) {
@@ -595,6 +630,7 @@ int avr_destroy(avr_sim *s) {
     DevGuard dg(s->cfg.device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (auto &x : s->gslot) drop_graph(x);
+    for (auto &x : s->rslot) drop_roll(x);
     for (void *p : s->allocs) (void)hipFree(p);
     if (s->d_state) (void)hipFree(s->d_state);
     if (s->d_km) (void)hipFree(s->d_km);
@@ -714,6 +750,167 @@ int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, ui
     HIPCHK(s, run_step(s, s->d_state, nullptr, d_obs ? d_obs : s->d_obs, d_rew ? d_rew : s->d_rew, d_done ? d_done : s->d_done,
                               d_info ? d_info : s->d_info, nullptr, 1, t));
     return 0;
+}
+
+// n device-random steps t0 .. t0 + n - 1 (avr_step_random_device's actions and results).  With
+// stacked = 0 every step writes the given buffers (the last step's outputs remain); with stacked = 1
+// step k writes slot k of [n][n_envs][...] arrays.  The steps run as graph replays in which each
+// env group runs AVR_ROLL_CHUNK steps (one step for the remainder) back to back, each step first
+// advancing the group's own step counter and slot on the device, so the groups are not joined
+// after every step: a group that finishes a step early starts the next while the others finish
+// theirs (envs are independent; every step of every env is computed as by n
+// avr_step_random_device calls, bit for bit).  Asynchronous; the handle's stream holds the rollout.
+// rollout replays, two ways (avr_rollout_random_device):
+//  - branches: a graph of AVR_ROLL_CHUNK steps per group branch, forked and joined once per replay;
+//  - per group: each group's own graph of AVR_ROLL_CHUNK steps replayed on its own stream (two
+//    alternating copies), joined once per rollout.
+// Measured (tools/gpu_r5_t18.sh, gpu_r5_t19_exp.sh): FeedingJaco 840k (branches) vs 884k (per group)
+// env-steps/s; ScratchItch 1.36M vs 0.74M and BedBathing 1.77M vs 1.09M -- separately launched graphs
+// dispatch at the direct-launch rate, which the PR2 tasks' short steps (22 launches per group) cannot
+// hide.  Per group for FeedingJaco, branches otherwise; AVR_ROLLOUT=branches|groups overrides.
+static bool per_group_rollout(const avr_sim *s) {
+    const char *e = getenv("AVR_ROLLOUT");
+    if (e && !strcmp(e, "branches")) return false;
+    if (e && !strcmp(e, "groups")) return true;
+    (void)s;
+    return AVR_TASK == AVR_TASK_FEEDING;
+}
+
+static int rollout_branches(avr_sim *s, int64_t t0, int32_t n, float *o, float *r, uint8_t *dn, float *in, int32_t stacked, const void *const *key) {
+    const size_t E = (size_t)s->cfg.n_envs;
+    avr_sim::RollSlot *rs = nullptr;
+    for (auto &x : s->rslot)
+        if (x.gexec[0] && memcmp(key, x.key, sizeof(x.key)) == 0) rs = &x;
+    if (!rs) {
+        for (auto &x : s->rslot)
+            if (!x.gexec[0] && !x.pgexec[0][0][0] && !rs) rs = &x;
+        if (!rs) {
+            rs = &s->rslot[0];
+            for (auto &x : s->rslot)
+                if (x.used < rs->used) rs = &x;
+            HIPCHK(s, hipStreamSynchronize(s->stream));     // (no replay of the graphs being dropped may still run)
+            drop_roll(*rs);
+        }
+        for (int c = 0; c < 2; c++) {
+            const int steps = c == 0 ? AVR_ROLL_CHUNK : 1;
+            HIPCHK(s, hipStreamBeginCapture(s->stream, hipStreamCaptureModeRelaxed));
+            hipError_t el = hipEventRecord(s->fork_ev, s->stream);
+            for (int g = 0; g < s->ngroups && el == hipSuccess; g++) {
+                hipStream_t st = g == 0 ? s->stream : s->gstream[g];
+                const int e0 = group_bound(s, g), e1 = group_bound(s, g + 1);
+                long long *ct = s->km.step_t + g, *ck = s->km.step_t + AVR_MAX_GROUPS + g;
+                if (g > 0) el = hipStreamWaitEvent(st, s->fork_ev, 0);
+                for (int q = 0; q < steps && el == hipSuccess; q++) {
+                    el = avr_launch_step_advance(ct, ck, st);
+                    if (el == hipSuccess)
+                        el = avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, stacked ? s->d_obs : o, stacked ? s->d_rew : r,
+                                             stacked ? s->d_done : dn, stacked ? s->d_info : in, nullptr, 1, -(g + 1), e0, e1, st, nullptr);
+                    if (el == hipSuccess && stacked)
+                        el = avr_launch_rollout_copy(ck, s->d_obs, s->d_rew, s->d_done, s->d_info, o, r, dn, in, e0, e1, (int)E, st);
+                }
+                if (g > 0 && el == hipSuccess) el = hipEventRecord(s->join_ev[g], st);
+            }
+            for (int g = 1; g < s->ngroups && el == hipSuccess; g++) el = hipStreamWaitEvent(s->stream, s->join_ev[g], 0);
+            hipError_t e = hipStreamEndCapture(s->stream, &rs->graph[c]);
+            if (e == hipSuccess && el == hipSuccess) e = hipGraphInstantiate(&rs->gexec[c], rs->graph[c], nullptr, nullptr, 0);
+            if (e != hipSuccess || el != hipSuccess) {
+                drop_roll(*rs);
+                HIPCHK(s, e != hipSuccess ? e : el);
+            }
+        }
+        memcpy(rs->key, key, sizeof(rs->key));
+        s->n_captures++;
+    }
+    rs->used = ++s->gclock;
+    for (int g = 0; g < s->ngroups; g++)      // (in stream order before the replays: the counters are the handle's)
+        HIPCHK(s, avr_launch_set_step2(s->km.step_t + g, t0 - 1, s->km.step_t + AVR_MAX_GROUPS + g, -1, s->stream));
+    for (int k = 0; k + AVR_ROLL_CHUNK <= n; k += AVR_ROLL_CHUNK) HIPCHK(s, hipGraphLaunch(rs->gexec[0], s->stream));
+    for (int k = n / AVR_ROLL_CHUNK * AVR_ROLL_CHUNK; k < n; k++) HIPCHK(s, hipGraphLaunch(rs->gexec[1], s->stream));
+    return 0;
+}
+
+
+static int rollout_per_group(avr_sim *s, int64_t t0, int32_t n, float *o, float *r, uint8_t *dn, float *in, int32_t stacked, const void *const *key) {
+    const size_t E = (size_t)s->cfg.n_envs;
+    avr_sim::RollSlot *rs = nullptr;
+    for (auto &x : s->rslot)
+        if (x.pgexec[0][0][0] && memcmp(key, x.key, sizeof(x.key)) == 0) rs = &x;
+    if (!rs) {
+        for (auto &x : s->rslot)
+            if (!x.pgexec[0][0][0] && !x.gexec[0] && !rs) rs = &x;
+        if (!rs) {
+            rs = &s->rslot[0];
+            for (auto &x : s->rslot)
+                if (x.used < rs->used) rs = &x;
+            HIPCHK(s, hipDeviceSynchronize());
+            drop_roll(*rs);
+        }
+        for (int c = 0; c < 2; c++)
+            for (int p = 0; p < 2; p++)
+                for (int g = 0; g < s->ngroups; g++) {
+                    hipStream_t st = g == 0 ? s->stream : s->gstream[g];
+                    const int e0 = group_bound(s, g), e1 = group_bound(s, g + 1);
+                    long long *ct = s->km.step_t + g, *ck = s->km.step_t + AVR_MAX_GROUPS + g;
+                    HIPCHK(s, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                    hipError_t el = hipSuccess;
+                    for (int q = 0; q < (c == 0 ? AVR_ROLL_CHUNK : 1) && el == hipSuccess; q++) {
+                        el = avr_launch_step_advance(ct, ck, st);
+                        if (el == hipSuccess)
+                            el = avr_launch_step(&s->km, s->d_km, s->d_state, nullptr, stacked ? s->d_obs : o, stacked ? s->d_rew : r,
+                                                 stacked ? s->d_done : dn, stacked ? s->d_info : in, nullptr, 1, -(g + 1), e0, e1, st, nullptr);
+                        if (el == hipSuccess && stacked)
+                            el = avr_launch_rollout_copy(ck, s->d_obs, s->d_rew, s->d_done, s->d_info, o, r, dn, in, e0, e1, (int)E, st);
+                    }
+                    hipError_t e = hipStreamEndCapture(st, &rs->pgraph[c][p][g]);
+                    if (e == hipSuccess && el == hipSuccess) e = hipGraphInstantiate(&rs->pgexec[c][p][g], rs->pgraph[c][p][g], nullptr, nullptr, 0);
+                    if (e != hipSuccess || el != hipSuccess) {
+                        drop_roll(*rs);
+                        HIPCHK(s, e != hipSuccess ? e : el);
+                    }
+                }
+        memcpy(rs->key, key, sizeof(rs->key));
+        s->n_captures++;
+    }
+    rs->used = ++s->gclock;
+    HIPCHK(s, hipEventRecord(s->fork_ev, s->stream));
+    for (int g = 0; g < s->ngroups; g++) {
+        hipStream_t st = g == 0 ? s->stream : s->gstream[g];
+        if (g > 0) HIPCHK(s, hipStreamWaitEvent(st, s->fork_ev, 0));
+        HIPCHK(s, avr_launch_set_step2(s->km.step_t + g, t0 - 1, s->km.step_t + AVR_MAX_GROUPS + g, -1, st));
+    }
+    int rep_ = 0;
+    for (int k = 0; k + AVR_ROLL_CHUNK <= n; k += AVR_ROLL_CHUNK, rep_++)
+        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[0][rep_ & 1][g], g == 0 ? s->stream : s->gstream[g]));
+    for (int k = n / AVR_ROLL_CHUNK * AVR_ROLL_CHUNK; k < n; k++, rep_++)
+        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[1][rep_ & 1][g], g == 0 ? s->stream : s->gstream[g]));
+    for (int g = 1; g < s->ngroups; g++) {
+        HIPCHK(s, hipEventRecord(s->join_ev[g], s->gstream[g]));
+        HIPCHK(s, hipStreamWaitEvent(s->stream, s->join_ev[g], 0));
+    }
+    return 0;
+}
+
+
+int avr_rollout_random_device(avr_sim *s, int64_t t0, int32_t n, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info, int32_t stacked) {
+    CHECK_SIM(s);
+    if (t0 < 0 || n < 0) return fail(s, -1, "avr_rollout_random_device: t0 %lld / n %d < 0", (long long)t0, n);
+    if (n == 0) return 0;
+    if (stacked && !(d_obs && d_rew && d_done && d_info)) return fail(s, -1, "avr_rollout_random_device: stacked outputs need all four buffers");
+    const size_t E = (size_t)s->cfg.n_envs;
+    float *o = d_obs ? d_obs : s->d_obs, *r = d_rew ? d_rew : s->d_rew, *in = d_info ? d_info : s->d_info;
+    uint8_t *dn = d_done ? d_done : s->d_done;
+    if (!s->use_graph || s->ngroups <= 1 || s->evlog.cap) {
+        for (int k = 0; k < n; k++) {
+            const size_t q = stacked ? (size_t)k : 0;
+            HIPCHK(s, run_step(s, s->d_state, nullptr, o + q * E * K_OBS_DIM, r + q * E, dn + q * E, in + q * E * AVR_INFO_DIM, nullptr, 1, t0 + k));
+        }
+        return 0;
+    }
+    // the groups' graphs for these outputs: step outputs straight to the caller's buffers, or
+    // (stacked) to the handle's buffers and a copy into slot k
+    const void *key[8] = {o, r, dn, in, (const void *)(size_t)(stacked + 1), nullptr, nullptr, nullptr};
+    if (per_group_rollout(s)) return rollout_per_group(s, t0, n, o, r, dn, in, stacked, key);
+    return rollout_branches(s, t0, n, o, r, dn, in, stacked, key);
 }
 
 int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {

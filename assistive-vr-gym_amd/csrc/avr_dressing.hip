@@ -796,6 +796,20 @@ int avr_step_random_device(avr_sim *s, int64_t t, float *d_obs, float *d_rew, ui
                      d_info ? d_info : s->d_info));
     return 0;
 }
+// (avr_rollout_random_device: one launch per step, step k's outputs to slot k when stacked)
+int avr_rollout_random_device(avr_sim *s, int64_t t0, int32_t n, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info, int32_t stacked) {
+    CHECK_SIM(s);
+    if (t0 < 0 || n < 0) return fail(s, -1, "avr_rollout_random_device: t0 %lld / n %d < 0", (long long)t0, n);
+    if (stacked && !(d_obs && d_rew && d_done && d_info)) return fail(s, -1, "avr_rollout_random_device: stacked outputs need all four buffers");
+    const size_t E = (size_t)s->cfg.n_envs;
+    float *o = d_obs ? d_obs : s->d_obs, *r = d_rew ? d_rew : s->d_rew, *in = d_info ? d_info : s->d_info;
+    uint8_t *dn = d_done ? d_done : s->d_done;
+    for (int k = 0; k < n; k++) {
+        const size_t q = stacked ? (size_t)k : 0;
+        HIPCHK(s, launch(s, nullptr, nullptr, DR_MODE_STEP_RANDOM, t0 + k, o + q * E * AVR_DR_OBS_DIM, r + q * E, dn + q * E, in + q * E * AVR_INFO_DIM));
+    }
+    return 0;
+}
 int avr_random_actions_device(avr_sim *s, int64_t t, float *d_act) {
     CHECK_SIM(s);
     if (t < 0) return fail(s, -1, "avr_random_actions_device: step index %lld < 0", (long long)t);

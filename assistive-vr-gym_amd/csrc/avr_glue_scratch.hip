@@ -16,7 +16,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const int env = env0 + 512 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
-    if (t < 0) t = *m.step_t;                  // graph replay: the counter written before the launch (run_step)
+    if (t < 0) t = m.step_t[-t - 1];           // graph replay: group -t - 1's counter, written before the launch (run_step, rollout)
     float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
     ws[WS_COOPROT] = 0.f;                       // the capped cooperative-pair window restarts every gym step (np_coop)

@@ -2728,7 +2728,7 @@ __global__ __launch_bounds__(64) void avr_take_step_kernel(const KModel *__restr
     const int env = env0 + 512 * (blockIdx.x >> 3) + (blockIdx.x & 7) + 8 * threadIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
     const KModel &m = *mp;
-    if (t < 0) t = *m.step_t;                  // graph replay: the counter written before the launch (run_step)
+    if (t < 0) t = m.step_t[-t - 1];           // graph replay: group -t - 1's counter, written before the launch (run_step, rollout)
     float *st = state + (size_t)env * K_STATE_WORDS;
     float *ws = env_ws(m, env);
     ws[WS_COOPROT] = 0.f;                       // the capped cooperative-pair window restarts every gym step (np_coop)
@@ -4206,6 +4206,51 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
 __global__ void avr_set_step_kernel(long long *dst, long long t) { *dst = t; }
 hipError_t avr_launch_set_step(long long *dst, long long t, hipStream_t stream) {
     hipLaunchKernelGGL(avr_set_step_kernel, dim3(1), dim3(1), 0, stream, dst, t);
+    return hipGetLastError();
+}
+// a rollout step's counters for one env group: its step index t and its slot k in the rollout
+__global__ void avr_set_step2_kernel(long long *dt, long long t, long long *dk, long long k) {
+    if (threadIdx.x == 0) *dt = t;
+    else *dk = k;
+}
+hipError_t avr_launch_set_step2(long long *dt, long long t, long long *dk, long long k, hipStream_t stream) {
+    hipLaunchKernelGGL(avr_set_step2_kernel, dim3(1), dim3(2), 0, stream, dt, t, dk, k);
+    return hipGetLastError();
+}
+// a rollout graph's step: the group's step index and slot advance by one (in stream order, before
+// the step's take_step reads them)
+__global__ void avr_step_advance_kernel(long long *dt, long long *dk) {
+    if (threadIdx.x == 0) *dt += 1;
+    else *dk += 1;
+}
+hipError_t avr_launch_step_advance(long long *dt, long long *dk, hipStream_t stream) {
+    hipLaunchKernelGGL(avr_step_advance_kernel, dim3(1), dim3(2), 0, stream, dt, dk);
+    return hipGetLastError();
+}
+// a stacked rollout: envs [env0, env1)'s outputs of the step just taken, from the handle's output
+// buffers to slot *kslot of the caller's [n][E][...] arrays (one thread per env and word)
+__global__ __launch_bounds__(256) void avr_rollout_copy_kernel(const long long *__restrict__ kslot, const float *__restrict__ obs, const float *__restrict__ rew,
+                                                               const unsigned char *__restrict__ done, const float *__restrict__ info, float *__restrict__ o_obs,
+                                                               float *__restrict__ o_rew, unsigned char *__restrict__ o_done, float *__restrict__ o_info,
+                                                               int env0, int env1, int E) {
+    constexpr int W = K_OBS_DIM + AVR_INFO_DIM + 2;
+    const long long k = *kslot;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int env = env0 + i / W, w = i % W;
+    if (env >= env1) return;
+    const size_t o = (size_t)k * E + env;
+    if (w < K_OBS_DIM) o_obs[o * K_OBS_DIM + w] = obs[(size_t)env * K_OBS_DIM + w];
+    else if (w < K_OBS_DIM + AVR_INFO_DIM) o_info[o * AVR_INFO_DIM + (w - K_OBS_DIM)] = info[(size_t)env * AVR_INFO_DIM + (w - K_OBS_DIM)];
+    else if (w == K_OBS_DIM + AVR_INFO_DIM) o_rew[o] = rew[env];
+    else o_done[o] = done[env];
+}
+hipError_t avr_launch_rollout_copy(const long long *kslot, const float *obs, const float *rew, const unsigned char *done, const float *info, float *o_obs,
+                                   float *o_rew, unsigned char *o_done, float *o_info, int env0, int env1, int E, hipStream_t stream) {
+    constexpr int W = K_OBS_DIM + AVR_INFO_DIM + 2;
+    const int n = (env1 - env0) * W;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(avr_rollout_copy_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, kslot, obs, rew, done, info, o_obs, o_rew, o_done, o_info,
+                       env0, env1, E);
     return hipGetLastError();
 }
 

@@ -266,8 +266,29 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
                 if j == G - 1:
                     D.gather_rollouts(roll.cpu() if gloo else roll, out=gathered)
 
-    for w in range(warmup):
-        one_step(w, w)
+    # the timed steps as rollouts (avr_rollout_random_device: the same steps, bit for bit, with
+    # the env groups joined at the end of each rollout instead of after every step); multi-GPU:
+    # rollouts of G steps with per-step outputs (stacked), packed and all-gathered after each
+    if not args.step_sync:
+        so, sr, sd, si = (torch.zeros(G, E, L.OBS_DIM, device=dev), torch.zeros(G, E, device=dev),
+                          torch.zeros(G, E, dtype=torch.uint8, device=dev), torch.zeros(G, E, L.INFO_DIM, device=dev)) if world > 1 else (None,) * 4
+
+    def run_steps(t0, n):
+        if args.step_sync:
+            for k in range(n):
+                one_step(t0 + k, k)
+            return
+        if world == 1:
+            sim.rollout_random_device(t0, n, obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr())
+            return
+        for c in range(0, n, G):
+            m = min(G, n - c)
+            sim.rollout_random_device(t0 + c, m, so.data_ptr(), sr.data_ptr(), sd.data_ptr(), si.data_ptr(), stacked=True)
+            with torch.cuda.stream(ext):
+                D.pack_rollout_stacked(roll, so, sr, si, sd, m)
+                D.gather_rollouts(roll.cpu() if gloo else roll, out=gathered)
+
+    run_steps(0, warmup)
     sim.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -276,8 +297,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(ext)
-    for k in range(steps):
-        one_step(warmup + k, k)
+    run_steps(warmup, steps)
     ev1.record(ext)
     sim.sync()
     torch.cuda.synchronize(dev)
@@ -333,7 +353,8 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
         'dtype': 'f32',
         'data': 'synthetic: random actions U(-1,1)^7 (Philox, device), reset states from the reset path (%d distinct per GPU, tiled)' % pool,
         'config': {'workload': T['workload'] % E, 'task': name, 'envs_per_gpu': E, 'impairment': args.impairment,
-                   'parallelism': 'env-sharded x%d' % world, 'env_groups': sim.env_groups()},
+                   'parallelism': 'env-sharded x%d' % world, 'env_groups': sim.env_groups(),
+                   'stepping': 'per-step joins' if args.step_sync else ('rollout' if world == 1 else 'rollout x%d steps' % G)},
         'roofline': {'bound': bound, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'limiter': limiter,
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
@@ -438,6 +459,8 @@ def main():
     ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default: the config\'s, 4096; DressingJaco 2048)')
     ap.add_argument('--settle', type=int, default=None, help='reset settle frames (FeedingJaco 100, ScratchItch 0)')
     ap.add_argument('--gather-every', type=int, default=16)
+    ap.add_argument('--step-sync', action='store_true',
+                    help='time avr_step_random_device per step (env groups joined after every step) instead of rollouts')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--other-steps', type=int, default=20,

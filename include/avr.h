@@ -93,6 +93,13 @@ int avr_step_device(avr_sim *sim, const float *d_act, float *d_obs, float *d_rew
  * keyed by (seed, env_offset + e, t) -- examples/random_actions.py semantics.  t >= 0 (a
  * negative t is rejected). */
 int avr_step_random_device(avr_sim *sim, int64_t t, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info);
+/* n device-random steps t0 .. t0+n-1, bit-identical to n avr_step_random_device calls.  stacked = 0:
+ * every step writes d_obs.. (NULL: the handle's buffers; the last step's outputs remain); stacked = 1:
+ * step k writes slot k of d_obs[n][n_envs][obs_dim], d_rew[n][n_envs], d_done[n][n_envs],
+ * d_info[n][n_envs][AVR_INFO_DIM] (all four required).  The env groups are joined every 16 steps
+ * (not after every step): a group that finishes a step early starts its next one.  Asynchronous;
+ * the handle's stream holds the whole rollout. */
+int avr_rollout_random_device(avr_sim *sim, int64_t t0, int32_t n, float *d_obs, float *d_rew, uint8_t *d_done, float *d_info, int32_t stacked);
 /* Device actions for inspection: d_act[n_envs*7] for step t (same Philox stream). */
 int avr_random_actions_device(avr_sim *sim, int64_t t, float *d_act);
 

@@ -111,3 +111,21 @@ def test_shard_blocks_cover_global_ids():
         off, n = D.shard(4096, r)
         seen.extend(range(off, off + n))
     assert seen == list(range(8 * 4096))
+
+
+def test_pack_rollout_stacked_equals_per_step_packs():
+    """bench.py's rollout path packs G stacked steps at once (dist.pack_rollout_stacked): the same
+    rows as packing each step's outputs (dist.pack_rollout), a short last chunk included."""
+    import torch
+    from avr import dist as D, _abi as ABI
+    G, E, od = 5, 7, ABI.OBS_DIM
+    g = torch.Generator().manual_seed(3)
+    obs, rew = torch.rand(G, E, od, generator=g), torch.rand(G, E, generator=g)
+    info, done = torch.rand(G, E, ABI.INFO_DIM, generator=g), (torch.rand(G, E, generator=g) > 0.5).to(torch.uint8)
+    W = D.roll_width(od)
+    for m in (G, 3):
+        a, b = torch.full((G, E, W), -1.0), torch.full((G, E, W), -1.0)
+        D.pack_rollout_stacked(a, obs, rew, info, done, m)
+        for j in range(m):
+            D.pack_rollout(b, j, obs[j], rew[j], info[j], done[j])
+        assert torch.equal(a, b)

@@ -296,6 +296,55 @@ def test_step_random_device_equals_host_actions(lib_and_scene):
     s1.close(); s2.close()
 
 
+@pytest.mark.parametrize('mode', ['groups', 'branches'])
+def test_rollout_equals_step_loop(lib_and_scene, mode, monkeypatch):
+    """avr_rollout_random_device (env groups not joined after every step; both replay forms:
+    per-group graphs, and a graph of per-group branches) == the same steps as
+    avr_step_random_device calls, bit for bit: the state, the last step's outputs (unstacked) and
+    every step's outputs (stacked), at 4096 envs (four env groups), over a 16-step chunk plus a
+    remainder."""
+    import torch
+    from avr import _abi as ABI
+    monkeypatch.setenv('AVR_ROLLOUT', mode)
+    A, md = lib_and_scene
+    n, K = 4096, 19
+    S = np.tile(reset_states(A, md, range(16), 'random'), (n // 16, 1))
+    sims = [make_sim(md, n) for _ in range(3)]
+    assert all(s.lib.avr_env_groups(s.h) == 4 for s in sims)
+    for s in sims:
+        s.set_state(S)
+        s.settle(3)
+    dev = 'cuda'
+
+    def bufs(lead=()):
+        return (torch.zeros(*lead, n, ABI.OBS_DIM, device=dev), torch.zeros(*lead, n, device=dev),
+                torch.zeros(*lead, n, dtype=torch.uint8, device=dev), torch.zeros(*lead, n, ABI.INFO_DIM, device=dev))
+    ptr = lambda b: [x.data_ptr() for x in b]
+    per_step = []
+    b0 = bufs()
+    for t in range(K):
+        sims[0].step_random_device(5 + t, *ptr(b0))
+        sims[0].sync()
+        per_step.append([x.clone() for x in b0])
+    b1 = bufs()
+    sims[1].rollout_random_device(5, K, *ptr(b1))
+    b2 = bufs((K,))
+    sims[2].rollout_random_device(5, K, *ptr(b2), stacked=True)
+    for s in sims[1:]:
+        s.sync()
+    torch.cuda.synchronize()
+    ref = sims[0].get_state()
+    for s in sims[1:]:
+        assert np.array_equal(s.get_state(), ref)
+    for x, y in zip(b1, per_step[-1]):
+        assert torch.equal(x, y)
+    for k in range(K):
+        for x, y in zip(b2, per_step[k]):
+            assert torch.equal(x[k], y)
+    for s in sims:
+        s.close()
+
+
 def test_deterministic_and_batch_independent(lib_and_scene):
     from avr import _lib
     A, md = lib_and_scene
