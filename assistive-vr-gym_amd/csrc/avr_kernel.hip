@@ -389,6 +389,30 @@ AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
     }
 }
 
+// the second robot endpoint of a row whose first endpoint's (J, M^-1 J^T) are in J, MJ: y = M^-1 x
+// row by row (minv_mul's sums), each y_i added to MJ_i and x_i y_i, x_i vq_i to den, rel in DoF
+// order, then x added to J -- the same roundings as storing the first endpoint's part and adding
+// the second's to it (add_robot) without the read-back of the first from memory
+AVR_DI void minv_mul_add(const EnvLDS &L, const float *x, float *J, float *MJ, float &den, float &rel) {
+#if AVR_MINV_LAUNDER
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const float *Mv = &L.u.d.Minv[0][0] + z;
+#else
+    const float *Mv = &L.u.d.Minv[0][0];
+#endif
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < MAXD; k++) s += Mv[i * MAXD + k] * x[k];
+        den += x[i] * s; rel += x[i] * L.vq[i];
+        MJ[i] += s;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) J[i] += x[i];
+}
+
 // Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping), result in L.h.
 // The forward recursion (parent p of link i, joint origin o_i, COM c_i):
 //   om_i = om_p + w_i                       (w_i = axis qd, revolute; 0 otherwise)
@@ -2119,24 +2143,6 @@ AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 #endif
 }
 
-// the second robot endpoint of a contact row: adds its (J, M^-1 J^T) to the part the first one
-// wrote (this lane's own stores, read back)
-AVR_DI void add_robot(float *w, const float *J, const float *MJ) {
-#if NDL == 2
-#pragma unroll
-    for (int d = 0; d < 16; d++) {
-        w[4 * d] += J[d]; w[4 * d + 1] += MJ[d];
-        if (d + 16 < MAXD) { w[4 * d + 2] += J[d + 16]; w[4 * d + 3] += MJ[d + 16]; }
-        if ((d & 3) == 3) asm volatile("" ::: "memory");    // (keeps the read-backs from being hoisted together)
-    }
-#else
-#pragma unroll
-    for (int d = 0; d < MAXD; d++) {
-        w[2 * d] += J[d]; w[2 * d + 1] += MJ[d];
-        if ((d & 3) == 3) asm volatile("" ::: "memory");
-    }
-#endif
-}
 
 // Non-contact rows (limits, motors, fixed constraint), one lane per row.
 // Row order restates btMultiBodyConstraintSolver's setup order: joint-limit rows
@@ -2383,12 +2389,21 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
             // the robot part (J, M^-1 J^T) goes to the row buffer endpoint by endpoint (the second
             // robot endpoint, if any, adds to the first's): one pair of MAXD arrays live at a time
             float *wr = rob ? row_rob(m, rows, slot) : nullptr;
+            const v3 nd = scl(lin, -1.f), angB = scl(angA, -1.f);
             if (kA == 1) {
                 float Ja[MAXD], Ma[MAXD];
                 robot_jac(m, L, iA, pa, lin, angA, Ja);
                 minv_mul(L, Ja, Ma);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; }
+                if (kB == 1) {
+                    // both endpoints on the articulated system (a robot link against a human-chain
+                    // link): the second endpoint's part is added in registers (minv_mul_add); the
+                    // read-back of the first from memory cost ~60 us per sub-step (ScratchItch)
+                    float Jb[MAXD];
+                    robot_jac(m, L, iB, pb, nd, angB, Jb);
+                    minv_mul_add(L, Jb, Ja, Ma, den, rel);
+                }
                 put_robot(wr, Ja, Ma);
                 put_free_zero(w + 4);
             } else if (kA == 2) {
@@ -2397,15 +2412,15 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 rel += free_dot(L, iA, lin, ja);
                 put_free(L, iA, w + 4, lin, ja);
             } else put_free_zero(w + 4);
-            const v3 nd = scl(lin, -1.f), angB = scl(angA, -1.f);
             if (kB == 1) {
-                float Jb[MAXD], Mb[MAXD];
-                robot_jac(m, L, iB, pb, nd, angB, Jb);
-                minv_mul(L, Jb, Mb);
+                if (kA != 1) {
+                    float Jb[MAXD], Mb[MAXD];
+                    robot_jac(m, L, iB, pb, nd, angB, Jb);
+                    minv_mul(L, Jb, Mb);
 #pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
-                if (kA == 1) add_robot(wr, Jb, Mb);
-                else put_robot(wr, Jb, Mb);
+                    for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
+                    put_robot(wr, Jb, Mb);
+                }
                 put_free_zero(w + 10);
             } else if (kB == 2) {
                 v3 jb = add(crs(rB, nd), angB), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);

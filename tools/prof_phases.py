@@ -43,3 +43,20 @@ for t in range(int(os.environ.get('PROF_STEPS', '3'))):
         print('  %-13s %6.2f%%  mean %.3g  max %.3g' % (nm, 100 * p[:, k].mean() / tot, p[:, k].mean(), p[:, k].max()))
 St = sim.get_state()
 print('ncp mean', St[:, L.S_TASK + L.T_NCP].mean(), 'flags', np.unique(St[:, L.S_TASK + L.T_FLAGS]))
+# the envs with the slowest contact-row phase: their contact count and robot endpoints (last step)
+c_rows = p[:, 8]
+top = np.argsort(-c_rows)[:6]
+bk = A['body_kind'] if 'body_kind' in A else None
+cpw = ABI.CP_WORDS if hasattr(ABI, 'CP_WORDS') else None
+for e in top:
+    ncp = int(St[e, L.S_TASK + L.T_NCP])
+    nrob = -1
+    if bk is not None and cpw is not None and hasattr(L, 'S_CP'):
+        cp = St[e, L.S_CP:L.S_CP + cpw * ncp].reshape(ncp, cpw)
+        sb = A['shape_body']
+        kinds = [(int(bk[sb[int(r[ABI.CP_SA])]]), int(bk[sb[int(r[ABI.CP_SB])]])) for r in cp]
+        nrob = sum(1 for a, b in kinds if a == ABI.BODY_ROBOT or b == ABI.BODY_ROBOT)
+        print('slow c_rows env %d: %.3g cycles/env-step, contacts %d, robot contacts %d, (kind A, kind B) %s, bodies %s'
+              % (e, c_rows[e], ncp, nrob, kinds, [(int(sb[int(r[ABI.CP_SA])]), int(sb[int(r[ABI.CP_SB])])) for r in cp]))
+    else:
+        print('slow c_rows env %d: %.3g cycles/env-step, contacts %d' % (e, c_rows[e], ncp))
