@@ -199,7 +199,9 @@ int avr_robot_self_contact(avr_sim *sim, int32_t n, const float *q, int32_t *out
  *   position, quaternion xyzw; then B's), contact threshold thr -> out8[8i..] = {rc (0 none,
  *   1 contact, 2 unresolved), normal on B xyz, point on B xyz, signed distance}.  The shape-level
  *   counterpart of p.getClosestPoints / the contact a pair adds to its manifold (btGjkEpa2 [ext]);
- *   lets the GJK / EPA be checked against the oracle pair by pair. */
+ *   lets the GJK / EPA be checked against the oracle pair by pair.  Runs the pair as the step
+ *   does: a pair whose fp32 lane GJK stalls with an open duality gap is answered by the
+ *   cooperative GJK with the double simplex solve, every other pair by the cooperative fp32 path. */
 int avr_narrowphase_query(avr_sim *sim, int32_t n, const int32_t *pairs, const float *poses14, float thr, float *out8);
 
 /* ---- device base-pose search (ScratchItchPR2, BedBathingPR2) ----
