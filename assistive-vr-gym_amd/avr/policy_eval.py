@@ -148,6 +148,11 @@ def evaluate(env_id, actor_critic, ob_rms, n_envs=64, steps=200, deterministic=T
         force = torch.zeros(n_envs, device=dev)
         info = None
         policy = _graphed_policy(actor_critic, ob_rms, obs, hxs, masks, deterministic) if graph else None
+        if policy is None:
+            # one untimed forward (the mode: no draw from the torch RNG the loop samples from), so
+            # that the BLAS handles and kernel code objects load outside the timed loop
+            with torch.no_grad():
+                actor_critic.act(normalize(obs, ob_rms), hxs, masks, deterministic=True)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(steps):
