@@ -6,9 +6,12 @@ on random relative poses from 3 cm apart to 3 cm deep.
 The Minkowski difference of a thin box core and a capsule's segment core is nearly degenerate:
 in fp32 the Voronoi-simplex GJK sometimes stops on a non-decreasing step and EPA on a
 non-minimal face (normal off by tens of degrees, depth by ~1 mm).  The fp32 build of the oracle
-does the same at a similar rate (tools/dbg_np.py: ~1 % of penetrating queries on both), so the bar
-is a rate: the GPU agrees with the fp64 restatement (normal within 2 deg, distance within 1e-4 m)
-on >= 97 % of the contacts, and misses no more than twice as often as the fp32 oracle + 1 %."""
+does so on ~1 % of penetrating queries (tools/dbg_np.py).  Since round 5 the GPU's lane GJK checks
+the duality gap when it stops and hands a stalled pair to the wave-cooperative solve, whose simplex
+step runs in double: measured, 0 of ~1470 contacts off the fp64 restatement per task (normal within
+2 deg, distance within 1e-4 m) against 0.7-1.2 % for the fp32 oracle
+(profiles/r05_narrowphase_near_contact.log).  The bar: misses <= 0.5 % and no more than the fp32
+oracle's rate + 0.1 %."""
 import numpy as np
 import pytest
 
@@ -89,4 +92,64 @@ def test_gpu_narrowphase_matches_fp64_oracle(task):
     a32, m32, _ = _miss(r32, r64)
     print('GPU vs fp64 oracle: contact agreement %.4f, misses %.4f of %d contacts; fp32 oracle %.4f / %.4f' % (ag, mg, n, a32, m32))
     assert n > 500 and ag >= 0.99
-    assert mg <= 0.03 and mg <= 2 * m32 + 0.01, (mg, m32)
+    assert mg <= 0.005 and mg <= m32 + 0.001, (mg, m32)
+
+
+def _near_contact(A, md, task, n, seed):
+    """_queries moved along the fp64 oracle's normal to a distance drawn from [-1, 3] mm: the
+    near-contact regime where an fp32 GJK stops on a thin simplex before it converges (the
+    round-5 duality-gap check hands those stops to the wave-cooperative solve with a double
+    simplex; avr_kernel.hip gjk_lane / simplex_closest_d)."""
+    from oracle.oracle import Oracle
+    pairs, X = _queries(A, *CASES[task], n, seed)
+    o = Oracle(md, 1, 'f64')
+    rng = np.random.default_rng(seed + 1)
+    keep = []
+    for k, (sa, sb) in enumerate(pairs):
+        r, out = o.narrowphase(int(sa), X[k, :7], int(sb), X[k, 7:], 0.02)
+        if r:
+            X[k, :3] += out[:3] * (rng.uniform(-0.001, 0.003) - out[6])
+            keep.append(k)
+    return pairs[keep], X[keep]
+
+
+def _near_miss(R, ref):
+    """share of queries whose contact flag differs, or whose distance is off by > 1e-5 m or normal
+    by > 2 deg from the fp64 restatement"""
+    both = (R[:, 0] > 0) & (ref[:, 0] > 0)
+    ang = np.degrees(np.arccos(np.clip((R[:, 1:4] * ref[:, 1:4]).sum(1), -1, 1)))
+    bad = ((R[:, 0] > 0) != (ref[:, 0] > 0)) | (both & ((np.abs(R[:, 7] - ref[:, 7]) > 1e-5) | (ang > 2)))
+    return float(bad.mean())
+
+
+@pytest.mark.parametrize('task', [1, 2], ids=['ScratchItchPR2', 'BedBathingPR2'])
+def test_fp32_oracle_near_contact_rate(task):
+    A = ABI.load_scene(task)
+    md = ABI.ModelDesc(A)
+    pairs, X = _near_contact(A, md, task, 600, 21)
+    r64, r32 = _oracle_np(md, pairs, X, 'f64'), _oracle_np(md, pairs, X, 'f32')
+    m32 = _near_miss(r32, r64)
+    print('fp32 oracle near contact: misses %.4f of %d' % (m32, len(pairs)))
+    assert len(pairs) > 500 and m32 < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('task', [1, 2], ids=['ScratchItchPR2', 'BedBathingPR2'])
+def test_gpu_narrowphase_near_contact(task):
+    """GPU narrowphase 1 mm from contact against the fp64 restatement, with the fp32 oracle's miss
+    rate on the same queries beside it (the fp32 restatement has no stall hand-over)."""
+    from avr import _lib
+    A = ABI.load_scene(task)
+    md = ABI.ModelDesc(A)
+    pairs, X = _near_contact(A, md, task, 3000, 22)
+    sim = _lib.Sim(md, 1)
+    try:
+        g = sim.narrowphase(pairs, X).astype(np.float64)
+    finally:
+        sim.close()
+    r64, r32 = _oracle_np(md, pairs, X, 'f64'), _oracle_np(md, pairs, X, 'f32')
+    mg, m32 = _near_miss(g, r64), _near_miss(r32, r64)
+    print('near contact, %d queries: GPU misses %.4f, fp32 oracle %.4f' % (len(pairs), mg, m32))
+    # measured: 0.03 % on both tasks against 0.44 / 0.55 % for the fp32 oracle
+    assert len(pairs) > 2500
+    assert mg <= 0.002 and mg <= m32, (mg, m32)
