@@ -28,13 +28,33 @@ def _hipcc():
     raise RuntimeError('hipcc not found')
 
 
+_COMPILER_ID = {}
+
+
+def _compiler_id(cc):
+    """The compiler's own version banner (first two lines of `<cc> --version`): recorded beside the
+    command line, so a library built by another hipcc / clang release is rebuilt from source."""
+    if cc not in _COMPILER_ID:
+        try:
+            out = subprocess.run([cc, '--version'], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True).stdout
+        except OSError:
+            out = ''
+        _COMPILER_ID[cc] = ' | '.join(out.strip().splitlines()[:2])
+    return _COMPILER_ID[cc]
+
+
+def _stamp(cmd):
+    return ' '.join(cmd) + '\n# compiler: ' + _compiler_id(cmd[0])
+
+
 def _stale(target, deps, cmd):
     """Rebuild when the target is missing, older than a dependency, or was built by a different
-    command line (recorded in <target>.cmd: flags and sources, so a flag change rebuilds)."""
+    command line or compiler release (recorded in <target>.cmd: flags, sources and the compiler's
+    version banner, so a flag change or another toolchain rebuilds)."""
     if not os.path.exists(target):
         return True
     side = target + '.cmd'
-    if not os.path.exists(side) or open(side).read() != ' '.join(cmd):
+    if not os.path.exists(side) or open(side).read() != _stamp(cmd):
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
@@ -105,7 +125,7 @@ def build_lib(force=False, extra=(), out=LIB):
     if any(p.wait() != 0 for p in procs):
         raise subprocess.CalledProcessError(1, 'hipcc (%s)' % out)
     subprocess.check_call([_hipcc(), '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out] + objs)
-    open(out + '.cmd', 'w').write(' '.join(cmd))
+    open(out + '.cmd', 'w').write(_stamp(cmd))
     return out
 
 

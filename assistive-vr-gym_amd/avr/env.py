@@ -216,6 +216,7 @@ class AVRVecEnv:
         self.action_robot_len, self.action_human_len = self.L.ACT_DIM, 0
         self.genders = None                # setup(): fixed gender for every reset
         self.participant, self.policy_name = -1, ''
+        self.hipbone_to_mouth_height = None   # setup(): kept, not modelled (see setup)
         self.episode = np.zeros(self.n, np.int64)
         # host mirror of the per-env iteration counters: the kernels' done is exactly
         # T_ITER >= max_steps (TimeLimit), so rollovers are known without reading the device
@@ -233,16 +234,16 @@ class AVRVecEnv:
     # ------------------------------------------------------------------ setup hook
     def setup(self, gender, participant, policy_name, hipbone_to_mouth_height=None):
         """FeedingEnv.setup / ScratchItchEnv.setup (feeding.py:20-28): the evaluation harness fixes
-        the participant's gender (every later reset uses it) and names the policy.  The compiled
-        human has the reference's default proportions (hipbone_to_mouth_height 0.6 male / 0.54
-        female, human_creation.py:60-63); other heights are a VR-calibration feature this build
-        does not model."""
-        default = 0.6 if gender == 'male' else 0.54
+        the participant's gender (every later reset uses it) and names the policy.
+
+        hipbone_to_mouth_height is accepted and kept (`self.hipbone_to_mouth_height`) but, as in
+        the reference's non-VR envs, does not shape the human: their reset overwrites it with the
+        gender's default before building the world (feeding.py:173-174, scratch_itch.py:161,
+        bed_bathing.py:187), so enjoy_vr.py's `env.setup(gender, participant, policy, 0.54)`
+        (enjoy_vr.py:50,63) runs unchanged for both genders."""
         if gender not in ('male', 'female'):
             raise ValueError('gender must be male or female')
-        if hipbone_to_mouth_height is not None and abs(float(hipbone_to_mouth_height) - default) > 1e-9:
-            raise NotImplementedError('hipbone_to_mouth_height %.3f: only the default %.2f (%s) is compiled'
-                                      % (hipbone_to_mouth_height, default, gender))
+        self.hipbone_to_mouth_height = None if hipbone_to_mouth_height is None else float(hipbone_to_mouth_height)
         self.genders = gender
         self.participant, self.policy_name = int(participant), str(policy_name)
         if self._prefetch:

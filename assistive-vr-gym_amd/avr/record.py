@@ -32,6 +32,7 @@ savemeta_reference() is replay_vr_savemeta.py over such directories.
 """
 import glob
 import json
+import math
 import os
 import pickle
 
@@ -194,7 +195,7 @@ class _DType:
 
     def __setstate__(self, state):
         # (version, byteorder, subdescr, names, fields, elsize, alignment, flags)
-        if not isinstance(state, tuple) or len(state) < 2 or state[1] not in ('<', '>', '=', '|'):
+        if not isinstance(state, tuple) or len(state) < 5 or state[1] not in ('<', '>', '=', '|'):
             raise pickle.UnpicklingError('dtype state %r' % (state,))
         if state[2] is not None or state[3] is not None or state[4] is not None:
             raise pickle.UnpicklingError('structured dtype')
@@ -206,6 +207,16 @@ def _as_dtype(d):
     if isinstance(d, _DType):
         return d.dtype
     raise pickle.UnpicklingError('expected a dtype, got %r' % type(d))
+
+
+def _shape(shape):
+    """An array shape as pickled: a tuple of non-negative Python ints (the element count is then
+    formed with Python ints, so a hostile shape cannot wrap around a fixed-width product)."""
+    if not isinstance(shape, (tuple, list)) or len(shape) > 32:
+        raise pickle.UnpicklingError('ndarray shape %r' % (shape,))
+    if not all(isinstance(s, int) and not isinstance(s, bool) and s >= 0 for s in shape):
+        raise pickle.UnpicklingError('ndarray shape %r' % (shape,))
+    return tuple(shape)
 
 
 class _ArrayBuilder:
@@ -226,8 +237,8 @@ class _ArrayBuilder:
             raw = raw.encode('latin1')
         if not isinstance(raw, (bytes, bytearray)):
             raise pickle.UnpicklingError('ndarray data of type %r' % type(raw))
-        shape = tuple(int(s) for s in shape)
-        n = int(np.prod(shape)) if shape else 1
+        shape = _shape(shape)
+        n = math.prod(shape)
         if n * dt.itemsize != len(raw):
             raise pickle.UnpicklingError('ndarray of shape %s / %s with %d data bytes' % (shape, dt, len(raw)))
         a = np.frombuffer(bytes(raw), dt, count=n).reshape(shape, order='F' if fortran else 'C')
@@ -238,8 +249,8 @@ def _frombuffer(buf, dt, shape, order):
     """numpy.core.numeric._frombuffer as pickled by protocol 5 (in-band buffer)."""
     dt = _as_dtype(dt)
     raw = bytes(buf)
-    shape = tuple(int(s) for s in shape)
-    n = int(np.prod(shape)) if shape else 1
+    shape = _shape(shape)
+    n = math.prod(shape)
     if n * dt.itemsize != len(raw) or order not in ('C', 'F'):
         raise pickle.UnpicklingError('ndarray buffer')
     return np.frombuffer(raw, dt, count=n).reshape(shape, order=order).astype(dt.newbyteorder('='), copy=True)
@@ -304,7 +315,13 @@ def load_reference_pickle(path):
     """Read a reference recording's pickle (setup.pkl / actions.pkl) without executing anything
     from the file (see the module docstring); raises pickle.UnpicklingError on anything else."""
     with open(path, 'rb') as f:
-        return _finish(_RestrictedUnpickler(f).load())
+        try:
+            return _finish(_RestrictedUnpickler(f).load())
+        except pickle.UnpicklingError:
+            raise
+        except (EOFError, ValueError, TypeError, IndexError, KeyError, AttributeError, OverflowError, MemoryError,
+                RecursionError, UnicodeError) as e:      # malformed input, whatever opcode it broke
+            raise pickle.UnpicklingError('%s: malformed pickle (%s: %s)' % (path, type(e).__name__, e)) from e
 
 
 def write_reference_recording(directory, robot_type, gender, hipbone_to_mouth_height, actions):

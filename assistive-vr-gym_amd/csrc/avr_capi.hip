@@ -842,7 +842,11 @@ static int rollout_per_group(avr_sim *s, int64_t t0, int32_t n, float *o, float 
             rs = &s->rslot[0];
             for (auto &x : s->rslot)
                 if (x.used < rs->used) rs = &x;
-            HIPCHK(s, hipDeviceSynchronize());
+            // only this handle's streams: every rollout joins its groups back into s->stream, and
+            // no replay of the graphs being dropped may still run (other handles, torch and RCCL
+            // streams on the device are not waited for)
+            HIPCHK(s, hipStreamSynchronize(s->stream));
+            for (int g = 1; g < s->ngroups; g++) HIPCHK(s, hipStreamSynchronize(s->gstream[g]));
             drop_roll(*rs);
         }
         for (int c = 0; c < 2; c++)

@@ -946,7 +946,11 @@ AVR_DI int simplex_closest_d(Simplex &S, v3 &vout, float lam[4]) {
     const float d2 = outside ? (float)ddot(cv, cv) : BIGF;
     float m = fminf(d2, __shfl_xor(d2, 1));
     m = fminf(m, __shfl_xor(m, 2));
-    const int bf = __builtin_ctzll(__ballot(outside && d2 == m) & 0xfull);
+    // no outside face attains m when every outside face's distance is NaN / inf: answer as the
+    // fp32 solve does for a simplex with no usable face (penetrating), not with ctz of an empty mask
+    const unsigned long long bmask = __ballot(outside && d2 == m) & 0xfull;
+    if (!bmask) { lam[0] = lam[1] = lam[2] = lam[3] = 0.f; vout = V(0, 0, 0); return 1; }
+    const int bf = __builtin_ctzll(bmask);
     const int bused = __shfl(used, bf);
     const double bla = __shfl(la, bf), blb = __shfl(lb, bf), blc = __shfl(lc, bf);
     vout = V(__shfl((float)cv.x, bf), __shfl((float)cv.y, bf), __shfl((float)cv.z, bf));

@@ -309,12 +309,31 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
         tt = torch.tensor([el], dtype=torch.float64, device='cpu' if gloo else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    t_next = warmup + steps
+    # the per-step API's rate beside the rollout headline (avr_step_random_device, env groups
+    # joined after every step): what a policy in the loop gets (enjoy_vr.py:106-116, a PPO
+    # rollout), which needs every step's observation before it can act
+    step_sync = None
+    if world == 1 and not args.step_sync and args.sync_steps > 0:
+        for k in range(2):                 # untimed: the per-step graph is captured on first use
+            one_step(t_next + k, k)
+        t_next += 2
+        sim.sync()
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        for k in range(args.sync_steps):
+            one_step(t_next + k, k)
+        sim.sync()
+        torch.cuda.synchronize(dev)
+        es = time.perf_counter() - ts
+        t_next += args.sync_steps
+        step_sync = {'value': E * args.sync_steps / es, 'ms_per_step': es / args.sync_steps * 1e3, 'steps': args.sync_steps}
     # per-kernel launch durations (HIP events between the launches of a step, on the sim
     # stream), from a separate short pass so the timed loop above carries no event overhead
     P = min(10, steps)
     sim.profile_kernels(True)
     for k in range(P):
-        one_step(warmup + steps + k, k)
+        one_step(t_next + k, k)
     kt = sim.kernel_times()
     sim.profile_kernels(False)
     kernels = {k: {'avg_ms': v[0] / max(v[1], 1), 'launches_per_step': v[1] / P, 'ms_per_step': v[0] / P} for k, v in kt.items() if v[1] > 0}
@@ -355,6 +374,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
         'config': {'workload': T['workload'] % E, 'task': name, 'envs_per_gpu': E, 'impairment': args.impairment,
                    'parallelism': 'env-sharded x%d' % world, 'env_groups': sim.env_groups(),
                    'stepping': 'per-step joins' if args.step_sync else ('rollout' if world == 1 else 'rollout x%d steps' % G)},
+        'step_sync': step_sync,
         'roofline': {'bound': bound, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'limiter': limiter,
                      'valu_busy': pmc.get('valu_busy_chip') if pmc else None,
@@ -395,7 +415,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
 # configs[4] as the build-defined DressingJaco),
 # timed after the headline in the same default run: extra keys of the one JSON line
 OTHER_TASKS = ('ScratchItchPR2-v0', 'BedBathingPR2-v0', 'DressingJaco-v0')
-OTHER_KEYS = ('value', 'ms_per_step', 'steps', 'nan_or_overflow_envs', 'cpu_baseline')
+OTHER_KEYS = ('value', 'ms_per_step', 'steps', 'step_sync', 'nan_or_overflow_envs', 'cpu_baseline')
 ROOF_KEYS = ('frac', 'achieved', 'traffic', 'valu_busy', 'limiter', 'dominant_kernel', 'dominant_avg_ms')
 # what each figure covers (kept out of the printed line, written to the detail file)
 SCOPE = ('one env-step = one gym step of one env: 1 take_step + S x (pairs, narrowphase, a, b4) + 1 task launch '
@@ -461,6 +481,9 @@ def main():
     ap.add_argument('--gather-every', type=int, default=16)
     ap.add_argument('--step-sync', action='store_true',
                     help='time avr_step_random_device per step (env groups joined after every step) instead of rollouts')
+    ap.add_argument('--sync-steps', type=int, default=20,
+                    help='N=1 rollout runs: also time this many per-step API steps (--step-sync mode) on the same handle, '
+                         'reported as step_sync (0 = skip)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--other-steps', type=int, default=20,

@@ -75,14 +75,19 @@ def test_policy_checkpoint_round_trip(tmp_path):
     assert rms2.count == 7.0
 
 
-def test_setup_rejects_uncompiled_heights():
+def test_setup_accepts_enjoy_vr_height_for_both_genders():
+    """enjoy_vr.py:50,63 calls env.setup(gender, participant, policy_name, 0.54) for every
+    participant; the reference's non-VR reset then overwrites the height with the gender's default
+    (feeding.py:173-174), so setup() accepts any height, keeps it, and leaves the resets alone."""
     from avr import env as E
-    v = object.__new__(E.AVRVecEnv)
-    v._prefetch = None
-    with pytest.raises(NotImplementedError):
-        E.AVRVecEnv.setup(v, 'female', 3, 'Static', 0.60)
-    E.AVRVecEnv.setup(v, 'female', 3, 'Static', 0.54)
-    assert v.genders == 'female' and v.participant == 3
+    for gender in ('male', 'female'):
+        v = object.__new__(E.AVRVecEnv)
+        v._prefetch = None
+        E.AVRVecEnv.setup(v, gender, 3, 'Static', 0.54)
+        assert v.genders == gender and v.participant == 3 and v.hipbone_to_mouth_height == 0.54
+        assert v._genders([0, 1]) == [gender, gender]
+    with pytest.raises(ValueError):
+        E.AVRVecEnv.setup(v, 'other', 3, 'Static', 0.54)
 
 
 # ------------------------------------------------------------------ GPU
@@ -134,6 +139,21 @@ def test_policy_evaluation_harness(tmp_path):
     assert a['task_success'].shape == (16,)
 
 
+@pytest.mark.gpu
+def test_enjoy_vr_setup_call_runs_for_a_male_participant():
+    """enjoy_vr.py:50,63's exact setup() call -- hipbone_to_mouth_height 0.54 for every participant --
+    on a male participant: the episode runs on the male default human (the reference's non-VR
+    reset overwrites the height, feeding.py:173-174) and equals an episode without the height."""
+    torch.manual_seed(2)
+    pol = PE.ActorCritic(25, 7)
+    rms = PE.RunningMeanStd((25,))
+    a = PE.evaluate('FeedingJaco-v0', pol, rms, n_envs=4, steps=20, setup=dict(gender='male', participant=1, policy_name='Static',
+                                                                               hipbone_to_mouth_height=0.54))
+    b = PE.evaluate('FeedingJaco-v0', pol, rms, n_envs=4, steps=20, setup=dict(gender='male', participant=1, policy_name='Static'))
+    assert np.all(np.isfinite(a['returns']))
+    np.testing.assert_array_equal(a['returns'], b['returns'])
+
+
 # ------------------------------------------------------------------ reference-format recordings
 class _Evil:
     def __reduce__(self):
@@ -170,6 +190,34 @@ def test_reference_pickle_reader_refuses_code_and_object_arrays(tmp_path):
             pickle.dump(obj, f)
         with pytest.raises(pickle.UnpicklingError):
             R.load_reference_pickle(str(p))
+
+
+def test_reference_pickle_reader_raises_unpicklingerror_on_malformed_input(tmp_path):
+    """Truncated files and hand-built hostile states (short dtype states, negative or wrapping
+    shapes, wrong data lengths) all surface as pickle.UnpicklingError, so a caller that skips bad
+    recordings on that error never crashes on another exception type."""
+    import pickle
+    import pickletools
+    good = pickle.dumps(['jaco', 'male', np.float64(0.6), np.arange(6, dtype=np.float32).reshape(2, 3)], protocol=2)
+    bad = [good[:k] for k in (1, 7, len(good) // 2, len(good) - 1)]
+    # a dtype whose BUILD state is a 2-tuple: ('numpy', 'dtype') ('f8', False, True) + state (3, '<')
+    bad.append(b'\x80\x02cnumpy\ndtype\nX\x02\x00\x00\x00f8\x89\x88\x87R(K\x03X\x01\x00\x00\x00<tb.')
+    # ndarray states with hostile shapes / lengths: _reconstruct(ndarray, (0,), b'b') + BUILD(state)
+    head = b'\x80\x02cnumpy.core.multiarray\n_reconstruct\ncnumpy\nndarray\nK\x00\x85C\x01b\x87R'
+    dt = b'cnumpy\ndtype\nX\x02\x00\x00\x00f4\x89\x88\x87R(K\x03X\x01\x00\x00\x00<NNNJ\xff\xff\xff\xffJ\xff\xff\xff\xffK\x00tb'
+    for shape, nbytes in ((b'J\xff\xff\xff\xff\x85', 0),                               # (-1,)
+                          (b'\x8a\x08\x00\x00\x00\x00\x00\x00\x00@\x8a\x08\x00\x00\x00\x00\x00\x00\x00@\x86', 0),  # (2**62, 2**62): wraps in int64
+                          (b'K\x03\x85', 8)):                                          # 3 floats, 8 bytes
+        bad.append(head + b'(K\x01' + shape + dt + b'\x89C' + bytes([nbytes]) + b'\x00' * nbytes + b'tb.')
+    for k, blob in enumerate(bad):
+        p = tmp_path / ('m%d.pkl' % k)
+        p.write_bytes(blob)
+        with pytest.raises(pickle.UnpicklingError):
+            R.load_reference_pickle(str(p))
+    pickletools.dis(good, out=open(os.devnull, 'w'))      # the well-formed blob itself is valid
+    p = tmp_path / 'ok.pkl'
+    p.write_bytes(good)
+    assert R.load_reference_pickle(str(p))[1] == 'male'
 
 
 def test_reference_env_id_from_directory_name():
