@@ -25,9 +25,12 @@
 #include "../../include/avr.h"
 #include "../../include/avr_dressing.h"
 
-// No contraction anywhere in this file: every multiply and add rounds on its own, in the order the
-// fp32 oracle (oracle/avr_oracle_dressing.c, gcc, no FMA) writes them, so the kernel and the fp32
-// oracle round alike and the contact-free sleeve matches it to the last bits (tests/test_dressing.py).
+// No implicit contraction in this file: every multiply and add rounds on its own unless it is an
+// explicit fmaf, in the order the fp32 oracle (oracle/avr_oracle_dressing.c) writes it with the same
+// fused multiply-adds at the same sites (FMA there), so the kernel and the fp32 oracle round alike
+// and the sleeve matches it to the last bits (tests/test_dressing.py).  The fused sites are the cloth
+// sub-step's hot arithmetic: the spring and contact dot products, the force accumulation, the
+// segment projection and the integration.
 #pragma clang fp contract(off)
 
 namespace avr_dressing {
@@ -97,22 +100,27 @@ AVR_DI void dr_fk(const DrModel &m, const float *q7, v3 &tool_p, qt &tool_q, v3 
     __syncthreads();
 }
 
+// the fused forms (the oracle's dotF / axpyF / lenF): x.y first as a product, then y and z fused in
+AVR_DI float dotF(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+AVR_DI float lenF(v3 a) { return sqrtf(dotF(a, a)); }
+AVR_DI v3 axpyF(v3 a, float s, v3 y) { return V(fmaf(a.x, s, y.x), fmaf(a.y, s, y.y), fmaf(a.z, s, y.z)); }   // y + a s
+
 AVR_DI v3 seg_closest(v3 a, v3 b, v3 x) {
     const v3 ab = sub(b, a);
-    const float l2 = dot(ab, ab);
-    float t = l2 > 0.f ? dot(sub(x, a), ab) / l2 : 0.f;
+    const float l2 = dotF(ab, ab);
+    float t = l2 > 0.f ? dotF(sub(x, a), ab) / l2 : 0.f;
     t = fminf(fmaxf(t, 0.f), 1.f);
-    return add(a, scl(ab, t));
+    return axpyF(ab, t, a);
 }
 
 AVR_DI v3 dr_contact(v3 x, v3 v, v3 c, float r) {
     const v3 d = sub(x, c);
-    const float dist = len(d);
+    const float dist = lenF(d);
     const float pen = r + (float)AVR_DR_THICK - dist;
     if (!(pen > 0.f) || !(dist > 1e-9f)) return V(0, 0, 0);
     const v3 n = scl(d, 1.f / dist);
-    const float vn = dot(v, n);
-    const float f = (float)AVR_DR_K_CONTACT * pen - (float)AVR_DR_C_CONTACT * fminf(vn, 0.f);
+    const float vn = dotF(v, n);
+    const float f = fmaf((float)AVR_DR_K_CONTACT, pen, -((float)AVR_DR_C_CONTACT * fminf(vn, 0.f)));
     return scl(n, f);
 }
 
@@ -136,11 +144,11 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const f
         const float L0 = s < 2 ? L_ring : s < 4 ? L_ax : s < 8 ? L_sh : s < 10 ? L_ring2 : 2.f * L_ax;
         const float4 xo = X[o], vo = Vv[o];
         const v3 d = sub(V(xo.x, xo.y, xo.z), x);
-        const float l = len(d);
+        const float l = lenF(d);
         if (!(l > 1e-9f)) continue;
         const v3 u = scl(d, 1.f / l);
-        const float fs = ks * (l - L0) + (float)AVR_DR_DAMP * dot(sub(V(vo.x, vo.y, vo.z), v), u);
-        f = add(f, scl(u, fs));
+        const float fs = fmaf(ks, l - L0, (float)AVR_DR_DAMP * dotF(sub(V(vo.x, vo.y, vo.z), v), u));
+        f = axpyF(u, fs, f);
     }
     v3 fc = V(0, 0, 0);
     fc = add(fc, dr_contact(x, v, seg_closest(ld3(geo + 12), ld3(geo + 15), x), geo[18]));
@@ -149,7 +157,7 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const f
     fc = add(fc, dr_contact(x, v, ld3(geo + 0), geo[27]));
     fc = add(fc, dr_contact(x, v, ld3(geo + 3), geo[28]));
     fc = add(fc, dr_contact(x, v, ld3(geo + 6), geo[29]));
-    fc_mag = len(fc);
+    fc_mag = lenF(fc);
     return add(f, fc);
 }
 
@@ -289,11 +297,11 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                     v0 = scl(sub(tg, x0), 1.f / dtc);
                     x0 = tg;
                 } else {
-                    v0 = add(v0, scl(F0, minv_dt));
-                    x0 = add(x0, scl(v0, dtc));
+                    v0 = axpyF(F0, minv_dt, v0);
+                    x0 = axpyF(v0, dtc, x0);
                 }
-                v1 = add(v1, scl(F1, minv_dt));
-                x1 = add(x1, scl(v1, dtc));
+                v1 = axpyF(F1, minv_dt, v1);
+                x1 = axpyF(v1, dtc, x1);
                 if (last) {
                     float s = 0.f;
                     for (int k = DR_NS; k < DR_NP; k++) s += red[k];

@@ -256,7 +256,8 @@ typedef struct {
     int nsp;
     int gender;
     real oldcp[K_MAX_CONTACTS * AVR_CP_WORDS];
-    long long stats_gjk, stats_epa, stats_rows, stats_iters, stats_solves;
+    long long stats_gjk, stats_epa, stats_rows, stats_iters, stats_solves, stats_stall;
+    int np_plain;          /* narrowphase without the lane GJK's stall rule (bb_closest) */
 } ws_t;
 
 typedef struct avr_oracle {
@@ -607,9 +608,127 @@ static int simplex_closest(simplex *S, v3 *vout, real lam[4]) {
     return 0;
 }
 
-enum { GJK_SEPARATED = 0, GJK_FAR = 1, GJK_PENETRATING = 2 };
+/* The closest point of the simplex to the origin with the Voronoi tests and the barycentric solve
+ * in double, the results rounded to `real` (the kernel's simplex_closest_d, avr_kernel.hip: float
+ * supports, double algebra -- the fp32 GJK's rerun after a stall, see gjk()).  A tetrahedron's
+ * faces compete by their distance rounded to `real`, the lowest face index on ties.  In the fp64
+ * build this is simplex_closest() itself. */
+typedef struct { double x, y, z; } d3_t;
+static d3_t D3(v3 a) { d3_t r = {(double)a.x, (double)a.y, (double)a.z}; return r; }
+static d3_t dadd(d3_t a, d3_t b) { d3_t r = {a.x + b.x, a.y + b.y, a.z + b.z}; return r; }
+static d3_t dsub(d3_t a, d3_t b) { d3_t r = {a.x - b.x, a.y - b.y, a.z - b.z}; return r; }
+static d3_t dscl(d3_t a, double k) { d3_t r = {a.x * k, a.y * k, a.z * k}; return r; }
+static d3_t dcrs(d3_t a, d3_t b) { d3_t r = {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; return r; }
+static double ddot(d3_t a, d3_t b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 dtor(d3_t a) { return V((real)a.x, (real)a.y, (real)a.z); }
 
-static int gjk(const wshape *A, const wshape *B, real maxdist2, v3 *pa, v3 *pb, real *dist, simplex *S) {
+/* Ericson's triangle test in double; used: 1 A, 2 B, 4 C, 3 AB, 5 AC, 6 BC, 7 ABC */
+static d3_t tri_cp_dbl(d3_t A, d3_t B, d3_t C, int *used, double *la, double *lb, double *lc) {
+    d3_t ab = dsub(B, A), ac = dsub(C, A), ap = dscl(A, -1.0);
+    double d1 = ddot(ab, ap), d2 = ddot(ac, ap);
+    *la = *lb = *lc = 0.0;
+    if (d1 <= 0.0 && d2 <= 0.0) { *used = 1; *la = 1.0; return A; }
+    d3_t bp = dscl(B, -1.0);
+    double d3 = ddot(ab, bp), d4 = ddot(ac, bp);
+    if (d3 >= 0.0 && d4 <= d3) { *used = 2; *lb = 1.0; return B; }
+    double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
+        double v = d1 / (d1 - d3);
+        *used = 3; *la = 1.0 - v; *lb = v; return dadd(A, dscl(ab, v));
+    }
+    d3_t cp = dscl(C, -1.0);
+    double d5 = ddot(ab, cp), d6 = ddot(ac, cp);
+    if (d6 >= 0.0 && d5 <= d6) { *used = 4; *lc = 1.0; return C; }
+    double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+        double wv = d2 / (d2 - d6);
+        *used = 5; *la = 1.0 - wv; *lc = wv; return dadd(A, dscl(ac, wv));
+    }
+    double va = d3 * d6 - d5 * d4;
+    if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
+        double wv = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        *used = 6; *lb = 1.0 - wv; *lc = wv; return dadd(B, dscl(dsub(C, B), wv));
+    }
+    double den = 1.0 / (va + vb + vc);
+    double v = vb * den, wv = vc * den;
+    *used = 7; *la = 1.0 - v - wv; *lb = v; *lc = wv;
+    return dadd(A, dadd(dscl(ab, v), dscl(ac, wv)));
+}
+
+static void sx_move(simplex *S, int to, int from) { S->w[to] = S->w[from]; S->a[to] = S->a[from]; S->b[to] = S->b[from]; }
+
+/* keep the triangle's feature `used` in slots 0.. in order; weights rounded to real */
+static void tri_compact_dbl(simplex *S, int used, double la, double lb, double lc, real lam[4]) {
+    switch (used) {
+    case 1: S->n = 1; lam[0] = (real)la; break;
+    case 2: sx_move(S, 0, 1); S->n = 1; lam[0] = (real)lb; break;
+    case 4: sx_move(S, 0, 2); S->n = 1; lam[0] = (real)lc; break;
+    case 3: S->n = 2; lam[0] = (real)la; lam[1] = (real)lb; break;
+    case 5: sx_move(S, 1, 2); S->n = 2; lam[0] = (real)la; lam[1] = (real)lc; break;
+    case 6: sx_move(S, 0, 1); sx_move(S, 1, 2); S->n = 2; lam[0] = (real)lb; lam[1] = (real)lc; break;
+    default: S->n = 3; lam[0] = (real)la; lam[1] = (real)lb; lam[2] = (real)lc; break;
+    }
+}
+
+static int simplex_closest_dbl(simplex *S, v3 *vout, real lam[4]) {
+    if (S->n == 1) { lam[0] = 1; *vout = S->w[0]; return 0; }
+    if (S->n == 2) {
+        d3_t A = D3(S->w[0]), B = D3(S->w[1]), ab = dsub(B, A);
+        double t = -ddot(A, ab), dd = ddot(ab, ab);
+        if (t <= 0.0 || dd <= 0.0) { S->n = 1; lam[0] = 1; *vout = S->w[0]; return 0; }
+        if (t >= dd) { sx_move(S, 0, 1); S->n = 1; lam[0] = 1; *vout = S->w[0]; return 0; }
+        t /= dd;
+        lam[0] = (real)(1.0 - t); lam[1] = (real)t;
+        *vout = dtor(dadd(A, dscl(ab, t)));
+        return 0;
+    }
+    if (S->n == 3) {
+        int used;
+        double la, lb, lc;
+        d3_t cv = tri_cp_dbl(D3(S->w[0]), D3(S->w[1]), D3(S->w[2]), &used, &la, &lb, &lc);
+        *vout = dtor(cv);
+        tri_compact_dbl(S, used, la, lb, lc, lam);
+        return 0;
+    }
+    static const int F[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
+    int bf = -1, bused = 7;
+    real best = (real)BT_LARGE;
+    double bla = 0, blb = 0, blc = 0;
+    d3_t bcv = {0, 0, 0};
+    for (int f = 0; f < 4; f++) {
+        d3_t A = D3(S->w[F[f][0]]), B = D3(S->w[F[f][1]]), C = D3(S->w[F[f][2]]), D = D3(S->w[F[f][3]]);
+        d3_t n = dcrs(dsub(B, A), dsub(C, A));
+        double sp = ddot(dscl(A, -1.0), n), sd = ddot(dsub(D, A), n);
+        if (sd * sd < 1e-30 || !(sp * sd < 0.0)) continue;
+        int used;
+        double la, lb, lc;
+        d3_t cv = tri_cp_dbl(A, B, C, &used, &la, &lb, &lc);
+        real d2 = (real)ddot(cv, cv);
+        if (bf < 0 || d2 < best) { best = d2; bf = f; bused = used; bla = la; blb = lb; blc = lc; bcv = cv; }
+    }
+    if (bf < 0) { lam[0] = lam[1] = lam[2] = lam[3] = 0; *vout = V(0, 0, 0); return 1; }
+    simplex T = *S;
+    for (int k = 0; k < 3; k++) { T.w[k] = S->w[F[bf][k]]; T.a[k] = S->a[F[bf][k]]; T.b[k] = S->b[F[bf][k]]; }
+    *S = T;
+    S->n = 3;
+    *vout = dtor(bcv);
+    tri_compact_dbl(S, bused, bla, blb, blc, lam);
+    return 0;
+}
+
+enum { GJK_SEPARATED = 0, GJK_FAR = 1, GJK_PENETRATING = 2 };
+#define GJK_NP_GAP 1e-4     /* largest duality gap (m) a no-progress stop may leave (kernel: gjk_lane) */
+enum { GJK_PLAIN = 0, GJK_LANE_RULE = 1, GJK_DOUBLE_SOLVE = 2 };
+
+/* GJK on the shape cores (btGjkPairDetector's loop).  mode GJK_LANE_RULE restates the kernel's
+ * lane path (gjk_lane, avr_kernel.hip): a step that makes no progress ends the GJK only when the
+ * duality gap at the final direction is closed (|v|^2 - v.w <= GJK_NP_GAP |v|, one more support
+ * query); otherwise the fp32 GJK has stalled on a thin simplex (its closest-point algebra cancelled),
+ * and the GJK is rerun from the start with that algebra in double (GJK_DOUBLE_SOLVE: the kernel's
+ * gjk_coop_d).  GJK_PLAIN: the sphere-hull point-core GJK (ph_step) and the closest-distance query
+ * (bb_closest), which the kernel runs without the rule.  In the fp64 build the rerun repeats the
+ * first pass's arithmetic exactly, so the rule changes nothing there. */
+static int gjk_mode(const wshape *A, const wshape *B, real maxdist2, v3 *pa, v3 *pb, real *dist, simplex *S, int mode, int *stalled) {
     v3 v = sub(A->t.p, B->t.p);
     if (len2(v) < R(1e-20)) v = V(1, 0, 0);
     S->n = 0;
@@ -628,10 +747,21 @@ static int gjk(const wshape *A, const wshape *B, real maxdist2, v3 *pa, v3 *pb, 
         if (S->n > 0 && vv - vw <= R(GJK_REL_EPS) * vv) break;
         S->w[S->n] = wv; S->a[S->n] = sa; S->b[S->n] = sb; S->n++;
         v3 nv;
-        if (simplex_closest(S, &nv, lam)) { status = GJK_PENETRATING; break; }
+        if (mode == GJK_DOUBLE_SOLVE ? simplex_closest_dbl(S, &nv, lam) : simplex_closest(S, &nv, lam)) { status = GJK_PENETRATING; break; }
         real nvv = len2(nv);
         if (nvv < R(1e-14) * (1 + len2(wv))) { status = GJK_PENETRATING; break; }
-        if (nvv >= prev) { v = nv; break; }
+        if (nvv >= prev) {
+            v = nv;
+            if (mode == GJK_LANE_RULE && it + 1 < GJK_MAX_IT) {     /* (the kernel's next iteration: its support query) */
+                v3 w2 = sub(support(A, scl(v, -1)), support(B, v));
+                real vv2 = len2(v), gap = vv2 - dot(v, w2);
+                if (gap > 0 && gap * gap > (R(GJK_NP_GAP) * R(GJK_NP_GAP)) * vv2) {
+                    *stalled = 1;
+                    return gjk_mode(A, B, maxdist2, pa, pb, dist, S, GJK_DOUBLE_SOLVE, stalled);
+                }
+            }
+            break;
+        }
         prev = nvv;
         v = nv;
     }
@@ -824,7 +954,12 @@ static int narrowphase(ws_t *o, const wshape *A, const wshape *B, real thr, v3 *
     real cd;
     simplex S;
     o->stats_gjk++;
-    int st = gjk(A, B, maxd * maxd, &pa, &pb, &cd, &S);
+    /* the kernel's lane rule for every general pair except sphere-hull (its point-core list) and
+     * the closest-distance query (o->np_plain) */
+    const int sph_hull = (ka == AVR_SPHERE && kb == AVR_HULL) || (ka == AVR_HULL && kb == AVR_SPHERE);
+    int stalled = 0;
+    int st = gjk_mode(A, B, maxd * maxd, &pa, &pb, &cd, &S, (sph_hull || o->np_plain) ? GJK_PLAIN : GJK_LANE_RULE, &stalled);
+    o->stats_stall += stalled;
     if (st == GJK_FAR) return 0;
     v3 n;
     real d;
@@ -1817,12 +1952,13 @@ EXPORT int avr_oracle_substep(avr_oracle *o, double dt) {
     return 0;
 }
 
-/* counters since creation: GJK runs, EPA runs, constraint rows built, PGS iterations run, PGS solves */
-EXPORT void avr_oracle_stats(avr_oracle *o, long long *out5) {
-    for (int k = 0; k < 5; k++) out5[k] = 0;
+/* counters since creation: GJK runs, EPA runs, constraint rows built, PGS iterations run, PGS solves,
+ * GJK runs rerun with the double simplex solve after a stall (gjk_mode) */
+EXPORT void avr_oracle_stats(avr_oracle *o, long long *out6) {
+    for (int k = 0; k < 6; k++) out6[k] = 0;
     for (int e = 0; e < o->n_envs; e++) {
-        out5[0] += o->ws[e].stats_gjk; out5[1] += o->ws[e].stats_epa; out5[2] += o->ws[e].stats_rows;
-        out5[3] += o->ws[e].stats_iters; out5[4] += o->ws[e].stats_solves;
+        out6[0] += o->ws[e].stats_gjk; out6[1] += o->ws[e].stats_epa; out6[2] += o->ws[e].stats_rows;
+        out6[3] += o->ws[e].stats_iters; out6[4] += o->ws[e].stats_solves; out6[5] += o->ws[e].stats_stall;
     }
 }
 

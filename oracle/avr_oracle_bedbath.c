@@ -80,6 +80,7 @@ static real bb_closest(const model *m, real *st, ws_t *w) {
     const real *f = st + S_FREE;
     tf ttf; ttf.p = ld3(f); ttf.q = ldq(f + 3);
     real thr = R(m->d.closest_distance), dmin = R(1e30);
+    w->np_plain = 1;        /* the kernel's bb_closest reruns stalled pairs in fp32: no stall rule */
     for (int b = 0; b < m->d.n_bodies; b++) {
         if (m->d.body_kind[b] != AVR_BODY_HUMAN) continue;
         const real *h = st + S_HUMAN + 7 * m->d.body_index[b];
@@ -95,6 +96,7 @@ static real bb_closest(const model *m, real *st, ws_t *w) {
             }
         }
     }
+    w->np_plain = 0;
     return dmin < R(1e29) ? dmin : thr;
 }
 

@@ -37,6 +37,16 @@ static inline v3 scl(v3 a, real s) { return V(a.x * s, a.y * s, a.z * s); }
 static inline real dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline v3 crs(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 static inline real len(v3 a) { return sqrt(dot(a, a)); }
+/* the fused multiply-adds of the kernel's cloth sub-step (avr_dressing.hip dotF / lenF / axpyF), at
+ * the same sites and in the same order, so that the fp32 build rounds as the kernel does */
+#ifdef AVR_ORACLE_FLOAT
+#define FMA(a, b, c) fmaf(a, b, c)
+#else
+#define FMA(a, b, c) fma(a, b, c)
+#endif
+static inline real dotF(v3 a, v3 b) { return FMA(a.z, b.z, FMA(a.y, b.y, a.x * b.x)); }
+static inline real lenF(v3 a) { return sqrt(dotF(a, a)); }
+static inline v3 axpyF(v3 a, real s, v3 y) { return V(FMA(a.x, s, y.x), FMA(a.y, s, y.y), FMA(a.z, s, y.z)); }
 static inline v3 ld3(const real *p) { return V(p[0], p[1], p[2]); }
 static inline void st3(real *p, v3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
 static inline qt Q(real x, real y, real z, real w) { qt r = {x, y, z, w}; return r; }
@@ -97,21 +107,21 @@ static void chain_fk(const chain_t *c, const real *q7, v3 *tool_p, qt *tool_q, v
 /* closest point on segment ab to x */
 static v3 seg_closest(v3 a, v3 b, v3 x) {
     const v3 ab = sub(b, a);
-    const real l2 = dot(ab, ab);
-    real t = l2 > 0 ? dot(sub(x, a), ab) / l2 : 0;
+    const real l2 = dotF(ab, ab);
+    real t = l2 > 0 ? dotF(sub(x, a), ab) / l2 : 0;
     t = t < 0 ? 0 : t > 1 ? 1 : t;
-    return add(a, scl(ab, t));
+    return axpyF(ab, t, a);
 }
 
 /* penalty contact force on a particle at x with velocity v against a sphere at c (radius r) */
 static v3 contact(v3 x, v3 v, v3 c, real r) {
     const v3 d = sub(x, c);
-    const real dist = len(d);
+    const real dist = lenF(d);
     const real pen = r + R(AVR_DR_THICK) - dist;
     if (!(pen > 0) || !(dist > R(1e-9))) return V(0, 0, 0);
     const v3 n = scl(d, 1 / dist);
-    const real vn = dot(v, n);
-    const real f = R(AVR_DR_K_CONTACT) * pen - R(AVR_DR_C_CONTACT) * (vn < 0 ? vn : 0);
+    const real vn = dotF(v, n);
+    const real f = FMA(R(AVR_DR_K_CONTACT), pen, -(R(AVR_DR_C_CONTACT) * (vn < 0 ? vn : 0)));
     return scl(n, f);
 }
 
@@ -140,11 +150,11 @@ static real cloth_substep(v3 *x, v3 *v, const v3 *tgt, const real *geo, real dt)
             const real ks = s < 4 ? (s < 2 ? R(AVR_DR_K_STRUCT) : R(AVR_DR_K_STRUCT)) : s < 8 ? R(AVR_DR_K_SHEAR) : R(AVR_DR_K_BEND);
             const real L0 = s < 2 ? L_ring : s < 4 ? L_ax : s < 8 ? L_sh : s < 10 ? L_ring2 : 2 * L_ax;
             const v3 d = sub(x[o], x[i]);
-            const real l = len(d);
+            const real l = lenF(d);
             if (!(l > R(1e-9))) continue;
             const v3 u = scl(d, 1 / l);
-            const real fs = ks * (l - L0) + R(AVR_DR_DAMP) * dot(sub(v[o], v[i]), u);
-            f = add(f, scl(u, fs));
+            const real fs = FMA(ks, l - L0, R(AVR_DR_DAMP) * dotF(sub(v[o], v[i]), u));
+            f = axpyF(u, fs, f);
         }
         /* penalty contact with the left arm: capsules (upper arm, forearm), hand sphere, cloth spheres */
         v3 fc = V(0, 0, 0);
@@ -154,7 +164,7 @@ static real cloth_substep(v3 *x, v3 *v, const v3 *tgt, const real *geo, real dt)
         fc = add(fc, contact(x[i], v[i], ld3(geo + 0), geo[27]));
         fc = add(fc, contact(x[i], v[i], ld3(geo + 3), geo[28]));
         fc = add(fc, contact(x[i], v[i], ld3(geo + 6), geo[29]));
-        ftot += len(fc);
+        ftot += lenF(fc);
         F[i] = add(f, fc);
     }
     for (int i = 0; i < NS; i++) {                 /* the held cuff: kinematic */
@@ -162,8 +172,8 @@ static real cloth_substep(v3 *x, v3 *v, const v3 *tgt, const real *geo, real dt)
         x[i] = tgt[i];
     }
     for (int i = NS; i < NP; i++) {
-        v[i] = add(v[i], scl(F[i], dt / m));
-        x[i] = add(x[i], scl(v[i], dt));
+        v[i] = axpyF(F[i], dt / m, v[i]);
+        x[i] = axpyF(v[i], dt, x[i]);
     }
     return ftot;
 }

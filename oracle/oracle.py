@@ -120,7 +120,7 @@ class Oracle:
             raise RuntimeError('substep failed')
 
     def stats(self):
-        s = np.zeros(5, np.int64)      # GJK runs, EPA runs, rows built, PGS iterations, PGS solves
+        s = np.zeros(6, np.int64)      # GJK runs, EPA runs, rows built, PGS iterations, PGS solves, stall reruns
         self.lib.avr_oracle_stats(self.h, s.ctypes.data)
         return s
 

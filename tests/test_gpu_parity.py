@@ -188,53 +188,65 @@ def test_contact_regime_episode_statistics_vs_fp64_oracle(lib_and_scene):
 
 def test_bench_launch_shape_sampled_envs_match_oracle(lib_and_scene):
     """The bench's launch shape -- 4096 envs in four concurrent env groups, graph replay -- against
-    the fp64 oracle on 32 sampled envs (every group, block boundaries included): settle + 5 gym
-    steps, per step the joint angles, the observation, the reward and done.  A pick whose own
-    oracle moves by more than 1e-3 under a 1e-4 perturbation of its actions sits at a bifurcation
-    (food bouncing in the spoon) and is only checked for finiteness; the calm picks are held to
-    1e-3 rad, obs 2e-3 (the force word relatively, 5e-2), reward 2e-3 relative, up to two picks
-    (as the PR2 tasks' launch-shape test, test_pr2_launch_shape.py)."""
-    from avr import _lib
+    the fp64 oracle on 32 sampled envs (every group, block boundaries included) over 5 gym steps:
+    per step the joint angles, the observation, the reward and done.  The envs start from the fp64
+    oracle's settled reset states (the 100 food-drop frames are chaotic in fp64 itself: a 1e-6
+    perturbation before them moves the arm by ~5e-4 rad; the settle's own parity is the golden
+    fixture's), so the 5 steps are what is compared.  Two 16-member oracle ensembles started from
+    1e-6 perturbations (joint angles, free-body positions) classify the picks (tests/ensemble_util.py):
+    a pick is chaotic only if the fp64 ensemble itself moves by >= 5e-4 rad; calm picks are held to
+    1e-3 rad, obs 2e-3 (the force word relatively, 5e-2), reward 2e-3 relative; chaotic picks to
+    twice the larger of the fp32 and fp64 ensembles' deviations.  No pick is excepted, none is
+    checked for finiteness only (measured on the CPU: every pick calm, both ensembles within 1e-4
+    rad of the fp64 oracle)."""
+    from avr import _lib, _abi as ABI
+    from ensemble_util import ensembles, launch_shape_verdict
     A, md = lib_and_scene
     E = 4096
     S_pool = reset_states(A, md, range(256), 'random')
+    o = oracle(md, 256)
+    o.set_state(S_pool.astype(np.float64))
+    o.settle(100)
+    S_pool = o.get_state().astype(np.float32)         # the fp64 oracle's settled reset states
     S = np.tile(S_pool, (E // 256, 1))
-    sim = make_sim(md, E)
-    assert sim.env_groups() == 4
-    sim.set_state(S)
-    sim.settle(100)
     pick = np.array([0, 1, 31, 32, 33, 511, 512, 1023, 1024, 1025, 1055, 1056, 1500, 2047, 2048, 2049, 2079, 2080,
                      2500, 3071, 3072, 3073, 3103, 3104, 3500, 3800, 4000, 4063, 4064, 4090, 4094, 4095])
     n = len(pick)
-    o, op = oracle(md, n), oracle(md, n)
-    for x in (o, op):
-        x.set_state(S[pick].astype(np.float64))
-        x.settle(100)
-    nd = dofs(md)
+    L = md.layout
+    nd = dofs(md).stop
+
+    def perturb(X, rng):
+        Y = X.astype(np.float64).copy()
+        Y[:, :nd] += 1e-6 * rng.standard_normal((len(Y), nd))
+        for f in range(ABI.MAX_FREE):
+            b = ABI.S_FREE + ABI.FB_WORDS * f
+            Y[:, b:b + 3] += 1e-6 * rng.standard_normal((len(Y), 3))
+        return Y
+    acts = lambda t: _lib.random_actions(1001, np.arange(E), t)[pick]
+    dev, _, traj = ensembles(md, S[pick], L, nd, perturb, 5, acts, None, seed=4)
+    sim = make_sim(md, E)
+    assert sim.env_groups() == 4
+    sim.set_state(S)
     od = 24                                  # the kinematic part of the 25-word obs; word 24 is the spoon force
     w = dict(dq=np.zeros(n), obs=np.zeros(n), rew=np.zeros(n), force=np.zeros(n))
-    spread = np.zeros(n)
-    rng = np.random.default_rng(4)
     for t in range(5):
         a = _lib.random_actions(1001, np.arange(E), t)
         ob, r, d, i = sim.step(a)
-        oc, rc, dc, ic = o.step(a[pick])
-        op.step((a[pick] + 1e-4 * rng.standard_normal((n, a.shape[1]))).astype(np.float32))
-        G, C = sim.get_state()[pick], o.get_state()
-        w['dq'] = np.maximum(w['dq'], np.abs(G[:, nd] - C[:, nd]).max(1))
+        oc, rc, dc, ic, C = traj[t]
+        G = sim.get_state()[pick]
+        w['dq'] = np.maximum(w['dq'], np.abs(G[:, :nd] - C[:, :nd]).max(1))
         w['obs'] = np.maximum(w['obs'], np.abs(ob[pick, :od] - oc[:, :od]).max(1))
         w['rew'] = np.maximum(w['rew'], np.abs(r[pick] - rc) / (1.0 + np.abs(rc)))
         w['force'] = np.maximum(w['force'], np.abs(ob[pick, od] - oc[:, od]) / (1.0 + np.abs(oc[:, od])))
-        spread = np.maximum(spread, np.abs(op.get_state()[:, nd] - C[:, nd]).max(1))
         assert np.array_equal(d[pick], dc)
-        assert np.all(np.isfinite(ob[pick])) and np.all(np.isfinite(r[pick]))
     sim.close()
-    calm = spread < 1e-3
-    ok = (w['dq'] < 1e-3) & (w['obs'] < 2e-3) & (w['rew'] < 2e-3) & (w['force'] < 5e-2)
-    print('FeedingJaco launch shape', {k: float(v[calm & ok].max()) for k, v in w.items()}, 'sensitive picks', int((~calm).sum()),
-          'calm picks off', [(int(pick[k]), float(w['dq'][k]), float(w['obs'][k])) for k in np.nonzero(calm & ~ok)[0]])
-    assert calm.sum() >= n // 2, spread
-    assert (calm & ~ok).sum() <= 2, w
+    tol = dict(dq=1e-3, obs=2e-3, rew=2e-3, force=5e-2)
+    ok, chaotic, bound = launch_shape_verdict(w, dev, tol, n // 2)
+    print('FeedingJaco launch shape: calm picks max GPU dev', {k: float(v[~chaotic].max()) for k, v in w.items()},
+          'chaotic picks (pick, fp64 ens, fp32 ens, GPU) dq',
+          [(int(pick[k]), float(dev['f64']['dq'][k]), float(dev['f32']['dq'][k]), float(w['dq'][k])) for k in np.nonzero(chaotic)[0]])
+    print('  failing picks', [(int(pick[k]), {q: (float(w[q][k]), float(bound[q][k])) for q in tol}) for k in np.nonzero(~ok)[0]])
+    assert ok.all()
 
 
 def _remove_food_and_bowl(S):
@@ -577,11 +589,14 @@ def test_coop_cap_bounds_a_pathological_env(lib_and_scene):
 def test_coop_capped_env_drift_vs_oracle(lib_and_scene):
     """The arm driven into the wheelchair's VHACD hulls (tests/golden/feeding_arm_in_wheelchair.npy)
     for 20 gym steps: on the GPU with the EPA budget (capped: 4 EPAs per sub-step once the overload
-    has lasted 20 sub-steps) and without it (every penetrating pair solved, as the oracle does), on
-    the fp64 oracle, and on an ensemble of fp32 oracles started from rounding-level perturbations
-    (1e-6 rad on the joint angles).  The state is ill-conditioned (56 penetrating contact points on
-    a light gripper): fp32 rounding alone carries the ensemble tenths of a radian from fp64 within
-    a few sub-steps.  Both GPU runs are held to twice the ensemble's largest deviation from fp64."""
+    has lasted 20 sub-steps) and without it (every penetrating pair solved, as the oracle does),
+    against the fp64 oracle, beside two 8-member ensembles started from 1e-6 rad perturbations of
+    the joint angles.  The state is ill-conditioned (56 penetrating contact points on a light
+    gripper).  Measured on the CPU: the fp64 ensemble spreads to 0.04 rad over the 20 steps
+    (physical sensitivity), the fp32 ensemble -- the kernel's arithmetic -- to 0.06-3.1 rad.
+    The unbudgeted GPU run has its own fixed bound, 0.3 rad (round 5 measured 0.11 rad; a
+    regression like round 4's 4.7 rad fails it); the budgeted run, a deliberate deviation, is
+    held to twice the fp32 ensemble's largest deviation."""
     from avr import _abi as ABI, _lib
     from oracle.oracle import Oracle
     A, md = lib_and_scene
@@ -596,28 +611,35 @@ def test_coop_capped_env_drift_vs_oracle(lib_and_scene):
     o64.set_state(bad.astype(np.float64))
     rng = np.random.default_rng(3)
     M = 8
-    ens = Oracle(md, M, 'f32')
-    ens.set_threads(8)
-    E = np.repeat(bad.reshape(1, -1).astype(np.float64), M, 0)
-    E[1:, ABI.S_Q:ABI.S_Q + 7] += 1e-6 * rng.standard_normal((M - 1, 7))
-    ens.set_state(E)
+    ens = {}
+    for prec in ('f32', 'f64'):
+        e = Oracle(md, M, prec)
+        e.set_threads(8)
+        X = np.repeat(bad.reshape(1, -1).astype(np.float64), M, 0)
+        X[1:, ABI.S_Q:ABI.S_Q + 7] += 1e-6 * rng.standard_normal((M - 1, 7))
+        e.set_state(X)
+        ens[prec] = e
     dq_cap = dq_full = 0.0
-    dq_ens = np.zeros(M)
+    dq_ens = {p: np.zeros(M) for p in ens}
     capped = False
     for t in range(20):
         a = _lib.random_actions(1001, np.arange(1), t)
-        sim.step(np.repeat(a, 2, 0)); o64.step(a); ens.step(np.repeat(a, M, 0))
-        G, C, X = sim.get_state(), o64.get_state(), ens.get_state()
+        sim.step(np.repeat(a, 2, 0)); o64.step(a)
+        G, C = sim.get_state(), o64.get_state()
+        for p, e in ens.items():
+            e.step(np.repeat(a, M, 0))
+            dq_ens[p] = np.maximum(dq_ens[p], np.abs(e.get_state()[:, :7] - C[0, :7]).max(1))
         dq_cap = max(dq_cap, float(np.abs(G[0, :7] - C[0, :7]).max()))
         dq_full = max(dq_full, float(np.abs(G[1, :7] - C[0, :7]).max()))
-        dq_ens = np.maximum(dq_ens, np.abs(X[:, :7] - C[0, :7]).max(1))
         fl = sim.get_flags()
         capped = capped or bool(fl[0] & 32)
         assert not fl[1] & 32
     sim.close()
     print('arm in wheelchair, max |dq| vs the fp64 oracle over 20 steps: GPU with the EPA budget %.3g rad, without %.3g rad; '
-          'fp32 ensemble %s (max %.3g)' % (dq_cap, dq_full, np.round(dq_ens, 3), dq_ens.max()))
+          'fp32 ensemble %s (max %.3g), fp64 ensemble %s (max %.3g)' % (
+              dq_cap, dq_full, np.round(dq_ens['f32'], 3), dq_ens['f32'].max(), np.round(dq_ens['f64'], 4), dq_ens['f64'].max()))
     assert capped
     assert np.all(np.isfinite(G))
-    assert dq_full <= 2.0 * dq_ens.max(), (dq_full, dq_ens)
-    assert dq_cap <= 2.0 * dq_ens.max(), (dq_cap, dq_ens)
+    assert dq_ens['f64'].max() < 0.3            # the bound below sits above the physics' own spread
+    assert dq_full <= 0.3, (dq_full, dq_ens)
+    assert dq_cap <= 2.0 * dq_ens['f32'].max(), (dq_cap, dq_ens)
