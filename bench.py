@@ -396,7 +396,11 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
                              dist_backend=args.dist_backend if world > 1 else None),
               'flagged_envs_by_bit': {fname: int(np.count_nonzero(flags & (1 << b))) for b, fname in enumerate(
                   ('nan_or_singular_mass', 'contact_pool_full', 'aabb_pairs_full', 'shape_pairs_full', 'nc_rows_full', 'coop_capped'))},
-              'reset_pool_sha1': pool_sha}
+              'reset_pool_sha1': pool_sha,
+              # the contact load at the end of the run (contact points per env), which sets the
+              # narrowphase, kernel-a and part-B work and traffic per env-step
+              'contact_points_per_env': {'mean': float(St[:, L.S_TASK + L.T_NCP].mean()), 'max': float(St[:, L.S_TASK + L.T_NCP].max()),
+                                         'envs_in_contact': float((St[:, L.S_TASK + L.T_NCP] > 0).mean())} if hasattr(L, 'T_NCP') else None}
     sim.close()
     if rank == 0 and world == 1 and cpu_seconds > 0:
         # the host threads this process may use: OMP_NUM_THREADS (the GPU box's CPU share, 16 per
