@@ -139,7 +139,7 @@ __constant__ int c_own[6] = {0, 2, 4, 5, 8, 10};          // owned slot k -> nei
 __constant__ int c_slot_own[12] = {0, -1, 1, -1, 2, 3, -1, -1, 4, -1, 5, -1};   // neighbour slot -> owned slot (-1: mirrored)
 __constant__ int c_mirror[12] = {1, 0, 3, 2, 7, 6, 5, 4, 9, 8, 11, 10};
 
-// the owned springs of particle i (ring k = i / NS): (u, fs) per owned slot into S[i][0..5]; fs
+// the owned springs of particle i (ring k = i / NS): (u, fs) per owned slot q into S[q][i]; fs
 // NaN marks a missing neighbour (past the last ring) or a degenerate spring (l <= 1e-9, which the
 // force sum skips)
 AVR_DI void dr_springs(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const float4 *Vv, float4 *S) {
@@ -164,7 +164,7 @@ AVR_DI void dr_springs(const DrModel &M, int i, v3 x, v3 v, const float4 *X, con
                 out = make_float4(u.x, u.y, u.z, fs);
             }
         }
-        S[i * 6 + q] = out;
+        S[q * DR_NP + i] = out;        // (slot-major: a lane's neighbours read consecutive float4s, no bank conflicts)
     }
 }
 
@@ -183,10 +183,10 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *S, const f
         const int q = c_slot_own[s];
         float4 e;
         if (q >= 0) {
-            e = S[i * 6 + q];
+            e = S[q * DR_NP + i];
         } else {        // the neighbour's owned spring back to i: -u, the same fs
             const int jj = (j + c_nb_dj[s] + DR_NS) % DR_NS;
-            e = S[(kk * DR_NS + jj) * 6 + c_slot_own[c_mirror[s]]];
+            e = S[c_slot_own[c_mirror[s]] * DR_NP + kk * DR_NS + jj];
             e.x = -e.x; e.y = -e.y; e.z = -e.z;
         }
         if (isnan(e.w)) continue;
