@@ -127,52 +127,10 @@ AVR_DI v3 dr_contact(v3 x, v3 v, v3 c, float r) {
 __constant__ int c_nb_dk[12] = {0, 0, 1, -1, 1, 1, -1, -1, 0, 0, 2, -2};
 __constant__ int c_nb_dj[12] = {1, -1, 0, 0, 1, -1, 1, -1, 2, -2, 0, 0};
 
-// Springs are evaluated once per spring, not once per endpoint.  Particle i owns its six springs
-// towards the neighbours of the "forward" directions (the oracle's neighbour slots 0, 2, 4, 5, 8,
-// 10); slot s's mirror (1, 3, 7, 6, 9, 11) is the same spring seen from the other end.  Seen from
-// there, d, u and the velocity difference are exact negations and l, 1 / l and the damping dot
-// product are bitwise equal (IEEE subtraction and negated products are sign-symmetric), so
-// u_mirror = -u and fs_mirror = fs exactly: the endpoint adds fmaf(-u, fs, f), which is what the
-// oracle's per-endpoint evaluation computes, and the forces keep the oracle's bits with half the
-// square roots, divisions and dot products.
-__constant__ int c_own[6] = {0, 2, 4, 5, 8, 10};          // owned slot k -> neighbour slot
-__constant__ int c_slot_own[12] = {0, -1, 1, -1, 2, 3, -1, -1, 4, -1, 5, -1};   // neighbour slot -> owned slot (-1: mirrored)
-__constant__ int c_mirror[12] = {1, 0, 3, 2, 7, 6, 5, 4, 9, 8, 11, 10};
-
-// the owned springs of particle i (ring k = i / NS): (u, fs) per owned slot q into S[q][i]; fs
-// NaN marks a missing neighbour (past the last ring) or a degenerate spring (l <= 1e-9, which the
-// force sum skips)
-AVR_DI void dr_springs(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const float4 *Vv, float4 *S) {
-    const float L_ring = M.l_ring, L_ax = (float)AVR_DR_SPACING, L_ring2 = M.l_ring2, L_sh = M.l_sh;
-    const int k = i / DR_NS, j = i % DR_NS;
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        const int s = c_own[q];
-        const int kk = k + c_nb_dk[s];
-        float4 out = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fc00000));
-        if (kk < DR_NR) {
-            const int jj = (j + c_nb_dj[s] + DR_NS) % DR_NS;
-            const int o = kk * DR_NS + jj;
-            const float ks = s < 4 ? (float)AVR_DR_K_STRUCT : s < 8 ? (float)AVR_DR_K_SHEAR : (float)AVR_DR_K_BEND;
-            const float L0 = s < 2 ? L_ring : s < 4 ? L_ax : s < 8 ? L_sh : s < 10 ? L_ring2 : 2.f * L_ax;
-            const float4 xo = X[o], vo = Vv[o];
-            const v3 d = sub(V(xo.x, xo.y, xo.z), x);
-            const float l = lenF(d);
-            if (l > 1e-9f) {
-                const v3 u = scl(d, 1.f / l);
-                const float fs = fmaf(ks, l - L0, (float)AVR_DR_DAMP * dotF(sub(V(vo.x, vo.y, vo.z), v), u));
-                out = make_float4(u.x, u.y, u.z, fs);
-            }
-        }
-        S[q * DR_NP + i] = out;        // (slot-major: a lane's neighbours read consecutive float4s, no bank conflicts)
-    }
-}
-
-// force on free particle i (ring k = i / NS >= 1) from the springs of the sub-step (S) and the
-// published positions / velocities: gravity, air drag, the 12 springs in the oracle's neighbour
-// order, then the penalty contacts with the arm
-AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *S, const float *geo, float &fc_mag) {
+// force on free particle i (ring k = i / NS >= 1) from the published positions / velocities
+AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const float4 *Vv, const float *geo, float &fc_mag) {
     const float m = M.pmass;
+    const float L_ring = M.l_ring, L_ax = (float)AVR_DR_SPACING, L_ring2 = M.l_ring2, L_sh = M.l_sh;
     const int k = i / DR_NS, j = i % DR_NS;
     v3 f = V(0, 0, (float)AVR_DR_GRAVITY * m);
     f = sub(f, scl(v, (float)AVR_DR_AIR));
@@ -180,17 +138,17 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *S, const f
     for (int s = 0; s < 12; s++) {
         const int kk = k + c_nb_dk[s];
         if (kk < 0 || kk >= DR_NR) continue;
-        const int q = c_slot_own[s];
-        float4 e;
-        if (q >= 0) {
-            e = S[q * DR_NP + i];
-        } else {        // the neighbour's owned spring back to i: -u, the same fs
-            const int jj = (j + c_nb_dj[s] + DR_NS) % DR_NS;
-            e = S[c_slot_own[c_mirror[s]] * DR_NP + kk * DR_NS + jj];
-            e.x = -e.x; e.y = -e.y; e.z = -e.z;
-        }
-        if (isnan(e.w)) continue;
-        f = axpyF(V(e.x, e.y, e.z), e.w, f);
+        const int jj = (j + c_nb_dj[s] + DR_NS) % DR_NS;
+        const int o = kk * DR_NS + jj;
+        const float ks = s < 4 ? (float)AVR_DR_K_STRUCT : s < 8 ? (float)AVR_DR_K_SHEAR : (float)AVR_DR_K_BEND;
+        const float L0 = s < 2 ? L_ring : s < 4 ? L_ax : s < 8 ? L_sh : s < 10 ? L_ring2 : 2.f * L_ax;
+        const float4 xo = X[o], vo = Vv[o];
+        const v3 d = sub(V(xo.x, xo.y, xo.z), x);
+        const float l = lenF(d);
+        if (!(l > 1e-9f)) continue;
+        const v3 u = scl(d, 1.f / l);
+        const float fs = fmaf(ks, l - L0, (float)AVR_DR_DAMP * dotF(sub(V(vo.x, vo.y, vo.z), v), u));
+        f = axpyF(u, fs, f);
     }
     v3 fc = V(0, 0, 0);
     fc = add(fc, dr_contact(x, v, seg_closest(ld3(geo + 12), ld3(geo + 15), x), geo[18]));
@@ -268,8 +226,8 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                                                             long long t, float *__restrict__ obs, float *__restrict__ rew,
                                                             unsigned char *__restrict__ done, float *__restrict__ info, int n_envs) {
     __shared__ float4 X[DR_NP], Vv[DR_NP];
-    __shared__ float4 Sp[DR_NP * 6];       // the owned springs of the sub-step (dr_springs)
     __shared__ float red[DR_NP];
+    __shared__ float4 Qc[AVR_DR_CSUB];         // the cuff's orientation at each cloth sub-step of a robot sub-step
     __shared__ FkLds fk;
     const int env = blockIdx.x;
     if (env >= n_envs || (mask && !mask[env])) return;
@@ -318,18 +276,23 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
             v3 tp1;
             qt tq1;
             dr_fk(m, q, tp1, tq1, torso, fk);
+            // the cuff orientations of the robot sub-step's cloth sub-steps, one per lane, side by
+            // side: the normalisation's double-precision square root and division run once per cloth
+            // sub-step in parallel, not on the pinned lanes' path of every cloth sub-step (the values
+            // are the same; the barrier at the top of the cloth sub-step publishes them)
+            if (lane < AVR_DR_CSUB) {
+                const qt qq = qnlerp(tq0, tq1, (float)(lane + 1) / AVR_DR_CSUB);
+                Qc[lane] = make_float4(qq.x, qq.y, qq.z, qq.w);
+            }
             for (int cs = 0; cs < AVR_DR_CSUB; cs++) {
                 X[i0] = make_float4(x0.x, x0.y, x0.z, 0.f);
                 X[i1] = make_float4(x1.x, x1.y, x1.z, 0.f);
                 Vv[i0] = make_float4(v0.x, v0.y, v0.z, 0.f);
                 Vv[i1] = make_float4(v1.x, v1.y, v1.z, 0.f);
                 __syncthreads();
-                dr_springs(m, i0, x0, v0, X, Vv, Sp);
-                dr_springs(m, i1, x1, v1, X, Vv, Sp);
-                __syncthreads();
                 float fm0 = 0.f, fm1 = 0.f;
-                const v3 F0 = pinned ? V(0, 0, 0) : dr_force(m, i0, x0, v0, Sp, geo, fm0);
-                const v3 F1 = dr_force(m, i1, x1, v1, Sp, geo, fm1);
+                const v3 F0 = pinned ? V(0, 0, 0) : dr_force(m, i0, x0, v0, X, Vv, geo, fm0);
+                const v3 F1 = dr_force(m, i1, x1, v1, X, Vv, geo, fm1);
                 // the dressing forces' sum over the free particles, at the step's last cloth sub-step
                 // (summed in particle order, as the oracle's loop)
                 const bool last = f == frames - 1 && r == AVR_DR_RSUB - 1 && cs == AVR_DR_CSUB - 1;
@@ -338,7 +301,8 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
                 if (pinned) {
                     const float s = (float)(cs + 1) / AVR_DR_CSUB;
                     const v3 p = add(tp0, scl(sub(tp1, tp0), s));
-                    const qt qq = qnlerp(tq0, tq1, s);
+                    const float4 qv = Qc[cs];
+                    const qt qq = Q(qv.x, qv.y, qv.z, qv.w);
                     const v3 tg = add(p, qrot(qq, ringl));
                     v0 = scl(sub(tg, x0), 1.f / dtc);
                     x0 = tg;

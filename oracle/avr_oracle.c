@@ -258,6 +258,7 @@ typedef struct {
     real oldcp[K_MAX_CONTACTS * AVR_CP_WORDS];
     long long stats_gjk, stats_epa, stats_rows, stats_iters, stats_solves, stats_stall;
     int np_plain;          /* narrowphase without the lane GJK's stall rule (bb_closest) */
+    int island_exit;       /* test-only: the PGS residual exit per island (solve_islands) */
 } ws_t;
 
 typedef struct avr_oracle {
@@ -1418,7 +1419,81 @@ static real resolve(const model *m, ws_t *w, row_t *r) {
     return res * res;
 }
 
+/* Test-only variant (avr_oracle_set_island_exit): the residual exit per island instead of per env.
+ * An island is a connected set of bodies through the rows -- nodes: the robot multibody, the human
+ * chain, each free body (static geometry joins nothing).  Each island leaves the PGS after its own
+ * first iteration whose largest squared row residual is within the threshold; the other islands go
+ * on.  This is what Bullet does when it solves islands as separate groups (splitIslands with
+ * islands of at least minimumSolverBatchSize rows, btSimulationIslandManager [ext]); the build's
+ * default treats the env as one group (tests/test_oracle_kat.py bounds the difference). */
+static int isl_find(int *par, int x) { while (par[x] != x) x = par[x] = par[par[x]]; return x; }
+static int row_node(const model *m, int kind, int idx) {
+    if (kind == 1) return idx < m->nl_robot ? 0 : 1;
+    if (kind == 2) return 2 + idx;
+    return -1;
+}
+static void solve_islands(const model *m, ws_t *w) {
+    int iters = m->d.solver_iterations;
+    w->stats_solves++;
+    enum { NN = 2 + K_MAX_FREE };
+    int par[NN];
+    for (int k = 0; k < NN; k++) par[k] = k;
+    for (int r = 0; r < w->nrows; r++) {
+        const int a = row_node(m, w->rows[r].kindA, w->rows[r].idxA), b = row_node(m, w->rows[r].kindB, w->rows[r].idxB);
+        if (a >= 0 && b >= 0) par[isl_find(par, a)] = isl_find(par, b);
+    }
+    int isl[MAX_ROWS];
+    for (int r = 0; r < w->nrows; r++) {
+        const int a = row_node(m, w->rows[r].kindA, w->rows[r].idxA), b = row_node(m, w->rows[r].kindB, w->rows[r].idxB);
+        isl[r] = isl_find(par, a >= 0 ? a : b >= 0 ? b : 0);
+    }
+    int done[NN] = {0};
+    for (int it = 0; it < iters; it++) {
+        real res[NN];
+        for (int k = 0; k < NN; k++) res[k] = 0;
+#define RESI(r, x) do { const real r_ = (x); if (r_ > res[isl[r]]) res[isl[r]] = r_; } while (0)
+        for (int j = 0; j < w->n_nc; j++) {
+            int k = (it & 1) ? j : w->n_nc - 1 - j;
+            const int r = w->nc_idx[k];
+            if (!done[isl[r]]) RESI(r, resolve(m, w, &w->rows[r]));
+        }
+        for (int j = 0; j < w->n_nrm; j++) {
+            const int r = w->nrm_idx[j];
+            if (!done[isl[r]]) RESI(r, resolve(m, w, &w->rows[r]));
+        }
+        for (int j = 0; j < w->n_fr; j++) {
+            const int r = w->fr_idx[j];
+            row_t *f = &w->rows[r];
+            real nimp = w->rows[w->nrm_idx[f->normal_row]].imp;
+            if (nimp > 0 && !done[isl[r]]) {
+                f->lo = -f->fric * nimp;
+                f->hi = f->fric * nimp;
+                RESI(r, resolve(m, w, f));
+            }
+        }
+        for (int j = 0; j < w->n_tor; j++) {
+            const int r = w->tor_idx[j];
+            row_t *f = &w->rows[r];
+            real nimp = w->rows[w->nrm_idx[f->normal_row]].imp;
+            if (nimp > 0 && !done[isl[r]]) {
+                f->lo = -f->fric * nimp;
+                f->hi = f->fric * nimp;
+                RESI(r, resolve(m, w, f));
+            }
+        }
+#undef RESI
+        w->stats_iters++;
+        int all = 1;
+        for (int r = 0; r < w->nrows; r++) {
+            if (!done[isl[r]] && res[isl[r]] <= R(BT_RESIDUAL_THRESHOLD)) done[isl[r]] = 1;
+        }
+        for (int r = 0; r < w->nrows; r++) all &= done[isl[r]];
+        if (all) break;
+    }
+}
+
 static void solve(const model *m, ws_t *w) {
+    if (w->island_exit) { solve_islands(m, w); return; }
     int iters = m->d.solver_iterations;
     w->stats_solves++;
 #define RES(x) do { const real r_ = (x); if (r_ > res) res = r_; } while (0)
@@ -1964,6 +2039,10 @@ EXPORT void avr_oracle_stats(avr_oracle *o, long long *out6) {
 
 /* threads used by avr_oracle_step / avr_oracle_settle (OpenMP over envs; 1 = serial) */
 EXPORT void avr_oracle_set_threads(avr_oracle *o, int n) { o->threads = n > 0 ? n : 1; }
+/* test-only: the PGS residual exit per island instead of per env (solve_islands) */
+EXPORT void avr_oracle_set_island_exit(avr_oracle *o, int on) {
+    for (int e = 0; e < o->n_envs; e++) o->ws[e].island_exit = on;
+}
 
 /* geometry query for tests: narrowphase between shapes sa (on body pose pa[7]) and sb (pb[7]) */
 EXPORT int avr_oracle_narrowphase(avr_oracle *o, int sa, const double *pa, int sb, const double *pb, double thr, double *out7) {

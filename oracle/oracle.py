@@ -39,6 +39,7 @@ def _load(precision, task=0):
         return lib
     lib.avr_oracle_substep.argtypes = [vp, C.c_double]
     lib.avr_oracle_stats.argtypes = [vp, vp]
+    lib.avr_oracle_set_island_exit.argtypes = [vp, C.c_int]
     lib.avr_oracle_narrowphase.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_double, vp]
     lib.avr_oracle_robot_fk.argtypes = [vp, C.c_int, vp]
     lib.avr_oracle_robot_self_contact.argtypes = [vp, C.c_int, vp, vp]
@@ -118,6 +119,10 @@ class Oracle:
     def substep(self, dt):
         if self.lib.avr_oracle_substep(self.h, float(dt)):
             raise RuntimeError('substep failed')
+
+    def set_island_exit(self, on=True):
+        """Test-only: the PGS residual exit per island instead of per env (solve_islands)."""
+        self.lib.avr_oracle_set_island_exit(self.h, int(bool(on)))
 
     def stats(self):
         s = np.zeros(6, np.int64)      # GJK runs, EPA runs, rows built, PGS iterations, PGS solves, stall reruns

@@ -587,3 +587,64 @@ def test_pgs_iterations_used_per_task(scene, oracle_built):
     st = o.stats() - s0
     print('FeedingJaco: %.1f iterations per solve of 10' % (st[3] / st[4]))
     assert st[4] == 10 and st[3] <= 10 * 10
+
+
+def _pr2_contact_pool(task):
+    """Reset and contact states of a PR2 task on the CPU (BedBathing's arm settle on the oracle)."""
+    from oracle.oracle import Oracle
+    if task == ABI.TASK_SCRATCH:
+        import scratch_util as U
+        A, md = U.scene()
+        S, meta = U.reset_states(A, md, range(16))
+        C = U.contact_states(A, md, S, meta)
+    else:
+        import bedbath_util as U
+        from avr import reset_bedbath as RBB
+        A = ABI.load_scene(ABI.TASK_BEDBATH)
+        md = ABI.ModelDesc(A)
+
+        def run(S, frames):
+            o = Oracle(md, len(S))
+            o.set_state(S)
+            o.settle(frames)
+            return o.get_state()
+        settled = RBB.settled_arms(A, md, runner=run)
+        S, _ = RBB.batch_reset_states(A, md, 1001, list(range(8)), attempts=6, iters=60, settled=settled)
+        C, _ = U.wipe_states(A, md, S, strict=False)
+    return A, md, np.concatenate([S, C]).astype(np.float64)
+
+
+@pytest.mark.parametrize('task', [ABI.TASK_SCRATCH, ABI.TASK_BEDBATH], ids=['ScratchItchPR2', 'BedBathingPR2'])
+def test_pgs_exit_per_env_vs_per_island(task, oracle_built):
+    """The build leaves the PGS when the whole env has converged (one solve group per env, DESIGN
+    section 8); Bullet checks the residual per solve group, and splits islands into groups of at least
+    minimumSolverBatchSize rows ([ext], not pinned by the reference).  The oracle's island variant
+    (avr_oracle_set_island_exit: each island -- robot, human chain, each free body and what rows
+    connect them -- leaves on its own residual) bounds what the assumption moves: reset and contact
+    states, 5 gym steps of small random actions, both variants from the same states.  Measured
+    (ScratchItch): joint angles within 8e-5 rad, velocities 7e-4 rad/s, rewards 4e-5 -- an order of
+    magnitude inside the 1e-3 rad parity tolerance; BedBathing: identical (its wiping states form
+    one island: the wiper welded to the gripper, pressed on the arm)."""
+    from oracle.oracle import Oracle
+    from avr import _lib
+    A, md, P = _pr2_contact_pool(task)
+    L = ABI.LAYOUTS[task]
+    n = len(P)
+    nd = md.n_dof + int(A['hc_n'])
+    runs = []
+    for island in (False, True):
+        o = Oracle(md, n)
+        o.set_threads(8)
+        o.set_state(P)
+        o.set_island_exit(island)
+        traj = []
+        for t in range(5):
+            _, r, _, _ = o.step(_lib.random_actions(1001, np.arange(n), t) * 0.2)
+            traj.append((o.get_state(), r))
+        runs.append((traj, o.stats()))
+    dq = max(float(np.abs(a[0][:, :nd] - b[0][:, :nd]).max()) for a, b in zip(runs[0][0], runs[1][0]))
+    dqd = max(float(np.abs(a[0][:, L.S_QD:L.S_QD + nd] - b[0][:, L.S_QD:L.S_QD + nd]).max()) for a, b in zip(runs[0][0], runs[1][0]))
+    drew = max(float(np.abs(a[1] - b[1]).max()) for a, b in zip(runs[0][0], runs[1][0]))
+    print('PGS exit per env vs per island over 5 steps: |dq| %.3g rad, |dqd| %.3g rad/s, |dreward| %.3g; iterations per solve %.1f / %.1f'
+          % (dq, dqd, drew, runs[0][1][3] / runs[0][1][4], runs[1][1][3] / runs[1][1][4]))
+    assert dq < 2e-4 and dqd < 5e-3 and drew < 1e-3, (dq, dqd, drew)
