@@ -59,11 +59,21 @@ enum { DR_MODE_STEP = 0, DR_MODE_STEP_RANDOM = 1, DR_MODE_OBS = 2 };
 
 // COM frames of the tool link and of link 0: lane 0 walks the chain (link frames in LDS, parents
 // first), every lane then reads the two frames (wave-uniform values)
-struct FkLds { float4 lp[DR_MAXL], lq[DR_MAXL], out[3]; float q[8]; };
+struct FkLds { float4 lp[DR_MAXL], lq[DR_MAXL], out[3]; float2 sc[8]; };
 AVR_DI void dr_fk(const DrModel &m, const float *q7, v3 &tool_p, qt &tool_q, v3 &torso, FkLds &F) {
-    if (threadIdx.x == 0) {
+    // the arm joints' half-angle sines and cosines, one joint per lane side by side (the double
+    // sin / cos are the FK's long latency; lane 0's chain walk below then only reads them)
+    if (threadIdx.x < 7) {
+        float qa = 0.f;
 #pragma unroll
-        for (int i = 0; i < 7; i++) F.q[i] = q7[i];
+        for (int i = 0; i < 7; i++)
+            if (i == (int)threadIdx.x) qa = q7[i];
+        const float h = qa * 0.5f;
+        // (double sin / cos rounded once to float: what the fp32 oracle's sin() of a float returns)
+        F.sc[threadIdx.x] = make_float2((float)sin((double)h), (float)cos((double)h));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
         for (int i = 0; i < m.nl; i++) {
             const int p = m.parent[i];
             const float4 a = p < 0 ? make_float4(m.base_p[0], m.base_p[1], m.base_p[2], 0.f) : F.lp[p];
@@ -74,11 +84,9 @@ AVR_DI void dr_fk(const DrModel &m, const float *q7, v3 &tool_p, qt &tool_q, v3 
             qt tq = qmul(pq, ldq(m.jquat[i]));
             if (m.jtype[i] == AVR_J_REVOLUTE) {
                 const int aj = m.ajoint[i];
-                const float qa = aj >= 0 ? F.q[aj] : 0.f;
-                const float h = qa * 0.5f;
-                // (double sin / cos rounded once to float: what the fp32 oracle's sin() of a float returns)
-                const float sn = (float)sin((double)h);
-                tq = qmul(tq, Q(m.axis[i][0] * sn, m.axis[i][1] * sn, m.axis[i][2] * sn, (float)cos((double)h)));
+                const float2 c = aj >= 0 ? F.sc[aj] : make_float2(0.f, 1.f);     // (sin 0, cos 0)
+                const float sn = c.x;
+                tq = qmul(tq, Q(m.axis[i][0] * sn, m.axis[i][1] * sn, m.axis[i][2] * sn, c.y));
             }
             F.lp[i] = make_float4(tp.x, tp.y, tp.z, 0.f);
             F.lq[i] = make_float4(tq.x, tq.y, tq.z, tq.w);
