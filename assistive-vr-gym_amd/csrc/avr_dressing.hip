@@ -123,8 +123,14 @@ AVR_DI v3 seg_closest(v3 a, v3 b, v3 x) {
 
 AVR_DI v3 dr_contact(v3 x, v3 v, v3 c, float r) {
     const v3 d = sub(x, c);
-    const float dist = lenF(d);
-    const float pen = r + (float)AVR_DR_THICK - dist;
+    const float d2 = dotF(d, d);
+    const float cr = r + (float)AVR_DR_THICK;
+    // |d| >= r + thickness exactly (the fused form's sign is the exact one): sqrt(d2) then rounds
+    // to >= cr and pen <= 0, so the result is the zero vector the full test returns -- without the
+    // square root (a wave whose particles are all clear of the shape skips it)
+    if (fmaf(-cr, cr, d2) >= 0.f) return V(0, 0, 0);
+    const float dist = sqrtf(d2);
+    const float pen = cr - dist;
     if (!(pen > 0.f) || !(dist > 1e-9f)) return V(0, 0, 0);
     const v3 n = scl(d, 1.f / dist);
     const float vn = dotF(v, n);
@@ -159,8 +165,13 @@ AVR_DI v3 dr_force(const DrModel &M, int i, v3 x, v3 v, const float4 *X, const f
         f = axpyF(u, fs, f);
     }
     v3 fc = V(0, 0, 0);
-    fc = add(fc, dr_contact(x, v, seg_closest(ld3(geo + 12), ld3(geo + 15), x), geo[18]));
-    fc = add(fc, dr_contact(x, v, seg_closest(ld3(geo + 19), ld3(geo + 22), x), geo[25]));
+    // a capsule whose bounding sphere (segment midpoint, half length + radius + thickness, widened
+    // by 0.1 %: far above the rounding of the exact path) the particle is clear of contributes the
+    // zero vector: the projection's division and the square root are skipped
+    const bool far0 = dotF(sub(x, ld3(geo + 30)), sub(x, ld3(geo + 30))) > geo[33];
+    const bool far1 = dotF(sub(x, ld3(geo + 34)), sub(x, ld3(geo + 34))) > geo[37];
+    fc = add(fc, far0 ? V(0, 0, 0) : dr_contact(x, v, seg_closest(ld3(geo + 12), ld3(geo + 15), x), geo[18]));
+    fc = add(fc, far1 ? V(0, 0, 0) : dr_contact(x, v, seg_closest(ld3(geo + 19), ld3(geo + 22), x), geo[25]));
     fc = add(fc, dr_contact(x, v, ld3(geo + 9), geo[26]));
     fc = add(fc, dr_contact(x, v, ld3(geo + 0), geo[27]));
     fc = add(fc, dr_contact(x, v, ld3(geo + 3), geo[28]));
@@ -242,9 +253,17 @@ __global__ __launch_bounds__(64) void avr_dress_step_kernel(const DrModel *__res
     const DrModel &m = *mp;
     const int lane = threadIdx.x;
     float *st = state + (size_t)env * DR_W;
-    float geo[30];
+    float geo[38];
 #pragma unroll
     for (int i = 0; i < 30; i++) geo[i] = st[AVR_DR_S_GEO + i];
+    // the two capsules' bounding spheres (dr_force's prefilter): midpoint, squared radius
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const v3 a = ld3(geo + 12 + 7 * c), b = ld3(geo + 15 + 7 * c);
+        const v3 mid = scl(add(a, b), 0.5f);
+        const float R = (0.5f * len(sub(b, a)) + geo[18 + 7 * c] + (float)AVR_DR_THICK) * 1.001f + 1e-6f;
+        geo[30 + 4 * c] = mid.x; geo[31 + 4 * c] = mid.y; geo[32 + 4 * c] = mid.z; geo[33 + 4 * c] = R * R;
+    }
     float q[7], qt_[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) { q[i] = st[AVR_DR_S_Q + i]; qt_[i] = st[AVR_DR_S_QT + i]; }
