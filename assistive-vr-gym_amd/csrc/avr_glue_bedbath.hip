@@ -114,12 +114,22 @@ AVR_DI BBForces bb_forces(const KModel &m, EnvLDS &L, BBShared &B, const float *
 // min over the closest points of the tool and the human (bed_bathing.py:61): every tool shape
 // against every human shape of the env's gender, the signed distance of each pair (negative:
 // penetration) when within `closest_distance` (4.0); the narrowphase's lane path, then the
-// wave-cooperative path (EPA) for the penetrating pairs it hands on.  A stalled lane GJK (rc 4)
-// is rerun on the cooperative fp32 GJK, not the double one the step uses (gjk_coop_d): its
-// registers would take this kernel from 211 to 256 VGPRs (one wave per SIMD; BedBathing -5 %).  Poses: the state after the
-// step (the tool's body frame, the human slots).
-AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
+// wave-cooperative path (EPA) for the penetrating pairs it hands on.  A lane GJK that stalls with
+// an open duality gap (rc 4) is queued in the env's workspace (WS_BB_*) for avr_bb_stall_kernel,
+// which reruns it with the double simplex solve (gjk_coop_d, as the step's narrowphase does) and
+// finishes the reward: the double code here would take this kernel from 211 to 256 VGPRs.  Pairs
+// past the queue's capacity rerun on the fp32 cooperative GJK.  Poses: the state after the step
+// (the tool's body frame, the human slots).
+#define WS_BB_N 64          // int bits: queued stalled pairs
+#define WS_BB_DMIN 65       // the minimum over the other pairs (BIGF: none within reach)
+#define WS_BB_WIPED 66      // the step's wiped-target count
+#define WS_BB_PREFS 67      // the human-preference terms
+#define WS_BB_PAIRS 68      // int bits: sa | sb << 16 of each queued pair
+#define WS_BB_CAP (WS_WORDS - WS_BB_PAIRS)
+static_assert(WS_FW + 4 * MAXF <= WS_BB_N, "the stalled-pair queue lies past the velocity words");
+AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E, float *ws, int &nq) {
     const int lane = lane_id();
+    nq = 0;
     const int tb = m.tool_body, ts0 = gld(m.body_shape_start + tb), nts = gld(m.body_shape_count + tb);
     int hs0 = 1 << 30, hs1 = 0;
     for (int b = 0; b < m.nb; b++)
@@ -134,7 +144,7 @@ AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
     for (int c0 = 0; c0 < npair; c0 += 64) {
         const int idx = c0 + lane;
         int sa = -1, sb = -1;
-        bool coop = false;
+        bool coop = false, stall = false;
         if (idx < npair) {
             sb = hs0 + idx / nts;
             sa = ts0 + idx % nts;
@@ -151,8 +161,19 @@ AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
                 int nit, nk;
                 const int rc = narrowphase<false>(m, E, A, Bs, thr, nB, pB, d, nit, nk);
                 if (rc == 1) dmin = fminf(dmin, d);
-                else if (rc == 2 || rc == 4) coop = true;
+                else if (rc == 4) stall = true;
+                else if (rc == 2) coop = true;
             }
+        }
+        // stalled pairs into the queue, in order; past its capacity onto the fp32 cooperative path
+        {
+            int tot;
+            const int pre = ballot_prefix(stall, &tot);
+            if (stall) {
+                if (nq + pre < WS_BB_CAP) ws[WS_BB_PAIRS + nq + pre] = __int_as_float(sa | sb << 16);
+                else coop = true;
+            }
+            nq = min(nq + tot, WS_BB_CAP);
         }
         unsigned long long cm = __ballot(coop);
         while (cm) {
@@ -170,7 +191,14 @@ AVR_DI float bb_closest(const KModel &m, const EnvLDS &L, EpaBuf &E) {
         }
     }
     for (int o = 32; o > 0; o >>= 1) dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
-    return dmin < BIGF ? dmin : thr;      // (no pair within reach: the query's own bound)
+    return dmin;
+}
+
+// the reward (bed_bathing.py:64-66, env.py:412-448), from the closest distance and the step's
+// other terms; one expression for the task kernel and avr_bb_stall_kernel
+AVR_DI float bb_reward(const KModel &m, float dmin, float asq, float wiped, float prefs) {
+    dmin = dmin < BIGF ? dmin : m.closest_distance;      // (no pair within reach: the query's own bound)
+    return m.w_distance * (-dmin) + m.w_action * (-asq) + m.w_wipe * wiped + prefs;
 }
 
 // Task glue after the frames (BedBathingEnv.step after take_step, bed_bathing.py:54-75); SETTLE
@@ -193,7 +221,9 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
         if (lane == 0) L.st[S_TASK + T_ITER] += 1.f;
         SYNC();
         const BBForces F = bb_forces(m, L, B, gcp, env_cs(m, env) + CS_BTF);
-        const float dmin = bb_closest(m, L, E);
+        float *ws = env_ws(m, env);
+        int nq;
+        const float dmin = bb_closest(m, L, E, ws, nq);
         const tf tb = ldtf(L.st + S_FREE);
         const v3 tip = qrot(tb.q, V(m.tool_tip[0], m.tool_tip[1], m.tool_tip[2]));
         // tool link 1's linear velocity (getLinkState(tool, 1, computeLinkVelocity=True)[6], :55)
@@ -201,10 +231,15 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
         bb_observe(m, L, F.tool, obs + (size_t)env * K_OBS_DIM);
         // human_preferences (env.py:412-448), wiping branch: tool_force_at_target = tool force on the human
         const float prefs = m.w_velocity * (-ee_vel) + m.w_force_nontarget * (-(F.on_human - F.at)) + m.w_high_forces * (F.at < 10.f ? 0.f : -F.at);
-        const float asq = env_ws(m, env)[WS_ASQ];
-        const float r = m.w_distance * (-dmin) + m.w_action * (-asq) + m.w_wipe * (float)F.wiped + prefs;
+        const float asq = ws[WS_ASQ];
+        const float r = bb_reward(m, dmin, asq, (float)F.wiped, prefs);
         SYNC();
         if (lane == 0) {
+            // (avr_bb_stall_kernel finishes the reward of an env with queued pairs)
+            ws[WS_BB_N] = __int_as_float(nq);
+            ws[WS_BB_DMIN] = dmin;
+            ws[WS_BB_WIPED] = (float)F.wiped;
+            ws[WS_BB_PREFS] = prefs;
             const float succ = L.st[S_TASK + T_SUCCESS] + (float)F.wiped;
             L.st[S_TASK + T_SUCCESS] = succ;
             rew[env] = r;
@@ -226,4 +261,36 @@ __global__ __launch_bounds__(64) void avr_task_kernel(const KModel *__restrict__
     SYNC();
     for (int i = lane; i < S_CP; i += 64) gst[i] = L.st[i];
     prof_flush(m, L, env);
+}
+
+// The closest-distance pairs whose lane GJK stalled (bb_closest's queue), rerun with the
+// cooperative GJK's double simplex solve -- the step narrowphase's treatment of the same stop --
+// and the reward finished from the full minimum (bb_reward).  One wave per env; an env with an
+// empty queue (nearly all) returns at once.
+__global__ __launch_bounds__(64) void avr_bb_stall_kernel(const KModel *__restrict__ mp, float *__restrict__ state, float *__restrict__ rew,
+                                                          const unsigned char *__restrict__ mask, int env0, int n_envs) {
+    __shared__ EpaBuf E;
+    const int env = env0 + blockIdx.x;
+    if (env >= n_envs || (mask && !mask[env])) return;
+    const KModel &m = *mp;
+    float *ws = env_ws(m, env);
+    const int nq = __float_as_int(ws[WS_BB_N]);
+    if (nq <= 0) return;
+    const float *gst = state + (size_t)env * K_STATE_WORDS;
+    const tf ttf = ldtf(gst + S_FREE);
+    const float thr = m.closest_distance;
+    float dmin = ws[WS_BB_DMIN];
+    for (int k = 0; k < nq; k++) {
+        const int key = __float_as_int(ws[WS_BB_PAIRS + k]);
+        const int sa = key & 0xffff, sb = key >> 16;
+        const int bb = gld(m.shape_body + sb);
+        const WShape A = make_wshape(m, sa, ttf), Bs = make_wshape(m, sb, ldtf(gst + S_HUMAN + 7 * gld(m.body_index + bb)));
+        v3 nB = V(0, 0, 0), pB = V(0, 0, 0);
+        float d = 0.f;
+        int nit, nk;
+        const int rc = narrowphase<true>(m, E, A, Bs, thr, nB, pB, d, nit, nk, nullptr, true);
+        SYNC();
+        if (rc == 1) dmin = fminf(dmin, d);
+    }
+    if (lane_id() == 0) rew[env] = bb_reward(m, dmin, ws[WS_ASQ], ws[WS_BB_WIPED], ws[WS_BB_PREFS]);
 }

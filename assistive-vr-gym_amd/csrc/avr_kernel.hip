@@ -4218,6 +4218,10 @@ hipError_t avr_launch_step(const KModel *h_m, const KModel *d_m, float *state, c
     }
     mark(AVR_K_TASK);
     hipLaunchKernelGGL(avr_task_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, obs, rew, done, info, mask, mode, env0, env1);
+#if AVR_TASK == AVR_TASK_BEDBATH
+    if (mode == MODE_STEP || mode == MODE_STEP_RANDOM)      // stalled closest-distance pairs (avr_glue_bedbath.hip)
+        hipLaunchKernelGGL(avr_bb_stall_kernel, dim3(n_envs), dim3(64), 0, stream, d_m, state, rew, mask, env0, env1);
+#endif
     mark(-1);
     return hipGetLastError();
 }

@@ -726,8 +726,8 @@ enum { GJK_PLAIN = 0, GJK_LANE_RULE = 1, GJK_DOUBLE_SOLVE = 2 };
  * duality gap at the final direction is closed (|v|^2 - v.w <= GJK_NP_GAP |v|, one more support
  * query); otherwise the fp32 GJK has stalled on a thin simplex (its closest-point algebra cancelled),
  * and the GJK is rerun from the start with that algebra in double (GJK_DOUBLE_SOLVE: the kernel's
- * gjk_coop_d).  GJK_PLAIN: the sphere-hull point-core GJK (ph_step) and the closest-distance query
- * (bb_closest), which the kernel runs without the rule.  In the fp64 build the rerun repeats the
+ * gjk_coop_d).  GJK_PLAIN: the sphere-hull point-core GJK (ph_step), which the kernel runs without
+ * the rule.  In the fp64 build the rerun repeats the
  * first pass's arithmetic exactly, so the rule changes nothing there. */
 static int gjk_mode(const wshape *A, const wshape *B, real maxdist2, v3 *pa, v3 *pb, real *dist, simplex *S, int mode, int *stalled) {
     v3 v = sub(A->t.p, B->t.p);
@@ -955,8 +955,8 @@ static int narrowphase(ws_t *o, const wshape *A, const wshape *B, real thr, v3 *
     real cd;
     simplex S;
     o->stats_gjk++;
-    /* the kernel's lane rule for every general pair except sphere-hull (its point-core list) and
-     * the closest-distance query (o->np_plain) */
+    /* the kernel's lane rule for every general pair except sphere-hull (its point-core list);
+     * o->np_plain (unset by the shipped paths) switches it off for experiments */
     const int sph_hull = (ka == AVR_SPHERE && kb == AVR_HULL) || (ka == AVR_HULL && kb == AVR_SPHERE);
     int stalled = 0;
     int st = gjk_mode(A, B, maxd * maxd, &pa, &pb, &cd, &S, (sph_hull || o->np_plain) ? GJK_PLAIN : GJK_LANE_RULE, &stalled);

@@ -73,14 +73,14 @@ static int bb_forces(const model *m, real *st, const ws_t *w, real *tool_force, 
 }
 
 /* min over getClosestPoints(tool, human, distance=4.0)[8]: every tool shape against every human
- * shape of the env's gender, the narrowphase distance (EPA depth when penetrating) */
+ * shape of the env's gender, the narrowphase distance (EPA depth when penetrating); the GJK with
+ * the lane path's stall rule, as the kernel's bb_closest + avr_bb_stall_kernel run it */
 static real bb_closest(const model *m, real *st, ws_t *w) {
     int tb = m->d.spoon_body, ts0 = m->d.body_shape_start[tb], nts = m->d.body_shape_count[tb];
     int g = (int)st[S_TASK + T_GENDER];
     const real *f = st + S_FREE;
     tf ttf; ttf.p = ld3(f); ttf.q = ldq(f + 3);
     real thr = R(m->d.closest_distance), dmin = R(1e30);
-    w->np_plain = 1;        /* the kernel's bb_closest reruns stalled pairs in fp32: no stall rule */
     for (int b = 0; b < m->d.n_bodies; b++) {
         if (m->d.body_kind[b] != AVR_BODY_HUMAN) continue;
         const real *h = st + S_HUMAN + 7 * m->d.body_index[b];
@@ -96,7 +96,6 @@ static real bb_closest(const model *m, real *st, ws_t *w) {
             }
         }
     }
-    w->np_plain = 0;
     return dmin < R(1e29) ? dmin : thr;
 }
 
