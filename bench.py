@@ -218,10 +218,20 @@ def facade_bench(args):
     v.close()
 
 
+def progress(msg):
+    """A progress line on stderr (long GPU-box runs must keep writing: DESIGN.md section 6)."""
+    sys.stderr.write('[bench %.0fs] %s\n' % (time.perf_counter() - T_START, msg))
+    sys.stderr.flush()
+
+
+T_START = time.perf_counter()
+
+
 def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu_seconds):
     """Time `steps` gym steps of task `name` (E = args.envs per GPU) after `warmup` untimed ones;
     returns the JSON object of its bench line (cpu_baseline when cpu_seconds > 0)."""
     import numpy as np
+    progress('%s: reset pool' % name)
     import torch
     from avr import _abi as ABI, _lib
     from avr import dist as D
@@ -243,6 +253,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
     import hashlib
     pool_sha = hashlib.sha1(S_pool.astype(np.float32).tobytes()).hexdigest()[:12]
     S = np.tile(S_pool, ((E + pool - 1) // pool, 1))[:E]
+    progress('%s: reset pool ready (%d distinct states)' % (name, pool))
     sim = _lib.Sim(md, E, device=local, seed=1001, env_offset=base_id)
     sim.set_state(S.astype(np.float32))
     sim.settle(settle)
@@ -289,6 +300,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
                 D.gather_rollouts(roll.cpu() if gloo else roll, out=gathered)
 
     run_steps(0, warmup)
+    progress('%s: warmed up, timing %d steps' % (name, steps))
     sim.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -406,6 +418,7 @@ def run_task(name, args, steps, warmup, world, rank, local, dist, gloo, dev, cpu
         # the host threads this process may use: OMP_NUM_THREADS (the GPU box's CPU share, 16 per
         # GPU; os.cpu_count() reports the whole machine there), else every CPU of this host
         threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+        progress('%s: CPU baseline (%.0f s on %d threads)' % (name, cpu_seconds, threads))
         cb = cpu_baseline(name, md, A, cpu_seconds, max(1, threads), args.impairment)
         detail['cpu_baseline'] = cb
         out['cpu_baseline'] = {k: cb[k] for k in ('value', 'unit', 'cores', 'kind')}
