@@ -29,8 +29,11 @@ def step_kernels(task):
     if task == 'DressingJaco-v0':          # one launch per gym step (csrc/avr_dressing.hip)
         return {'avr_dress_step_kernel': 1}
     n = SUBSTEPS[task]
-    return {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n,
-            'avr_substep_a_kernel': n, 'avr_substep_b4_kernel': n, 'avr_task_kernel': 1}
+    k = {'avr_take_step_kernel': 1, 'avr_substep_pairs_kernel': n, 'avr_narrowphase_kernel': n,
+         'avr_substep_a_kernel': n, 'avr_substep_b4_kernel': n, 'avr_task_kernel': 1}
+    if task == 'BedBathingPR2-v0':        # the closest distance's stalled pairs (round 6, avr_glue_bedbath.hip)
+        k['avr_bb_stall_kernel'] = 1
+    return k
 
 
 STEP_KERNELS = step_kernels('FeedingJaco-v0')
