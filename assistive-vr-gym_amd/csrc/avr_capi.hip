@@ -35,7 +35,6 @@ struct avr_sim {
     // collision waves of another (envs are independent; fork/join events keep the handle's
     // stream the single point of ordering for callers)
     int ngroups;
-    bool g0own;                            // AVR_G0_STREAM=1: rollouts run group 0 on gstream[0] too (experiment)
     hipStream_t gstream[AVR_MAX_GROUPS];
     hipEvent_t fork_ev, join_ev[AVR_MAX_GROUPS];
     avr_evlog evlog;                       // per-kernel timing (avr_profile_kernels)
@@ -234,14 +233,6 @@ int avr_create(const avr_config *cfg, const avr_model_desc *d, avr_sim **out) {
         for (int i = 1; i < ng; i++) {      // (group 0 runs on the handle's stream)
             HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[i], hipStreamNonBlocking));
             HIPCHK(s, hipEventCreateWithFlags(&s->join_ev[i], hipEventDisableTiming));
-        }
-        // (experiment) a stream of its own for group 0's rollout graphs, created last so that it
-        // shares a hardware queue with the handle's stream, which is idle during a rollout
-        const char *g0 = getenv("AVR_G0_STREAM");
-        s->g0own = g0 && atoi(g0) && ng > 1;
-        if (s->g0own) {
-            HIPCHK(s, hipStreamCreateWithFlags(&s->gstream[0], hipStreamNonBlocking));
-            HIPCHK(s, hipEventCreateWithFlags(&s->join_ev[0], hipEventDisableTiming));
         }
     }
     KModel &k = s->km;
@@ -839,9 +830,6 @@ static int rollout_branches(avr_sim *s, int64_t t0, int32_t n, float *o, float *
 }
 
 
-// the stream of env group g in the per-group rollout (group 0: the handle's stream, or its own)
-static hipStream_t gstream_of(const avr_sim *s, int g) { return (g == 0 && !s->g0own) ? s->stream : s->gstream[g]; }
-
 static int rollout_per_group(avr_sim *s, int64_t t0, int32_t n, float *o, float *r, uint8_t *dn, float *in, int32_t stacked, const void *const *key) {
     const size_t E = (size_t)s->cfg.n_envs;
     avr_sim::RollSlot *rs = nullptr;
@@ -858,13 +846,13 @@ static int rollout_per_group(avr_sim *s, int64_t t0, int32_t n, float *o, float 
             // no replay of the graphs being dropped may still run (other handles, torch and RCCL
             // streams on the device are not waited for)
             HIPCHK(s, hipStreamSynchronize(s->stream));
-            for (int g = s->g0own ? 0 : 1; g < s->ngroups; g++) HIPCHK(s, hipStreamSynchronize(s->gstream[g]));
+            for (int g = 1; g < s->ngroups; g++) HIPCHK(s, hipStreamSynchronize(s->gstream[g]));
             drop_roll(*rs);
         }
         for (int c = 0; c < 2; c++)
             for (int p = 0; p < 2; p++)
                 for (int g = 0; g < s->ngroups; g++) {
-                    hipStream_t st = gstream_of(s, g);
+                    hipStream_t st = g == 0 ? s->stream : s->gstream[g];
                     const int e0 = group_bound(s, g), e1 = group_bound(s, g + 1);
                     long long *ct = s->km.step_t + g, *ck = s->km.step_t + AVR_MAX_GROUPS + g;
                     HIPCHK(s, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
@@ -890,16 +878,16 @@ static int rollout_per_group(avr_sim *s, int64_t t0, int32_t n, float *o, float 
     rs->used = ++s->gclock;
     HIPCHK(s, hipEventRecord(s->fork_ev, s->stream));
     for (int g = 0; g < s->ngroups; g++) {
-        hipStream_t st = gstream_of(s, g);
-        if (st != s->stream) HIPCHK(s, hipStreamWaitEvent(st, s->fork_ev, 0));
+        hipStream_t st = g == 0 ? s->stream : s->gstream[g];
+        if (g > 0) HIPCHK(s, hipStreamWaitEvent(st, s->fork_ev, 0));
         HIPCHK(s, avr_launch_set_step2(s->km.step_t + g, t0 - 1, s->km.step_t + AVR_MAX_GROUPS + g, -1, st));
     }
     int rep_ = 0;
     for (int k = 0; k + AVR_ROLL_CHUNK <= n; k += AVR_ROLL_CHUNK, rep_++)
-        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[0][rep_ & 1][g], gstream_of(s, g)));
+        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[0][rep_ & 1][g], g == 0 ? s->stream : s->gstream[g]));
     for (int k = n / AVR_ROLL_CHUNK * AVR_ROLL_CHUNK; k < n; k++, rep_++)
-        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[1][rep_ & 1][g], gstream_of(s, g)));
-    for (int g = s->g0own ? 0 : 1; g < s->ngroups; g++) {
+        for (int g = 0; g < s->ngroups; g++) HIPCHK(s, hipGraphLaunch(rs->pgexec[1][rep_ & 1][g], g == 0 ? s->stream : s->gstream[g]));
+    for (int g = 1; g < s->ngroups; g++) {
         HIPCHK(s, hipEventRecord(s->join_ev[g], s->gstream[g]));
         HIPCHK(s, hipStreamWaitEvent(s->stream, s->join_ev[g], 0));
     }
