@@ -32,6 +32,9 @@ VARIANTS = {
     'noepa': ('-DAVR_COOP_CAP=0', '-DAVR_COOP_PERSIST=0'),     # diagnostic only: no EPA / cooperative pair ever runs
     'noepawt': ('-DAVR_COOP_CAP=0', '-DAVR_COOP_PERSIST=0', '-DAVR_WAVETIME'),
     'coopk5': ('-DAVR_COOP_KERNEL=1',), 'np5': ('-DNP_WAVES=5',), 'dc2r5': ('-DB4_DC=2',),
+    # round 6: the AMDGPU machine scheduler's strategies
+    'mclause': ('-mllvm', '-amdgpu-sched-strategy=max-memory-clause'), 'ilp': ('-mllvm', '-amdgpu-sched-strategy=max-ilp'),
+    'itilp': ('-mllvm', '-amdgpu-sched-strategy=iterative-ilp'),
     'nonl': ('-DB4_NC_LDS=0',), 'fnl': ('-DB4_NC_LDS=1',), 'fnl12': ('-DB4_NC_LDS=1', '-DB4_LDSW=12288'), 'fnl11': ('-DB4_NC_LDS=1', '-DB4_LDSW=11264'), 'dnl2': ('-DB4_DNL=2',), 'noml': ('-DAVR_MINV_LAUNDER=0',),
 }
 
