@@ -60,3 +60,11 @@ for e in top:
               % (e, c_rows[e], ncp, nrob, kinds, [(int(sb[int(r[ABI.CP_SA])]), int(sb[int(r[ABI.CP_SB])])) for r in cp]))
     else:
         print('slow c_rows env %d: %.3g cycles/env-step, contacts %d' % (e, c_rows[e], ncp))
+# kernel a's slowest envs (the launch's tail): their phases against the median env's (last step)
+ka = p[:, 3] + p[:, 6] + p[:, 7] + p[:, 8]
+med = np.median(p, axis=0)
+cols = [(3, 'narrow+mf'), (17, 'coop'), (18, 'manifold'), (6, 'dyn'), (7, 'nc_rows'), (8, 'c_rows'), (24, 'M'), (25, 'chol'), (26, 'Minv'), (27, 'bias')]
+print('kernel a per env-step cycles: median %.3g, p99 %.3g, max %.3g' % (np.median(ka), np.percentile(ka, 99), ka.max()))
+print('  median env   ' + ' '.join('%s %.3g' % (nm, med[k]) for k, nm in cols))
+for e in np.argsort(-ka)[:8]:
+    print('  env %4d %.3g ncp %2d ' % (e, ka[e], int(St[e, L.S_TASK + L.T_NCP])) + ' '.join('%s %.3g' % (nm, p[e, k]) for k, nm in cols))
