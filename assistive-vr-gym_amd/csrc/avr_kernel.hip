@@ -389,11 +389,15 @@ AVR_DI void minv_mul(const EnvLDS &L, const float *x, float *y) {
     }
 }
 
-// the second robot endpoint of a row whose first endpoint's (J, M^-1 J^T) are in J, MJ: y = M^-1 x
-// row by row (minv_mul's sums), each y_i added to MJ_i and x_i y_i, x_i vq_i to den, rel in DoF
-// order, then x added to J -- the same roundings as storing the first endpoint's part and adding
-// the second's to it (add_robot) without the read-back of the first from memory
-AVR_DI void minv_mul_add(const EnvLDS &L, const float *x, float *J, float *MJ, float &den, float &rel) {
+// y = M^-1 x for an endpoint on articulated link `link`, within the link's block of M: a robot
+// link's Jacobian is zero on the human chain's DoFs (no chain DoF is an ancestor of a robot link)
+// and a chain link's on the robot's, and M^-1 is block diagonal with exact zeros off the blocks
+// (chol_solve_block), so the terms skipped are products of zeros that minv_mul would add to its
+// sums, leaving them unchanged: the same bits with K_ND^2 (robot) instead of MAXD^2 products -- the
+// serial tail of an env's contact rows when one lane holds a robot contact (FeedingJaco: 100 of 196
+// products per row; the PR2 tasks 196 of 576)
+template <int LO, int HI>
+AVR_DI void minv_mul_blk(const EnvLDS &L, const float *x, float *y) {
 #if AVR_MINV_LAUNDER
     int z = 0;
     asm volatile("" : "+v"(z));
@@ -403,14 +407,47 @@ AVR_DI void minv_mul_add(const EnvLDS &L, const float *x, float *J, float *MJ, f
 #endif
 #pragma unroll
     for (int i = 0; i < MAXD; i++) {
+        if (i < LO || i >= HI) { y[i] = 0.f; continue; }
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < MAXD; k++) s += Mv[i * MAXD + k] * x[k];
+        for (int k = LO; k < HI; k++) s += Mv[i * MAXD + k] * x[k];
+        y[i] = s;
+    }
+}
+AVR_DI void minv_mul_link(const KModel &m, const EnvLDS &L, int link, const float *x, float *y) {
+    if (link < m.nl) minv_mul_blk<0, K_ND>(L, x, y);
+    else minv_mul_blk<K_ND, MAXD>(L, x, y);
+}
+
+// the second robot endpoint of a row whose first endpoint's (J, M^-1 J^T) are in J, MJ: y = M^-1 x
+// row by row (minv_mul's sums), each y_i added to MJ_i and x_i y_i, x_i vq_i to den, rel in DoF
+// order, then x added to J -- the same roundings as storing the first endpoint's part and adding
+// the second's to it (add_robot) without the read-back of the first from memory
+template <int LO, int HI>
+AVR_DI void minv_mul_add_blk(const EnvLDS &L, const float *x, float *J, float *MJ, float &den, float &rel) {
+#if AVR_MINV_LAUNDER
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const float *Mv = &L.u.d.Minv[0][0] + z;
+#else
+    const float *Mv = &L.u.d.Minv[0][0];
+#endif
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) {
+        // (outside x's block: s = 0 and x_i = 0 exactly, so den, rel and MJ_i keep their values)
+        if (i < LO || i >= HI) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int k = LO; k < HI; k++) s += Mv[i * MAXD + k] * x[k];
         den += x[i] * s; rel += x[i] * L.vq[i];
         MJ[i] += s;
     }
 #pragma unroll
     for (int i = 0; i < MAXD; i++) J[i] += x[i];
+}
+AVR_DI void minv_mul_add(const KModel &m, const EnvLDS &L, int link, const float *x, float *J, float *MJ, float &den, float &rel) {
+    if (link < m.nl) minv_mul_add_blk<0, K_ND>(L, x, J, MJ, den, rel);
+    else minv_mul_add_blk<K_ND, MAXD>(L, x, J, MJ, den, rel);
 }
 
 // Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping), result in L.h.
@@ -2261,7 +2298,7 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
             jbl = V(0, 0, 0);
             jba = scl(an, -1.f);
         }
-        minv_mul(L, JA, MA);
+        minv_mul_blk<0, K_ND>(L, JA, MA);          // (the weld's robot link: the robot block)
         float den = 0.f, rel = 0.f;
 #pragma unroll
         for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
@@ -2397,7 +2434,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
             if (kA == 1) {
                 float Ja[MAXD], Ma[MAXD];
                 robot_jac(m, L, iA, pa, lin, angA, Ja);
-                minv_mul(L, Ja, Ma);
+                minv_mul_link(m, L, iA, Ja, Ma);
 #pragma unroll
                 for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; }
                 if (kB == 1) {
@@ -2406,7 +2443,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                     // read-back of the first from memory cost ~60 us per sub-step (ScratchItch)
                     float Jb[MAXD];
                     robot_jac(m, L, iB, pb, nd, angB, Jb);
-                    minv_mul_add(L, Jb, Ja, Ma, den, rel);
+                    minv_mul_add(m, L, iB, Jb, Ja, Ma, den, rel);
                 }
                 put_robot(wr, Ja, Ma);
                 put_free_zero(w + 4);
@@ -2420,7 +2457,7 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
                 if (kA != 1) {
                     float Jb[MAXD], Mb[MAXD];
                     robot_jac(m, L, iB, pb, nd, angB, Jb);
-                    minv_mul(L, Jb, Mb);
+                    minv_mul_link(m, L, iB, Jb, Mb);
 #pragma unroll
                     for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
                     put_robot(wr, Jb, Mb);
