@@ -410,7 +410,7 @@ AVR_DI void minv_mul_blk(const EnvLDS &L, const float *x, float *y) {
         if (i < LO || i >= HI) { y[i] = 0.f; continue; }
         float s = 0.f;
 #pragma unroll
-        for (int k = LO; k < HI; k++) s += Mv[i * MAXD + k] * x[k];
+        for (int k = LO; k < HI; k++) s = fmaf(Mv[i * MAXD + k], x[k], s);
         y[i] = s;
     }
 }
@@ -438,8 +438,8 @@ AVR_DI void minv_mul_add_blk(const EnvLDS &L, const float *x, float *J, float *M
         if (i < LO || i >= HI) continue;
         float s = 0.f;
 #pragma unroll
-        for (int k = LO; k < HI; k++) s += Mv[i * MAXD + k] * x[k];
-        den += x[i] * s; rel += x[i] * L.vq[i];
+        for (int k = LO; k < HI; k++) s = fmaf(Mv[i * MAXD + k], x[k], s);
+        den = fmaf(x[i], s, den); rel = fmaf(x[i], L.vq[i], rel);
         MJ[i] += s;
     }
 #pragma unroll
@@ -2048,21 +2048,33 @@ AVR_DI void collide_contacts(const KModel &m, EnvLDS &L, const float *cs, float 
 }
 
 // --------------------------------------------------------------------------- constraint rows
+// Jacobian entry of DoF d (< MAXD) for a point p on the link with ancestor mask am, direction
+// (lin, ang): lin . (axis x (p - origin)) + ang . axis (revolute), lin . axis (prismatic).  The
+// multiply-adds are spelled out (fmaf) so that the contact's lane (robot_jac, all DoFs unrolled)
+// and the wave-cooperative row (one DoF per lane) round alike: left to contraction, the compiler
+// fuses different products of the two forms (which product of a sum it fuses depends on how
+// often each is used after CSE).
+AVR_DI float jac_entry(const KModel &m, const EnvLDS &L, unsigned am, int d, v3 p, v3 lin, v3 ang) {
+    float v = 0.f;
+    if (d < m.nd + m.hc_n) {               // chain DoFs are never ancestors of a robot link
+        const int k = gld(m.dof_link + (d));
+        if ((am >> k) & 1u) {
+            const v3 a = ld3(L.ax[k]);
+            if (gld(m.rl_jtype + (k)) == AVR_J_REVOLUTE) {
+                const v3 r = sub(p, ld3(L.org[k]));
+                const v3 cl = V(fmaf(a.y, r.z, -(a.z * r.y)), fmaf(a.z, r.x, -(a.x * r.z)), fmaf(a.x, r.y, -(a.y * r.x)));
+                v = fmaf(lin.z, cl.z, fmaf(lin.y, cl.y, lin.x * cl.x)) + fmaf(ang.z, a.z, fmaf(ang.y, a.y, ang.x * a.x));
+            } else {
+                v = fmaf(lin.z, a.z, fmaf(lin.y, a.y, lin.x * a.x)) + fmaf(ang.z, 0.f, fmaf(ang.y, 0.f, ang.x * 0.f));
+            }
+        }
+    }
+    return v;
+}
 AVR_DI void robot_jac(const KModel &m, const EnvLDS &L, int link, v3 p, v3 lin, v3 ang, float *J) {
     const unsigned am = gld(m.anc_mask + (link));
 #pragma unroll
-    for (int d = 0; d < MAXD; d++) {
-        float v = 0.f;
-        if (d < m.nd + m.hc_n) {           // chain DoFs are never ancestors of a robot link
-            int k = gld(m.dof_link + (d));
-            if ((am >> k) & 1u) {
-                v3 cl, ca;
-                dof_col(m, L, k, p, cl, ca);
-                v = dot(lin, cl) + dot(ang, ca);
-            }
-        }
-        J[d] = v;
-    }
+    for (int d = 0; d < MAXD; d++) J[d] = jac_entry(m, L, am, d, p, lin, ang);
 }
 
 AVR_DI float free_dot(const EnvLDS &L, int f, v3 lin, v3 ang) {
@@ -2359,6 +2371,120 @@ AVR_DI float torsion_coeff(const float *c, const KModel &m, int ba, int bb) {
     const float x = gld(c + ba) * gld(m.body_friction + bb) + gld(c + bb) * gld(m.body_friction + ba);
     return fminf(fmaxf(x, -10.f), 10.f);
 }
+// A row's robot part built by the whole wave (lane d: DoF d) instead of by the contact's lane alone:
+// the Jacobian entries (jac_entry), M^-1 J^T entry d from the Jacobian broadcast through LDS (the
+// sums of minv_mul_blk / minv_mul_add_blk, in their order), den and rel summed over the DoFs in DoF
+// order on every lane -- the per-lane builder's roundings, with the robot_jac + M^-1 product chain
+// (~K_ND^2 dependent LDS reads and fmas on one lane) cut to ~K_ND.  An env whose contact rows
+// hold few robot endpoints (FeedingJaco: one spoon or arm contact against the human, in a wave
+// whose other lanes are done) no longer waits for the one lane that builds them.
+// lA, lB: the articulated links of endpoints A, B (-1: not articulated); (den, rel) enter holding
+// the free A endpoint's part (0 without one) and leave with the robot part added.
+// The robot part on the contact's own lane: endpoint A's (articulated link lA, -1: none) Jacobian
+// and M^-1 J^T, then endpoint B's (lB) added (minv_mul_add); (den, rel) enter holding the free A
+// endpoint's part.  One pair of MAXD arrays live at a time.
+AVR_DI void lane_robot_part(const KModel &m, const EnvLDS &L, int lA, int lB, v3 pa, v3 pb, v3 lin, v3 angA, float &den, float &rel,
+                            float *J, float *MJ) {
+    const v3 nd = scl(lin, -1.f), angB = scl(angA, -1.f);
+    if (lA >= 0) {
+        robot_jac(m, L, lA, pa, lin, angA, J);
+        minv_mul_link(m, L, lA, J, MJ);
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) { den = fmaf(J[d], MJ[d], den); rel = fmaf(J[d], L.vq[d], rel); }
+        if (lB >= 0) {
+            // both endpoints on the articulated system (a robot link against a human-chain link):
+            // the second endpoint's part is added in registers (minv_mul_add); the read-back of
+            // the first from memory cost ~60 us per sub-step (ScratchItch)
+            float Jb[MAXD];
+            robot_jac(m, L, lB, pb, nd, angB, Jb);
+            minv_mul_add(m, L, lB, Jb, J, MJ, den, rel);
+        }
+    } else {
+        robot_jac(m, L, lB, pb, nd, angB, J);
+        minv_mul_link(m, L, lB, J, MJ);
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) { den = fmaf(J[d], MJ[d], den); rel = fmaf(J[d], L.vq[d], rel); }
+    }
+}
+#ifdef AVR_COOP_CHECK
+// diagnostic build: the cooperative row against the per-lane one, bit for bit (device printf)
+__device__ int g_coop_check;
+AVR_DI void coop_check(const KModel &m, const EnvLDS &L, const float *wr, int lA, int lB, v3 pa, v3 pb, v3 lin, v3 ang,
+                       float den, float rel, float cden, float crel) {
+    float J[MAXD], MJ[MAXD];
+    lane_robot_part(m, L, lA, lB, pa, pb, lin, ang, den, rel, J, MJ);
+    int bad = -1;
+    for (int d = 0; d < MAXD && bad < 0; d++) {
+        const float *q = wr + (NDL == 2 ? 4 * (d & 15) + 2 * (d >> 4) : 2 * d);
+        if (__float_as_int(q[0]) != __float_as_int(J[d]) || __float_as_int(q[1]) != __float_as_int(MJ[d])) bad = d;
+    }
+    if (bad >= 0 || __float_as_int(den) != __float_as_int(cden) || __float_as_int(rel) != __float_as_int(crel)) {
+        if (atomicAdd(&g_coop_check, 1) < 24) {
+            const int d = bad < 0 ? 0 : bad;
+            const float *q = wr + (NDL == 2 ? 4 * (d & 15) + 2 * (d >> 4) : 2 * d);
+            printf("coop mismatch lA %d lB %d den %a/%a rel %a/%a dof %d J %a/%a MJ %a/%a\n", lA, lB, cden, den, crel, rel, bad,
+                   q[0], J[d], q[1], MJ[d]);
+        }
+    }
+}
+#endif
+#ifndef AVR_COOP_ROWS
+#define AVR_COOP_ROWS 64     // build a contact-row pass's robot rows wave-cooperatively when at most this many lanes hold one
+#endif
+template <int LO, int HI>
+AVR_DI float minv_entry(const EnvLDS &L, const float *x, int d) {
+    if (d < LO || d >= HI) return 0.f;
+    const float *Mv = &L.u.d.Minv[0][0] + d * MAXD;
+    float s = 0.f;
+#pragma unroll
+    for (int k = LO; k < HI; k++) s = fmaf(Mv[k], x[k], s);
+    return s;
+}
+AVR_DI void coop_robot_row(const KModel &m, EnvLDS &L, float *X, float *wr, int lA, int lB, v3 pa, v3 pb, v3 lin, v3 ang,
+                           float &den, float &rel) {
+    const int d = lane_id();
+    float *XJ = X, *XM = X + MAXD, *XJ2 = X + 2 * MAXD, *XM2 = X + 3 * MAXD;
+    const bool fa = lA >= 0;
+    const int lF = fa ? lA : lB;
+    const v3 pF = fa ? pa : pb, linF = fa ? lin : scl(lin, -1.f), angF = fa ? ang : scl(ang, -1.f);
+    const float jF = d < MAXD ? jac_entry(m, L, gld(m.anc_mask + (lF)), d, pF, linF, angF) : 0.f;
+    if (d < MAXD) XJ[d] = jF;
+    SYNC();
+    float mF = lF < m.nl ? minv_entry<0, K_ND>(L, XJ, d) : minv_entry<K_ND, MAXD>(L, XJ, d);
+    if (d < MAXD) XM[d] = mF;
+    SYNC();
+#pragma unroll
+    for (int k = 0; k < MAXD; k++) { const float j = XJ[k]; den = fmaf(j, XM[k], den); rel = fmaf(j, L.vq[k], rel); }
+    float J = jF;
+    if (fa && lB >= 0) {                     // the second articulated endpoint (minv_mul_add)
+        const float jS = d < MAXD ? jac_entry(m, L, gld(m.anc_mask + (lB)), d, pb, scl(lin, -1.f), scl(ang, -1.f)) : 0.f;
+        if (d < MAXD) XJ2[d] = jS;
+        SYNC();
+        const bool rs = lB < m.nl;
+        const float sS = rs ? minv_entry<0, K_ND>(L, XJ2, d) : minv_entry<K_ND, MAXD>(L, XJ2, d);
+        if (d < MAXD) XM2[d] = sS;
+        SYNC();
+        if (rs) {
+#pragma unroll
+            for (int i = 0; i < K_ND; i++) { const float x = XJ2[i]; den = fmaf(x, XM2[i], den); rel = fmaf(x, L.vq[i], rel); }
+        } else {
+#pragma unroll
+            for (int i = K_ND; i < MAXD; i++) { const float x = XJ2[i]; den = fmaf(x, XM2[i], den); rel = fmaf(x, L.vq[i], rel); }
+        }
+        if (rs ? d < K_ND : d >= K_ND && d < MAXD) mF += sS;
+        J = jF + jS;
+    }
+    // put_robot's layout, one (J, M^-1 J^T) pair per lane
+    if (d < 16 * NDL) {
+        const bool in = d < MAXD;
+        float2 v;
+        v.x = in ? J : 0.f; v.y = in ? mF : 0.f;
+        *(float2 *)(wr + (NDL == 2 ? 4 * (d & 15) + 2 * (d >> 4) : 2 * d)) = v;
+    }
+    SYNC();                                  // (X is reused by the next row)
+}
+static_assert(sizeof(((EnvLDS *)0)->u.d.rn) >= 4 * MAXD * sizeof(float), "cooperative row scratch");
+
 AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
     const int ncp = (int)L.st[S_TASK + T_NCP];
@@ -2394,7 +2520,8 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         int ttot;
         const int ti = nt + ballot_prefix(trs, &ttot);
         nt += ttot;
-        if (!act) continue;
+        // (inactive lanes run on contact 0's data, ncp > 0 here: every lane takes part in the
+        // wave-cooperative robot rows)
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         v3 pa = tfpt(ta, ld3(c + AVR_CP_LA)), pb = tfpt(tb, ld3(c + AVR_CP_LB));
         v3 n = ld3(c + AVR_CP_N);
@@ -2405,8 +2532,10 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
         const int info = own_mask(kA == 2 ? iA : -1, kB == 2 ? iB : -1);
         float imA = kA == 2 ? 1.f / gld(m.fb_mass + (iA)) : 0.f, imB = kB == 2 ? 1.f / gld(m.fb_mass + (iB)) : 0.f;
         float rlim1 = 0.f;                           // the first friction row's residual limit
+        const int kmax = __ballot(act && trs) ? 6 : 3;
 #pragma unroll 1
-        for (int k = 0; k < nrow; k++) {
+        for (int k = 0; k < kmax; k++) {
+            bool live = act && k < nrow;
             const int kd = k < 3 ? k : k - 3;
             v3 dir = kd == 0 ? n : (kd == 1 ? t1 : t2);
             const int slot = rob ? slot0 + k : -1;
@@ -2416,10 +2545,10 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
             // torsional rows (k >= 3): angular axis dir, no linear part
             const bool tor = k >= 3;
             const float tcoef = k == 3 ? spin : roll;
-            if (tor && !(tcoef > 0.f)) {          // null record: no endpoint, inv = rhs = coefficient = 0
+            if (live && tor && !(tcoef > 0.f)) {  // null record: no endpoint, inv = rhs = coefficient = 0
 #pragma unroll
                 for (int q = 0; q < CRW; q++) w[q] = 0.f;
-                continue;
+                live = false;
             }
             const v3 lin = tor ? V(0, 0, 0) : dir, angA = tor ? dir : V(0, 0, 0);
 #else
@@ -2431,39 +2560,39 @@ AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, floa
             // robot endpoint, if any, adds to the first's): one pair of MAXD arrays live at a time
             float *wr = rob ? row_rob(m, rows, slot) : nullptr;
             const v3 nd = scl(lin, -1.f), angB = scl(angA, -1.f);
-            if (kA == 1) {
-                float Ja[MAXD], Ma[MAXD];
-                robot_jac(m, L, iA, pa, lin, angA, Ja);
-                minv_mul_link(m, L, iA, Ja, Ma);
-#pragma unroll
-                for (int d = 0; d < MAXD; d++) { den += Ja[d] * Ma[d]; rel += Ja[d] * L.vq[d]; }
-                if (kB == 1) {
-                    // both endpoints on the articulated system (a robot link against a human-chain
-                    // link): the second endpoint's part is added in registers (minv_mul_add); the
-                    // read-back of the first from memory cost ~60 us per sub-step (ScratchItch)
-                    float Jb[MAXD];
-                    robot_jac(m, L, iB, pb, nd, angB, Jb);
-                    minv_mul_add(m, L, iB, Jb, Ja, Ma, den, rel);
+            if (live) {
+                if (kA == 2) {
+                    v3 ja = add(crs(rA, lin), angA), ma = iinv_mul(L, iA, ja), ml = scl(lin, imA);
+                    den += dot(lin, ml) + dot(ja, ma);
+                    rel += free_dot(L, iA, lin, ja);
+                    put_free(L, iA, w + 4, lin, ja);
+                } else put_free_zero(w + 4);
+            }
+            const unsigned long long rq = __ballot(live && rob);
+            if (rq && __popcll(rq) <= AVR_COOP_ROWS) {
+                float *X = &L.u.d.rn[0][0][0];       // (the RNEA temporaries are dead)
+                for (unsigned long long q = rq; q; q &= q - 1ull) {
+                    const int src = __builtin_ctzll(q);
+                    const int lA = __builtin_amdgcn_readlane(kA == 1 ? iA : -1, src), lB = __builtin_amdgcn_readlane(kB == 1 ? iB : -1, src);
+                    const int sl = __builtin_amdgcn_readlane(slot, src);
+                    const v3 spa = V(rdl_f(pa.x, src), rdl_f(pa.y, src), rdl_f(pa.z, src));
+                    const v3 spb = V(rdl_f(pb.x, src), rdl_f(pb.y, src), rdl_f(pb.z, src));
+                    const v3 sln = V(rdl_f(lin.x, src), rdl_f(lin.y, src), rdl_f(lin.z, src));
+                    const v3 san = V(rdl_f(angA.x, src), rdl_f(angA.y, src), rdl_f(angA.z, src));
+                    float cden = rdl_f(den, src), crel = rdl_f(rel, src);
+                    coop_robot_row(m, L, X, row_rob(m, rows, sl), lA, lB, spa, spb, sln, san, cden, crel);
+#ifdef AVR_COOP_CHECK
+                    if (lane == src) coop_check(m, L, row_rob(m, rows, sl), lA, lB, pa, pb, lin, angA, den, rel, cden, crel);
+#endif
+                    if (lane == src) { den = cden; rel = crel; }
                 }
-                put_robot(wr, Ja, Ma);
-                put_free_zero(w + 4);
-            } else if (kA == 2) {
-                v3 ja = add(crs(rA, lin), angA), ma = iinv_mul(L, iA, ja), ml = scl(lin, imA);
-                den += dot(lin, ml) + dot(ja, ma);
-                rel += free_dot(L, iA, lin, ja);
-                put_free(L, iA, w + 4, lin, ja);
-            } else put_free_zero(w + 4);
-            if (kB == 1) {
-                if (kA != 1) {
-                    float Jb[MAXD], Mb[MAXD];
-                    robot_jac(m, L, iB, pb, nd, angB, Jb);
-                    minv_mul_link(m, L, iB, Jb, Mb);
-#pragma unroll
-                    for (int d = 0; d < MAXD; d++) { den += Jb[d] * Mb[d]; rel += Jb[d] * L.vq[d]; }
-                    put_robot(wr, Jb, Mb);
-                }
-                put_free_zero(w + 10);
-            } else if (kB == 2) {
+            } else if (live && rob) {
+                float J[MAXD], MJ[MAXD];
+                lane_robot_part(m, L, kA == 1 ? iA : -1, kB == 1 ? iB : -1, pa, pb, lin, angA, den, rel, J, MJ);
+                put_robot(wr, J, MJ);
+            }
+            if (!live) continue;
+            if (kB == 2) {
                 v3 jb = add(crs(rB, nd), angB), mb = iinv_mul(L, iB, jb), ml = scl(nd, imB);
                 den += dot(nd, ml) + dot(jb, mb);
                 rel += free_dot(L, iB, nd, jb);
