@@ -1522,8 +1522,16 @@ struct MfNew { float p[AVR_CP_WORDS]; };
 
 AVR_DI int mf_idx(unsigned pk, int j) { return (int)((pk >> (8 * j)) & 255u); }
 AVR_DI unsigned mf_set(unsigned pk, int j, int v) { return (pk & ~(255u << (8 * j))) | ((unsigned)v << (8 * j)); }
+// (branch-free: the pool word is read at a clamped index either way and the register word
+// selected, so a refresh over a manifold holding the new point runs no divergent branches)
 AVR_DI float mf_rd(const lds_f *cp, const MfNew &nw, int idx, int w) {
-    return idx == MF_NEW ? nw.p[w] : cp[AVR_CP_WORDS * idx + w];
+    const bool nu = idx == MF_NEW;
+    const float x = cp[AVR_CP_WORDS * (nu ? 0 : idx) + w];
+    return nu ? nw.p[w] : x;
+}
+AVR_DI v3 cp_rd3(const lds_f *cp, int idx, int w) {
+    const lds_f *q = cp + AVR_CP_WORDS * idx + w;
+    return V(q[0], q[1], q[2]);
 }
 AVR_DI v3 mf_rd3(const lds_f *cp, const MfNew &nw, int idx, int w) {
     return V(mf_rd(cp, nw, idx, w), mf_rd(cp, nw, idx, w + 1), mf_rd(cp, nw, idx, w + 2));
@@ -1543,10 +1551,10 @@ AVR_DI int sort_cached(const lds_f *cp, const MfNew &nw, unsigned pk, v3 la_new,
     v3 p[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        int id = mf_idx(pk, i);
-        float d = mf_rd(cp, nw, id, AVR_CP_DIST);
+        int id = mf_idx(pk, i);                 // (a full manifold holds old points only)
+        float d = cp[AVR_CP_WORDS * id + AVR_CP_DIST];
         if (d < maxpen) { maxi = i; maxpen = d; }
-        p[i] = mf_rd3(cp, nw, id, AVR_CP_LA);
+        p[i] = cp_rd3(cp, id, AVR_CP_LA);
     }
     float res[4] = {0, 0, 0, 0};
     if (maxi != 0) res[0] = len2(crs(sub(la_new, p[1]), sub(p[3], p[2])));
@@ -1561,7 +1569,9 @@ AVR_DI int sort_cached(const lds_f *cp, const MfNew &nw, unsigned pk, v3 la_new,
     return bi;
 }
 
-// btManifoldResult::addContactPoint (getCacheEntry / replaceContactPoint / addManifoldPoint)
+// btManifoldResult::addContactPoint (getCacheEntry / replaceContactPoint / addManifoldPoint).  The
+// manifold holds old points only when a pair's one narrowphase point arrives: a replaced point is
+// rewritten in the LDS pool, an appended one goes to the registers (nw).
 AVR_DI void manifold_add(lds_f *cp, MfNew &nw, unsigned &pk, int &n, int sa, int sb, int pair, tf ta, tf tb, v3 nB, v3 pB,
                          float dist, float thr) {
     if (dist > thr) return;
@@ -1572,61 +1582,59 @@ AVR_DI void manifold_add(lds_f *cp, MfNew &nw, unsigned &pk, int &n, int sa, int
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         if (k < n) {
-            float d2 = len2(sub(mf_rd3(cp, nw, mf_idx(pk, k), AVR_CP_LA), la));
+            float d2 = len2(sub(cp_rd3(cp, mf_idx(pk, k), AVR_CP_LA), la));
             if (d2 < shortest) { shortest = d2; near = k; }
         }
     }
-    int id;
-    if (near >= 0) id = mf_idx(pk, near);
-    else if (n == AVR_MANIFOLD_POINTS) {
-        id = mf_idx(pk, sort_cached(cp, nw, pk, la, dist));
-        mf_wr(cp, nw, id, AVR_CP_IMP, 0.f);
-        mf_wr(cp, nw, id, AVR_CP_LIFE, 0.f);
+    if (near >= 0 || n == AVR_MANIFOLD_POINTS) {
+        const int id = mf_idx(pk, near >= 0 ? near : sort_cached(cp, nw, pk, la, dist));
+        lds_f *q = cp + AVR_CP_WORDS * id;
+        if (near < 0) { q[AVR_CP_IMP] = 0.f; q[AVR_CP_LIFE] = 0.f; }
+        q[AVR_CP_SA] = (float)sa; q[AVR_CP_SB] = (float)sb; q[AVR_CP_PAIR] = (float)pair; q[AVR_CP_SLOT] = 0.f;
+        q[AVR_CP_LA + 0] = la.x; q[AVR_CP_LA + 1] = la.y; q[AVR_CP_LA + 2] = la.z;
+        q[AVR_CP_LB + 0] = lb.x; q[AVR_CP_LB + 1] = lb.y; q[AVR_CP_LB + 2] = lb.z;
+        q[AVR_CP_N + 0] = nB.x; q[AVR_CP_N + 1] = nB.y; q[AVR_CP_N + 2] = nB.z;
+        q[AVR_CP_DIST] = dist;
     } else {
-        id = MF_NEW;
         pk = mf_set(pk, n, MF_NEW);
         n++;
-        nw.p[AVR_CP_IMP] = 0.f;
-        nw.p[AVR_CP_LIFE] = 0.f;
+        nw.p[AVR_CP_IMP] = 0.f; nw.p[AVR_CP_LIFE] = 0.f;
+        nw.p[AVR_CP_SA] = (float)sa; nw.p[AVR_CP_SB] = (float)sb; nw.p[AVR_CP_PAIR] = (float)pair; nw.p[AVR_CP_SLOT] = 0.f;
+        nw.p[AVR_CP_LA + 0] = la.x; nw.p[AVR_CP_LA + 1] = la.y; nw.p[AVR_CP_LA + 2] = la.z;
+        nw.p[AVR_CP_LB + 0] = lb.x; nw.p[AVR_CP_LB + 1] = lb.y; nw.p[AVR_CP_LB + 2] = lb.z;
+        nw.p[AVR_CP_N + 0] = nB.x; nw.p[AVR_CP_N + 1] = nB.y; nw.p[AVR_CP_N + 2] = nB.z;
+        nw.p[AVR_CP_DIST] = dist;
     }
-    mf_wr(cp, nw, id, AVR_CP_SA, (float)sa);
-    mf_wr(cp, nw, id, AVR_CP_SB, (float)sb);
-    mf_wr(cp, nw, id, AVR_CP_PAIR, (float)pair);
-    mf_wr(cp, nw, id, AVR_CP_SLOT, 0.f);
-    mf_wr(cp, nw, id, AVR_CP_LA + 0, la.x); mf_wr(cp, nw, id, AVR_CP_LA + 1, la.y); mf_wr(cp, nw, id, AVR_CP_LA + 2, la.z);
-    mf_wr(cp, nw, id, AVR_CP_LB + 0, lb.x); mf_wr(cp, nw, id, AVR_CP_LB + 1, lb.y); mf_wr(cp, nw, id, AVR_CP_LB + 2, lb.z);
-    mf_wr(cp, nw, id, AVR_CP_N + 0, nB.x); mf_wr(cp, nw, id, AVR_CP_N + 1, nB.y); mf_wr(cp, nw, id, AVR_CP_N + 2, nB.z);
-    mf_wr(cp, nw, id, AVR_CP_DIST, dist);
 }
 
-// btPersistentManifold::refreshContactPoints
+// btPersistentManifold::refreshContactPoints.  Its second sweep (removal, last slot moved into the
+// removed one, from the top slot down) decides each point on that point's own refreshed data, and a
+// moved point has been decided already, so the decisions are taken in the first sweep with the
+// world points it computes, and the second sweep only compacts.
 AVR_DI void manifold_refresh(lds_f *cp, MfNew &nw, unsigned &pk, int &n, tf ta, tf tb, float thr) {
+    bool rm[4];
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
+        rm[k] = false;
         if (k < n) {
             int id = mf_idx(pk, k);
             v3 pa = tfpt(ta, mf_rd3(cp, nw, id, AVR_CP_LA)), pb = tfpt(tb, mf_rd3(cp, nw, id, AVR_CP_LB));
-            mf_wr(cp, nw, id, AVR_CP_DIST, dot(sub(pa, pb), mf_rd3(cp, nw, id, AVR_CP_N)));
+            const v3 nrm = mf_rd3(cp, nw, id, AVR_CP_N);
+            const float dd = dot(sub(pa, pb), nrm);
+            mf_wr(cp, nw, id, AVR_CP_DIST, dd);
             mf_wr(cp, nw, id, AVR_CP_LIFE, mf_rd(cp, nw, id, AVR_CP_LIFE) + 1.f);
+            if (dd > thr) rm[k] = true;
+            else {
+                v3 df = sub(pb, sub(pa, scl(nrm, dd)));
+                if (len2(df) > thr * thr) rm[k] = true;
+            }
         }
     }
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
-        if (k < n) {
-            int id = mf_idx(pk, k);
-            float dd = mf_rd(cp, nw, id, AVR_CP_DIST);
-            bool rm = false;
-            if (dd > thr) rm = true;
-            else {
-                v3 pa = tfpt(ta, mf_rd3(cp, nw, id, AVR_CP_LA)), pb = tfpt(tb, mf_rd3(cp, nw, id, AVR_CP_LB));
-                v3 nrm = mf_rd3(cp, nw, id, AVR_CP_N);
-                v3 df = sub(pb, sub(pa, scl(nrm, dd)));
-                if (len2(df) > thr * thr) rm = true;
-            }
-            if (rm) {   // removeContactPoint: the last slot moves into slot k
-                pk = mf_set(pk, k, mf_idx(pk, n - 1));
-                n--;
-            }
+        if (k < n && rm[k]) {   // removeContactPoint: the last slot moves into slot k
+            pk = mf_set(pk, k, mf_idx(pk, n - 1));
+            n--;
         }
     }
 }
@@ -1676,6 +1684,7 @@ AVR_DI void pair_in(const float *cs, int k, int nsp, PairIn &P) {
     P.r1 = gld((const float4 *)(cs + CS_RES) + 2 * k + 1);
 }
 
+static_assert(K_MAX_CONTACTS % 4 == 0, "the old pool's keys are read four at a time");
 AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const PairIn &in, int k0, int nq, lds_f *oldcp, int nold, float *newcp, int &nnew) {
     const int lane = lane_id();
     PROF_START(pb);
@@ -1702,13 +1711,62 @@ AVR_DI void collide_batch(const KModel &m, EnvLDS &L, const PairIn &in, int k0, 
     if (lane < nq) {
         float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
         const int key = sa | (sb << 16);
-        const lds_i *ok = (const lds_i *)L.u.k.okey;
-        for (int i = 0; i < nold; i++)      // (no early exit: the key reads stay independent)
-            if (ok[i] == key && n < AVR_MANIFOLD_POINTS) { pk = mf_set(pk, n, i); n++; }
+        // the old pool's points of this pair: a bit mask over the pool (keys read four at a time,
+        // every read in flight together), then its first AVR_MANIFOLD_POINTS set bits in pool order
+        // -- the points the in-order scan would take, at ~3 VALU per old point instead of ~10
+        const lds_f4 *ok = (const lds_f4 *)L.u.k.okey;
+        constexpr int NW = (K_MAX_CONTACTS + 31) / 32;
+        unsigned mb[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            unsigned b = 0u;
+            if (32 * w < nold) {
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    if (32 * w + 4 * c < K_MAX_CONTACTS) {
+                        const f4v q = ok[8 * w + c];
+                        b |= (__float_as_int(q.x) == key ? 1u : 0u) << (4 * c) | (__float_as_int(q.y) == key ? 2u : 0u) << (4 * c)
+                           | (__float_as_int(q.z) == key ? 4u : 0u) << (4 * c) | (__float_as_int(q.w) == key ? 8u : 0u) << (4 * c);
+                    }
+                }
+                const int r = nold - 32 * w;      // (keys past the pool are stale)
+                if (r < 32) b &= (1u << r) - 1u;
+            }
+            mb[w] = b;
+        }
+#pragma unroll
+        for (int t = 0; t < AVR_MANIFOLD_POINTS; t++) {
+            int ws = -1;
+            unsigned bw = 0u;
+#pragma unroll
+            for (int w = NW - 1; w >= 0; w--)
+                if (mb[w]) { ws = w; bw = mb[w]; }
+            if (ws >= 0) {
+                pk |= (unsigned)(32 * ws + __builtin_ctz(bw)) << (8 * t);
+                n = t + 1;
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    if (w == ws) mb[w] &= mb[w] - 1u;
+            }
+        }
+#ifdef AVR_PROF
+    }
+    PROF_STOP(40, pb);
+    if (lane < nq) {
+        float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
+#endif
         tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
         if (rc == 1) manifold_add(oldcp, nw, pk, n, sa, sb, p, ta, tb, nB, pB, d, thr);
+#ifdef AVR_PROF
+    }
+    PROF_STOP(41, pb);
+    if (lane < nq) {
+        float thr = fminf(gld(m.body_threshold + (ba)), gld(m.body_threshold + (bb)));
+        tf ta = ldtf(L.btf[ba]), tb = ldtf(L.btf[bb]);
+#endif
         manifold_refresh(oldcp, nw, pk, n, ta, tb, thr);
     }
+    PROF_STOP(42, pb);
     int incl = n;
     for (int o = 1; o < 64; o <<= 1) {
         int y = __shfl_up(incl, o, 64);

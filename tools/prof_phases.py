@@ -27,7 +27,7 @@ sim.set_state(S.astype(np.float32)); sim.settle(100 if TASK == 0 else 0)
 names = ['fk', 'bodies+broad', 'childpairs', 'narrow+mf', '#culleditems', '#xcd-mismatch', 'dyn', 'nc_rows', 'c_rows', 'solve', 'integrate', '#cooppairs', 'task', 'collide', '#shapepairs', '#bodypairs', ' lane-narrow', ' coop', ' manifold', '#coop sph-hull', '#coop hull-hull', '#coop other', '#coop bighull', '-',
          ' M entries', ' cholesky', ' M^-1 cols', ' bias (RNEA)', '#coop GJK it', '#coop cycles', '#coop max cyc', '-',
          '#np sph-hull', '#np other', '#np refill trips', '#np ph_steps', '#np GJK it', '#np GJK it max', '#np GJK pairs', '#np closed form',
-         '-', '-', '-', '-', '-', '-', '-', '-']
+         '  mf match', '  mf add', '  mf refresh', '-', '-', '-', '-', '-']
 for t in range(int(os.environ.get('PROF_STEPS', '3'))):
     prof.zero_()
     t0 = time.time(); sim.step(_lib.random_actions(1001, np.arange(N), t)); el = time.time() - t0
@@ -63,7 +63,7 @@ for e in top:
 # kernel a's slowest envs (the launch's tail): their phases against the median env's (last step)
 ka = p[:, 3] + p[:, 6] + p[:, 7] + p[:, 8]
 med = np.median(p, axis=0)
-cols = [(3, 'narrow+mf'), (17, 'coop'), (18, 'manifold'), (6, 'dyn'), (7, 'nc_rows'), (8, 'c_rows'), (24, 'M'), (25, 'chol'), (26, 'Minv'), (27, 'bias')]
+cols = [(3, 'narrow+mf'), (17, 'coop'), (40, 'mf match'), (41, 'mf add'), (42, 'mf refresh'), (18, 'mf pool'), (6, 'dyn'), (7, 'nc_rows'), (8, 'c_rows'), (24, 'M'), (25, 'chol'), (26, 'Minv'), (27, 'bias')]
 print('kernel a per env-step cycles: median %.3g, p99 %.3g, max %.3g' % (np.median(ka), np.percentile(ka, 99), ka.max()))
 print('  median env   ' + ' '.join('%s %.3g' % (nm, med[k]) for k, nm in cols))
 for e in np.argsort(-ka)[:8]:
