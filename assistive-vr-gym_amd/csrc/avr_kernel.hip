@@ -450,6 +450,17 @@ AVR_DI void minv_mul_add(const KModel &m, const EnvLDS &L, int link, const float
     else minv_mul_add_blk<K_ND, MAXD>(L, x, J, MJ, den, rel);
 }
 
+// entry d of M^-1 x within the block [LO, HI) of M (minv_mul_blk's sum for row d; one lane per row)
+template <int LO, int HI>
+AVR_DI float minv_entry(const EnvLDS &L, const float *x, int d) {
+    if (d < LO || d >= HI) return 0.f;
+    const float *Mv = &L.u.d.Minv[0][0] + d * MAXD;
+    float s = 0.f;
+#pragma unroll
+    for (int k = LO; k < HI; k++) s = fmaf(Mv[k], x[k], s);
+    return s;
+}
+
 // Recursive Newton-Euler bias forces (Coriolis, gyroscopic, btMultiBody damping), result in L.h.
 // The forward recursion (parent p of link i, joint origin o_i, COM c_i):
 //   om_i = om_p + w_i                       (w_i = axis qd, revolute; 0 otherwise)
@@ -2255,6 +2266,9 @@ AVR_DI void put_robot(float *w, const float *J, const float *MJ) {
 }
 
 
+#ifdef AVR_COOP_CHECK
+__device__ int g_coop_check;     // (diagnostic build: mismatches reported)
+#endif
 // Non-contact rows (limits, motors, fixed constraint), one lane per row.
 // Row order restates btMultiBodyConstraintSolver's setup order: joint-limit rows
 // of violated limits (link order, lower then upper), motor rows (link order), fixed rows.
@@ -2313,6 +2327,45 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     const v3 pivB = tb.p;
 #endif
     const m3 FA = qmat(frA), FB = qmat(tb.q);
+    const v3 c0 = V(FA.m[0][0], FA.m[1][0], FA.m[2][0]), c1 = V(FA.m[0][1], FA.m[1][1], FA.m[2][1]), c2 = V(FA.m[0][2], FA.m[1][2], FA.m[2][2]);
+    // The weld's six robot parts, built by the whole wave (lane d: DoF d; coop_robot_row's scheme for
+    // six rows at once): every row's Jacobian entry at the pivot, M^-1 J^T from the Jacobians
+    // broadcast through LDS, and the parts stored in put_robot's layout; each weld lane then sums
+    // its own row's den and rel in DoF order.  (Per lane, a weld row's robot_jac and K_ND^2 M^-1
+    // product were the longest chain of the non-contact rows.)
+    float (*WJ)[MAXD] = (float (*)[MAXD])&L.u.d.rn[1][0][0];     // [6][MAXD] J, then [6][MAXD] M^-1 J^T
+    float (*WM)[MAXD] = WJ + 6;
+    {
+        const int d = lane;
+        const unsigned am = gld(m.anc_mask + (link));
+        const int wslot = nrow - 6;
+        float j[6], mj[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const v3 lin = r < 3 ? V(r == 0 ? 1.f : 0.f, r == 1 ? 1.f : 0.f, r == 2 ? 1.f : 0.f) : V(0, 0, 0);
+            const v3 an = r < 3 ? V(0, 0, 0) : (r == 3 ? c0 : r == 4 ? c1 : c2);
+            j[r] = d < MAXD ? jac_entry(m, L, am, d, pivA, lin, an) : 0.f;
+            if (d < MAXD) WJ[r][d] = j[r];
+        }
+        SYNC();
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            mj[r] = minv_entry<0, K_ND>(L, WJ[r], d);         // (the weld's robot link: the robot block)
+            if (d < MAXD) WM[r][d] = mj[r];
+        }
+        if (d < 16 * NDL) {
+            const bool in = d < MAXD;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                if (wslot + r < MAXNC) {
+                    float2 v;
+                    v.x = in ? j[r] : 0.f; v.y = in ? mj[r] : 0.f;
+                    *(float2 *)(row_rob(m, rows, wslot + r) + (NDL == 2 ? 4 * (d & 15) + 2 * (d >> 4) : 2 * d)) = v;
+                }
+            }
+        }
+        SYNC();
+    }
     if (kind == 0 || kind == 1 || kind == 2) {
         // J = +-e_dof: M^-1 J^T is a signed column of M^-1
         const float sg = kind == 1 ? -1.f : 1.f;
@@ -2337,12 +2390,10 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
     } else if (kind == 3) {
         v3 lin = V(0, 0, 0);
         float pos;
-        float JA[MAXD], MA[MAXD];
         v3 jbl, jba;
         if (fix < 3) {
             if (fix == 0) lin.x = 1.f; else if (fix == 1) lin.y = 1.f; else lin.z = 1.f;
             pos = dot(sub(pivA, pivB), lin);
-            robot_jac(m, L, link, pivA, lin, V(0, 0, 0), JA);
             jbl = scl(lin, -1.f);
             jba = crs(sub(pivB, tb.p), jbl);
         } else {
@@ -2361,17 +2412,33 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
                 else ang = V(-atan2f(ME(3), ME(4)), -1.5707963267948966f, 0.f);
             } else ang = V(atan2f(ME(3), ME(4)), 1.5707963267948966f, 0.f);
 #undef ME
-            const v3 c0 = V(FA.m[0][0], FA.m[1][0], FA.m[2][0]), c1 = V(FA.m[0][1], FA.m[1][1], FA.m[2][1]), c2 = V(FA.m[0][2], FA.m[1][2], FA.m[2][2]);
             const v3 an = fix == 3 ? c0 : (fix == 4 ? c1 : c2);
             pos = fix == 3 ? ang.x : fix == 4 ? ang.y : ang.z;
-            robot_jac(m, L, link, pivA, V(0, 0, 0), an, JA);
             jbl = V(0, 0, 0);
             jba = scl(an, -1.f);
         }
-        minv_mul_blk<0, K_ND>(L, JA, MA);          // (the weld's robot link: the robot block)
         float den = 0.f, rel = 0.f;
 #pragma unroll
-        for (int d = 0; d < MAXD; d++) { den += JA[d] * MA[d]; rel += JA[d] * L.vq[d]; }
+        for (int d = 0; d < MAXD; d++) { const float j = WJ[fix][d]; den = fmaf(j, WM[fix][d], den); rel = fmaf(j, L.vq[d], rel); }
+#ifdef AVR_COOP_CHECK
+        {
+            float JA[MAXD], MA[MAXD];
+            v3 l2 = V(0, 0, 0), a2 = V(0, 0, 0);
+            if (fix < 3) { if (fix == 0) l2.x = 1.f; else if (fix == 1) l2.y = 1.f; else l2.z = 1.f; }
+            else a2 = fix == 3 ? c0 : (fix == 4 ? c1 : c2);
+            robot_jac(m, L, link, pivA, l2, a2, JA);
+            minv_mul_blk<0, K_ND>(L, JA, MA);
+            float d2 = 0.f, r2 = 0.f;
+            for (int d = 0; d < MAXD; d++) { d2 += JA[d] * MA[d]; r2 += JA[d] * L.vq[d]; }
+            int bad = -1;
+            for (int d = 0; d < MAXD && bad < 0; d++)
+                if (__float_as_int(JA[d]) != __float_as_int(WJ[fix][d]) || __float_as_int(MA[d]) != __float_as_int(WM[fix][d])) bad = d;
+            if ((bad >= 0 || __float_as_int(d2) != __float_as_int(den) || __float_as_int(r2) != __float_as_int(rel)) && atomicAdd(&g_coop_check, 1) < 24) {
+                const int d = bad < 0 ? 0 : bad;
+                printf("weld mismatch fix %d den %a/%a rel %a/%a dof %d J %a/%a MJ %a/%a\n", fix, den, d2, rel, r2, bad, WJ[fix][d], JA[d], WM[fix][d], MA[d]);
+            }
+        }
+#endif
         const float im = 1.f / gld(m.fb_mass + (fb));
         const v3 mbl = scl(jbl, im), mba = iinv_mul(L, fb, jba);
         den += dot(jbl, mbl) + dot(jba, mba);
@@ -2382,7 +2449,6 @@ AVR_DI int build_noncontact_rows(const KModel &m, EnvLDS &L, float *rows, float 
         put_hdr(w, own_mask(-1, fb), inv, (-pos * erp / dt - rel) * inv, -mi, mi, lane);
         put_free_zero(w + 8);
         put_free(L, fb, w + 14, jbl, jba);
-        put_robot(row_rob(m, rows, lane), JA, MA);
     }
     if (nrow > MAXNC) { if (lane == 0) L.flags |= 16; nrow = MAXNC; }
     if (lane == 0) L.n_nc = nrow;
@@ -2466,7 +2532,6 @@ AVR_DI void lane_robot_part(const KModel &m, const EnvLDS &L, int lA, int lB, v3
 }
 #ifdef AVR_COOP_CHECK
 // diagnostic build: the cooperative row against the per-lane one, bit for bit (device printf)
-__device__ int g_coop_check;
 AVR_DI void coop_check(const KModel &m, const EnvLDS &L, const float *wr, int lA, int lB, v3 pa, v3 pb, v3 lin, v3 ang,
                        float den, float rel, float cden, float crel) {
     float J[MAXD], MJ[MAXD];
@@ -2489,15 +2554,6 @@ AVR_DI void coop_check(const KModel &m, const EnvLDS &L, const float *wr, int lA
 #ifndef AVR_COOP_ROWS
 #define AVR_COOP_ROWS 64     // build a contact-row pass's robot rows wave-cooperatively when at most this many lanes hold one
 #endif
-template <int LO, int HI>
-AVR_DI float minv_entry(const EnvLDS &L, const float *x, int d) {
-    if (d < LO || d >= HI) return 0.f;
-    const float *Mv = &L.u.d.Minv[0][0] + d * MAXD;
-    float s = 0.f;
-#pragma unroll
-    for (int k = LO; k < HI; k++) s = fmaf(Mv[k], x[k], s);
-    return s;
-}
 AVR_DI void coop_robot_row(const KModel &m, EnvLDS &L, float *X, float *wr, int lA, int lB, v3 pa, v3 pb, v3 lin, v3 ang,
                            float &den, float &rel) {
     const int d = lane_id();
@@ -2542,6 +2598,7 @@ AVR_DI void coop_robot_row(const KModel &m, EnvLDS &L, float *X, float *wr, int 
     SYNC();                                  // (X is reused by the next row)
 }
 static_assert(sizeof(((EnvLDS *)0)->u.d.rn) >= 4 * MAXD * sizeof(float), "cooperative row scratch");
+static_assert(sizeof(((EnvLDS *)0)->u.d.rn) - sizeof(((EnvLDS *)0)->u.d.rn[0]) >= 12 * MAXD * sizeof(float), "weld row scratch");
 
 AVR_DI int build_contact_rows(const KModel &m, EnvLDS &L, const float *gcp, float *rows, int n_nc, float dt) {
     const int lane = lane_id();
