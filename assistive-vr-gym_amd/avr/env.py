@@ -119,15 +119,25 @@ _SCENES = {}
 _TASK_OF = {'feeding': ABI.TASK_FEEDING, 'scratch_itch': ABI.TASK_SCRATCH, 'bed_bathing': ABI.TASK_BEDBATH, 'dressing': ABI.TASK_DRESSING}
 
 
-def _scene(task):
-    if task not in _SCENES:
+def _scene(task, heights=None):
+    """(arrays, ModelDesc) of a task's scene with the human at per-gender hipbone_to_mouth_height
+    `heights` (None: the defaults, the committed npz; otherwise rebuilt by the model compiler
+    from its asset cache, human_creation.py:60-63,75)."""
+    from . import model_compiler as MC
+    H = MC.human_heights(heights)
+    key = (task,) + tuple(H[g] for g in ('male', 'female'))
+    if key not in _SCENES:
         if task == 'dressing':
+            if not MC.default_heights(H):
+                raise NotImplementedError('DressingJaco-v0: only the default human proportions are built')
             from . import reset_dressing as RD
             A = RD.dressing_scene()
-        else:
+        elif MC.default_heights(H):
             A = ABI.load_scene(_TASK_OF[task])
-        _SCENES[task] = (A, ABI.ModelDesc(A))
-    return _SCENES[task]
+        else:
+            A = MC.scene_arrays(ABI.SCENES[_TASK_OF[task]], H)
+        _SCENES[key] = (A, ABI.ModelDesc(A))
+    return _SCENES[key]
 
 
 class _Prefetch:
@@ -184,11 +194,16 @@ class AVRVecEnv:
     avr_reset).
     reset_stream: FeedingJaco's reset draws, 'philox' (counter-based, vectorised; default) or
     'numpy' (the per-env Generator stream of the bench's reset pools and the golden fixtures).
+    human_heights: the human's proportions, {gender: hipbone_to_mouth_height} (create_human's
+    hmhs = height / 0.6 male, / 0.54 female, human_creation.py:60-63: capsule lengths and joint
+    offsets scale by it, BedBathing's wipe targets too, bed_bathing.py:359-370); a gender not
+    named keeps its default.  One set per handle: the reference builds its human at the height
+    the env holds (a replay's setup.pkl, feeding.py:153-156; setup(), feeding.py:20-28).
     """
 
     def __init__(self, env_id='FeedingJaco-v0', n_envs=1, device=0, seed=1001, env_offset=0, auto_reset=True,
                  impairment='random', reset_ik='device', prefetch=True, scratch_attempts=100, scratch_iters=200,
-                 reset_stream='philox'):
+                 reset_stream='philox', human_heights=None):
         if env_id not in REGISTRY:
             raise KeyError('unknown env id %r' % env_id)
         task, robot, ok = REGISTRY[env_id]
@@ -200,7 +215,9 @@ class AVRVecEnv:
         self.env_offset = int(env_offset)
         self.auto_reset = auto_reset
         self.impairment = impairment
-        self.A, self.md = _scene(task)
+        self.A, self.md = _scene(task, human_heights)
+        from . import model_compiler as MC
+        self.human_heights = MC.human_heights(human_heights)
         self.task = self.md.task
         self.L = self.md.layout
         self.device_ik = self.task == ABI.TASK_FEEDING and reset_ik == 'device'

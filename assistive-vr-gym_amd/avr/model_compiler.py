@@ -17,7 +17,10 @@ ships.  Nothing here is on the step path.  What it restates, with reference cita
 * Collision filters: Jaco self-collision except parent/child (`world_creation.py:282`),
   spoon vs gripper links 7..14 off (`world_creation.py:359-361`), static-vs-static never.
 """
+import copy
+import functools
 import os
+import pickle
 import re
 import struct
 import xml.etree.ElementTree as ET
@@ -29,6 +32,44 @@ from . import geom as G
 
 REF_ASSETS = '/root/reference/assistive_gym/envs/assets'
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
+
+# Every builder that reads the reference's assets goes through asset_cached: its result is kept
+# in data/asset_cache.pkl (written by compile_all in the build container, this module's own
+# output), so that scene_arrays can rebuild a scene at another human height where the reference's
+# assets are absent (the GPU box).  The cache holds the builders' parsed and hulled geometry,
+# the same numbers the committed scene npz files hold, not the asset files.
+ASSET_CACHE = os.path.join(DATA_DIR, 'asset_cache.pkl')
+_asset_memo = None
+
+
+def _memo():
+    global _asset_memo
+    if _asset_memo is None:
+        _asset_memo = {}
+        if os.path.exists(ASSET_CACHE):
+            with open(ASSET_CACHE, 'rb') as f:
+                _asset_memo = pickle.load(f)
+    return _asset_memo
+
+
+def asset_cached(fn):
+    @functools.wraps(fn)
+    def wrapper(*args):
+        M = _memo()
+        key = (fn.__name__,) + tuple(args)
+        if key not in M:
+            if not os.path.isdir(REF_ASSETS):
+                raise RuntimeError('%s%r: not in %s and the reference assets (%s) are absent; run '
+                                   'model_compiler.compile_all in the build container' % (fn.__name__, args, ASSET_CACHE, REF_ASSETS))
+            M[key] = fn(*args)
+        return copy.deepcopy(M[key])
+    return wrapper
+
+
+def save_asset_cache(path=ASSET_CACHE):
+    with open(path, 'wb') as f:
+        pickle.dump(_memo(), f, protocol=4)
+
 
 URDF_MARGIN = 0.001          # gUrdfDefaultCollisionMargin (assumed Bullet default)
 CONTACT_BREAKING = 0.02      # gContactBreakingThreshold (assumed Bullet default)
@@ -286,6 +327,40 @@ def _sphere(radius, pos=(0, 0, 0)):
     return Shape(SPHERE, pos, (0, 0, 0, 1), radius=radius)
 
 
+DEFAULT_HEIGHT = {'male': 0.6, 'female': 0.54}          # feeding.py:174, scratch_itch.py:161, bed_bathing.py:187
+
+
+def human_heights(heights=None):
+    """Per-gender hipbone_to_mouth_height of a compiled scene: None (both defaults) or a dict
+    {gender: height}; a missing gender keeps its default."""
+    h = dict(DEFAULT_HEIGHT)
+    for g, v in (heights or {}).items():
+        if g not in h:
+            raise ValueError('heights: gender must be male or female, got %r' % (g,))
+        if v is not None:
+            v = float(v)
+            if not 0.3 <= v <= 1.0:
+                raise ValueError('hipbone_to_mouth_height %.4f outside [0.3, 1.0] m' % v)
+            h[g] = v
+    return h
+
+
+def default_heights(heights):
+    return human_heights(heights) == DEFAULT_HEIGHT
+
+
+@asset_cached
+def head_hulls(head_file):
+    """The head's VHACD parts at meshScale 0.89 (human_creation.py:98-99,141-142)."""
+    return [Hull(g * 0.89) for g in obj_groups(os.path.join(REF_ASSETS, 'head_female_male', head_file))]
+
+
+@asset_cached
+def bed_frame_hulls():
+    """The hospital bed frame's VHACD parts at meshScale [1, 1.2, 1] (bed_bathing.py:214-216)."""
+    return [Hull(g * np.array([1, 1.2, 1])) for g in obj_groups(os.path.join(REF_ASSETS, 'bed', 'hospital_bed_frame_vhacd.obj'))]
+
+
 def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
     """Restatement of HumanCreation.create_human (human_creation.py:57-301), non-`new`,
     non-cloth.  Returns (base_shapes, links[DFS]); each link dict carries parent (DFS index or
@@ -299,7 +374,6 @@ def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
     q_y90 = G.quat_from_euler([0, np.pi / 2, 0])
     q_x90 = G.quat_from_euler([np.pi / 2, 0, 0])
     head_orient = G.quat_from_euler([np.pi / 2.0, 0, 0])
-    head_dir = os.path.join(REF_ASSETS, 'head_female_male')
     if gender == 'male':                                          # human_creation.py:76-115
         chest = _capsule(0.127 * rs, 0.056, orient=q_y90)
         r_sh = _capsule(0.106 * rs, 0.253 / 8, pos=[-0.253 / 2.5 + 0.253 / 16, 0, 0], orient=q_y90)
@@ -357,8 +431,7 @@ def build_human(gender, hipbone_to_mouth_height=None, limit_scale=1.0):
         shin_p = [0, 0, -0.391 * hs]
         foot_p = [0, 0, -0.367 * hs - 0.045 / 2]
     gidx = 0 if gender == 'male' else 1
-    head_shapes = [Shape(HULL, head_pos, head_orient, hull=Hull(g * 0.89), gender=gidx)
-                   for g in obj_groups(os.path.join(head_dir, head_file))]
+    head_shapes = [Shape(HULL, head_pos, head_orient, hull=h, gender=gidx) for h in head_hulls(head_file)]
     jp = [0, 0, 0]
     d = np.deg2rad
     R, F = J_REVOLUTE, J_FIXED
@@ -497,6 +570,7 @@ class Scene:
         return len(self.bodies) - 1
 
 
+@asset_cached
 def build_jaco():
     links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, 'jaco', 'j2s7s300_gym.urdf'))
     rob = dict(name=[], parent=[], jtype=[], dof=[], jpos=[], jquat=[], axis=[], com_pos=[], com_quat=[],
@@ -534,6 +608,7 @@ def build_jaco():
     return rob
 
 
+@asset_cached
 def build_free_urdf(rel):
     links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, rel))
     assert not dfs
@@ -543,14 +618,18 @@ def build_free_urdf(rel):
     return dict(mass=L.mass, inertia=box_inertia(L.mass, lo, hi), shapes=shapes, friction=L.friction)
 
 
+@asset_cached
 def build_static_urdf(rel):
     links, root, dfs = parse_urdf(os.path.join(REF_ASSETS, rel))
     L = links[root]
     return dict(shapes=urdf_shapes(L), friction=L.friction)
 
 
-def compile_feeding_jaco():
-    """FeedingJaco-v0 scene (feeding.py:144-331 + world_creation.py:27-93,274-293,330-365)."""
+def compile_feeding_jaco(heights=None):
+    """FeedingJaco-v0 scene (feeding.py:144-331 + world_creation.py:27-93,274-293,330-365).
+    heights: per-gender hipbone_to_mouth_height (human_heights); the human is built at it
+    (human_creation.py:60-63,75)."""
+    H = human_heights(heights)
     S = Scene()
     rob = build_jaco()
     S.robot = rob
@@ -590,7 +669,7 @@ def compile_feeding_jaco():
     S.human = {}
     human_body = {}
     for gender in ('male', 'female'):
-        base_shapes, hl = build_human(gender)
+        base_shapes, hl = build_human(gender, H[gender])
         S.human[gender] = (base_shapes, hl)
     # human slot list: base + DFS links that carry shapes; the slot set is identical for both
     # genders, shapes differ -> store per-gender shapes on the same slot (gender-tagged).
@@ -714,6 +793,7 @@ def pr2_fk(dfs, q_of):
     return P, Q
 
 
+@asset_cached
 def build_pr2():
     """The PR2 as ScratchItchPR2-v0 simulates it (world_creation.py:181-217, env.py:450-464):
     fixed base, inertia from file, no self-collision.  Its articulated part is the left arm's
@@ -787,6 +867,7 @@ def build_pr2():
     return rob, groups, torso_com, sub
 
 
+@asset_cached
 def pr2_frozen_joints():
     """The PR2 joints the build holds at the reset pose (every joint outside the left arm's
     subtree), in the base_footprint frame: per DFS index the parent, the joint type (J_*), the
@@ -855,6 +936,7 @@ def build_composite_tool(rel, tip_link):
                 pivot=-c, tip=tip - c, handle_shapes=lead)
 
 
+@asset_cached
 def build_scratcher():
     """tool_scratch.urdf (world_creation.py:344): handle (base) + tool cylinder + tip sphere; the
     tool-force-at-target rule counts tool links 0 and 1 (scratch_itch.py:95), i.e. every shape
@@ -865,16 +947,20 @@ def build_scratcher():
     return t
 
 
+@asset_cached
 def build_wiper():
     """bed_bathing/wiper.urdf (world_creation.py:346): handle (base) + 'tool' box + 'cloth' box;
     bed_bathing.py counts and wipes with tool link 1 only (the cloth, :97)."""
     return build_composite_tool('bed_bathing/wiper.urdf', 'cloth')
 
 
-def compile_scratch_pr2():
+def compile_scratch_pr2(heights=None):
     """ScratchItchPR2-v0 scene (scratch_itch.py:130-273 + world_creation.py:27-93,181-217,
     330-365): plane, wheelchair, the human (right arm 7..13 articulated: controllable joints
-    4..13 keep their masses, world_creation.py:157-161), the PR2 and the scratcher."""
+    4..13 keep their masses, world_creation.py:157-161), the PR2 and the scratcher.  heights:
+    per-gender hipbone_to_mouth_height (human_heights).  The scratch target stays on the
+    unscaled capsule (generate_target uses the default lengths, scratch_itch.py:277-280)."""
+    H = human_heights(heights)
     S = Scene()
     rob, groups, torso_com, sub = build_pr2()
     S.robot = rob
@@ -898,7 +984,7 @@ def compile_scratch_pr2():
     S.human = {}
     human_body = {}
     for gender in ('male', 'female'):
-        S.human[gender] = build_human(gender)
+        S.human[gender] = build_human(gender, H[gender])
     slot_links = [-1] + [i for i, L in enumerate(S.human['male'][1]) if L['shapes']]
     S.human_slots = slot_links
     for si, li in enumerate(slot_links):
@@ -980,24 +1066,29 @@ def capsule_points(p1, p2, radius, distance_between_points=0.05, position_scale=
     return np.array(out)
 
 
-def bed_targets():
-    """generate_targets (bed_bathing.py:359-380) at the default hipbone_to_mouth_height (hmhs 1):
-    wipe targets on the upper arm (link 9) and forearm (link 11) capsules, 3 cm apart, in the
-    link frame, per gender."""
+def bed_targets(heights=None):
+    """generate_targets (bed_bathing.py:359-380): wipe targets on the upper arm (link 9) and
+    forearm (link 11) capsules, 3 cm apart, in the link frame, per gender.  The ring count
+    follows the unscaled capsule length and the axial positions scale by hmhs
+    (position_scale, :369-370); hmhs 1 at the default heights."""
+    H = human_heights(heights)
     limbs = {'male': ((9, 0.279, 0.043), (11, 0.257, 0.033)), 'female': ((9, 0.264, 0.0355), (11, 0.234, 0.027))}
     out = {}
     for g, ((lu, Lu, ru), (lf, Lf, rf)) in limbs.items():
-        out[g] = (capsule_points([0, 0, 0], [0, 0, -Lu], ru, 0.03), capsule_points([0, 0, 0], [0, 0, -Lf], rf, 0.03))
+        hmhs = H[g] / DEFAULT_HEIGHT[g]
+        kw = {} if hmhs == 1.0 else dict(position_scale=hmhs)
+        out[g] = (capsule_points([0, 0, 0], [0, 0, -Lu], ru, 0.03, **kw), capsule_points([0, 0, 0], [0, 0, -Lf], rf, 0.03, **kw))
     return out
 
 
-def compile_bedbath_pr2():
+def compile_bedbath_pr2(heights=None):
     """BedBathingPR2-v0 scene (bed_bathing.py:155-357 + world_creation.py:27-93,181-217,330-365):
     plane, the two mattress boxes and the VHACD bed frame (bed_bathing.py:201-218; the bed loaded
     by create_new_world is removed at :202), the human lying on the bed (base at [0, 0, 0.7]
     pitched -30 deg, :194; right arm 7..13 articulated for the reset's 100-frame settle onto the
     mattress under gravity -1, :283-289, static during the episode, :292-300), the PR2 and the
-    wiper."""
+    wiper.  heights: per-gender hipbone_to_mouth_height (human_heights)."""
+    H = human_heights(heights)
     S = Scene()
     rob, groups, torso_com, sub = build_pr2()
     S.robot = rob
@@ -1014,7 +1105,7 @@ def compile_bedbath_pr2():
     plane = build_static_urdf('plane/plane.urdf')
     m1 = [Shape(BOX, (0, 0, 0.15 / 2.0), half_extents=(0.88 / 2.0, 1.25 / 2.0, 0.15 / 2.0))]
     m2 = [Shape(BOX, (0, 0.7 / 2.0, 0), half_extents=(0.88 / 2.0, 0.7 / 2.0, 0.15 / 2.0))]
-    frame = [Shape(HULL, hull=Hull(g * np.array([1, 1.2, 1]))) for g in obj_groups(os.path.join(REF_ASSETS, 'bed', 'hospital_bed_frame_vhacd.obj'))]
+    frame = [Shape(HULL, hull=h) for h in bed_frame_hulls()]
     S.static = [dict(name='plane', pos=np.zeros(3), quat=np.array([0, 0, 0, 1.0])),
                 dict(name='mattress', pos=np.array([0, BED_Y_OFFSET, 0.4]), quat=np.array([0, 0, 0, 1.0])),
                 dict(name='mattress_head', pos=np.array([0, 1.25 / 2.0 + BED_Y_OFFSET, 0.4 + 0.15 / 2.0]), quat=G.quat_from_euler([np.deg2rad(60), 0, 0])),
@@ -1026,7 +1117,7 @@ def compile_bedbath_pr2():
     S.human = {}
     human_body = {}
     for gender in ('male', 'female'):
-        S.human[gender] = build_human(gender)
+        S.human[gender] = build_human(gender, H[gender])
     slot_links = [-1] + [i for i, L in enumerate(S.human['male'][1]) if L['shapes']]
     S.human_slots = slot_links
     for si, li in enumerate(slot_links):
@@ -1073,7 +1164,7 @@ def compile_bedbath_pr2():
         tool_link=sub.index(PR2_TOOL_LINK), torso_com=torso_com,
         tool_pos_offset=np.zeros(3), tool_orient_offset=np.array([0, 0, 0, 1.0]),   # bed_bathing.py:320
         tool_pivot=tool['pivot'], tool_tip=tool['tip'], tool_handle_shapes=tool['handle_shapes'],
-        targets=bed_targets(),
+        targets=bed_targets(H),
     )
     return S
 
@@ -1181,9 +1272,8 @@ def _human_tables(S, A):
     A['n_pairs_base'] = np.int32(S.n_pairs_base)
 
 
-def compile_feeding(out_dir=DATA_DIR):
-    os.makedirs(out_dir, exist_ok=True)
-    S = compile_feeding_jaco()
+def feeding_arrays(heights=None):
+    S = compile_feeding_jaco(heights)
     A = to_arrays(S)
     _human_tables(S, A)
     A.update(head_chain(S, HEAD_CHAIN, cap=4))
@@ -1202,14 +1292,19 @@ def compile_feeding(out_dir=DATA_DIR):
     A['task_table_body'] = np.int32(S.table_body)
     A['task_human_body0'] = np.int32(S.human_body[S.human_slots[0]])
     A['task_head_slot'] = np.int32(S.human_slots.index(t['head_link']))
+    return A
+
+
+def compile_feeding(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    A = feeding_arrays()
     path = os.path.join(out_dir, 'feeding_jaco.npz')
     np.savez_compressed(path, **A)
     return path, A
 
 
-def compile_scratch(out_dir=DATA_DIR):
-    os.makedirs(out_dir, exist_ok=True)
-    S = compile_scratch_pr2()
+def scratch_arrays(heights=None):
+    S = compile_scratch_pr2(heights)
     A = to_arrays(S)
     _human_tables(S, A)
     A.update(head_chain(S, ARM_CHAIN, cap=HC_CAP))
@@ -1228,14 +1323,19 @@ def compile_scratch(out_dir=DATA_DIR):
     A['n_rstatic'] = np.int32(len(S.rstatic))
     A['rl_urdf'] = np.array(S.robot['urdf'], np.int32)
     A.update(pr2_frozen_joints())
+    return A
+
+
+def compile_scratch(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    A = scratch_arrays()
     path = os.path.join(out_dir, 'scratch_itch_pr2.npz')
     np.savez_compressed(path, **A)
     return path, A
 
 
-def compile_bedbath(out_dir=DATA_DIR):
-    os.makedirs(out_dir, exist_ok=True)
-    S = compile_bedbath_pr2()
+def bedbath_arrays(heights=None):
+    S = compile_bedbath_pr2(heights)
     A = to_arrays(S)
     _human_tables(S, A)
     A.update(head_chain(S, ARM_CHAIN, cap=HC_CAP))
@@ -1268,16 +1368,37 @@ def compile_bedbath(out_dir=DATA_DIR):
     A['bb_joint_slots'] = np.array([S.human_slots.index(9), S.human_slots.index(11), S.human_slots.index(13)], np.int32)
     A['bb_human_base'] = np.concatenate(BED_HUMAN_BASE)
     A['bb_bed_bodies'] = np.array(S.static_body[1:], np.int32)
+    return A
+
+
+def compile_bedbath(out_dir=DATA_DIR):
+    os.makedirs(out_dir, exist_ok=True)
+    A = bedbath_arrays()
     path = os.path.join(out_dir, 'bed_bathing_pr2.npz')
     np.savez_compressed(path, **A)
     return path, A
 
 
+SCENE_ARRAYS = {'feeding_jaco': feeding_arrays, 'scratch_itch_pr2': scratch_arrays, 'bed_bathing_pr2': bedbath_arrays}
+
+
+def scene_arrays(name, heights=None):
+    """A compiled scene's arrays (what the committed npz holds at the default heights) with the
+    human built at per-gender hipbone_to_mouth_height `heights` (human_heights)."""
+    A = SCENE_ARRAYS[name](heights)
+    A['human_heights'] = np.array([human_heights(heights)[g] for g in ('male', 'female')])
+    return A
+
+
 def compile_all(out_dir=DATA_DIR):
-    """All compiled scenes; returns the FeedingJaco one (path, arrays) first."""
+    """All compiled scenes, and the asset cache scene_arrays rebuilds them from; returns the
+    FeedingJaco one (path, arrays) first."""
+    global _asset_memo
+    _asset_memo = {}                     # rebuilt from the reference's assets
     out = compile_feeding(out_dir)
     compile_scratch(out_dir)
     compile_bedbath(out_dir)
+    save_asset_cache(os.path.join(out_dir, 'asset_cache.pkl'))
     return out
 
 

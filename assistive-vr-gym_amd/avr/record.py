@@ -354,9 +354,11 @@ class ReferenceReplayEnv:
     each step() re-simulates the next recorded action (the action passed in is ignored, as in
     feeding.py:38); done after the last recorded action (feeding.py:79-80: 200).
 
-    The compiled humans have the reference's default proportions; a recording with another
-    hipbone_to_mouth_height raises NotImplementedError unless default_proportions=True, which
-    replays it on the default human (noted in `self.proportions`)."""
+    The human is built at the recording's hipbone_to_mouth_height (feeding.py:153-156 reads it
+    from setup.pkl before create_new_world; AVRVecEnv's human_heights), on this build's non-VR
+    human model -- the reference builds its VR human for replays (world_creation.py:19-20), a
+    model this build does not compile.  default_proportions=True replays on the default human
+    instead (noted in `self.proportions`).  The recording's frame_%d.bullet states are not read."""
 
     def __init__(self, directory, env_id=None, device=0, seed=1001, default_proportions=False):
         from . import env as EV
@@ -369,20 +371,19 @@ class ReferenceReplayEnv:
             raise ValueError('%s/setup.pkl: expected [robot_type, gender, hipbone_to_mouth_height]' % directory)
         self.robot_type, self.gender, hip = setup
         self.hipbone_to_mouth_height = None if hip is None else float(hip)
+        if self.gender not in ('male', 'female'):
+            raise ValueError('%s/setup.pkl: gender %r' % (directory, self.gender))
         acts = load_reference_pickle(os.path.join(directory, 'actions.pkl'))
         self.action_list = np.asarray([np.asarray(a, np.float32).reshape(-1) for a in acts], np.float32)
-        self.env = EV.AVRVecEnv(self.env_id, 1, device=device, seed=seed, auto_reset=False, prefetch=False)
-        if self.action_list.ndim != 2 or self.action_list.shape[1] != self.env.L.ACT_DIM:
-            raise ValueError('%s/actions.pkl: actions of shape %s, the task takes %d' % (directory, self.action_list.shape, self.env.L.ACT_DIM))
-        default = 0.6 if self.gender == 'male' else 0.54
-        self.proportions = 'recorded'
         hip = self.hipbone_to_mouth_height
-        if hip is not None and abs(hip - default) > 1e-9:
-            if not default_proportions:
-                self.env.close()
-                raise NotImplementedError('%s: hipbone_to_mouth_height %.4f; only the default %.2f (%s) is compiled '
-                                          '(default_proportions=True replays on it)' % (directory, hip, default, self.gender))
+        self.proportions = 'recorded' if hip is not None else 'default'
+        if hip is not None and default_proportions:
             hip, self.proportions = None, 'default (recorded %.4f)' % self.hipbone_to_mouth_height
+        self.env = EV.AVRVecEnv(self.env_id, 1, device=device, seed=seed, auto_reset=False, prefetch=False,
+                                human_heights={self.gender: hip})
+        if self.action_list.ndim != 2 or self.action_list.shape[1] != self.env.L.ACT_DIM:
+            self.env.close()
+            raise ValueError('%s/actions.pkl: actions of shape %s, the task takes %d' % (directory, self.action_list.shape, self.env.L.ACT_DIM))
         self.env.setup(self.gender, -1, '', hip)
         self.iteration = 0
 

@@ -254,6 +254,35 @@ def test_reference_recording_replays_its_actions(tmp_path):
     np.testing.assert_array_equal(np.array(rews, np.float32), v['rewards'].astype(np.float32))
     z = np.load(str(tmp_path / 'meta.npz'), allow_pickle=False)
     assert z['0_actions'].shape == (200, 7)
-    R.write_reference_recording(str(d), 'jaco', 'female', 0.571, acts)
-    with pytest.raises(NotImplementedError):
-        R.ReferenceReplayEnv(str(d))
+
+
+@pytest.mark.gpu
+def test_reference_recording_replays_at_its_height(tmp_path):
+    """A recording whose setup.pkl holds a non-default hipbone_to_mouth_height (0.57, female)
+    replays on a human built at that height (feeding.py:153-156, human_creation.py:60-63): it
+    equals a live env built with human_heights={'female': 0.57} and driven by the same actions,
+    and differs from the default-height replay (the mouth, hence the observation, moves)."""
+    from avr import env as EV
+    rng = np.random.default_rng(4)
+    acts = [rng.uniform(-1, 1, 7).astype(np.float32) for _ in range(20)]
+    d = tmp_path / 'participant_2' / 'feeding_vr_data_jaco_ppo_participant_2'
+    R.write_reference_recording(str(d), 'jaco', 'female', 0.57, acts)
+    r = R.ReferenceReplayEnv(str(d))
+    assert r.proportions == 'recorded' and r.env.human_heights == {'male': 0.6, 'female': 0.57}
+    o0 = r.reset()
+    rep = [r.step() for _ in acts]
+    r.close()
+    live = EV.AVRVecEnv('FeedingJaco-v0', 1, auto_reset=False, prefetch=False, human_heights={'female': 0.57})
+    live.setup('female', -1, '')
+    l0 = live.reset()
+    np.testing.assert_array_equal(o0, l0)
+    for (o, rw, _, _), a in zip(rep, acts):
+        lo, lr, _, _ = live.step(a[None])
+        np.testing.assert_array_equal(o, lo)
+        np.testing.assert_array_equal(rw, lr)
+    live.close()
+    r = R.ReferenceReplayEnv(str(d), default_proportions=True)
+    assert r.proportions.startswith('default')
+    od = r.reset()
+    r.close()
+    assert np.abs(od - o0).max() > 1e-3
