@@ -19,8 +19,8 @@ ships.  Nothing here is on the step path.  What it restates, with reference cita
 """
 import copy
 import functools
+import json
 import os
-import pickle
 import re
 import struct
 import xml.etree.ElementTree as ET
@@ -34,12 +34,49 @@ REF_ASSETS = '/root/reference/assistive_gym/envs/assets'
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 
 # Every builder that reads the reference's assets goes through asset_cached: its result is kept
-# in data/asset_cache.pkl (written by compile_all in the build container, this module's own
-# output), so that scene_arrays can rebuild a scene at another human height where the reference's
-# assets are absent (the GPU box).  The cache holds the builders' parsed and hulled geometry,
-# the same numbers the committed scene npz files hold, not the asset files.
-ASSET_CACHE = os.path.join(DATA_DIR, 'asset_cache.pkl')
+# in data/asset_cache.npz (written by compile_all in the build container), so that scene_arrays
+# can rebuild a scene at another human height where the reference's assets are absent (the GPU
+# box).  The cache holds the builders' parsed and hulled geometry -- the same numbers the
+# committed scene npz files hold, not the asset files -- as JSON (structure) plus arrays, read
+# with np.load(allow_pickle=False): nothing in it executes.
+ASSET_CACHE = os.path.join(DATA_DIR, 'asset_cache.npz')
 _asset_memo = None
+
+
+def _enc(x, arrs):
+    if isinstance(x, np.ndarray):
+        arrs.append(x)
+        return {'__nd__': len(arrs) - 1}
+    if isinstance(x, (Shape, Hull)):
+        return {'__%s__' % type(x).__name__: {k: _enc(v, arrs) for k, v in vars(x).items()}}
+    if isinstance(x, dict):
+        assert all(isinstance(k, str) for k in x)
+        return {'__dict__': {k: _enc(v, arrs) for k, v in x.items()}}
+    if isinstance(x, tuple):
+        return {'__tuple__': [_enc(v, arrs) for v in x]}
+    if isinstance(x, list):
+        return [_enc(v, arrs) for v in x]
+    assert x is None or isinstance(x, (str, bool, int, float)), type(x)
+    return x
+
+
+def _dec(x, arrs):
+    if isinstance(x, list):
+        return [_dec(v, arrs) for v in x]
+    if not isinstance(x, dict):
+        return x
+    (tag, v), = x.items()
+    if tag == '__nd__':
+        return arrs['a%d' % v]
+    if tag in ('__Shape__', '__Hull__'):
+        o = object.__new__(Shape if tag == '__Shape__' else Hull)
+        o.__dict__.update({k: _dec(w, arrs) for k, w in v.items()})
+        return o
+    if tag == '__dict__':
+        return {k: _dec(w, arrs) for k, w in v.items()}
+    if tag == '__tuple__':
+        return tuple(_dec(w, arrs) for w in v)
+    raise ValueError('asset cache: unknown tag %r' % tag)
 
 
 def _memo():
@@ -47,8 +84,10 @@ def _memo():
     if _asset_memo is None:
         _asset_memo = {}
         if os.path.exists(ASSET_CACHE):
-            with open(ASSET_CACHE, 'rb') as f:
-                _asset_memo = pickle.load(f)
+            with np.load(ASSET_CACHE, allow_pickle=False) as z:
+                arrs = {k: z[k] for k in z.files}
+            meta = json.loads(bytes(arrs.pop('meta')).decode())
+            _asset_memo = {tuple(k): _dec(v, arrs) for k, v in meta}
     return _asset_memo
 
 
@@ -67,8 +106,11 @@ def asset_cached(fn):
 
 
 def save_asset_cache(path=ASSET_CACHE):
-    with open(path, 'wb') as f:
-        pickle.dump(_memo(), f, protocol=4)
+    arrs = []
+    meta = [[list(k), _enc(v, arrs)] for k, v in _memo().items()]
+    out = {'a%d' % i: a for i, a in enumerate(arrs)}
+    out['meta'] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+    np.savez_compressed(path, **out)
 
 
 URDF_MARGIN = 0.001          # gUrdfDefaultCollisionMargin (assumed Bullet default)
@@ -1398,7 +1440,7 @@ def compile_all(out_dir=DATA_DIR):
     out = compile_feeding(out_dir)
     compile_scratch(out_dir)
     compile_bedbath(out_dir)
-    save_asset_cache(os.path.join(out_dir, 'asset_cache.pkl'))
+    save_asset_cache(os.path.join(out_dir, 'asset_cache.npz'))
     return out
 
 
