@@ -463,22 +463,28 @@ def write_detail(details):
         return None
 
 
-def policy_eval_bench(args):
+def policy_eval_run(name, E, steps=200):
     """enjoy_vr.py's evaluation loop (avr.policy_eval.evaluate: policy forward on the normalised
-    obs, then AVRTorchVecEnv.step with the policy's fresh action tensor) for one 200-step trial in
-    each of --envs envs; env-steps/s of the stepping loop (env creation and reset excluded)."""
-    import numpy as np
+    obs, then AVRTorchVecEnv.step with the policy's fresh action tensor) for one `steps`-step trial
+    in each of E envs: (evaluate's result, seconds including env creation and reset)."""
     import torch
     from avr import policy_eval as PE, _abi as ABI
-    name = args.task
     L = ABI.LAYOUTS[TASKS[name]['task']]
     torch.manual_seed(0)
     pol = PE.ActorCritic(L.OBS_DIM, L.ACT_DIM)
     rms = PE.RunningMeanStd((L.OBS_DIM,))
     t0 = time.perf_counter()
+    r = PE.evaluate(name, pol, rms, n_envs=E, steps=steps, deterministic=False, device=0)
+    return r, time.perf_counter() - t0
+
+
+def policy_eval_bench(args):
+    """policy_eval_run for 200 steps in each of --envs envs; env-steps/s of the stepping loop
+    (env creation and reset excluded)."""
+    import numpy as np
+    name = args.task
     E = args.envs if args.envs is not None else TASKS[name].get('envs', 4096)
-    r = PE.evaluate(name, pol, rms, n_envs=E, steps=200, deterministic=False, device=0)
-    total = time.perf_counter() - t0
+    r, total = policy_eval_run(name, E)
     out = {'metric': 'policy-eval env-steps/sec (avr.policy_eval.evaluate: enjoy_vr.py loop, fresh action tensor per step)',
            'value': E * 200 / r['loop_s'], 'unit': 'env-steps/s', 'n_gpus': 1, 'steps': 200, 'warmup': 0,
            'ms_per_step': r['loop_s'] / 200 * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
@@ -518,6 +524,9 @@ def main():
     ap.add_argument('--policy-eval', action='store_true',
                     help='time avr.policy_eval.evaluate (enjoy_vr.py harness: synthetic MLP policy, VecNormalize eval) at --envs '
                          'envs for 200 steps')
+    ap.add_argument('--policy-eval-steps', type=int, default=200,
+                    help='N=1 FeedingJaco runs: also time this many steps of the policy-evaluation loop (policy in the '
+                         'loop, per-step observations), reported as policy_eval (0 = skip)')
     ap.add_argument('--dist-backend', default='nccl', choices=('nccl', 'gloo'),
                     help="torch.distributed backend for --gpus > 1: nccl (RCCL over xGMI, the product path); gloo only "
                          "rehearses the multi-rank flow where ranks share a GPU (rollouts gathered through host memory)")
@@ -555,6 +564,14 @@ def main():
             o, det = run_task(name, args, args.other_steps, args.warmup, world, rank, local, dist, gloo, dev, min(cpu_s, 5.0))
             out['other_tasks'][name] = compact_other(o)
             details.append(det)
+    if rank == 0 and world == 1 and args.task == 'FeedingJaco-v0' and args.policy_eval_steps > 0:
+        # the trainer-facing rate: a policy in the loop needs every step's observation (enjoy_vr.py:106-116)
+        progress('FeedingJaco-v0: policy-eval loop')
+        E = args.envs if args.envs is not None else TASKS[args.task].get('envs', 4096)
+        r, _ = policy_eval_run(args.task, E, args.policy_eval_steps)
+        out['policy_eval'] = {'value': E * args.policy_eval_steps / r['loop_s'], 'ms_per_step': r['loop_s'] / args.policy_eval_steps * 1e3,
+                              'steps': args.policy_eval_steps, 'envs': E,
+                              'loop': 'avr.policy_eval.evaluate: random-init MLP actor-critic forward + AVRTorchVecEnv.step per step'}
     if rank == 0:
         out['detail'] = write_detail(details)
         print(json.dumps(out, separators=(',', ':')), flush=True)
