@@ -26,7 +26,6 @@ import struct
 import xml.etree.ElementTree as ET
 
 import numpy as np
-from scipy.spatial import ConvexHull
 
 from . import geom as G
 
@@ -172,6 +171,7 @@ class Hull:
     """Convex hull of a point set: hull vertices + merged face planes n.x <= d (core, no margin)."""
 
     def __init__(self, pts):
+        from scipy.spatial import ConvexHull     # (build container only: cached hulls need no scipy)
         pts = np.asarray(pts, float)
         h = ConvexHull(pts)
         self.verts = pts[h.vertices]
