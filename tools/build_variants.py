@@ -36,7 +36,6 @@ VARIANTS = {
     'mclause': ('-mllvm', '-amdgpu-sched-strategy=max-memory-clause'), 'ilp': ('-mllvm', '-amdgpu-sched-strategy=max-ilp'),
     'itilp': ('-mllvm', '-amdgpu-sched-strategy=iterative-ilp'),
     'nonl': ('-DB4_NC_LDS=0',), 'fnl': ('-DB4_NC_LDS=1',), 'fnl12': ('-DB4_NC_LDS=1', '-DB4_LDSW=12288'), 'fnl11': ('-DB4_NC_LDS=1', '-DB4_LDSW=11264'), 'dnl2': ('-DB4_DNL=2',), 'noml': ('-DAVR_MINV_LAUNDER=0',),
-    'mpf': ('-DAVR_M_PF=1',),
     'cr0': ('-DAVR_COOP_ROWS=0',), 'ccheck': ('-DAVR_COOP_CHECK',), 'cr2': ('-DAVR_COOP_ROWS=2',), 'cr8': ('-DAVR_COOP_ROWS=8',),
 }
 
